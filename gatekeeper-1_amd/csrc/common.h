@@ -1,0 +1,188 @@
+// Shared host/device definitions for the MI355X policy-evaluation engine.
+//
+// Everything the kernels read lives in flat, 16-byte-aligned arrays in HBM:
+//   * Node      — one JSON value of a review / constraint-parameter / literal
+//                 document (children of an object/array are contiguous);
+//   * StrEnt    — interned string table (global ids; equal bytes == equal id);
+//   * NumEnt    — number table (int64 + exact 64-bit-mantissa big.Float form);
+//   * Ins       — predicate bytecode compiled from ConstraintTemplate Rego;
+//   * MatchSpec — a constraint's compiled `spec.match` (kinds / namespaces /
+//                 selectors / scope), evaluated by the match stage;
+//   * ReviewCol — per-review match columns extracted by the host flattener.
+#pragma once
+#include <stdint.h>
+
+namespace gk {
+
+// ----------------------------------------------------------------- documents
+enum NodeType : uint8_t { NT_NONE = 0, NT_NULL = 1, NT_FALSE = 2, NT_TRUE = 3, NT_NUM = 4, NT_STR = 5, NT_ARR = 6, NT_OBJ = 7 };
+
+struct Node {
+  uint32_t key;    // object member: key string id; array element: index
+  uint32_t val;    // NT_STR: string id; NT_NUM: number id
+  uint32_t first;  // NT_ARR/NT_OBJ: absolute index of first child
+  uint16_t n;      // child count
+  uint8_t type;    // NodeType
+  uint8_t flags;
+};
+static_assert(sizeof(Node) == 16, "Node must be 16 bytes");
+
+struct StrEnt {
+  uint32_t off;    // byte offset into the string pool
+  uint32_t len;    // byte length
+};
+
+enum StrFlags : uint8_t { SF_ASCII_PRINT = 1, SF_NEEDS_ESC = 2, SF_NON_ASCII = 4 };
+
+enum NumFlags : uint32_t { NF_INT64 = 1, NF_BF_OK = 2, NF_PRINT_OK = 4 };
+
+struct NumEnt {
+  int64_t i;        // value when NF_INT64 (json.Number.Int64 parses)
+  uint64_t mant;    // big.Float at prec 64: mant in [2^63,2^64) (0 for zero)
+  int32_t exp;      // value = mant * 2^exp
+  uint32_t flags;
+  uint32_t text;    // string id of the literal text (Term.String)
+  uint32_t print;   // string id of the Go %v text (int / float64 conversion)
+  uint32_t neg;
+  uint32_t pad;
+};
+static_assert(sizeof(NumEnt) == 40, "NumEnt layout");
+
+// ----------------------------------------------------------------- values
+// 64-bit tagged VM values: tag in bits 60..63.
+enum Tag : uint32_t {
+  V_UNDEF = 0, V_NULL = 1, V_BOOL = 2, V_NUM = 3,  // NUM: number-table id
+  V_STR = 4,                                       // STR: string id
+  V_NODE = 5,                                      // NODE: node index (array/object)
+  V_INT = 6,                                       // INT: computed int (48-bit two's complement)
+  V_BFN = 7,                                       // BFN: heap word index of a computed big-float
+  V_HSTR = 8,                                      // HSTR: lane byte-buffer string (off:16 | len:16)
+  V_LIST = 9,                                      // LIST: heap list (set/array/object); kind in bits 56..59
+  V_SLICE = 10,                                    // SLICE: string id:32 | start:14 | len:14
+};
+enum ListKind : uint32_t { LK_SET = 1, LK_ARR = 2, LK_OBJ = 3 };
+
+// ----------------------------------------------------------------- bytecode
+enum Op : uint16_t {
+  OP_END = 0,
+  OP_JMP,          // x
+  OP_JUNDEF,       // a, x : jump if R[a] undefined
+  OP_JFALSE,       // a, x : jump if R[a] == false
+  OP_JTRUE,        // a, x : jump if R[a] == true
+  OP_LOADK,        // a, x : R[a] = K[x]
+  OP_LOADREV,      // a    : R[a] = review root
+  OP_LOADPARAM,    // a    : R[a] = constraint parameters
+  OP_MOV,          // a, b
+  OP_GET,          // a, b, c : R[a] = R[b][R[c]]
+  OP_GETK,         // a, b, x : R[a] = R[b][K[x]]
+  OP_ITER_INIT,    // a(iter base: a=coll, a+1=pos), b=coll
+  OP_ITER_NEXT,    // a(iter base), b(key dst|0xffff), c(val dst|0xffff), x=exit
+  OP_CMP,          // a, b, c, y=cmp kind : R[a] = bool
+  OP_ARITH,        // a, b, c, y=kind
+  OP_LIST_NEW,     // a, y=kind
+  OP_LIST_ADD,     // a(list), b(value)      : set/array append (set dedupes)
+  OP_OBJ_PUT,      // a(obj), b(key), c(value)
+  OP_YIELD,        // a(out), b(val) : conflict check + assign
+  OP_CALL,         // a(dst), b(arg base), c(nargs), y=builtin id
+  OP_SPRINTF,      // a(dst), b(args list), x=format index
+  OP_EMIT,         // a(msg), b(details), y=rule index
+  OP_LEN_EQ,       // a(dst bool), b(value), y=n : collection length test (array patterns)
+  OP_FAIL_FALLBACK,// y=reason : unsupported construct reached at run time
+  OP_COUNT_
+};
+
+struct Ins {
+  uint16_t op, a, b, c;
+  uint32_t x, y;
+};
+static_assert(sizeof(Ins) == 16, "Ins must be 16 bytes");
+
+enum CmpKind : uint32_t { CMP_EQ = 0, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE };
+enum ArithKind : uint32_t { AR_PLUS = 0, AR_MINUS, AR_MUL, AR_DIV, AR_REM, AR_OR, AR_AND };
+
+enum Builtin : uint32_t {
+  BI_COUNT = 0, BI_ANY, BI_ALL, BI_STARTSWITH, BI_ENDSWITH, BI_CONTAINS, BI_RE_MATCH, BI_TO_NUMBER,
+  BI_REPLACE, BI_SUBSTRING, BI_IS_NUMBER, BI_IS_STRING, BI_IS_BOOLEAN, BI_IS_ARRAY, BI_IS_OBJECT,
+  BI_IS_SET, BI_IS_NULL, BI_LOWER, BI_UPPER, BI_TRIM, BI_SPLIT, BI_CONCAT, BI_INDEXOF,
+  BI_TRIM_PREFIX, BI_TRIM_SUFFIX, BI_COUNT_
+};
+
+// per-(review) outcome flags
+enum ReviewFlags : uint32_t {
+  RF_ERROR = 1u,      // the reference Query would return an error for this review
+  RF_FALLBACK = 2u,   // evaluation needs the CPU OPA driver (value/builtin outside the GPU subset)
+  RF_OVERFLOW = 4u,   // output buffer overflow (host re-runs)
+};
+
+// fallback reason codes (diagnostics)
+enum Reason : uint32_t {
+  FB_NONE = 0, FB_HEAP, FB_MSG_LEN, FB_NUMBER, FB_UNICODE, FB_DEEP_EQ, FB_REGEX, FB_PRINT, FB_TYPE,
+  FB_UNSUPPORTED, FB_MATCH, FB_STRING,
+};
+
+// ----------------------------------------------------------------- match
+constexpr uint32_t NO_ID = 0xffffffffu;
+
+// A label selector compiled for the match stage (target_template_source.go:185-230).
+// Encoded in the constraint side table as u32 words:
+//   [n_match_labels, (key, val)*n, n_exprs, (op, key, n_vals, vals...)*]
+enum SelOp : uint32_t { SO_IN = 1, SO_NOTIN = 2, SO_EXISTS = 3, SO_DOESNOTEXIST = 4, SO_OTHER = 5 };
+
+enum MatchFlags : uint32_t {
+  MF_HAS_NAMESPACES = 1, MF_HAS_EXCLUDED = 2, MF_HAS_NSSEL = 4, MF_SCOPE_PRESENT = 8,
+  MF_SCOPE_ANY = 16, MF_SCOPE_NS = 32, MF_SCOPE_CLUSTER = 64, MF_FALLBACK = 128, MF_ERROR = 256,
+};
+
+struct MatchSpec {
+  uint32_t flags;
+  uint32_t kinds_off;     // word offset in the match word table: [n_sel, (n_groups, g.., n_kinds, k..)*]
+  uint32_t ns_off;        // [n, ids...]
+  uint32_t exns_off;      // [n, ids...]
+  uint32_t labelsel_off;  // selector words
+  uint32_t nssel_off;     // selector words
+  uint32_t prog;          // program index of the template
+  uint32_t params;        // node index of spec.parameters (or NO_ID => {})
+};
+
+enum ReviewColFlags : uint32_t {
+  RC_KIND_OK = 1,         // review.kind.{group,kind} are strings
+  RC_IS_NS = 2,           // kind.group == "" && kind.kind == "Namespace"
+  RC_HAS_NS = 4,          // review.namespace defined (string)
+  RC_NS_EMPTY = 8,        // get_default(review, "namespace", "") == ""
+  RC_UNSTABLE_NS = 16,    // review._unstable.namespace is truthy (object)
+  RC_NS_CACHED = 32,      // namespace object found in data.external cluster cache
+  RC_LABELS_OBJ = 64,     // any_labelselector_match uses object labels
+  RC_LABELS_OLD = 128,    // any_labelselector_match uses oldObject labels
+  RC_NAME_OK = 256,       // object.metadata.name defined (for Namespace kinds)
+  RC_FALLBACK = 512,      // review shape outside the match fast path
+  RC_REVIEW_DEF = 1024,   // input.review defined
+};
+
+struct ReviewCol {
+  uint32_t root;      // review document root node
+  uint32_t group;     // string ids
+  uint32_t kind;
+  uint32_t ns;        // namespace string id (review.namespace) or NO_ID
+  uint32_t nsname;    // is_ns ? object.metadata.name : review.namespace
+  uint32_t labels;    // node of object labels ({} => NO_ID)
+  uint32_t old_labels;
+  uint32_t ns_labels; // labels node of the namespace object used by namespaceSelector
+  uint32_t flags;
+  uint32_t pad[3];
+};
+static_assert(sizeof(ReviewCol) == 48, "ReviewCol layout");
+
+// ----------------------------------------------------------------- output
+struct Viol {
+  uint32_t review;
+  uint32_t constraint;
+  uint32_t seq;       // emission order within (review, constraint)
+  uint32_t rule;      // template rule index (0xffff = autoreject)
+  uint32_t msg_off, msg_len;
+  uint32_t det_off, det_len;
+};
+static_assert(sizeof(Viol) == 32, "Viol layout");
+
+constexpr uint32_t RULE_AUTOREJECT = 0xffffu;
+
+}  // namespace gk

@@ -1,0 +1,891 @@
+// Rego -> loop-nest bytecode compiler (continuation-passing codegen).
+//
+// compile_term(t, fail, k): emits code that computes every value of term t;
+// for each value it runs continuation k(reg, fail') where fail' is the label
+// to jump to for the next value (backtracking).  Generators (unbound ref
+// selectors, partial-set references) open ITER loops whose NEXT label is the
+// continuation's failure label; when a loop is exhausted control goes to the
+// enclosing failure label.  Solution-collecting constructs (function calls,
+// complete rules, comprehensions, negation) compile their inner body with a
+// fresh "done" label and continue after it.
+#include "compiler.h"
+
+#include <functional>
+#include <map>
+#include <set>
+
+namespace gk {
+using namespace rego;
+
+std::vector<std::shared_ptr<Rule>> ModuleSet::rules(const std::vector<std::string>& pkg, const std::string& name) const {
+  std::vector<std::shared_ptr<Rule>> out;
+  auto it = by_pkg.find(pkg);
+  if (it == by_pkg.end()) return out;
+  for (auto& m : it->second)
+    for (auto& r : m->rules)
+      if (r->name == name) out.push_back(r);
+  return out;
+}
+
+namespace {
+
+constexpr uint16_t NOREG = 0xffff;
+
+struct Env {
+  std::map<std::string, int> vars;
+  Env* parent = nullptr;
+  const Module* mod = nullptr;
+  int lookup(const std::string& v) const {
+    for (const Env* e = this; e; e = e->parent) {
+      auto it = e->vars.find(v);
+      if (it != e->vars.end()) return it->second;
+    }
+    return -1;
+  }
+};
+
+using K = std::function<void(int reg, int fail)>;
+using KE = std::function<void(int fail)>;
+
+const std::map<std::string, uint32_t> kBuiltins = {
+    {"count", BI_COUNT}, {"any", BI_ANY}, {"all", BI_ALL}, {"startswith", BI_STARTSWITH},
+    {"endswith", BI_ENDSWITH}, {"contains", BI_CONTAINS}, {"re_match", BI_RE_MATCH}, {"regex.match", BI_RE_MATCH},
+    {"to_number", BI_TO_NUMBER}, {"replace", BI_REPLACE}, {"substring", BI_SUBSTRING},
+    {"is_number", BI_IS_NUMBER}, {"is_string", BI_IS_STRING}, {"is_boolean", BI_IS_BOOLEAN},
+    {"is_array", BI_IS_ARRAY}, {"is_object", BI_IS_OBJECT}, {"is_set", BI_IS_SET}, {"is_null", BI_IS_NULL},
+    {"lower", BI_LOWER}, {"upper", BI_UPPER}, {"trim", BI_TRIM}, {"split", BI_SPLIT}, {"concat", BI_CONCAT},
+    {"indexof", BI_INDEXOF}, {"trim_prefix", BI_TRIM_PREFIX}, {"trim_suffix", BI_TRIM_SUFFIX},
+};
+const std::map<uint32_t, int> kArity = {
+    {BI_COUNT, 1}, {BI_ANY, 1}, {BI_ALL, 1}, {BI_STARTSWITH, 2}, {BI_ENDSWITH, 2}, {BI_CONTAINS, 2},
+    {BI_RE_MATCH, 2}, {BI_TO_NUMBER, 1}, {BI_REPLACE, 3}, {BI_SUBSTRING, 3}, {BI_IS_NUMBER, 1},
+    {BI_IS_STRING, 1}, {BI_IS_BOOLEAN, 1}, {BI_IS_ARRAY, 1}, {BI_IS_OBJECT, 1}, {BI_IS_SET, 1},
+    {BI_IS_NULL, 1}, {BI_LOWER, 1}, {BI_UPPER, 1}, {BI_TRIM, 2}, {BI_SPLIT, 2}, {BI_CONCAT, 2},
+    {BI_INDEXOF, 2}, {BI_TRIM_PREFIX, 2}, {BI_TRIM_SUFFIX, 2},
+};
+const std::map<std::string, uint32_t> kCmp = {{"equal", CMP_EQ}, {"neq", CMP_NE}, {"lt", CMP_LT},
+                                              {"lte", CMP_LE}, {"gt", CMP_GT}, {"gte", CMP_GE}};
+const std::map<std::string, uint32_t> kArith = {{"plus", AR_PLUS}, {"minus", AR_MINUS}, {"mul", AR_MUL},
+                                                {"div", AR_DIV}, {"rem", AR_REM}, {"or", AR_OR}, {"and", AR_AND}};
+
+class Comp {
+ public:
+  Comp(Store& st, const ModuleSet& mods, CodeBank& bank) : st_(st), mods_(mods), bank_(bank) {}
+
+  Program run(const std::vector<std::string>& pkg) {
+    auto rules = mods_.rules(pkg, "violation");
+    if (rules.empty()) throw Unsupported("template has no violation rule");
+    int rule_idx = 0;
+    for (auto& r : rules) {
+      if (r->kind != Rule::PSET) throw Unsupported("violation must be a partial set rule");
+      int Lr = label();
+      Env env;
+      env.mod = r->mod;
+      int save = reg_top_;
+      const auto& body = cbody(r, {});
+      int idx = rule_idx++;
+      body_k(body, 0, &env, Lr, [&, idx](int f) { emit_violation(r, &env, idx, f); });
+      place(Lr);
+      reg_top_ = save;
+      prog_.rules.push_back(r->name);
+    }
+    emit(OP_END);
+    return finish();
+  }
+
+ private:
+  Store& st_;
+  const ModuleSet& mods_;
+  CodeBank& bank_;
+  std::vector<Ins> code_;
+  std::vector<int> labels_;
+  std::map<uint64_t, uint32_t> kidx_;
+  int reg_top_ = 0, max_reg_ = 0;
+  int inline_depth_ = 0;
+  std::vector<int> loop_base_;  // register base of each enclosing ITER loop (innermost last)
+  Program prog_;
+
+  // Loops the value written to `dst` escapes: depths (lo, hi] (1-based), packed
+  // into an instruction's y field as lo | hi << 8.  A register allocated before
+  // loop j started lives outside loop j, so a heap value stored into it must
+  // survive loop j's per-iteration heap reset.
+  uint32_t escape_range(int dst) {
+    int dd = 0;
+    for (int b : loop_base_) if (b <= dst) ++dd;
+    int cd = (int)loop_base_.size();
+    if (dd >= cd) return 0;
+    return (uint32_t)(dd + 1) | ((uint32_t)cd << 8);
+  }
+  void open_loop(int it, int coll) {
+    if (loop_base_.size() >= 15) throw Unsupported("loop nesting too deep");
+    emit(OP_ITER_INIT, (uint16_t)it, (uint16_t)coll, 0, 0, (uint32_t)loop_base_.size() + 1);
+    loop_base_.push_back(reg_top_);
+  }
+  void close_loop() { loop_base_.pop_back(); }
+  int depth() const { return (int)loop_base_.size(); }
+  std::map<std::pair<const Rule*, std::string>, std::vector<ExprP>> cbody_cache_;
+
+  // ---------------------------------------------------------------- emit
+  int label() { labels_.push_back(-1); return (int)labels_.size() - 1; }
+  void place(int l) { labels_[l] = (int)code_.size(); }
+  void emit(uint16_t op, uint16_t a = 0, uint16_t b = 0, uint16_t c = 0, uint32_t x = 0, uint32_t y = 0) {
+    code_.push_back(Ins{op, a, b, c, x, y});
+  }
+  void emit_jmp(uint16_t op, int a, int lbl) { emit(op, (uint16_t)a, 0, 0, (uint32_t)lbl, 0); }
+  int alloc(int n = 1) {
+    int r = reg_top_;
+    reg_top_ += n;
+    if (reg_top_ > max_reg_) max_reg_ = reg_top_;
+    if (reg_top_ > 4000) throw Unsupported("register pressure");
+    return r;
+  }
+  uint32_t kconst(uint64_t v) {
+    auto it = kidx_.find(v);
+    if (it != kidx_.end()) return it->second;
+    uint32_t i = (uint32_t)bank_.consts.size();
+    bank_.consts.push_back(v);
+    kidx_[v] = i;
+    return i;
+  }
+  int loadk(uint64_t v) {
+    int r = alloc();
+    emit(OP_LOADK, (uint16_t)r, 0, 0, kconst(v));
+    return r;
+  }
+
+  Program finish() {
+    prog_.code_off = (uint32_t)bank_.code.size();
+    prog_.code_len = (uint32_t)code_.size();
+    for (auto& in : code_) {
+      switch (in.op) {
+        case OP_JMP: case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT:
+          if (labels_[in.x] < 0) throw std::runtime_error("unplaced label");
+          in.x = prog_.code_off + (uint32_t)labels_[in.x];
+          break;
+        default: break;
+      }
+      bank_.code.push_back(in);
+    }
+    prog_.nregs = (uint32_t)max_reg_;
+    return prog_;
+  }
+
+  // ---------------------------------------------------------------- values
+  uint64_t scalar_val(const TermP& t) {
+    switch (t->stype) {
+      case S_NULL: return tag_val(V_NULL, 0);
+      case S_FALSE: return tag_val(V_BOOL, 0);
+      case S_TRUE: return tag_val(V_BOOL, 1);
+      case S_NUM: return tag_val(V_NUM, st_.number(t->s.data(), t->s.size()));
+      case S_STR: return tag_val(V_STR, st_.intern(t->s));
+    }
+    throw Unsupported("bad scalar");
+  }
+  bool is_const(const TermP& t) {
+    if (t->k == T_SCALAR) return true;
+    if (t->k == T_ARRAY) { for (auto& x : t->items) if (!is_const(x)) return false; return true; }
+    if (t->k == T_OBJECT) {
+      for (size_t i = 0; i < t->items.size(); i += 2) {
+        if (t->items[i]->k != T_SCALAR || t->items[i]->stype != S_STR) return false;
+        if (!is_const(t->items[i + 1])) return false;
+      }
+      return true;
+    }
+    return false;
+  }
+  // fill node `idx` from constant term t
+  void fill_const(uint32_t idx, const TermP& t, uint32_t key) {
+    Node n{};
+    n.key = key;
+    if (t->k == T_SCALAR) {
+      switch (t->stype) {
+        case S_NULL: n.type = NT_NULL; break;
+        case S_FALSE: n.type = NT_FALSE; break;
+        case S_TRUE: n.type = NT_TRUE; break;
+        case S_NUM: n.type = NT_NUM; n.val = st_.number(t->s.data(), t->s.size()); break;
+        case S_STR: n.type = NT_STR; n.val = st_.intern(t->s); break;
+      }
+      st_.nodes()[idx] = n;
+      return;
+    }
+    bool obj = t->k == T_OBJECT;
+    uint32_t cnt = obj ? (uint32_t)t->items.size() / 2 : (uint32_t)t->items.size();
+    n.type = obj ? NT_OBJ : NT_ARR;
+    n.n = (uint16_t)cnt;
+    n.first = st_.reserve(cnt);
+    st_.nodes()[idx] = n;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      if (obj) fill_const(n.first + i, t->items[2 * i + 1], st_.intern(t->items[2 * i]->s));
+      else fill_const(n.first + i, t->items[i], i);
+    }
+  }
+  uint64_t const_value(const TermP& t) {
+    if (t->k == T_SCALAR) return scalar_val(t);
+    if (t->k == T_OBJECT && t->items.empty()) return tag_val(V_NODE, 0);
+    uint32_t idx = st_.reserve(1);
+    fill_const(idx, t, 0);
+    return tag_val(V_NODE, idx);
+  }
+
+  // ---------------------------------------------------------------- scope
+  bool is_global(const Env* env, const std::string& v) {
+    if (v == "input" || v == "data") return true;
+    if (env->mod) {
+      if (!mods_.rules(env->mod->pkg, v).empty()) return true;
+      for (auto& im : env->mod->imports) if (im.second == v) return true;
+    }
+    return false;
+  }
+  bool unbound(const Env* env, const TermP& t) {
+    return t->k == T_VAR && env->lookup(t->s) < 0 && !is_global(env, t->s);
+  }
+  bool ground(const Env* env, const TermP& t) {
+    std::vector<std::string> vs;
+    term_vars(t, vs);
+    for (auto& v : vs) if (env->lookup(v) < 0 && !is_global(env, v)) return false;
+    return true;
+  }
+
+  const std::vector<ExprP>& cbody(const std::shared_ptr<Rule>& r, const std::vector<std::string>& safe) {
+    std::string key;
+    for (auto& s : safe) key += s + ",";
+    auto ck = std::make_pair((const Rule*)r.get(), key);
+    auto it = cbody_cache_.find(ck);
+    if (it != cbody_cache_.end()) return it->second;
+    Env tmp;
+    tmp.mod = r->mod;
+    std::vector<std::string> sf = safe;
+    for (auto& a : r->args) term_vars(a, sf);
+    auto b = compile_body(r->body, sf, [&](const std::string& v) { return is_global(&tmp, v); });
+    return cbody_cache_[ck] = b;
+  }
+
+  // ---------------------------------------------------------------- bodies
+  void body_k(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    if (i == body.size()) { succ(fail); return; }
+    expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
+  }
+
+  void expr(const ExprP& e, Env* env, int fail, const KE& k) {
+    if (!e->withs.empty()) throw Unsupported("with modifier in template");
+    if (e->kind == Expr::SOME) { k(fail); return; }
+    if (e->negated) {
+      int save = reg_top_;
+      int flag = loadk(tag_val(V_BOOL, 0));
+      int Ld = label();
+      Env inner;
+      inner.parent = env;
+      inner.mod = env->mod;
+      int t = loadk(tag_val(V_BOOL, 1));
+      expr_pos(e, &inner, Ld, [&](int f) { emit(OP_MOV, (uint16_t)flag, (uint16_t)t); emit_jmp(OP_JMP, 0, f); });
+      place(Ld);
+      emit_jmp(OP_JTRUE, flag, fail);
+      k(fail);
+      reg_top_ = save;
+      return;
+    }
+    expr_pos(e, env, fail, k);
+  }
+
+  void expr_pos(const ExprP& e, Env* env, int fail, const KE& k) {
+    if (e->kind == Expr::TERM) {
+      const TermP& t = e->terms[0];
+      if (t->k == T_CALL) {
+        call(t, env, fail, true, [&](int r, int f) { emit_jmp(OP_JFALSE, r, f); k(f); });
+      } else {
+        term(t, env, fail, [&](int r, int f) { emit_jmp(OP_JFALSE, r, f); k(f); });
+      }
+      return;
+    }
+    unify(e->terms[0], e->terms[1], env, fail, k);
+  }
+
+  // ---------------------------------------------------------------- unify
+  void bind(Env* env, const std::string& v, int r) { env->vars[v] = r; }
+  void unbind(Env* env, const std::string& v) { env->vars.erase(v); }
+
+  bool pattern_has_unbound(const Env* env, const TermP& t) {
+    std::vector<std::string> vs;
+    term_vars(t, vs);
+    for (auto& v : vs) if (env->lookup(v) < 0 && !is_global(env, v)) return true;
+    return false;
+  }
+
+  void unify(const TermP& a, const TermP& b, Env* env, int fail, const KE& k) {
+    if (unbound(env, a)) {
+      term(b, env, fail, [&](int r, int f) {
+        if (env->lookup(a->s) >= 0) {  // bound by a generator inside b
+          int t = alloc();
+          emit(OP_CMP, (uint16_t)t, (uint16_t)env->lookup(a->s), (uint16_t)r, 0, CMP_EQ);
+          emit_jmp(OP_JFALSE, t, f);
+          k(f);
+          return;
+        }
+        bind(env, a->s, r);
+        k(f);
+        unbind(env, a->s);
+      });
+      return;
+    }
+    if (unbound(env, b)) { unify(b, a, env, fail, k); return; }
+    if ((a->k == T_ARRAY || a->k == T_OBJECT) && pattern_has_unbound(env, a)) {
+      term(b, env, fail, [&](int r, int f) { unify_value(a, r, env, f, k); });
+      return;
+    }
+    if ((b->k == T_ARRAY || b->k == T_OBJECT) && pattern_has_unbound(env, b)) {
+      term(a, env, fail, [&](int r, int f) { unify_value(b, r, env, f, k); });
+      return;
+    }
+    term(a, env, fail, [&](int ra, int f) {
+      term(b, env, f, [&](int rb, int f2) {
+        int t = alloc();
+        emit(OP_CMP, (uint16_t)t, (uint16_t)ra, (uint16_t)rb, 0, CMP_EQ);
+        emit_jmp(OP_JFALSE, t, f2);
+        k(f2);
+      });
+    });
+  }
+
+  // unify a pattern term with the value in register r
+  void unify_value(const TermP& p, int r, Env* env, int fail, const KE& k) {
+    if (unbound(env, p)) {
+      bind(env, p->s, r);
+      k(fail);
+      unbind(env, p->s);
+      return;
+    }
+    if (p->k == T_ARRAY && pattern_has_unbound(env, p)) {
+      int t = alloc();
+      emit(OP_LEN_EQ, (uint16_t)t, (uint16_t)r, 0, 0, (uint32_t)p->items.size() | (LK_ARR << 24));
+      emit_jmp(OP_JFALSE, t, fail);
+      unify_items(p, r, 0, env, fail, k, false);
+      return;
+    }
+    if (p->k == T_OBJECT && pattern_has_unbound(env, p)) {
+      for (size_t i = 0; i < p->items.size(); i += 2)
+        if (p->items[i]->k != T_SCALAR) throw Unsupported("object pattern with non-constant key");
+      int t = alloc();
+      emit(OP_LEN_EQ, (uint16_t)t, (uint16_t)r, 0, 0, (uint32_t)(p->items.size() / 2) | (LK_OBJ << 24));
+      emit_jmp(OP_JFALSE, t, fail);
+      unify_items(p, r, 0, env, fail, k, true);
+      return;
+    }
+    term(p, env, fail, [&](int rp, int f) {
+      int t = alloc();
+      emit(OP_CMP, (uint16_t)t, (uint16_t)rp, (uint16_t)r, 0, CMP_EQ);
+      emit_jmp(OP_JFALSE, t, f);
+      k(f);
+    });
+  }
+  void unify_items(const TermP& p, int r, size_t i, Env* env, int fail, const KE& k, bool obj) {
+    size_t n = obj ? p->items.size() / 2 : p->items.size();
+    if (i == n) { k(fail); return; }
+    int v = alloc();
+    uint64_t key = obj ? scalar_val(p->items[2 * i]) : tag_val(V_INT, i);
+    emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(key));
+    emit_jmp(OP_JUNDEF, v, fail);
+    const TermP& sub = obj ? p->items[2 * i + 1] : p->items[i];
+    unify_value(sub, v, env, fail, [&, i](int f) { unify_items(p, r, i + 1, env, f, k, obj); });
+  }
+
+  // ---------------------------------------------------------------- terms
+  void term(const TermP& t, Env* env, int fail, const K& k) {
+    switch (t->k) {
+      case T_SCALAR: { int r = loadk(scalar_val(t)); k(r, fail); return; }
+      case T_VAR: {
+        int r = env->lookup(t->s);
+        if (r >= 0) { k(r, fail); return; }
+        auto tmp = std::make_shared<Term>();
+        tmp->k = T_REF;
+        tmp->head = t;
+        ref(tmp, env, fail, k);
+        return;
+      }
+      case T_REF: ref(t, env, fail, k); return;
+      case T_CALL: call(t, env, fail, false, k); return;
+      case T_ARRAY: case T_OBJECT:
+        if (is_const(t)) { int r = loadk(const_value(t)); k(r, fail); return; }
+        // fallthrough
+      case T_SET: build_list(t, env, fail, k); return;
+      case T_ARRCOMPR: case T_SETCOMPR: case T_OBJCOMPR: compr(t, env, fail, k); return;
+    }
+  }
+
+  void build_list(const TermP& t, Env* env, int fail, const K& k) {
+    uint32_t kind = t->k == T_SET ? LK_SET : t->k == T_ARRAY ? LK_ARR : LK_OBJ;
+    items_k(t->items, 0, {}, env, fail, [&, kind](const std::vector<int>& regs, int f) {
+      int l = alloc();
+      emit(OP_LIST_NEW, (uint16_t)l, 0, 0, 0, kind);
+      if (kind == LK_OBJ) {
+        for (size_t i = 0; i < regs.size(); i += 2) emit(OP_OBJ_PUT, (uint16_t)l, (uint16_t)regs[i], (uint16_t)regs[i + 1], 0, escape_range(l));
+      } else {
+        for (int r : regs) emit(OP_LIST_ADD, (uint16_t)l, (uint16_t)r, 0, 0, escape_range(l));
+      }
+      k(l, f);
+    });
+  }
+
+  using KV = std::function<void(const std::vector<int>&, int)>;
+  void items_k(const std::vector<TermP>& items, size_t i, std::vector<int> acc, Env* env, int fail, const KV& k) {
+    if (i == items.size()) { k(acc, fail); return; }
+    term(items[i], env, fail, [&, i, acc](int r, int f) {
+      auto a2 = acc;
+      a2.push_back(r);
+      items_k(items, i + 1, a2, env, f, k);
+    });
+  }
+
+  void compr(const TermP& t, Env* env, int fail, const K& k) {
+    int save = reg_top_;
+    uint32_t kind = t->k == T_SETCOMPR ? LK_SET : t->k == T_ARRCOMPR ? LK_ARR : LK_OBJ;
+    int out = alloc();
+    emit(OP_LIST_NEW, (uint16_t)out, 0, 0, 0, kind);
+    int Ld = label();
+    Env inner;
+    inner.parent = env;
+    inner.mod = env->mod;
+    body_k(t->body, 0, &inner, Ld, [&](int f) {
+      if (kind == LK_OBJ) {
+        term(t->key, &inner, f, [&](int kr, int f2) {
+          term(t->value, &inner, f2, [&](int vr, int f3) {
+            emit(OP_OBJ_PUT, (uint16_t)out, (uint16_t)kr, (uint16_t)vr, 0, escape_range(out));
+            emit_jmp(OP_JMP, 0, f3);
+          });
+        });
+      } else {
+        term(t->key, &inner, f, [&](int vr, int f2) {
+          emit(OP_LIST_ADD, (uint16_t)out, (uint16_t)vr, 0, 0, escape_range(out));
+          emit_jmp(OP_JMP, 0, f2);
+        });
+      }
+    });
+    place(Ld);
+    k(out, fail);
+    reg_top_ = save;
+  }
+
+  // ---------------------------------------------------------------- refs
+  void ref(const TermP& t, Env* env, int fail, const K& k) {
+    const TermP& head = t->head;
+    const auto& path = t->items;
+    if (head->k == T_CALL) {
+      call(head, env, fail, false, [&](int r, int f) { walk(r, path, 0, env, f, k); });
+      return;
+    }
+    if (head->k != T_VAR) throw Unsupported("ref head");
+    int r = env->lookup(head->s);
+    if (r >= 0) { walk(r, path, 0, env, fail, k); return; }
+    if (head->s == "input") {
+      if (path.empty()) throw Unsupported("whole input document");
+      const TermP& p0 = path[0];
+      if (p0->k != T_SCALAR || p0->stype != S_STR) throw Unsupported("dynamic input key");
+      std::vector<TermP> rest(path.begin() + 1, path.end());
+      int rr = alloc();
+      if (p0->s == "review") emit(OP_LOADREV, (uint16_t)rr);
+      else if (p0->s == "parameters") emit(OP_LOADPARAM, (uint16_t)rr);
+      else { emit_jmp(OP_JMP, 0, fail); return; }  // input.<other> is undefined
+      walk(rr, rest, 0, env, fail, k);
+      return;
+    }
+    if (head->s == "data") { data_ref(path, env, fail, k); return; }
+    if (env->mod) {
+      auto rules = mods_.rules(env->mod->pkg, head->s);
+      if (!rules.empty()) { rule_ref(rules, path, 0, env, fail, k); return; }
+      for (auto& im : env->mod->imports) {
+        if (im.second == head->s) {
+          if (im.first.empty() || im.first[0] != "data") throw Unsupported("import of non-data document");
+          std::vector<TermP> p2;
+          for (size_t i = 1; i < im.first.size(); ++i) p2.push_back(mk_scalar(S_STR, im.first[i]));
+          p2.insert(p2.end(), path.begin(), path.end());
+          data_ref(p2, env, fail, k);
+          return;
+        }
+      }
+    }
+    throw Unsupported("unsafe variable " + head->s);
+  }
+
+  void data_ref(const std::vector<TermP>& path, Env* env, int fail, const K& k) {
+    std::vector<std::string> pkg;
+    for (size_t i = 0; i < path.size(); ++i) {
+      if (path[i]->k != T_SCALAR || path[i]->stype != S_STR) break;
+      if (mods_.has_pkg(pkg)) {
+        auto rules = mods_.rules(pkg, path[i]->s);
+        if (!rules.empty()) { rule_ref(rules, path, i + 1, env, fail, k); return; }
+      }
+      pkg.push_back(path[i]->s);
+    }
+    if (!path.empty() && path[0]->k == T_SCALAR && path[0]->s == "inventory") throw Unsupported("data.inventory (cross-resource join)");
+    throw Unsupported("reference to base data");
+  }
+
+  void walk(int r, const std::vector<TermP>& path, size_t i, Env* env, int fail, const K& k) {
+    if (i == path.size()) { k(r, fail); return; }
+    const TermP& sel = path[i];
+    if (unbound(env, sel)) {
+      int it = alloc(2);
+      int kr = alloc(), vr = alloc();
+      open_loop(it, r);
+      int Ln = label();
+      place(Ln);
+      emit(OP_ITER_NEXT, (uint16_t)it, (uint16_t)kr, (uint16_t)vr, (uint32_t)fail, (uint32_t)depth());
+      bind(env, sel->s, kr);
+      walk(vr, path, i + 1, env, Ln, k);
+      unbind(env, sel->s);
+      emit_jmp(OP_JMP, 0, Ln);
+      close_loop();
+      return;
+    }
+    if (sel->k == T_SCALAR) {
+      int v = alloc();
+      emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(scalar_val(sel)));
+      emit_jmp(OP_JUNDEF, v, fail);
+      walk(v, path, i + 1, env, fail, k);
+      return;
+    }
+    if ((sel->k == T_ARRAY || sel->k == T_OBJECT) && pattern_has_unbound(env, sel)) {
+      // pattern selector: iterate members and unify
+      int it = alloc(2);
+      int kr = alloc(), vr = alloc();
+      open_loop(it, r);
+      int Ln = label();
+      place(Ln);
+      emit(OP_ITER_NEXT, (uint16_t)it, (uint16_t)kr, (uint16_t)vr, (uint32_t)fail, (uint32_t)depth());
+      unify_value(sel, kr, env, Ln, [&](int f) { walk(vr, path, i + 1, env, f, k); });
+      emit_jmp(OP_JMP, 0, Ln);
+      close_loop();
+      return;
+    }
+    term(sel, env, fail, [&, r, i](int kr, int f) {
+      int v = alloc();
+      emit(OP_GET, (uint16_t)v, (uint16_t)r, (uint16_t)kr);
+      emit_jmp(OP_JUNDEF, v, f);
+      walk(v, path, i + 1, env, f, k);
+    });
+  }
+
+  // ---------------------------------------------------------------- rules
+  void rule_ref(const std::vector<std::shared_ptr<Rule>>& rules, const std::vector<TermP>& path, size_t i, Env* env,
+                int fail, const K& k) {
+    auto kind = rules[0]->kind;
+    if (kind == Rule::FUNC) throw Unsupported("function referenced without call");
+    if (kind == Rule::COMPLETE) {
+      complete_value(rules, fail, [&](int r, int f) { walk(r, path, i, env, f, k); });
+      return;
+    }
+    if (kind == Rule::POBJ) throw Unsupported("partial object rule");
+    // partial set
+    if (i == path.size()) { full_set(rules, fail, k); return; }
+    const TermP& key = path[i];
+    for (auto& r : rules) {
+      if (r->is_else) throw Unsupported("else");
+      int save = reg_top_;
+      int Lr = label();
+      Env renv;
+      renv.mod = r->mod;
+      // prebind rule-head variables from ground parts of the caller's key
+      std::vector<std::string> pre;
+      std::vector<std::pair<std::string, TermP>> pre_terms;
+      if (r->key->k == T_VAR && ground(env, key)) pre_terms.push_back({r->key->s, key});
+      if (r->key->k == T_OBJECT && key->k == T_OBJECT) {
+        for (size_t a = 0; a < key->items.size(); a += 2) {
+          if (key->items[a]->k != T_SCALAR) continue;
+          for (size_t b = 0; b < r->key->items.size(); b += 2) {
+            const TermP& hk = r->key->items[b];
+            if (hk->k == T_SCALAR && hk->stype == key->items[a]->stype && hk->s == key->items[a]->s &&
+                r->key->items[b + 1]->k == T_VAR && ground(env, key->items[a + 1]))
+              pre_terms.push_back({r->key->items[b + 1]->s, key->items[a + 1]});
+          }
+        }
+      }
+      prebind(pre_terms, 0, env, &renv, Lr, [&, r](int f) {
+        std::vector<std::string> safe;
+        for (auto& pt : pre_terms) safe.push_back(pt.first);
+        const auto& body = cbody(r, safe);
+        body_k(body, 0, &renv, f, [&](int f2) {
+          term(r->key, &renv, f2, [&](int kv, int f3) {
+            unify_value(key, kv, env, f3, [&](int f4) { walk(kv, path, i + 1, env, f4, k); });
+          });
+        });
+      });
+      place(Lr);
+      reg_top_ = save;
+    }
+    emit_jmp(OP_JMP, 0, fail);
+  }
+
+  void prebind(const std::vector<std::pair<std::string, TermP>>& pts, size_t i, Env* caller, Env* renv, int fail,
+               const KE& k) {
+    if (i == pts.size()) { k(fail); return; }
+    term(pts[i].second, caller, fail, [&, i](int r, int f) {
+      bind(renv, pts[i].first, r);
+      prebind(pts, i + 1, caller, renv, f, k);
+    });
+  }
+
+  void full_set(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    int save = reg_top_;
+    int out = alloc();
+    emit(OP_LIST_NEW, (uint16_t)out, 0, 0, 0, LK_SET);
+    for (auto& r : rules) {
+      int Lr = label();
+      Env renv;
+      renv.mod = r->mod;
+      body_k(cbody(r, {}), 0, &renv, Lr, [&](int f) {
+        term(r->key, &renv, f, [&](int kv, int f2) { emit(OP_LIST_ADD, (uint16_t)out, (uint16_t)kv, 0, 0, escape_range(out)); emit_jmp(OP_JMP, 0, f2); });
+      });
+      place(Lr);
+    }
+    k(out, fail);
+    reg_top_ = save;
+  }
+
+  void complete_value(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    int save = reg_top_;
+    int out = loadk(tag_val(V_UNDEF, 0));
+    TermP def;
+    for (auto& r : rules) {
+      if (r->is_else) throw Unsupported("else");
+      if (r->is_default) { def = r->value; continue; }
+      int Lr = label();
+      Env renv;
+      renv.mod = r->mod;
+      body_k(cbody(r, {}), 0, &renv, Lr, [&](int f) {
+        term(r->value, &renv, f, [&](int v, int f2) { emit(OP_YIELD, (uint16_t)out, (uint16_t)v, 0, 0, escape_range(out)); emit_jmp(OP_JMP, 0, f2); });
+      });
+      place(Lr);
+    }
+    if (def) {
+      if (!is_const(def)) throw Unsupported("non-constant default");
+      int Lh = label();
+      int dv = loadk(const_value(def));
+      int Lskip = label();
+      emit_jmp(OP_JUNDEF, out, Lh);
+      emit_jmp(OP_JMP, 0, Lskip);
+      place(Lh);
+      emit(OP_MOV, (uint16_t)out, (uint16_t)dv);
+      place(Lskip);
+    }
+    emit_jmp(OP_JUNDEF, out, fail);
+    k(out, fail);
+    reg_top_ = save;
+  }
+
+  // ---------------------------------------------------------------- calls
+  std::vector<std::shared_ptr<Rule>> resolve_func(const std::vector<std::string>& op, const Env* env) {
+    if (op.size() == 1 && env->mod) {
+      auto r = mods_.rules(env->mod->pkg, op[0]);
+      if (!r.empty()) return r;
+      for (auto& im : env->mod->imports)
+        if (im.second == op[0] && !im.first.empty() && im.first[0] == "data") {
+          std::vector<std::string> pkg(im.first.begin() + 1, im.first.end() - 1);
+          return mods_.rules(pkg, im.first.back());
+        }
+      return {};
+    }
+    std::vector<std::string> full;
+    if (op[0] == "data") full.assign(op.begin() + 1, op.end());
+    else if (env->mod) {
+      for (auto& im : env->mod->imports)
+        if (im.second == op[0] && !im.first.empty() && im.first[0] == "data") {
+          full.assign(im.first.begin() + 1, im.first.end());
+          full.insert(full.end(), op.begin() + 1, op.end());
+        }
+    }
+    if (full.empty()) return {};
+    std::vector<std::string> pkg(full.begin(), full.end() - 1);
+    return mods_.rules(pkg, full.back());
+  }
+
+  void call(const TermP& t, Env* env, int fail, bool stmt, const K& k) {
+    std::string name;
+    for (size_t i = 0; i < t->op.size(); ++i) name += (i ? "." : "") + t->op[i];
+    auto rules = resolve_func(t->op, env);
+    if (!rules.empty()) {
+      if (rules[0]->kind != Rule::FUNC) throw Unsupported("call of non-function rule " + name);
+      size_t nargs = rules[0]->args.size();
+      bool has_out = t->items.size() == nargs + 1;
+      if (!has_out && t->items.size() != nargs) throw Unsupported("arity mismatch " + name);
+      std::vector<TermP> args(t->items.begin(), t->items.begin() + nargs);
+      items_k(args, 0, {}, env, fail, [&, has_out](const std::vector<int>& regs, int f) {
+        int out = loadk(tag_val(V_UNDEF, 0));
+        if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
+        for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
+        --inline_depth_;
+        emit_jmp(OP_JUNDEF, out, f);
+        if (has_out) {
+          unify_value(t->items.back(), out, env, f, [&](int f2) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f2); });
+        } else {
+          k(out, f);
+        }
+      });
+      return;
+    }
+    std::string op = name;
+    auto ci = kCmp.find(op);
+    auto ai = kArith.find(op);
+    if (ci != kCmp.end() || ai != kArith.end()) {
+      bool has_out = t->items.size() == 3;
+      if (t->items.size() != 2 && !has_out) throw Unsupported("operator arity");
+      std::vector<TermP> args(t->items.begin(), t->items.begin() + 2);
+      items_k(args, 0, {}, env, fail, [&, has_out](const std::vector<int>& regs, int f) {
+        int d = alloc();
+        if (ci != kCmp.end()) emit(OP_CMP, (uint16_t)d, (uint16_t)regs[0], (uint16_t)regs[1], 0, ci->second);
+        else emit(OP_ARITH, (uint16_t)d, (uint16_t)regs[0], (uint16_t)regs[1], 0, ai->second);
+        finish_call(t, d, has_out, env, f, k);
+      });
+      return;
+    }
+    if (op == "sprintf") {
+      bool has_out = t->items.size() == 3;
+      const TermP& fmt = t->items[0];
+      if (fmt->k != T_SCALAR || fmt->stype != S_STR) throw Unsupported("sprintf with non-constant format");
+      uint32_t fidx = parse_format(fmt->s);
+      term(t->items[1], env, fail, [&, has_out, fidx](int ar, int f) {
+        int d = alloc();
+        emit(OP_SPRINTF, (uint16_t)d, (uint16_t)ar, 0, fidx);
+        finish_call(t, d, has_out, env, f, k);
+      });
+      return;
+    }
+    auto bi = kBuiltins.find(op);
+    if (bi == kBuiltins.end()) throw Unsupported("builtin " + op);
+    int arity = kArity.at(bi->second);
+    bool has_out = (int)t->items.size() == arity + 1;
+    if ((int)t->items.size() != arity && !has_out) throw Unsupported("builtin arity " + op);
+    if (bi->second == BI_RE_MATCH) {
+      prog_.uses_regex = true;
+      if (t->items[0]->k == T_SCALAR && t->items[0]->stype == S_STR) prog_.regex_literals.push_back(st_.intern(t->items[0]->s));
+    }
+    std::vector<TermP> args(t->items.begin(), t->items.begin() + arity);
+    uint32_t id = bi->second;
+    items_k(args, 0, {}, env, fail, [&, has_out, id, arity](const std::vector<int>& regs, int f) {
+      int base = alloc(arity);
+      for (int i = 0; i < arity; ++i) emit(OP_MOV, (uint16_t)(base + i), (uint16_t)regs[i]);
+      int d = alloc();
+      emit(OP_CALL, (uint16_t)d, (uint16_t)base, (uint16_t)arity, 0, id);
+      finish_call(t, d, has_out, env, f, k);
+    });
+  }
+
+  void finish_call(const TermP& t, int d, bool has_out, Env* env, int f, const K& k) {
+    if (has_out) {
+      unify_value(t->items.back(), d, env, f, [&](int f2) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f2); });
+    } else {
+      k(d, f);
+    }
+  }
+
+  void inline_func(const std::shared_ptr<Rule>& r, const std::vector<int>& args, int out, bool stmt) {
+    if (r->is_else) throw Unsupported("else in function");
+    int save = reg_top_;
+    int Lend = label();
+    Env fenv;
+    fenv.mod = r->mod;
+    args_k(r, args, 0, &fenv, Lend, [&](int f) {
+      body_k(cbody(r, {}), 0, &fenv, f, [&](int f2) {
+        term(r->value, &fenv, f2, [&](int v, int f3) {
+          if (stmt) emit_jmp(OP_JFALSE, v, f3);
+          emit(OP_YIELD, (uint16_t)out, (uint16_t)v, 0, 0, escape_range(out));
+          emit_jmp(OP_JMP, 0, f3);
+        });
+      });
+    });
+    place(Lend);
+    reg_top_ = save;
+  }
+
+  void args_k(const std::shared_ptr<Rule>& r, const std::vector<int>& args, size_t i, Env* fenv, int fail, const KE& k) {
+    if (i == args.size()) { k(fail); return; }
+    const TermP& p = r->args[i];
+    if (p->k == T_VAR && fenv->lookup(p->s) < 0) {
+      bind(fenv, p->s, args[i]);
+      args_k(r, args, i + 1, fenv, fail, k);
+      return;
+    }
+    unify_value(p, args[i], fenv, fail, [&, i](int f) { args_k(r, args, i + 1, fenv, f, k); });
+  }
+
+  // ---------------------------------------------------------------- sprintf
+  // format words: [nseg, (kind, a)...]; kind 0 literal (a = string id), 1 = %v/%s/%d arg (a = arg idx | verb<<16),
+  // 2 = extra-args marker (Go %!(EXTRA ...)) handled at run time, 3 = missing arg (a = verb)
+  uint32_t parse_format(const std::string& f) {
+    std::vector<uint32_t> w;
+    std::string lit;
+    uint32_t argi = 0;
+    auto flush = [&]() {
+      if (!lit.empty()) { w.push_back(0); w.push_back(st_.intern(lit)); lit.clear(); }
+    };
+    for (size_t i = 0; i < f.size(); ++i) {
+      if (f[i] != '%') { lit.push_back(f[i]); continue; }
+      if (i + 1 >= f.size()) throw Unsupported("sprintf: trailing %");
+      char v = f[++i];
+      if (v == '%') { lit.push_back('%'); continue; }
+      if (v != 'v' && v != 's' && v != 'd') throw Unsupported(std::string("sprintf verb %") + v);
+      flush();
+      w.push_back(1);
+      w.push_back(argi++ | ((uint32_t)v << 16));
+    }
+    flush();
+    uint32_t off = (uint32_t)bank_.fmt.size();
+    bank_.fmt.push_back((uint32_t)w.size() / 2);
+    bank_.fmt.push_back(argi);  // expected arg count
+    bank_.fmt.insert(bank_.fmt.end(), w.begin(), w.end());
+    return off;
+  }
+
+  // ---------------------------------------------------------------- emit
+  void emit_violation(const std::shared_ptr<Rule>& r, Env* env, int idx, int f) {
+    const TermP& key = r->key;
+    if (key->k == T_OBJECT) {
+      TermP msg, det;
+      bool ok = true;
+      for (size_t i = 0; i < key->items.size(); i += 2) {
+        if (key->items[i]->k != T_SCALAR) { ok = false; break; }
+        if (key->items[i]->stype == S_STR && key->items[i]->s == "msg") msg = key->items[i + 1];
+        if (key->items[i]->stype == S_STR && key->items[i]->s == "details") det = key->items[i + 1];
+      }
+      if (ok) {
+        if (!msg) { emit_jmp(OP_JMP, 0, f); return; }
+        term(msg, env, f, [&](int mr, int f2) {
+          if (det) {
+            term(det, env, f2, [&](int dr, int f3) {
+              emit(OP_EMIT, (uint16_t)mr, (uint16_t)dr, 0, 0, (uint32_t)idx);
+              emit_jmp(OP_JMP, 0, f3);
+            });
+          } else {
+            emit(OP_EMIT, (uint16_t)mr, NOREG, 0, 0, (uint32_t)idx);
+            emit_jmp(OP_JMP, 0, f2);
+          }
+        });
+        return;
+      }
+    }
+    term(key, env, f, [&](int kv, int f2) {
+      int m = alloc(), d = alloc();
+      emit(OP_GETK, (uint16_t)m, (uint16_t)kv, 0, kconst(tag_val(V_STR, st_.s_msg)));
+      emit_jmp(OP_JUNDEF, m, f2);
+      emit(OP_GETK, (uint16_t)d, (uint16_t)kv, 0, kconst(tag_val(V_STR, st_.s_details)));
+      emit(OP_EMIT, (uint16_t)m, (uint16_t)d, 0, 0, (uint32_t)idx);
+      emit_jmp(OP_JMP, 0, f2);
+    });
+  }
+};
+
+}  // namespace
+
+Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank) {
+  // compile into a scratch bank first so a failed template leaves no code behind
+  size_t code0 = bank.code.size(), k0 = bank.consts.size(), f0 = bank.fmt.size();
+  try {
+    Comp c(st, mods, bank);
+    return c.run(pkg);
+  } catch (...) {
+    bank.code.resize(code0);
+    bank.consts.resize(k0);
+    bank.fmt.resize(f0);
+    throw;
+  }
+}
+
+}  // namespace gk

@@ -1,0 +1,62 @@
+// ConstraintTemplate Rego -> predicate bytecode (host).
+//
+// Each template's `violation` rules compile into one loop-nest program that
+// the GPU VM runs per (review, constraint) pair: generators (`x[_]`, unbound
+// selector variables, partial-set rule references) become ITER loops,
+// functions / complete rules / comprehensions / `not` are inlined as
+// solution-collecting sub-blocks with OPA's semantics (functions yield once,
+// conflicting values are an error, `false` from a statement call is
+// undefined; eval.go:1405-1497), and every solution of a `violation` body
+// EMITs (msg, details).  Anything outside the supported subset throws
+// Unsupported and the template is served by the CPU OPA fallback.
+#pragma once
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "rego.h"
+#include "store.h"
+
+namespace gk {
+
+struct Unsupported : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+struct Program {
+  uint32_t code_off = 0;   // offset into the global code array
+  uint32_t code_len = 0;
+  uint32_t nregs = 0;
+  bool uses_regex = false;
+  std::vector<uint32_t> regex_literals;  // string ids of literal patterns
+  std::vector<std::string> rules;
+};
+
+// All modules known to the driver, indexed by package path.
+struct ModuleSet {
+  std::map<std::vector<std::string>, std::vector<std::shared_ptr<rego::Module>>> by_pkg;
+  void clear() { by_pkg.clear(); }
+  void add(const std::shared_ptr<rego::Module>& m) { by_pkg[m->pkg].push_back(m); }
+  // rules named `name` in package `pkg` (all modules of the package)
+  std::vector<std::shared_ptr<rego::Rule>> rules(const std::vector<std::string>& pkg, const std::string& name) const;
+  bool has_pkg(const std::vector<std::string>& pkg) const { return by_pkg.count(pkg) > 0; }
+};
+
+// Global code / constant tables shared by all programs (uploaded to HBM).
+struct CodeBank {
+  std::vector<Ins> code;
+  std::vector<uint64_t> consts;    // K table (tagged values)
+  std::vector<uint32_t> fmt;       // sprintf format words
+  void clear() { code.clear(); consts.clear(); fmt.clear(); }
+};
+
+// Compile the template entry package `pkg` (must define `violation`).
+Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank);
+
+// Tagged-value helpers shared with the engine.
+inline uint64_t tag_val(uint32_t tag, uint64_t payload) { return ((uint64_t)tag << 60) | (payload & 0x0fffffffffffffffull); }
+
+}  // namespace gk

@@ -1,0 +1,1388 @@
+// gkgpu engine: drivers.Driver state, review flattening, constraint match
+// compilation, device residency, kernel launch and result decoding.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gkgpu.h"
+#include "common.h"
+#include "compiler.h"
+#include "json.h"
+#include "rego.h"
+#include "regex.h"
+#include "store.h"
+
+namespace gk {
+struct DevArgs;
+}
+extern "C" int gk_launch_audit(const void* args, hipStream_t stream);
+extern "C" size_t gk_devargs_size();
+
+namespace gk {
+
+static const char* TARGET = "admission.k8s.gatekeeper.sh";
+static const char* CGROUP = "constraints.gatekeeper.sh";
+static const char* EMPTY_NS_JSON = "{\"metadata\":{\"creationTimestamp\":null},\"spec\":{},\"status\":{}}";
+
+using Clock = std::chrono::steady_clock;
+static double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
+// mirror of kernels.hip DevArgs (kept in sync; size checked at runtime)
+struct HostDevArgs {
+  const Node* nodes;
+  const StrEnt* strs;
+  const uint8_t* pool;
+  const uint8_t* sflags;
+  const NumEnt* nums;
+  const Ins* code;
+  const uint64_t* K;
+  const uint32_t* fmt;
+  const MatchSpec* cons;
+  const uint32_t* mwords;
+  const uint32_t* prog_off;
+  const ReviewCol* revs;
+  const uint32_t* dfa_keys;
+  const uint32_t* dfa_meta;
+  const uint32_t* dfa_words;
+  uint32_t ndfa;
+  uint32_t ncode;
+  uint32_t ncons;
+  uint32_t nrev;
+  uint32_t ntiles;
+  Viol* out;
+  uint32_t out_cap;
+  uint32_t* counters;
+  char* bytes;
+  uint32_t bytes_cap;
+  uint32_t* rflags;
+  uint32_t* totals;
+  uint32_t* rreason;
+};
+
+// ------------------------------------------------------------------ device buffers
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  size_t used = 0;  // bytes uploaded (append-only arrays upload the tail)
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    size_t nc = std::max(n, cap * 2);
+    nc = std::max<size_t>(nc, 4096);
+    void* q = nullptr;
+    if (hipMalloc(&q, nc) != hipSuccess) return false;
+    if (p && used) hipMemcpy(q, p, used, hipMemcpyDeviceToDevice);
+    if (p) hipFree(p);
+    p = q;
+    cap = nc;
+    return true;
+  }
+  bool upload(const void* src, size_t n, bool append_only) {
+    if (!reserve(n)) return false;
+    size_t from = append_only ? std::min(used, n) : 0;
+    if (n > from && hipMemcpy((char*)p + from, (const char*)src + from, n - from, hipMemcpyHostToDevice) != hipSuccess)
+      return false;
+    used = n;
+    return true;
+  }
+  void free_() { if (p) hipFree(p); p = nullptr; cap = used = 0; }
+};
+
+// ------------------------------------------------------------------ engine state
+struct TemplateEnt {
+  std::string kind;
+  bool supported = false;
+  std::string reason;
+  int prog = -1;
+};
+
+struct ConstraintEnt {
+  std::string kind, name;
+  uint32_t root = NO_ID;   // node of the whole constraint (permanent region)
+  MatchSpec spec{};
+  std::string ea;          // enforcementAction as returned in results
+  bool ea_error = false;   // non-string enforcementAction: Query fails
+  bool kind_ok = true;
+};
+
+struct ResultRow {
+  uint32_t review, constraint, seq, rule;
+  std::string msg, details;
+};
+
+}  // namespace gk
+
+struct gk_results {
+  std::vector<gk::ResultRow> rows;
+  std::vector<uint32_t> status, reason;
+  std::vector<uint64_t> totals;
+  std::vector<std::string> ckind, cname, cea;
+  double ms[5] = {0, 0, 0, 0, 0};
+};
+
+struct gk_batch {
+  uint64_t gen = 0;
+  uint32_t nrev = 0;
+  uint32_t node_begin = 0, node_end = 0;
+  std::vector<gk::ReviewCol> cols;
+  gk::DBuf d_revs;
+  uint64_t dev_bytes = 0;
+};
+
+struct gk_engine {
+  std::mutex mu;
+  std::string err;
+  int device = 0;
+  bool dev_ok = false;
+  hipStream_t stream = nullptr;
+  gk::Store st;
+  // modules
+  std::map<std::string, std::string> modules;  // name -> source
+  gk::ModuleSet mods;
+  gk::CodeBank bank;
+  std::vector<gk::Program> progs;
+  std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
+  bool modules_dirty = true;
+  // data
+  std::map<std::pair<std::string, std::string>, gk::ConstraintEnt> constraints;
+  std::vector<gk::ConstraintEnt*> corder;
+  std::vector<uint32_t> mwords;
+  bool constraints_dirty = true;
+  std::map<std::string, std::string> inventory;  // external path -> json
+  std::map<std::string, uint32_t> ns_cache;       // namespace name -> node (permanent)
+  std::map<std::string, std::string> other_data;
+  uint32_t perm_nodes = 0;                        // nodes below this are permanent
+  uint64_t gen = 1;                               // bumps on any mutation
+  // regex
+  std::map<uint32_t, std::pair<uint32_t, uint32_t>> dfa_index;  // pattern sid -> (word offset, status)
+  std::vector<uint32_t> dfa_words;
+  std::vector<uint32_t> dfa_keys, dfa_meta;
+  // device mirrors
+  gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
+      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason;
+  size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
+};
+
+namespace gk {
+
+// ------------------------------------------------------------------ node helpers (host)
+static uint32_t nget(const Store& st, uint32_t node, uint32_t key) {
+  if (node == NO_ID) return NO_ID;
+  const Node& n = st.nodes()[node];
+  if (n.type != NT_OBJ) return NO_ID;
+  for (uint32_t i = 0; i < n.n; ++i) if (st.nodes()[n.first + i].key == key) return n.first + i;
+  return NO_ID;
+}
+static uint32_t nget(Store& st, uint32_t node, const char* key) {
+  uint32_t k = st.find(key, strlen(key));
+  return k == NO_ID ? NO_ID : nget(st, node, k);
+}
+static inline uint8_t ntype(const Store& st, uint32_t n) { return n == NO_ID ? NT_NONE : st.nodes()[n].type; }
+static bool nstr(const Store& st, uint32_t n, uint32_t* sid) {
+  if (n == NO_ID || st.nodes()[n].type != NT_STR) return false;
+  *sid = st.nodes()[n].val;
+  return true;
+}
+static bool is_empty_obj(const Store& st, uint32_t n) { return n != NO_ID && st.nodes()[n].type == NT_OBJ && st.nodes()[n].n == 0; }
+static bool truthy(const Store& st, uint32_t n) { return n != NO_ID && st.nodes()[n].type != NT_FALSE; }
+
+// get_default (target_template_source.go:110-125): missing / null -> default (NO_ID == {})
+static uint32_t gdef(Store& st, uint32_t obj, const char* key) {
+  uint32_t v = nget(st, obj, key);
+  if (v == NO_ID || st.nodes()[v].type == NT_NULL) return NO_ID;
+  return v;
+}
+
+// ------------------------------------------------------------------ path helpers
+static std::vector<std::string> split_path(const std::string& p) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < p.size()) {
+    while (i < p.size() && p[i] == '/') ++i;
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    if (j > i) {
+      std::string seg = p.substr(i, j - i);
+      // storage.ParsePathEscaped: url.PathUnescape each segment
+      std::string u;
+      for (size_t k = 0; k < seg.size(); ++k) {
+        if (seg[k] == '%' && k + 2 < seg.size() + 0 && isxdigit((unsigned char)seg[k + 1]) && isxdigit((unsigned char)seg[k + 2])) {
+          u.push_back((char)std::stoi(seg.substr(k + 1, 2), nullptr, 16));
+          k += 2;
+        } else u.push_back(seg[k]);
+      }
+      out.push_back(u);
+    }
+    i = j;
+  }
+  return out;
+}
+
+// `templates["t"]["K"]` / `hooks["t"].library` -> path segments
+static std::vector<std::string> pkg_path(const std::string& name) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < name.size()) {
+    if (name[i] == '.') { ++i; continue; }
+    if (name[i] == '[') {
+      size_t q = name.find('"', i);
+      size_t q2 = name.find('"', q + 1);
+      out.push_back(name.substr(q + 1, q2 - q - 1));
+      i = name.find(']', q2) + 1;
+      continue;
+    }
+    size_t j = i;
+    while (j < name.size() && name[j] != '.' && name[j] != '[') ++j;
+    out.push_back(name.substr(i, j - i));
+    i = j;
+  }
+  return out;
+}
+
+}  // namespace gk
+
+using namespace gk;
+
+static int fail(gk_engine* e, int code, const std::string& m) {
+  e->err = m;
+  return code;
+}
+
+// ------------------------------------------------------------------ modules
+static void rebuild_modules(gk_engine* e) {
+  if (!e->modules_dirty) return;
+  e->mods.clear();
+  e->bank.clear();
+  e->progs.clear();
+  e->templates.clear();
+  // drop the transient region before appending new permanent constant nodes
+  e->st.nodes().resize(e->perm_nodes);
+  std::vector<std::shared_ptr<rego::Module>> parsed;
+  for (auto& kv : e->modules) {
+    auto m = rego::parse_module(kv.second);
+    // the frameworks hooks + target library are served natively
+    if (!m->pkg.empty() && m->pkg[0] == "hooks") continue;
+    e->mods.add(m);
+    parsed.push_back(m);
+  }
+  for (auto& m : parsed) {
+    if (m->pkg.size() != 3 || m->pkg[0] != "templates" || m->pkg[1] != TARGET) continue;
+    const std::string& kind = m->pkg[2];
+    if (e->templates.count(kind)) continue;
+    TemplateEnt te;
+    te.kind = kind;
+    try {
+      Program p = compile_template(e->st, e->mods, m->pkg, e->bank);
+      if (p.nregs > 192) throw Unsupported("register file too large");
+      // structural validation of the bytecode before it can reach the device
+      for (uint32_t k = 0; k < p.code_len; ++k) {
+        const Ins& in = e->bank.code[p.code_off + k];
+        auto reg_ok = [&](uint16_t r) { return r < p.nregs || r == 0xffff; };
+        if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
+        if (!reg_ok(in.a) || !reg_ok(in.b) || !reg_ok(in.c)) throw std::runtime_error("internal: register out of range");
+        if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
+        if (in.op == OP_CALL && in.b + (uint32_t)in.c > p.nregs) throw std::runtime_error("internal: call args");
+        bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || in.op == OP_ITER_NEXT;
+        if (jmp && (in.x < p.code_off || in.x >= p.code_off + p.code_len)) throw std::runtime_error("internal: jump target");
+        if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x >= e->bank.consts.size()) throw std::runtime_error("internal: constant index");
+        if (in.op == OP_SPRINTF && in.x >= e->bank.fmt.size()) throw std::runtime_error("internal: format index");
+      }
+      te.prog = (int)e->progs.size();
+      te.supported = true;
+      e->progs.push_back(p);
+    } catch (const std::exception& ex) {
+      te.supported = false;
+      te.reason = ex.what();
+    }
+    e->templates[kind] = te;
+  }
+  e->perm_nodes = (uint32_t)e->st.nodes().size();
+  e->modules_dirty = false;
+  e->constraints_dirty = true;
+  e->gen++;
+}
+
+// ------------------------------------------------------------------ constraint match compile
+// Encodes a label selector (target_template_source.go:185-230) into match words.
+static void encode_selector(Store& st, uint32_t sel, std::vector<uint32_t>& w) {
+  size_t head = w.size();
+  w.push_back(0);  // flags: 1 never, 2 error
+  uint32_t flags = 0;
+  // matchLabels := get_default(selector, "matchLabels", {})
+  uint32_t ml = st.nodes().size() && sel != NO_ID && ntype(st, sel) == NT_OBJ ? gdef(st, sel, "matchLabels") : NO_ID;
+  std::vector<std::pair<uint32_t, uint32_t>> pairs;
+  uint8_t mt = ntype(st, ml);
+  if (ml != NO_ID) {
+    if (mt == NT_OBJ) {
+      const Node n = st.nodes()[ml];
+      for (uint32_t i = 0; i < n.n; ++i) {
+        const Node& c = st.nodes()[n.first + i];
+        pairs.push_back({c.key, c.type == NT_STR ? c.val : NO_ID});
+      }
+    } else if (mt == NT_ARR) {
+      if (st.nodes()[ml].n > 0) flags |= 1;
+    } else if (mt == NT_STR) {
+      if (st.str(st.nodes()[ml].val).size() > 0) flags |= 1;
+    } else {
+      flags |= 2;  // count(number/bool)
+    }
+  }
+  w.push_back((uint32_t)pairs.size());
+  for (auto& p : pairs) { w.push_back(p.first); w.push_back(p.second); }
+  // matchExpressions := get_default(selector, "matchExpressions", [])
+  uint32_t me = ntype(st, sel) == NT_OBJ ? gdef(st, sel, "matchExpressions") : NO_ID;
+  size_t nex_pos = w.size();
+  w.push_back(0);
+  uint32_t nex = 0;
+  uint8_t met = ntype(st, me);
+  if (met == NT_ARR || met == NT_OBJ) {
+    const Node n = st.nodes()[me];
+    for (uint32_t i = 0; i < n.n; ++i) {
+      uint32_t ex = n.first + i;
+      if (ntype(st, ex) != NT_OBJ) continue;  // me["operator"] undefined
+      uint32_t opn = nget(st, ex, "operator"), keyn = nget(st, ex, "key");
+      if (opn == NO_ID || keyn == NO_ID) continue;
+      uint32_t op = SO_OTHER, ops;
+      if (nstr(st, opn, &ops)) {
+        if (ops == st.s_In) op = SO_IN;
+        else if (ops == st.s_NotIn) op = SO_NOTIN;
+        else if (ops == st.s_Exists) op = SO_EXISTS;
+        else if (ops == st.s_DoesNotExist) op = SO_DOESNOTEXIST;
+      }
+      uint32_t key = NO_ID;
+      nstr(st, keyn, &key);
+      uint32_t vals = gdef(st, ex, "values");
+      uint32_t vflags = 0;
+      std::vector<uint32_t> vs;
+      uint8_t vt = ntype(st, vals);
+      if (vals == NO_ID) {
+        // [] : count 0
+      } else if (vt == NT_ARR || vt == NT_OBJ) {
+        const Node vn = st.nodes()[vals];
+        if (vn.n > 0) vflags |= 1;
+        for (uint32_t j = 0; j < vn.n; ++j) {
+          uint32_t s;
+          if (nstr(st, vn.first + j, &s)) vs.push_back(s);
+        }
+      } else if (vt == NT_STR) {
+        if (st.str(st.nodes()[vals].val).size() > 0) vflags |= 1;
+      } else {
+        vflags |= 2;
+      }
+      w.push_back(op);
+      w.push_back(key);
+      w.push_back(vflags);
+      w.push_back((uint32_t)vs.size());
+      for (auto s : vs) w.push_back(s);
+      ++nex;
+    }
+  }
+  w[nex_pos] = nex;
+  w[head] = flags;
+}
+
+static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
+  Store& st = e->st;
+  MatchSpec m{};
+  m.prog = NO_ID;
+  m.params = NO_ID;
+  auto& W = e->mwords;
+  uint32_t root = c.root;
+  // spec := get_default(constraint, "spec", {}); match := get_default(spec, "match", {})
+  uint32_t spec = gdef(st, root, "spec");
+  uint32_t match = ntype(st, spec) == NT_OBJ ? gdef(st, spec, "match") : NO_ID;
+  if (ntype(st, match) != NT_OBJ) match = NO_ID;
+  // kinds
+  m.kinds_off = (uint32_t)W.size();
+  uint32_t kinds = match == NO_ID ? NO_ID : gdef(st, match, "kinds");
+  if (kinds == NO_ID) {
+    W.push_back(1);
+    W.push_back(1); W.push_back(0xfffffffeu);
+    W.push_back(1); W.push_back(0xfffffffeu);
+  } else {
+    uint8_t kt = ntype(st, kinds);
+    std::vector<uint32_t> sel;
+    uint32_t nsel = 0;
+    if (kt == NT_ARR || kt == NT_OBJ) {
+      const Node kn = st.nodes()[kinds];
+      for (uint32_t i = 0; i < kn.n; ++i) {
+        uint32_t ks = kn.first + i;
+        std::vector<uint32_t> gs, ks2;
+        for (int which = 0; which < 2; ++which) {
+          uint32_t lst = ntype(st, ks) == NT_OBJ ? nget(st, ks, which == 0 ? "apiGroups" : "kinds") : NO_ID;
+          uint8_t lt = ntype(st, lst);
+          if (lt == NT_ARR || lt == NT_OBJ) {
+            const Node ln = st.nodes()[lst];
+            for (uint32_t j = 0; j < ln.n; ++j) {
+              uint32_t s;
+              if (nstr(st, ln.first + j, &s)) (which == 0 ? gs : ks2).push_back(s == st.s_star ? 0xfffffffeu : s);
+            }
+          }
+        }
+        sel.push_back((uint32_t)gs.size());
+        sel.insert(sel.end(), gs.begin(), gs.end());
+        sel.push_back((uint32_t)ks2.size());
+        sel.insert(sel.end(), ks2.begin(), ks2.end());
+        ++nsel;
+      }
+    }
+    W.push_back(nsel);
+    W.insert(W.end(), sel.begin(), sel.end());
+  }
+  auto enc_list = [&](const char* f, uint32_t flag, uint32_t* off) {
+    *off = (uint32_t)W.size();
+    uint32_t n = match == NO_ID ? NO_ID : nget(st, match, f);
+    if (n == NO_ID) { W.push_back(0); return; }
+    m.flags |= flag;
+    std::vector<uint32_t> ids;
+    uint8_t t = ntype(st, n);
+    if (t == NT_ARR || t == NT_OBJ) {
+      const Node ln = st.nodes()[n];
+      for (uint32_t j = 0; j < ln.n; ++j) { uint32_t s; if (nstr(st, ln.first + j, &s)) ids.push_back(s); }
+    }
+    W.push_back((uint32_t)ids.size());
+    W.insert(W.end(), ids.begin(), ids.end());
+  };
+  enc_list("namespaces", MF_HAS_NAMESPACES, &m.ns_off);
+  enc_list("excludedNamespaces", MF_HAS_EXCLUDED, &m.exns_off);
+  // namespaceSelector
+  m.nssel_off = (uint32_t)W.size();
+  if (match != NO_ID && nget(st, match, "namespaceSelector") != NO_ID) {
+    m.flags |= MF_HAS_NSSEL;
+    encode_selector(st, gdef(st, match, "namespaceSelector"), W);
+  } else {
+    encode_selector(st, NO_ID, W);
+  }
+  // scope
+  uint32_t scope = match == NO_ID ? NO_ID : nget(st, match, "scope");
+  if (scope != NO_ID) {
+    m.flags |= MF_SCOPE_PRESENT;
+    uint32_t s;
+    if (nstr(st, scope, &s)) {
+      std::string_view sv = st.str(s);
+      if (sv == "*") m.flags |= MF_SCOPE_ANY;
+      else if (sv == "Namespaced") m.flags |= MF_SCOPE_NS;
+      else if (sv == "Cluster") m.flags |= MF_SCOPE_CLUSTER;
+    }
+  }
+  m.labelsel_off = (uint32_t)W.size();
+  encode_selector(st, match == NO_ID ? NO_ID : gdef(st, match, "labelSelector"), W);
+  // hooks-level get_default (regolib/src.go:77-85): defined values (incl. null) win
+  uint32_t hspec = nget(st, root, "spec");
+  uint32_t params = ntype(st, hspec) == NT_OBJ ? nget(st, hspec, "parameters") : NO_ID;
+  m.params = params;
+  uint32_t ea = ntype(st, hspec) == NT_OBJ ? nget(st, hspec, "enforcementAction") : NO_ID;
+  c.ea_error = false;
+  if (ea == NO_ID) c.ea = "deny";
+  else if (ntype(st, ea) == NT_STR) c.ea = std::string(st.str(st.nodes()[ea].val));
+  else if (ntype(st, ea) == NT_NULL) c.ea = "";
+  else { c.ea = ""; c.ea_error = true; }
+  auto it = e->templates.find(c.kind);
+  if (it != e->templates.end()) {
+    if (it->second.supported) m.prog = (uint32_t)it->second.prog;
+    else m.flags |= MF_FALLBACK;  // template served by CPU OPA
+  }
+  c.spec = m;
+}
+
+static void rebuild_constraints(gk_engine* e) {
+  rebuild_modules(e);
+  if (!e->constraints_dirty) return;
+  e->mwords.clear();
+  e->corder.clear();
+  for (auto& kv : e->constraints) {
+    compile_constraint(e, kv.second);
+    e->corder.push_back(&kv.second);
+  }
+  e->constraints_dirty = false;
+}
+
+// ------------------------------------------------------------------ regex tables
+static void rebuild_regex(gk_engine* e) {
+  // literal patterns of templates + every string in constraint parameters when a
+  // template calls re_match with a computed pattern
+  bool any_regex = false;
+  std::vector<uint32_t> pats;
+  for (auto& p : e->progs) {
+    if (p.uses_regex) any_regex = true;
+    pats.insert(pats.end(), p.regex_literals.begin(), p.regex_literals.end());
+  }
+  if (!any_regex) return;
+  for (auto* c : e->corder) {
+    uint32_t pr = c->spec.params;
+    if (pr == NO_ID) continue;
+    std::vector<uint32_t> stack{pr};
+    while (!stack.empty()) {
+      uint32_t n = stack.back();
+      stack.pop_back();
+      const Node nd = e->st.nodes()[n];
+      if (nd.type == NT_STR) pats.push_back(nd.val);
+      if (nd.type == NT_ARR || nd.type == NT_OBJ) for (uint32_t i = 0; i < nd.n; ++i) stack.push_back(nd.first + i);
+    }
+  }
+  bool changed = false;
+  for (uint32_t sid : pats) {
+    if (e->dfa_index.count(sid)) continue;
+    std::vector<uint32_t> words;
+    int status = compile_regex_dfa(std::string(e->st.str(sid)), words);
+    uint32_t off = (uint32_t)e->dfa_words.size();
+    if (status == RX_OK) e->dfa_words.insert(e->dfa_words.end(), words.begin(), words.end());
+    e->dfa_index[sid] = {off, (uint32_t)status};
+    changed = true;
+  }
+  if (changed) {
+    e->dfa_keys.clear();
+    e->dfa_meta.clear();
+    for (auto& kv : e->dfa_index) {
+      e->dfa_keys.push_back(kv.first);
+      e->dfa_meta.push_back(kv.second.first | (kv.second.second << 30));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ review flattening
+struct ReviewBuild {
+  ReviewCol col{};
+};
+
+// Computes match columns for a flattened review document (target_template_source.go).
+static ReviewCol review_columns(gk_engine* e, uint32_t root) {
+  Store& st = e->st;
+  ReviewCol rc{};
+  rc.root = root;
+  rc.group = rc.kind = rc.ns = rc.nsname = NO_ID;
+  rc.labels = rc.old_labels = rc.ns_labels = NO_ID;
+  if (root == NO_ID) return rc;  // input.review undefined: nothing matches
+  if (ntype(st, root) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  rc.flags |= RC_REVIEW_DEF;
+  uint32_t kind = nget(st, root, st.s_kind);
+  if (kind != NO_ID) {
+    if (ntype(st, kind) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_KIND_OK;
+    uint32_t g = nget(st, kind, st.s_group), k = nget(st, kind, st.s_kind);
+    if (g != NO_ID && ntype(st, g) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    if (k != NO_ID && ntype(st, k) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    if (g != NO_ID) rc.group = st.nodes()[g].val;
+    if (k != NO_ID) rc.kind = st.nodes()[k].val;
+    if (rc.group == st.s_empty && rc.kind == st.s_Namespace) rc.flags |= RC_IS_NS;
+  }
+  uint32_t ns = nget(st, root, st.s_namespace);
+  if (ns != NO_ID) {
+    if (ntype(st, ns) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_HAS_NS;
+    rc.ns = st.nodes()[ns].val;
+    if (rc.ns == st.s_empty) rc.flags |= RC_NS_EMPTY;
+  } else {
+    rc.flags |= RC_NS_EMPTY;
+  }
+  uint32_t obj = nget(st, root, st.s_object);
+  uint32_t old = nget(st, root, st.s_oldObject);
+  if (rc.flags & RC_IS_NS) {
+    uint32_t nm = NO_ID;
+    uint32_t md = ntype(st, obj) == NT_OBJ ? nget(st, obj, st.s_metadata) : NO_ID;
+    if (ntype(st, md) == NT_OBJ) nm = nget(st, md, st.s_name);
+    if (nm != NO_ID) {
+      if (ntype(st, nm) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+      rc.nsname = st.nodes()[nm].val;
+      rc.flags |= RC_NAME_OK;
+    }
+  } else {
+    rc.nsname = rc.ns;
+  }
+  // object / oldObject emptiness: get_default(review, "object", {}) == {}
+  auto empty = [&](uint32_t n) { return n == NO_ID || ntype(st, n) == NT_NULL || is_empty_obj(st, n); };
+  auto labels_of = [&](uint32_t o, uint32_t* out) -> bool {
+    uint32_t md = ntype(st, o) == NT_OBJ ? gdef(st, o, "metadata") : NO_ID;
+    if (md != NO_ID && ntype(st, md) != NT_OBJ) { *out = NO_ID; return ntype(st, o) == NT_OBJ ? false : true; }
+    uint32_t lb = md == NO_ID ? NO_ID : gdef(st, md, "labels");
+    if (lb == NO_ID) { *out = NO_ID; return true; }
+    if (ntype(st, lb) != NT_OBJ) return false;
+    const Node ln = st.nodes()[lb];
+    for (uint32_t i = 0; i < ln.n; ++i) if (st.nodes()[ln.first + i].type != NT_STR) return false;
+    *out = lb;
+    return true;
+  };
+  bool oe = empty(obj), le = empty(old);
+  if (!oe && ntype(st, obj) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  if (!le && ntype(st, old) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  if (!oe) { if (!labels_of(obj, &rc.labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OBJ; }
+  if (!le) { if (!labels_of(old, &rc.old_labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OLD; }
+  // namespace object for namespaceSelector: _unstable.namespace, else the cache
+  uint32_t un = nget(st, root, st.s_unstable);
+  uint32_t unns = ntype(st, un) == NT_OBJ ? nget(st, un, st.s_namespace) : NO_ID;
+  if (un != NO_ID && ntype(st, un) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  auto ns_labels = [&](uint32_t nsobj) -> bool {
+    uint32_t md = gdef(st, nsobj, "metadata");
+    if (md != NO_ID && ntype(st, md) != NT_OBJ) return false;
+    uint32_t lb = md == NO_ID ? NO_ID : gdef(st, md, "labels");
+    if (lb != NO_ID) {
+      if (ntype(st, lb) != NT_OBJ) return false;
+      const Node ln = st.nodes()[lb];
+      for (uint32_t i = 0; i < ln.n; ++i) if (st.nodes()[ln.first + i].type != NT_STR) return false;
+    }
+    rc.ns_labels = lb;
+    return true;
+  };
+  if (unns != NO_ID) {
+    if (ntype(st, unns) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_UNSTABLE_NS;
+    if (!ns_labels(unns)) { rc.flags |= RC_FALLBACK; return rc; }
+  } else if (rc.flags & RC_HAS_NS) {
+    auto it = e->ns_cache.find(std::string(st.str(rc.ns)));
+    if (it != e->ns_cache.end()) {
+      uint32_t nsn = it->second;
+      if (ntype(st, nsn) == NT_FALSE) {
+        // falsy cached value: not "cached" for autoreject, no get_ns solution
+      } else {
+        if (ntype(st, nsn) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+        rc.flags |= RC_NS_CACHED;
+        if (!ns_labels(nsn)) { rc.flags |= RC_FALLBACK; return rc; }
+      }
+    }
+  }
+  return rc;
+}
+
+// Review(AugmentedUnstructured{obj, ns}) envelope (pkg/target/target.go:129-163,
+// admission/v1beta1 AdmissionRequest json field order).
+static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const JDoc& nd, int nj) {
+  Store& st = e->st;
+  std::string apiv, kind, name;
+  int av = od.get(oj, "apiVersion");
+  if (av >= 0 && od.nodes[av].type == NT_STR) apiv = od.sval(av);
+  int kd = od.get(oj, "kind");
+  if (kd >= 0 && od.nodes[kd].type == NT_STR) kind = od.sval(kd);
+  int md = od.get(oj, "metadata");
+  if (md >= 0) { int nm = od.get(md, "name"); if (nm >= 0 && od.nodes[nm].type == NT_STR) name = od.sval(nm); }
+  std::string group, version;
+  size_t slash = apiv.find('/');
+  if (slash == std::string::npos) version = apiv;
+  else if (apiv.find('/', slash + 1) == std::string::npos) { group = apiv.substr(0, slash); version = apiv.substr(slash + 1); }
+  std::string nsname;
+  int nmd = nd.get(nj, "metadata");
+  if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
+  // children: uid kind resource [name] [namespace] operation userInfo object oldObject options _unstable
+  uint32_t nch = 9 + (name.empty() ? 0 : 1) + (nsname.empty() ? 0 : 1);
+  uint32_t root = st.add_node(Node{});
+  uint32_t first = st.reserve(nch);
+  {
+    Node& r = st.nodes()[root];
+    r.type = NT_OBJ;
+    r.first = first;
+    r.n = (uint16_t)nch;
+  }
+  uint32_t i = first;
+  auto str_node = [&](uint32_t idx, uint32_t key, const std::string& v) {
+    Node n{};
+    n.key = key;
+    n.type = NT_STR;
+    n.val = st.intern(v);
+    st.nodes()[idx] = n;
+  };
+  auto obj3 = [&](uint32_t idx, uint32_t key, uint32_t k1, const std::string& v1, uint32_t k2, const std::string& v2,
+                  uint32_t k3, const std::string& v3) {
+    uint32_t f = st.reserve(3);
+    str_node(f, k1, v1);
+    str_node(f + 1, k2, v2);
+    str_node(f + 2, k3, v3);
+    Node n{};
+    n.key = key;
+    n.type = NT_OBJ;
+    n.first = f;
+    n.n = 3;
+    st.nodes()[idx] = n;
+  };
+  str_node(i++, st.s_uid, "");
+  obj3(i++, st.s_kind, st.s_group, group, st.s_version, version, st.s_kind, kind);
+  obj3(i++, st.s_resource, st.s_group, "", st.s_version, "", st.s_resource, "");
+  if (!name.empty()) str_node(i++, st.s_name, name);
+  if (!nsname.empty()) str_node(i++, st.s_namespace, nsname);
+  str_node(i++, st.s_operation, "");
+  { Node n{}; n.key = st.s_userInfo; n.type = NT_OBJ; st.nodes()[i++] = n; }
+  uint32_t objslot = i++;
+  { Node n{}; n.key = st.s_oldObject; n.type = NT_NULL; st.nodes()[i++] = n; }
+  { Node n{}; n.key = st.s_options; n.type = NT_NULL; st.nodes()[i++] = n; }
+  uint32_t unslot = i++;
+  // object subtree
+  uint32_t o = st.add_doc(od, oj);
+  {
+    Node n = st.nodes()[o];
+    n.key = st.s_object;
+    st.nodes()[objslot] = n;
+  }
+  // _unstable: {"namespace": <ns>}
+  uint32_t nsroot = st.add_doc(nd, nj);
+  uint32_t uf = st.reserve(1);
+  {
+    Node n = st.nodes()[nsroot];
+    n.key = st.s_namespace;
+    st.nodes()[uf] = n;
+    Node u{};
+    u.key = st.s_unstable;
+    u.type = NT_OBJ;
+    u.first = uf;
+    u.n = 1;
+    st.nodes()[unslot] = u;
+  }
+  return root;
+}
+
+// ------------------------------------------------------------------ device sync + launch
+static bool ensure_device(gk_engine* e) {
+  if (e->dev_ok) return true;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= e->device) return false;
+  if (hipSetDevice(e->device) != hipSuccess) return false;
+  if (hipStreamCreate(&e->stream) != hipSuccess) return false;
+  e->dev_ok = true;
+  return true;
+}
+
+template <class T>
+static bool up(DBuf& b, const std::vector<T>& v, bool append_only) {
+  return b.upload(v.data(), v.size() * sizeof(T), append_only);
+}
+
+static bool sync_tables(gk_engine* e) {
+  Store& st = e->st;
+  bool ok = true;
+  ok &= up(e->d_nodes, st.nodes(), false);
+  ok &= up(e->d_strs, st.strings(), true);
+  ok &= e->d_pool.upload(st.pool().data(), st.pool().size(), true);
+  ok &= up(e->d_sflags, st.str_flags(), true);
+  ok &= up(e->d_nums, st.numbers(), true);
+  ok &= up(e->d_code, e->bank.code, false);
+  ok &= up(e->d_K, e->bank.consts, false);
+  std::vector<uint32_t> fmt = e->bank.fmt;
+  if (fmt.empty()) fmt.push_back(0);
+  ok &= up(e->d_fmt, fmt, false);
+  std::vector<MatchSpec> cons;
+  for (auto* c : e->corder) cons.push_back(c->spec);
+  if (cons.empty()) cons.push_back(MatchSpec{});
+  ok &= up(e->d_cons, cons, false);
+  std::vector<uint32_t> mw = e->mwords;
+  if (mw.empty()) mw.push_back(0);
+  ok &= up(e->d_mwords, mw, false);
+  std::vector<uint32_t> po;
+  for (auto& p : e->progs) po.push_back(p.code_off);
+  if (po.empty()) po.push_back(0);
+  ok &= up(e->d_progoff, po, false);
+  std::vector<uint32_t> dk = e->dfa_keys, dm = e->dfa_meta, dw = e->dfa_words;
+  if (dk.empty()) { dk.push_back(NO_ID); dm.push_back(2u << 30); }
+  if (dw.empty()) dw.push_back(0);
+  ok &= up(e->d_dfa_keys, dk, false);
+  ok &= up(e->d_dfa_meta, dm, false);
+  ok &= up(e->d_dfa_words, dw, false);
+  return ok;
+}
+
+// runs the kernel over `cols` (already resident in d_revs when `resident`)
+static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, DBuf* revbuf, bool decode,
+                              gk_results* res) {
+  uint32_t nrev = (uint32_t)cols.size();
+  uint32_t ncons = (uint32_t)e->corder.size();
+  res->status.assign(nrev, 0);
+  res->reason.assign(nrev, 0);
+  res->totals.assign(ncons, 0);
+  for (auto* c : e->corder) { res->ckind.push_back(c->kind); res->cname.push_back(c->name); res->cea.push_back(c->ea); }
+  if (nrev == 0) return GK_OK;
+  // reviews flagged for fallback on the host never reach the device when there are no constraints
+  if (ncons == 0) {
+    for (uint32_t r = 0; r < nrev; ++r) if (cols[r].flags & RC_FALLBACK) res->status[r] = GK_REVIEW_FALLBACK;
+    return GK_OK;
+  }
+  if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
+  auto t0 = Clock::now();
+  if (!sync_tables(e)) return fail(e, GK_EDEVICE, "device upload failed");
+  if (revbuf == &e->d_revs || !revbuf->p || revbuf->used != cols.size() * sizeof(ReviewCol)) {
+    if (!up(*revbuf, cols, false)) return fail(e, GK_EDEVICE, "device upload failed");
+  }
+  bool ok = true;
+  ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 4) &&
+        e->d_counters.reserve(64) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
+  if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
+  res->ms[1] = ms_since(t0);
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    hipMemsetAsync(e->d_rflags.p, 0, nrev * 4, e->stream);
+    hipMemsetAsync(e->d_rreason.p, 0, nrev * 4, e->stream);
+    hipMemsetAsync(e->d_totals.p, 0, ncons * 4, e->stream);
+    hipMemsetAsync(e->d_counters.p, 0, 64, e->stream);
+    HostDevArgs a{};
+    a.nodes = (const Node*)e->d_nodes.p;
+    a.strs = (const StrEnt*)e->d_strs.p;
+    a.pool = (const uint8_t*)e->d_pool.p;
+    a.sflags = (const uint8_t*)e->d_sflags.p;
+    a.nums = (const NumEnt*)e->d_nums.p;
+    a.code = (const Ins*)e->d_code.p;
+    a.K = (const uint64_t*)e->d_K.p;
+    a.fmt = (const uint32_t*)e->d_fmt.p;
+    a.cons = (const MatchSpec*)e->d_cons.p;
+    a.mwords = (const uint32_t*)e->d_mwords.p;
+    a.prog_off = (const uint32_t*)e->d_progoff.p;
+    a.revs = (const ReviewCol*)revbuf->p;
+    a.dfa_keys = (const uint32_t*)e->d_dfa_keys.p;
+    a.dfa_meta = (const uint32_t*)e->d_dfa_meta.p;
+    a.dfa_words = (const uint32_t*)e->d_dfa_words.p;
+    a.ndfa = (uint32_t)std::max<size_t>(e->dfa_keys.size(), 1);
+    a.ncode = (uint32_t)e->bank.code.size();
+    a.ncons = ncons;
+    a.nrev = nrev;
+    a.ntiles = (nrev + 63) / 64;
+    a.out = (Viol*)e->d_out.p;
+    a.out_cap = (uint32_t)e->out_cap;
+    a.counters = (uint32_t*)e->d_counters.p;
+    a.bytes = (char*)e->d_bytes.p;
+    a.bytes_cap = (uint32_t)e->bytes_cap;
+    a.rflags = (uint32_t*)e->d_rflags.p;
+    a.totals = (uint32_t*)e->d_totals.p;
+    a.rreason = (uint32_t*)e->d_rreason.p;
+    hipEvent_t ev0, ev1;
+    hipEventCreate(&ev0);
+    hipEventCreate(&ev1);
+    hipEventRecord(ev0, e->stream);
+    int lr = gk_launch_audit(&a, e->stream);
+    hipEventRecord(ev1, e->stream);
+    if (lr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed: ") + hipGetErrorString((hipError_t)lr));
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
+    float kms = 0;
+    hipEventElapsedTime(&kms, ev0, ev1);
+    hipEventDestroy(ev0);
+    hipEventDestroy(ev1);
+    res->ms[2] += kms;
+    auto t1 = Clock::now();
+    uint32_t counters[2];
+    hipMemcpy(counters, e->d_counters.p, 8, hipMemcpyDeviceToHost);
+    if (counters[0] > e->out_cap || counters[1] > e->bytes_cap) {
+      e->out_cap = std::max<size_t>(e->out_cap * 2, counters[0] + 1024);
+      e->bytes_cap = std::max<size_t>(e->bytes_cap * 2, (size_t)counters[1] + 65536);
+      if (!e->d_out.reserve(e->out_cap * sizeof(Viol)) || !e->d_bytes.reserve(e->bytes_cap))
+        return fail(e, GK_EDEVICE, "device allocation failed");
+      continue;
+    }
+    std::vector<uint32_t> tot(ncons);
+    hipMemcpy(tot.data(), e->d_totals.p, ncons * 4, hipMemcpyDeviceToHost);
+    for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
+    hipMemcpy(res->status.data(), e->d_rflags.p, nrev * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(res->reason.data(), e->d_rreason.p, nrev * 4, hipMemcpyDeviceToHost);
+    bool flagged = false;
+    for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+    bool ea_err = false;
+    for (auto* c : e->corder) ea_err |= c->ea_error;
+    if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); return GK_OK; }
+    std::vector<Viol> vs(counters[0]);
+    std::string bytes;
+    if (counters[0]) hipMemcpy(vs.data(), e->d_out.p, counters[0] * sizeof(Viol), hipMemcpyDeviceToHost);
+    if (decode) {
+      bytes.assign(counters[1], '\0');
+      if (counters[1]) hipMemcpy(&bytes[0], e->d_bytes.p, counters[1], hipMemcpyDeviceToHost);
+    }
+    res->ms[3] = ms_since(t1);
+    auto t2 = Clock::now();
+    // constraint errors: non-string enforcementAction fails the whole Query
+    for (auto& v : vs) {
+      if (e->corder[v.constraint]->ea_error) res->status[v.review] |= GK_REVIEW_ERROR;
+    }
+    // totals count only reviews the engine answered (flagged ones go to CPU OPA)
+    std::fill(res->totals.begin(), res->totals.end(), 0);
+    for (auto& v : vs)
+      if (!(res->status[v.review] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK))) res->totals[v.constraint]++;
+    if (!decode) {
+      for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+      res->ms[4] = ms_since(t2);
+      return GK_OK;
+    }
+    // deterministic order: review, autoreject first, constraint order, emission order
+    std::sort(vs.begin(), vs.end(), [](const Viol& x, const Viol& y) {
+      if (x.review != y.review) return x.review < y.review;
+      bool ax = x.rule == RULE_AUTOREJECT, ay = y.rule == RULE_AUTOREJECT;
+      if (ax != ay) return ax;
+      if (x.constraint != y.constraint) return x.constraint < y.constraint;
+      return x.seq < y.seq;
+    });
+    res->rows.reserve(vs.size());
+    for (auto& v : vs) {
+      if (res->status[v.review] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK)) continue;
+      ResultRow row;
+      row.review = v.review;
+      row.constraint = v.constraint;
+      row.seq = v.seq;
+      row.rule = v.rule;
+      row.msg.assign(bytes.data() + v.msg_off, v.msg_len);
+      row.details.assign(bytes.data() + v.det_off, v.det_len);
+      res->rows.push_back(std::move(row));
+    }
+    for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+    res->ms[4] = ms_since(t2);
+    return GK_OK;
+  }
+  return fail(e, GK_EDEVICE, "output buffer overflow");
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int gk_device_available(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+int gk_engine_create(const char* opts_json, gk_engine** out) {
+  if (!out) return GK_EINVAL;
+  if (gk_devargs_size() != sizeof(HostDevArgs)) return GK_EINVAL;
+  auto* e = new gk_engine();
+  if (opts_json && *opts_json) {
+    JDoc d;
+    JsonReader rd(opts_json, strlen(opts_json), &d);
+    int r = rd.parse();
+    if (r >= 0) {
+      int dv = d.get(r, "device");
+      if (dv >= 0 && d.nodes[dv].type == NT_NUM) e->device = atoi(d.str(d.nodes[dv]));
+      int mv = d.get(r, "max_violations");
+      if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap = (size_t)atoll(d.str(d.nodes[mv]));
+    }
+  }
+  e->perm_nodes = (uint32_t)e->st.nodes().size();
+  *out = e;
+  return GK_OK;
+}
+
+void gk_engine_destroy(gk_engine* e) {
+  if (!e) return;
+  for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
+                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
+                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason})
+    b->free_();
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char* gk_last_error(gk_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int gk_init(gk_engine* e) {
+  if (!e) return GK_EINVAL;
+  return GK_OK;
+}
+
+int gk_put_module(gk_engine* e, const char* name, const char* src, size_t len) {
+  if (!e || !name || !src) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::string s(src, len);
+  try {
+    rego::parse_module(s);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  e->modules[name] = s;
+  e->modules_dirty = true;
+  e->gen++;
+  return GK_OK;
+}
+
+static int delete_modules_locked(gk_engine* e, const std::string& prefix) {
+  std::string p = "__modset_" + prefix + "_idx_";
+  int n = 0;
+  for (auto it = e->modules.begin(); it != e->modules.end();) {
+    if (it->first.compare(0, p.size(), p) == 0) { it = e->modules.erase(it); ++n; }
+    else ++it;
+  }
+  if (n) { e->modules_dirty = true; e->gen++; }
+  return n;
+}
+
+int gk_put_modules(gk_engine* e, const char* prefix, const char* const* srcs, const size_t* lens, size_t n) {
+  if (!e || !prefix) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::vector<std::string> ss;
+  for (size_t i = 0; i < n; ++i) {
+    std::string s(srcs[i], lens ? lens[i] : strlen(srcs[i]));
+    try {
+      rego::parse_module(s);
+    } catch (const std::exception& ex) {
+      return fail(e, GK_EPARSE, ex.what());
+    }
+    ss.push_back(s);
+  }
+  delete_modules_locked(e, prefix);
+  for (size_t i = 0; i < ss.size(); ++i)
+    e->modules["__modset_" + std::string(prefix) + "_idx_" + std::to_string(i)] = ss[i];
+  e->modules_dirty = true;
+  e->gen++;
+  return GK_OK;
+}
+
+int gk_delete_module(gk_engine* e, const char* name, int* deleted) {
+  if (!e || !name) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  int d = (int)e->modules.erase(name);
+  if (d) { e->modules_dirty = true; e->gen++; }
+  if (deleted) *deleted = d;
+  return GK_OK;
+}
+
+int gk_delete_modules(gk_engine* e, const char* prefix, int* count) {
+  if (!e || !prefix) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  int n = delete_modules_locked(e, prefix);
+  if (count) *count = n;
+  return GK_OK;
+}
+
+int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
+  if (!e || !path || !json) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  auto p = split_path(path);
+  JDoc d;
+  JsonReader rd(json, len, &d);
+  int root = rd.parse();
+  if (root < 0) return fail(e, GK_EINVAL, "invalid JSON: " + d.err);
+  e->gen++;
+  if (p.size() == 6 && p[0] == "constraints" && p[1] == TARGET && p[2] == "cluster" && p[3] == CGROUP) {
+    rebuild_modules(e);
+    e->st.nodes().resize(e->perm_nodes);
+    ConstraintEnt c;
+    c.kind = p[4];
+    c.name = p[5];
+    c.root = e->st.add_doc(d, root);
+    e->perm_nodes = (uint32_t)e->st.nodes().size();
+    e->constraints[{c.kind, c.name}] = c;
+    e->constraints_dirty = true;
+    return GK_OK;
+  }
+  if (p.size() >= 2 && p[0] == "external" && p[1] == TARGET) {
+    std::string key(path);
+    e->inventory[key] = std::string(json, len);
+    if (p.size() == 6 && p[2] == "cluster" && p[3] == "v1" && p[4] == "Namespace") {
+      rebuild_modules(e);
+      e->st.nodes().resize(e->perm_nodes);
+      e->ns_cache[p[5]] = e->st.add_doc(d, root);
+      e->perm_nodes = (uint32_t)e->st.nodes().size();
+    }
+    return GK_OK;
+  }
+  e->other_data[path] = std::string(json, len);
+  return GK_OK;
+}
+
+int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
+  if (!e || !path) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  auto p = split_path(path);
+  int d = 0;
+  e->gen++;
+  auto prefix_match = [&](const std::vector<std::string>& q) {
+    if (q.size() < p.size()) return false;
+    for (size_t i = 0; i < p.size(); ++i) if (q[i] != p[i]) return false;
+    return true;
+  };
+  for (auto it = e->constraints.begin(); it != e->constraints.end();) {
+    std::vector<std::string> q{"constraints", TARGET, "cluster", CGROUP, it->first.first, it->first.second};
+    if (prefix_match(q)) { it = e->constraints.erase(it); d = 1; e->constraints_dirty = true; }
+    else ++it;
+  }
+  for (auto it = e->inventory.begin(); it != e->inventory.end();) {
+    if (prefix_match(split_path(it->first))) { it = e->inventory.erase(it); d = 1; }
+    else ++it;
+  }
+  for (auto it = e->ns_cache.begin(); it != e->ns_cache.end();) {
+    std::vector<std::string> q{"external", TARGET, "cluster", "v1", "Namespace", it->first};
+    if (prefix_match(q)) { it = e->ns_cache.erase(it); d = 1; }
+    else ++it;
+  }
+  for (auto it = e->other_data.begin(); it != e->other_data.end();) {
+    if (prefix_match(split_path(it->first))) { it = e->other_data.erase(it); d = 1; }
+    else ++it;
+  }
+  if (p.empty()) { e->constraints.clear(); e->inventory.clear(); e->ns_cache.clear(); e->other_data.clear(); d = 1; }
+  if (deleted) *deleted = d;
+  return GK_OK;
+}
+
+static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, size_t>>& inputs, gk_results** out) {
+  auto* res = new gk_results();
+  try {
+    rebuild_constraints(e);
+    rebuild_regex(e);
+  } catch (const std::exception& ex) {
+    delete res;
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  auto t0 = Clock::now();
+  e->st.nodes().resize(e->perm_nodes);
+  std::vector<ReviewCol> cols;
+  cols.reserve(inputs.size());
+  JDoc d;
+  for (auto& in : inputs) {
+    JsonReader rd(in.first, in.second, &d);
+    int root = rd.parse();
+    if (root < 0) { delete res; return fail(e, GK_EINVAL, "invalid input JSON: " + d.err); }
+    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
+    uint32_t rn = rv >= 0 ? e->st.add_doc(d, rv) : NO_ID;
+    cols.push_back(review_columns(e, rn));
+  }
+  res->ms[0] = ms_since(t0);
+  int rc = launch_and_collect(e, cols, &e->d_revs, true, res);
+  if (rc != GK_OK) { delete res; return rc; }
+  *out = res;
+  return GK_OK;
+}
+
+int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len, gk_results** out) {
+  if (!e || !path || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::string p(path);
+  std::string viol = std::string("hooks[\"") + TARGET + "\"].violation";
+  std::string aud = std::string("hooks[\"") + TARGET + "\"].audit";
+  if (p == viol) {
+    std::vector<std::pair<const char*, size_t>> in;
+    in.push_back({input_json ? input_json : "null", input_json ? len : 4});
+    return eval_inputs(e, in, out);
+  }
+  if (p == aud) {
+    // hooks.audit: reviews synthesized from the synced inventory
+    // (target_template_source.go:46-89: make_review / add_field)
+    std::vector<std::string> docs;
+    std::string prefix = std::string("/external/") + TARGET + "/";
+    for (auto& kv : e->inventory) {
+      auto q = split_path(kv.first);
+      std::string ns, gv, kind, name;
+      if (q.size() == 7 && q[2] == "namespace") { ns = q[3]; gv = q[4]; kind = q[5]; name = q[6]; }
+      else if (q.size() == 6 && q[2] == "cluster") { gv = q[3]; kind = q[4]; name = q[5]; }
+      else continue;
+      std::string group, version;
+      size_t s = gv.find('/');
+      if (s == std::string::npos) version = gv;
+      else if (gv.find('/', s + 1) == std::string::npos) { group = gv.substr(0, s); version = gv.substr(s + 1); }
+      else continue;
+      auto js = [](const std::string& v) {
+        std::string o = "\"";
+        for (char c : v) { if (c == '"' || c == '\\') o.push_back('\\'); o.push_back(c); }
+        return o + "\"";
+      };
+      std::string r = "{\"review\":{\"kind\":{\"group\":" + js(group) + ",\"version\":" + js(version) + ",\"kind\":" +
+                      js(kind) + "},\"name\":" + js(name) + ",\"object\":" + kv.second +
+                      (q.size() == 7 ? ",\"namespace\":" + js(ns) : std::string()) + "}}";
+      docs.push_back(r);
+    }
+    std::vector<std::pair<const char*, size_t>> in;
+    for (auto& s : docs) in.push_back({s.data(), s.size()});
+    return eval_inputs(e, in, out);
+  }
+  return fail(e, GK_EQUERY, "unsupported query path: " + p);
+}
+
+int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n, gk_results** out) {
+  if (!e || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::vector<std::pair<const char*, size_t>> in;
+  for (size_t i = 0; i < n; ++i) in.push_back({inputs[i], lens ? lens[i] : strlen(inputs[i])});
+  return eval_inputs(e, in, out);
+}
+
+static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                           const size_t* ns_lens, size_t n, std::vector<ReviewCol>& cols) {
+  JDoc od, nd;
+  std::string empty_ns = EMPTY_NS_JSON;
+  // namespace docs are shared by all objects of a namespace: parse each distinct text once
+  for (size_t i = 0; i < n; ++i) {
+    JsonReader ro(objs[i], obj_lens ? obj_lens[i] : strlen(objs[i]), &od);
+    int oj = ro.parse();
+    if (oj < 0) return fail(e, GK_EINVAL, "invalid object JSON at " + std::to_string(i) + ": " + od.err);
+    const char* ns = (ns_json && ns_json[i]) ? ns_json[i] : nullptr;
+    size_t nl = ns ? (ns_lens ? ns_lens[i] : strlen(ns)) : 0;
+    if (!ns || nl == 0) { ns = empty_ns.data(); nl = empty_ns.size(); }
+    JsonReader rn(ns, nl, &nd);
+    int nj = rn.parse();
+    if (nj < 0) return fail(e, GK_EINVAL, "invalid namespace JSON at " + std::to_string(i) + ": " + nd.err);
+    uint32_t root = build_object_review(e, od, oj, nd, nj);
+    cols.push_back(review_columns(e, root));
+  }
+  return GK_OK;
+}
+
+int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                      const size_t* ns_lens, size_t n, gk_results** out) {
+  if (!e || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  auto* res = new gk_results();
+  try {
+    rebuild_constraints(e);
+    rebuild_regex(e);
+  } catch (const std::exception& ex) {
+    delete res;
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  auto t0 = Clock::now();
+  e->st.nodes().resize(e->perm_nodes);
+  std::vector<ReviewCol> cols;
+  cols.reserve(n);
+  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, cols);
+  if (rc != GK_OK) { delete res; return rc; }
+  res->ms[0] = ms_since(t0);
+  rc = launch_and_collect(e, cols, &e->d_revs, true, res);
+  if (rc != GK_OK) { delete res; return rc; }
+  *out = res;
+  return GK_OK;
+}
+
+int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                           const size_t* ns_lens, size_t n, gk_batch** out) {
+  if (!e || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    rebuild_constraints(e);
+    rebuild_regex(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  auto* b = new gk_batch();
+  e->st.nodes().resize(e->perm_nodes);
+  b->node_begin = (uint32_t)e->st.nodes().size();
+  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols);
+  if (rc != GK_OK) { delete b; return rc; }
+  b->node_end = (uint32_t)e->st.nodes().size();
+  b->nrev = (uint32_t)n;
+  b->gen = e->gen;
+  if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
+  if (!sync_tables(e) || !up(b->d_revs, b->cols, false)) { delete b; return fail(e, GK_EDEVICE, "upload failed"); }
+  b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
+  *out = b;
+  return GK_OK;
+}
+
+int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
+  if (!e || !b || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
+  auto* res = new gk_results();
+  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res);
+  if (rc != GK_OK) { delete res; return rc; }
+  *out = res;
+  return GK_OK;
+}
+
+void gk_batch_free(gk_batch* b) {
+  if (!b) return;
+  b->d_revs.free_();
+  delete b;
+}
+
+uint64_t gk_batch_device_bytes(const gk_batch* b) { return b ? b->dev_bytes : 0; }
+
+int gk_dump(gk_engine* e, char** out) {
+  if (!e || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::string s = "{\"modules\":[";
+  bool first = true;
+  for (auto& kv : e->modules) {
+    if (!first) s += ",";
+    first = false;
+    s += "\"";
+    for (char c : kv.first) { if (c == '"' || c == '\\') s.push_back('\\'); s.push_back(c); }
+    s += "\"";
+  }
+  s += "],\"constraints\":" + std::to_string(e->constraints.size()) + ",\"templates\":{";
+  first = true;
+  for (auto& kv : e->templates) {
+    if (!first) s += ",";
+    first = false;
+    s += "\"" + kv.first + "\":" + (kv.second.supported ? "\"gpu\"" : "\"fallback\"");
+  }
+  s += "}}";
+  *out = strdup(s.c_str());
+  return GK_OK;
+}
+
+void gk_free_string(char* s) { free(s); }
+
+size_t gk_results_count(const gk_results* r) { return r ? r->rows.size() : 0; }
+
+int gk_results_get(const gk_results* r, size_t i, gk_result_view* out) {
+  if (!r || !out || i >= r->rows.size()) return GK_EINVAL;
+  const ResultRow& row = r->rows[i];
+  out->review = row.review;
+  out->constraint = row.constraint;
+  out->constraint_kind = r->ckind[row.constraint].c_str();
+  out->constraint_name = r->cname[row.constraint].c_str();
+  out->msg = row.msg.data();
+  out->msg_len = row.msg.size();
+  out->details_json = row.details.data();
+  out->details_len = row.details.size();
+  out->enforcement_action = r->cea[row.constraint].c_str();
+  return GK_OK;
+}
+
+size_t gk_results_reviews(const gk_results* r) { return r ? r->status.size() : 0; }
+uint32_t gk_results_review_status(const gk_results* r, size_t i) { return r && i < r->status.size() ? r->status[i] : 0; }
+uint32_t gk_results_review_reason(const gk_results* r, size_t i) { return r && i < r->reason.size() ? r->reason[i] : 0; }
+size_t gk_results_constraints(const gk_results* r) { return r ? r->totals.size() : 0; }
+uint64_t gk_results_constraint_total(const gk_results* r, size_t c) { return r && c < r->totals.size() ? r->totals[c] : 0; }
+int gk_results_timing(const gk_results* r, double* ms5) {
+  if (!r || !ms5) return GK_EINVAL;
+  for (int i = 0; i < 5; ++i) ms5[i] = r->ms[i];
+  return GK_OK;
+}
+void gk_results_free(gk_results* r) { delete r; }
+
+int gk_template_status(gk_engine* e, const char* kind, const char** reason) {
+  if (!e || !kind) return -1;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    rebuild_modules(e);
+  } catch (const std::exception& ex) {
+    e->err = ex.what();
+    return -1;
+  }
+  auto it = e->templates.find(kind);
+  if (it == e->templates.end()) return -1;
+  if (reason) *reason = it->second.reason.c_str();
+  return it->second.supported ? 1 : 0;
+}
+
+size_t gk_constraint_count(gk_engine* e) {
+  if (!e) return 0;
+  std::lock_guard<std::mutex> g(e->mu);
+  rebuild_constraints(e);
+  return e->corder.size();
+}
+
+int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  rebuild_constraints(e);
+  if (i >= e->corder.size()) return GK_EINVAL;
+  if (kind) *kind = e->corder[i]->kind.c_str();
+  if (name) *name = e->corder[i]->name.c_str();
+  return GK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ diagnostics
+extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
+  if (!e || !kind || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  rebuild_modules(e);
+  auto it = e->templates.find(kind);
+  if (it == e->templates.end() || !it->second.supported) return GK_ENOTFOUND;
+  const Program& p = e->progs[it->second.prog];
+  static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
+                                "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",
+                                "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK"};
+  std::string s = "nregs=" + std::to_string(p.nregs) + " len=" + std::to_string(p.code_len) + "\n";
+  for (uint32_t i = 0; i < p.code_len; ++i) {
+    const Ins& in = e->bank.code[p.code_off + i];
+    char buf[160];
+    snprintf(buf, sizeof buf, "%5u %-10s a=%u b=%u c=%u x=%u y=%u\n", p.code_off + i,
+             in.op < OP_COUNT_ ? names[in.op] : "?", in.a, in.b, in.c, in.x, in.y);
+    s += buf;
+  }
+  *out = strdup(s.c_str());
+  return GK_OK;
+}

@@ -1,0 +1,390 @@
+// Host-side interned store (strings, numbers, node arena) + exact number
+// conversions matching Go's math/big / strconv behaviour.
+#include "store.h"
+
+#include <charconv>
+#include <cmath>
+#include <cstdlib>
+#include <deque>
+
+namespace gk {
+
+// ------------------------------------------------------------------ bignum
+namespace {
+struct Big {
+  std::vector<uint32_t> w;  // little endian
+  void trim() { while (!w.empty() && w.back() == 0) w.pop_back(); }
+  bool zero() const { return w.empty(); }
+  int bitlen() const {
+    if (w.empty()) return 0;
+    return (int)(w.size() - 1) * 32 + (32 - __builtin_clz(w.back()));
+  }
+  void mul_small(uint32_t m) {
+    uint64_t c = 0;
+    for (auto& x : w) { uint64_t v = (uint64_t)x * m + c; x = (uint32_t)v; c = v >> 32; }
+    if (c) w.push_back((uint32_t)c);
+  }
+  void add_small(uint32_t a) {
+    uint64_t c = a;
+    for (auto& x : w) { if (!c) break; uint64_t v = (uint64_t)x + c; x = (uint32_t)v; c = v >> 32; }
+    if (c) w.push_back((uint32_t)c);
+  }
+  void shl(int s) {
+    if (zero() || s == 0) return;
+    int ws = s / 32, bs = s % 32;
+    std::vector<uint32_t> r(w.size() + ws + 1, 0);
+    for (size_t i = 0; i < w.size(); ++i) {
+      uint64_t v = (uint64_t)w[i] << bs;
+      r[i + ws] |= (uint32_t)v;
+      r[i + ws + 1] |= (uint32_t)(v >> 32);
+    }
+    w.swap(r);
+    trim();
+  }
+  bool bit(int i) const { return (size_t)(i / 32) < w.size() && ((w[i / 32] >> (i % 32)) & 1); }
+  static int cmp(const Big& a, const Big& b) {
+    if (a.w.size() != b.w.size()) return a.w.size() < b.w.size() ? -1 : 1;
+    for (size_t i = a.w.size(); i-- > 0;) if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
+    return 0;
+  }
+  void sub(const Big& b) {  // *this >= b
+    int64_t br = 0;
+    for (size_t i = 0; i < w.size(); ++i) {
+      int64_t v = (int64_t)w[i] - (i < b.w.size() ? b.w[i] : 0) - br;
+      br = v < 0;
+      w[i] = (uint32_t)(v + (br ? (1ll << 32) : 0));
+    }
+    trim();
+  }
+  // quotient bits (q) and remainder (r) of a / b, via shift-subtract
+  static void divmod(const Big& a, const Big& b, Big& q, Big& r) {
+    q.w.assign(a.w.size() + 1, 0);
+    r.w.clear();
+    for (int i = a.bitlen() - 1; i >= 0; --i) {
+      r.shl(1);
+      if (a.bit(i)) { if (r.w.empty()) r.w.push_back(1); else r.w[0] |= 1; }
+      if (cmp(r, b) >= 0) { r.sub(b); q.w[i / 32] |= 1u << (i % 32); }
+    }
+    q.trim();
+  }
+  uint64_t low64() const { return (w.size() > 0 ? w[0] : 0) | ((uint64_t)(w.size() > 1 ? w[1] : 0) << 32); }
+};
+}  // namespace
+
+bool decimal_to_bf64(const char* s, size_t n, uint64_t* mant, int32_t* exp, bool* neg) {
+  size_t i = 0;
+  *neg = false;
+  if (i < n && (s[i] == '-' || s[i] == '+')) { *neg = s[i] == '-'; ++i; }
+  Big d;
+  int ndig = 0, frac = 0;
+  bool seen_dot = false, any = false;
+  for (; i < n; ++i) {
+    char c = s[i];
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (!d.zero() || c != '0') { d.mul_small(10); d.add_small(c - '0'); if (d.w.empty() && c != '0') d.w.push_back(c - '0'); ++ndig; }
+      if (seen_dot) ++frac;
+    } else if (c == '.' && !seen_dot) {
+      seen_dot = true;
+    } else break;
+  }
+  if (!any) return false;
+  long e10 = 0;
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    ++i;
+    bool en = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { en = s[i] == '-'; ++i; }
+    if (i >= n) return false;
+    long v = 0;
+    for (; i < n; ++i) {
+      if (s[i] < '0' || s[i] > '9') return false;
+      v = v * 10 + (s[i] - '0');
+      if (v > 100000) return false;
+    }
+    e10 = en ? -v : v;
+  }
+  if (i != n) return false;
+  if (ndig > 800) return false;
+  e10 -= frac;
+  if (d.zero()) { *mant = 0; *exp = 0; return true; }
+  if (e10 > 800 || e10 < -800) return false;
+  if (e10 >= 0) {
+    for (long k = 0; k < e10; ++k) d.mul_small(10);
+    int L = d.bitlen();
+    if (L <= 64) {
+      uint64_t v = d.low64();
+      *mant = v << (64 - L);
+      *exp = L - 64;
+      return true;
+    }
+    int sh = L - 64;
+    // q = d >> sh, remainder bits
+    Big q = d;
+    // shift right by sh
+    {
+      int ws = sh / 32, bs = sh % 32;
+      std::vector<uint32_t> r;
+      for (size_t j = ws; j < q.w.size(); ++j) {
+        uint64_t v = q.w[j] >> bs;
+        if (bs && j + 1 < q.w.size()) v |= (uint64_t)q.w[j + 1] << (32 - bs);
+        r.push_back((uint32_t)v);
+      }
+      q.w.swap(r);
+      q.trim();
+    }
+    uint64_t m = q.low64();
+    bool half = d.bit(sh - 1);
+    bool rest = false;
+    for (int b = 0; b < sh - 1 && !rest; ++b) rest = d.bit(b);
+    bool up = half && (rest || (m & 1));
+    int32_t e = sh;
+    if (up) { ++m; if (m == 0) { m = 1ull << 63; ++e; } }
+    *mant = m;
+    *exp = e;
+    return true;
+  }
+  // d / 10^k
+  Big den;
+  den.w.push_back(1);
+  for (long k = 0; k < -e10; ++k) den.mul_small(10);
+  int t = 64 + den.bitlen() - d.bitlen();
+  for (int iter = 0; iter < 4; ++iter) {
+    Big num = d;
+    if (t > 0) num.shl(t);
+    Big denx = den;
+    if (t < 0) denx.shl(-t);
+    Big q, r;
+    Big::divmod(num, denx, q, r);
+    int ql = q.bitlen();
+    if (ql > 64) { --t; continue; }
+    if (ql < 64) { ++t; continue; }
+    uint64_t m = q.low64();
+    // round half even: compare 2r with denx
+    r.shl(1);
+    int c = Big::cmp(r, denx);
+    int32_t e = -t;
+    if (c > 0 || (c == 0 && (m & 1))) { ++m; if (m == 0) { m = 1ull << 63; ++e; } }
+    *mant = m;
+    *exp = e;
+    return true;
+  }
+  return false;
+}
+
+bool parse_int64(const char* s, size_t n, int64_t* out) {
+  if (n == 0) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+  if (i >= n) return false;
+  unsigned __int128 v = 0;
+  for (; i < n; ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (s[i] - '0');
+    if (v > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && v > (((unsigned __int128)1 << 63) - 1)) return false;
+  *out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+// Go strconv 'g' shortest formatting (%v of float64): %e when exp < -4 || exp >= 6
+static std::string go_float_v(double f) {
+  if (std::isinf(f)) return f > 0 ? "+Inf" : "-Inf";
+  if (std::isnan(f)) return "NaN";
+  if (f == 0) return std::signbit(f) ? "-0" : "0";
+  char buf[64];
+  auto res = std::to_chars(buf, buf + sizeof(buf), std::fabs(f), std::chars_format::scientific);
+  std::string sci(buf, res.ptr);
+  size_t epos = sci.find('e');
+  std::string mant = sci.substr(0, epos);
+  int ex = atoi(sci.c_str() + epos + 1);
+  std::string digits;
+  for (char c : mant) if (c != '.') digits.push_back(c);
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  int dp = ex + 1;
+  std::string out;
+  if (ex < -4 || ex >= 6) {
+    out = digits.substr(0, 1);
+    if (digits.size() > 1) out += "." + digits.substr(1);
+    out += "e";
+    out += ex < 0 ? "-" : "+";
+    int ae = ex < 0 ? -ex : ex;
+    if (ae < 10) out += "0";
+    out += std::to_string(ae);
+  } else if (dp <= 0) {
+    out = "0." + std::string(-dp, '0') + digits;
+  } else if ((size_t)dp >= digits.size()) {
+    out = digits + std::string(dp - digits.size(), '0');
+  } else {
+    out = digits.substr(0, dp) + "." + digits.substr(dp);
+  }
+  return (f < 0 ? "-" : "") + out;
+}
+
+std::string go_number_print(const char* s, size_t n) {
+  int64_t v;
+  if (parse_int64(s, n, &v)) return std::to_string(v);
+  std::string t(s, n);
+  char* end = nullptr;
+  double f = strtod(t.c_str(), &end);
+  if (end != t.c_str() + t.size()) return t;
+  if (std::isinf(f)) return t;  // Float64() fails -> number text
+  return go_float_v(f);
+}
+
+// ------------------------------------------------------------------ Store
+Store::Store() {
+  table_.assign(1 << 12, 0);
+  num_table_.assign(1 << 10, 0);
+  s_empty = intern("", 0);
+  s_review = intern("review"); s_parameters = intern("parameters"); s_kind = intern("kind");
+  s_group = intern("group"); s_version = intern("version"); s_name = intern("name");
+  s_namespace = intern("namespace"); s_object = intern("object"); s_oldObject = intern("oldObject");
+  s_metadata = intern("metadata"); s_labels = intern("labels"); s_unstable = intern("_unstable");
+  s_msg = intern("msg"); s_details = intern("details"); s_uid = intern("uid"); s_resource = intern("resource");
+  s_operation = intern("operation"); s_userInfo = intern("userInfo"); s_options = intern("options");
+  s_deny = intern("deny"); s_creationTimestamp = intern("creationTimestamp"); s_spec = intern("spec");
+  s_status = intern("status"); s_star = intern("*"); s_In = intern("In"); s_NotIn = intern("NotIn");
+  s_Exists = intern("Exists"); s_DoesNotExist = intern("DoesNotExist"); s_Namespace = intern("Namespace");
+  s_apiGroups = intern("apiGroups"); s_kinds = intern("kinds"); s_true = intern("true");
+  s_false = intern("false"); s_null = intern("null");
+  // node 0 is a permanent empty object ({}), node 1 null, node 2 false, node 3 true
+  Node e{};
+  e.type = NT_OBJ;
+  nodes_.push_back(e);
+  e.type = NT_NULL; nodes_.push_back(e);
+  e.type = NT_FALSE; nodes_.push_back(e);
+  e.type = NT_TRUE; nodes_.push_back(e);
+}
+
+void Store::grow() {
+  std::vector<uint32_t> t(table_.size() * 2, 0);
+  size_t mask = t.size() - 1;
+  for (uint32_t id = 0; id < strs_.size(); ++id) {
+    size_t h = fnv1a(pool_.data() + strs_[id].off, strs_[id].len) & mask;
+    while (t[h]) h = (h + 1) & mask;
+    t[h] = id + 1;
+  }
+  table_.swap(t);
+}
+
+uint32_t Store::find(const char* p, size_t n) const {
+  size_t mask = table_.size() - 1;
+  size_t h = fnv1a(p, n) & mask;
+  while (uint32_t e = table_[h]) {
+    const StrEnt& s = strs_[e - 1];
+    if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return e - 1;
+    h = (h + 1) & mask;
+  }
+  return NO_ID;
+}
+
+uint32_t Store::intern(const char* p, size_t n) {
+  size_t mask = table_.size() - 1;
+  size_t h = fnv1a(p, n) & mask;
+  while (uint32_t e = table_[h]) {
+    const StrEnt& s = strs_[e - 1];
+    if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return e - 1;
+    h = (h + 1) & mask;
+  }
+  uint32_t id = (uint32_t)strs_.size();
+  StrEnt se{(uint32_t)pool_.size(), (uint32_t)n};
+  pool_.append(p, n);
+  strs_.push_back(se);
+  uint8_t fl = SF_ASCII_PRINT;
+  for (size_t i = 0; i < n; ++i) {
+    unsigned char c = (unsigned char)p[i];
+    if (c >= 0x80) { fl |= SF_NON_ASCII; fl &= ~SF_ASCII_PRINT; }
+    else if (c < 0x20 || c == 0x7f) { fl &= ~SF_ASCII_PRINT; }
+    else if (c == '"' || c == '\\') fl |= SF_NEEDS_ESC;
+  }
+  sflags_.push_back(fl);
+  table_[h] = id + 1;
+  if (strs_.size() * 2 > table_.size()) grow();
+  return id;
+}
+
+void Store::grow_num() {
+  std::vector<uint32_t> t(num_table_.size() * 2, 0);
+  size_t mask = t.size() - 1;
+  for (uint32_t id = 0; id < nums_.size(); ++id) {
+    size_t h = (size_t)nums_[id].text * 2654435761u & mask;
+    while (t[h]) h = (h + 1) & mask;
+    t[h] = id + 1;
+  }
+  num_table_.swap(t);
+}
+
+uint32_t Store::number(const char* p, size_t n) {
+  uint32_t text = intern(p, n);
+  size_t mask = num_table_.size() - 1;
+  size_t h = (size_t)text * 2654435761u & mask;
+  while (uint32_t e = num_table_[h]) {
+    if (nums_[e - 1].text == text) return e - 1;
+    h = (h + 1) & mask;
+  }
+  NumEnt ne{};
+  ne.text = text;
+  int64_t iv;
+  if (parse_int64(p, n, &iv)) { ne.i = iv; ne.flags |= NF_INT64; }
+  uint64_t m; int32_t e; bool neg;
+  if (decimal_to_bf64(p, n, &m, &e, &neg)) { ne.mant = m; ne.exp = e; ne.neg = neg; ne.flags |= NF_BF_OK; }
+  std::string pr = go_number_print(p, n);
+  ne.print = intern(pr);
+  ne.flags |= NF_PRINT_OK;
+  uint32_t id = (uint32_t)nums_.size();
+  nums_.push_back(ne);
+  num_table_[h] = id + 1;
+  if (nums_.size() * 2 > num_table_.size()) grow_num();
+  return id;
+}
+
+uint32_t Store::add_node(const Node& n) {
+  nodes_.push_back(n);
+  return (uint32_t)nodes_.size() - 1;
+}
+
+uint32_t Store::reserve(uint32_t n) {
+  uint32_t f = (uint32_t)nodes_.size();
+  nodes_.resize(nodes_.size() + n);
+  return f;
+}
+
+uint32_t Store::add_doc(const JDoc& d, int j) {
+  uint32_t root = (uint32_t)nodes_.size();
+  nodes_.push_back(Node{});
+  std::deque<std::pair<int, uint32_t>> q;
+  q.emplace_back(j, root);
+  while (!q.empty()) {
+    auto [jn, an] = q.front();
+    q.pop_front();
+    const JNode& x = d.nodes[jn];
+    Node& out = nodes_[an];
+    out.type = x.type;
+    switch (x.type) {
+      case NT_STR: out.val = intern(d.buf.data() + x.s_off, x.s_len); break;
+      case NT_NUM: out.val = number(d.buf.data() + x.s_off, x.s_len); break;
+      case NT_ARR:
+      case NT_OBJ: {
+        uint32_t cnt = x.n;
+        if (cnt > 0xffff) { nodes_[an].flags |= 1; cnt = 0xffff; }
+        uint32_t first = (uint32_t)nodes_.size();
+        nodes_.resize(nodes_.size() + cnt);
+        Node& o2 = nodes_[an];
+        o2.first = first;
+        o2.n = (uint16_t)cnt;
+        uint32_t i = 0;
+        for (int c = x.first; c >= 0 && i < cnt; c = d.nodes[c].next, ++i) {
+          nodes_[first + i].key = x.type == NT_OBJ ? intern(d.buf.data() + d.nodes[c].k_off, d.nodes[c].k_len) : i;
+          q.emplace_back(c, first + i);
+        }
+        break;
+      }
+      default: break;
+    }
+  }
+  return root;
+}
+
+}  // namespace gk

@@ -1,0 +1,128 @@
+"""Mirror of the frameworks Client calls that reach the driver.
+
+Follows vendor/github.com/open-policy-agent/frameworks/constraint/pkg/client/client.go
+(AddTemplate :350-395, AddConstraint :535-577, AddData :91-113, Review :763-800,
+Audit :805-833) and the K8s target handler pkg/target/target.go
+(ProcessData :62-89, HandleReview / augmentedUnstructuredToAdmissionRequest
+:91-163).  The template package rewrite stands in for regorewriter's
+AST rewrite (client.go:280-347): the entry module's `package` clause becomes
+`templates["<target>"]["<Kind>"]`.
+"""
+from __future__ import annotations
+
+import json
+import re
+import urllib.parse
+from typing import Optional
+
+TARGET = "admission.k8s.gatekeeper.sh"
+CONSTRAINT_GROUP = "constraints.gatekeeper.sh"
+
+# corev1.Namespace{} marshalled by encoding/json (cluster-scoped objects in audit)
+EMPTY_NAMESPACE = {"metadata": {"creationTimestamp": None}, "spec": {}, "status": {}}
+
+
+def template_kind(template: dict) -> str:
+    return template["spec"]["crd"]["spec"]["names"]["kind"]
+
+
+def template_modules(template: dict):
+    """(prefix, [entry module, libs...]) as createTemplateArtifacts builds them."""
+    kind = template_kind(template)
+    tgt = template["spec"]["targets"][0]
+    src = tgt["rego"]
+    prefix = 'templates["%s"]["%s"]' % (TARGET, kind)
+    src = re.sub(r"^\s*package\s+\S+", "package " + prefix, src, count=1, flags=re.M)
+    return prefix, [src] + list(tgt.get("libs", []))
+
+
+def constraint_path(constraint: dict) -> str:
+    return "/constraints/%s/cluster/%s/%s/%s" % (TARGET, CONSTRAINT_GROUP, constraint["kind"], constraint["metadata"]["name"])
+
+
+def group_version(api_version: str):
+    if "/" not in api_version:
+        return "", api_version
+    parts = api_version.split("/")
+    if len(parts) == 2:
+        return parts[0], parts[1]
+    return "", ""
+
+
+def data_path(obj: dict) -> str:
+    """K8sValidationTarget.ProcessData (target.go:62-76)."""
+    gv = obj.get("apiVersion", "")
+    kind = obj.get("kind", "")
+    name = obj.get("metadata", {}).get("name", "")
+    ns = obj.get("metadata", {}).get("namespace", "")
+    esc = urllib.parse.quote(gv, safe="")
+    if not ns:
+        return "/external/%s/cluster/%s/%s/%s" % (TARGET, esc, kind, name)
+    return "/external/%s/namespace/%s/%s/%s/%s" % (TARGET, ns, esc, kind, name)
+
+
+def augmented_review(obj: dict, ns: Optional[dict]) -> dict:
+    """gkReview JSON for Review(AugmentedUnstructured{obj, ns}) (target.go:129-163):
+    admission/v1beta1 AdmissionRequest field order, omitempty name/namespace."""
+    group, version = group_version(obj.get("apiVersion", "") if isinstance(obj.get("apiVersion"), str) else "")
+    kind = obj.get("kind", "") if isinstance(obj.get("kind"), str) else ""
+    md = obj.get("metadata") if isinstance(obj.get("metadata"), dict) else {}
+    name = md.get("name", "") if isinstance(md.get("name"), str) else ""
+    nsobj = ns if ns is not None else EMPTY_NAMESPACE
+    nsmd = nsobj.get("metadata") if isinstance(nsobj.get("metadata"), dict) else {}
+    nsname = nsmd.get("name", "") if isinstance(nsmd.get("name"), str) else ""
+    r = {"uid": "", "kind": {"group": group, "version": version, "kind": kind},
+         "resource": {"group": "", "version": "", "resource": ""}}
+    if name:
+        r["name"] = name
+    if nsname:
+        r["namespace"] = nsname
+    r.update({"operation": "", "userInfo": {}, "object": obj, "oldObject": None, "options": None,
+              "_unstable": {"namespace": nsobj}})
+    return r
+
+
+class Client:
+    """The driver-facing half of frameworks client.Client for the K8s target."""
+
+    def __init__(self, driver):
+        self.driver = driver
+        # Client.init (client.go:667-722): target hooks + match library modules.
+        # The engine serves both natively; their packages are what it keys on.
+        driver.put_module('hooks["%s"].hooks_builtin' % TARGET, 'package hooks["%s"]\n' % TARGET)
+        driver.put_module('hooks["%s"].library' % TARGET, 'package hooks["%s"].library\n' % TARGET)
+        driver.init()
+
+    def add_template(self, template: dict):
+        prefix, mods = template_modules(template)
+        self.driver.put_modules(prefix, mods)
+        return template_kind(template)
+
+    def remove_template(self, template: dict):
+        prefix, _ = template_modules(template)
+        return self.driver.delete_modules(prefix)
+
+    def add_constraint(self, constraint: dict):
+        self.driver.put_data(constraint_path(constraint), constraint)
+
+    def remove_constraint(self, constraint: dict):
+        return self.driver.delete_data(constraint_path(constraint))
+
+    def add_data(self, obj: dict):
+        self.driver.put_data(data_path(obj), obj)
+
+    def remove_data(self, obj: dict):
+        return self.driver.delete_data(data_path(obj))
+
+    def review(self, review: dict):
+        return self.driver.query('hooks["%s"].violation' % TARGET, {"review": review})
+
+    def review_objects(self, objs, namespaces):
+        return self.driver.review_objects(objs, namespaces)
+
+    def audit(self):
+        return self.driver.query('hooks["%s"].audit' % TARGET, None)
+
+    def reset(self):
+        self.driver.delete_data("/external/%s" % TARGET)
+        self.driver.delete_data("/constraints/%s" % TARGET)

@@ -1,0 +1,325 @@
+"""ctypes binding of the gkgpu C ABI (include/gkgpu.h).
+
+Each method cites the drivers.Driver method it implements
+(vendor/github.com/open-policy-agent/frameworks/constraint/pkg/client/drivers/interface.go).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+GK_REVIEW_ERROR = 1
+GK_REVIEW_FALLBACK = 2
+
+TARGET = "admission.k8s.gatekeeper.sh"
+
+EXPORTS = [
+    "gk_engine_create", "gk_engine_destroy", "gk_last_error", "gk_device_available", "gk_init", "gk_put_module",
+    "gk_put_modules", "gk_delete_module", "gk_delete_modules", "gk_put_data", "gk_delete_data", "gk_query", "gk_dump",
+    "gk_free_string", "gk_query_batch", "gk_review_objects", "gk_batch_stage_objects", "gk_batch_eval",
+    "gk_batch_free", "gk_batch_device_bytes", "gk_results_count", "gk_results_get", "gk_results_reviews",
+    "gk_results_review_status", "gk_results_review_reason", "gk_results_constraints", "gk_results_constraint_total",
+    "gk_results_timing", "gk_results_free", "gk_template_status", "gk_constraint_count", "gk_constraint_info",
+]
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class QueryError(RuntimeError):
+    pass
+
+
+class _View(C.Structure):
+    _fields_ = [
+        ("review", C.c_uint32), ("constraint", C.c_uint32), ("constraint_kind", C.c_char_p),
+        ("constraint_name", C.c_char_p), ("msg", C.c_void_p), ("msg_len", C.c_size_t),
+        ("details_json", C.c_void_p), ("details_len", C.c_size_t), ("enforcement_action", C.c_char_p),
+    ]
+
+
+def lib_path() -> str:
+    return os.environ.get("GKGPU_LIB", os.path.join(_HERE, "libgkgpu.so"))
+
+
+def load_library():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    p = lib_path()
+    if not os.path.exists(p):
+        raise EngineUnavailable("libgkgpu.so not built (%s); run __graft_entry__.build()" % p)
+    lib = C.CDLL(p)
+    vp = C.c_void_p
+    sz = C.c_size_t
+    cp = C.c_char_p
+    ppc = C.POINTER(C.c_char_p)
+    psz = C.POINTER(C.c_size_t)
+    lib.gk_engine_create.argtypes = [cp, C.POINTER(vp)]
+    lib.gk_engine_destroy.argtypes = [vp]
+    lib.gk_last_error.argtypes = [vp]
+    lib.gk_last_error.restype = cp
+    lib.gk_device_available.restype = C.c_int
+    lib.gk_init.argtypes = [vp]
+    lib.gk_put_module.argtypes = [vp, cp, cp, sz]
+    lib.gk_put_modules.argtypes = [vp, cp, ppc, psz, sz]
+    lib.gk_delete_module.argtypes = [vp, cp, C.POINTER(C.c_int)]
+    lib.gk_delete_modules.argtypes = [vp, cp, C.POINTER(C.c_int)]
+    lib.gk_put_data.argtypes = [vp, cp, cp, sz]
+    lib.gk_delete_data.argtypes = [vp, cp, C.POINTER(C.c_int)]
+    lib.gk_query.argtypes = [vp, cp, cp, sz, C.POINTER(vp)]
+    lib.gk_dump.argtypes = [vp, C.POINTER(vp)]
+    lib.gk_free_string.argtypes = [vp]
+    lib.gk_query_batch.argtypes = [vp, ppc, psz, sz, C.POINTER(vp)]
+    lib.gk_review_objects.argtypes = [vp, ppc, psz, ppc, psz, sz, C.POINTER(vp)]
+    lib.gk_batch_stage_objects.argtypes = [vp, ppc, psz, ppc, psz, sz, C.POINTER(vp)]
+    lib.gk_batch_eval.argtypes = [vp, vp, C.c_int, C.POINTER(vp)]
+    lib.gk_batch_free.argtypes = [vp]
+    lib.gk_batch_device_bytes.argtypes = [vp]
+    lib.gk_batch_device_bytes.restype = C.c_uint64
+    lib.gk_results_count.argtypes = [vp]
+    lib.gk_results_count.restype = sz
+    lib.gk_results_get.argtypes = [vp, sz, C.POINTER(_View)]
+    lib.gk_results_reviews.argtypes = [vp]
+    lib.gk_results_reviews.restype = sz
+    lib.gk_results_review_status.argtypes = [vp, sz]
+    lib.gk_results_review_status.restype = C.c_uint32
+    lib.gk_results_review_reason.argtypes = [vp, sz]
+    lib.gk_results_review_reason.restype = C.c_uint32
+    lib.gk_results_constraints.argtypes = [vp]
+    lib.gk_results_constraints.restype = sz
+    lib.gk_results_constraint_total.argtypes = [vp, sz]
+    lib.gk_results_constraint_total.restype = C.c_uint64
+    lib.gk_results_timing.argtypes = [vp, C.POINTER(C.c_double)]
+    lib.gk_results_free.argtypes = [vp]
+    lib.gk_template_status.argtypes = [vp, cp, C.POINTER(cp)]
+    lib.gk_template_status.restype = C.c_int
+    lib.gk_constraint_count.argtypes = [vp]
+    lib.gk_constraint_count.restype = sz
+    lib.gk_constraint_info.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(cp)]
+    _LIB = lib
+    return lib
+
+
+def _b(s) -> bytes:
+    return s.encode("utf-8", "surrogateescape") if isinstance(s, str) else s
+
+
+@dataclass
+class Result:
+    """One types.Result (vendor/.../frameworks/constraint/pkg/types/validation.go:11-29)."""
+    review: int
+    constraint: int
+    constraint_kind: str
+    constraint_name: str
+    msg: str
+    details_json: str
+    enforcement_action: str
+
+
+@dataclass
+class Results:
+    results: List[Result]
+    status: List[int]          # per review: GK_REVIEW_ERROR / GK_REVIEW_FALLBACK bits
+    reason: List[int]
+    totals: List[int]          # per constraint (device counters)
+    timing_ms: List[float] = field(default_factory=list)  # flatten, upload, kernel, download, decode
+
+    def for_review(self, i):
+        return [r for r in self.results if r.review == i]
+
+
+def _collect(lib, h, decode=True) -> Results:
+    try:
+        n = lib.gk_results_count(h)
+        out = []
+        v = _View()
+        for i in range(n):
+            lib.gk_results_get(h, i, C.byref(v))
+            msg = C.string_at(v.msg, v.msg_len).decode("utf-8", "surrogateescape") if v.msg_len else ""
+            det = C.string_at(v.details_json, v.details_len).decode("utf-8", "surrogateescape") if v.details_len else ""
+            out.append(Result(v.review, v.constraint, v.constraint_kind.decode(), v.constraint_name.decode(), msg, det,
+                              v.enforcement_action.decode()))
+        nr = lib.gk_results_reviews(h)
+        status = [lib.gk_results_review_status(h, i) for i in range(nr)]
+        reason = [lib.gk_results_review_reason(h, i) for i in range(nr)]
+        nc = lib.gk_results_constraints(h)
+        totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
+        t = (C.c_double * 5)()
+        lib.gk_results_timing(h, t)
+        return Results(out, status, reason, totals, list(t))
+    finally:
+        lib.gk_results_free(h)
+
+
+def _arr(strings: Sequence):
+    bs = [_b(s) if s is not None else None for s in strings]
+    arr = (C.c_char_p * len(bs))(*bs)
+    lens = (C.c_size_t * len(bs))(*[len(x) if x is not None else 0 for x in bs])
+    return arr, lens, bs
+
+
+class Batch:
+    """A device-resident set of reviews (gk_batch_*)."""
+
+    def __init__(self, drv, handle, n):
+        self._drv = drv
+        self._h = handle
+        self.n = n
+
+    def eval(self, decode=True) -> Results:
+        lib = self._drv._lib
+        out = C.c_void_p()
+        rc = lib.gk_batch_eval(self._drv._e, self._h, 1 if decode else 0, C.byref(out))
+        self._drv._check(rc)
+        return _collect(lib, out)
+
+    def device_bytes(self) -> int:
+        return self._drv._lib.gk_batch_device_bytes(self._h)
+
+    def free(self):
+        if self._h:
+            self._drv._lib.gk_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Driver:
+    """drivers.Driver over libgkgpu (interface.go:21-39)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        e = C.c_void_p()
+        rc = self._lib.gk_engine_create(_b(json.dumps({"device": device})), C.byref(e))
+        if rc != 0:
+            raise EngineUnavailable("gk_engine_create failed (%d)" % rc)
+        self._e = e
+
+    def close(self):
+        if self._e:
+            self._lib.gk_engine_destroy(self._e)
+            self._e = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            msg = self._lib.gk_last_error(self._e).decode("utf-8", "replace")
+            if rc == 4:
+                raise EngineUnavailable(msg)
+            if rc == 3:
+                raise QueryError(msg)
+            raise RuntimeError("gkgpu error %d: %s" % (rc, msg))
+
+    @staticmethod
+    def device_available() -> bool:
+        return bool(load_library().gk_device_available())
+
+    # -- Driver.Init (interface.go:22)
+    def init(self):
+        self._check(self._lib.gk_init(self._e))
+
+    # -- Driver.PutModule (interface.go:24)
+    def put_module(self, name: str, src: str):
+        s = _b(src)
+        self._check(self._lib.gk_put_module(self._e, _b(name), s, len(s)))
+
+    # -- Driver.PutModules (interface.go:26)
+    def put_modules(self, prefix: str, srcs: Sequence[str]):
+        arr, lens, _keep = _arr(srcs)
+        self._check(self._lib.gk_put_modules(self._e, _b(prefix), arr, lens, len(srcs)))
+
+    # -- Driver.DeleteModule (interface.go:28)
+    def delete_module(self, name: str) -> bool:
+        d = C.c_int()
+        self._check(self._lib.gk_delete_module(self._e, _b(name), C.byref(d)))
+        return bool(d.value)
+
+    # -- Driver.DeleteModules (interface.go:30)
+    def delete_modules(self, prefix: str) -> int:
+        d = C.c_int()
+        self._check(self._lib.gk_delete_modules(self._e, _b(prefix), C.byref(d)))
+        return d.value
+
+    # -- Driver.PutData (interface.go:32)
+    def put_data(self, path: str, data):
+        js = _b(data if isinstance(data, str) else json.dumps(data))
+        self._check(self._lib.gk_put_data(self._e, _b(path), js, len(js)))
+
+    # -- Driver.DeleteData (interface.go:34)
+    def delete_data(self, path: str) -> bool:
+        d = C.c_int()
+        self._check(self._lib.gk_delete_data(self._e, _b(path), C.byref(d)))
+        return bool(d.value)
+
+    # -- Driver.Query (interface.go:36)
+    def query(self, path: str, input_val=None) -> Results:
+        js = _b(input_val if isinstance(input_val, str) else json.dumps(input_val))
+        out = C.c_void_p()
+        self._check(self._lib.gk_query(self._e, _b(path), js, len(js), C.byref(out)))
+        return _collect(self._lib, out)
+
+    # -- Driver.Dump (interface.go:38)
+    def dump(self) -> str:
+        p = C.c_void_p()
+        self._check(self._lib.gk_dump(self._e, C.byref(p)))
+        s = C.string_at(p).decode()
+        self._lib.gk_free_string(p)
+        return s
+
+    # -- batch extensions
+    def query_batch(self, inputs: Sequence) -> Results:
+        strs = [x if isinstance(x, str) else json.dumps(x) for x in inputs]
+        arr, lens, _keep = _arr(strs)
+        out = C.c_void_p()
+        self._check(self._lib.gk_query_batch(self._e, arr, lens, len(strs), C.byref(out)))
+        return _collect(self._lib, out)
+
+    def review_objects(self, objs: Sequence, namespaces: Sequence) -> Results:
+        o = [x if isinstance(x, str) else json.dumps(x) for x in objs]
+        n = [None if x is None else (x if isinstance(x, str) else json.dumps(x)) for x in namespaces]
+        oa, ol, _k1 = _arr(o)
+        na, nl, _k2 = _arr(n)
+        out = C.c_void_p()
+        self._check(self._lib.gk_review_objects(self._e, oa, ol, na, nl, len(o), C.byref(out)))
+        return _collect(self._lib, out)
+
+    def stage_objects(self, objs: Sequence, namespaces: Sequence) -> Batch:
+        o = [x if isinstance(x, str) else json.dumps(x) for x in objs]
+        n = [None if x is None else (x if isinstance(x, str) else json.dumps(x)) for x in namespaces]
+        oa, ol, _k1 = _arr(o)
+        na, nl, _k2 = _arr(n)
+        out = C.c_void_p()
+        self._check(self._lib.gk_batch_stage_objects(self._e, oa, ol, na, nl, len(o), C.byref(out)))
+        return Batch(self, out, len(o))
+
+    # -- introspection
+    def template_status(self, kind: str):
+        r = C.c_char_p()
+        st = self._lib.gk_template_status(self._e, _b(kind), C.byref(r))
+        return st, (r.value.decode() if r.value else "")
+
+    def constraints(self):
+        n = self._lib.gk_constraint_count(self._e)
+        out = []
+        for i in range(n):
+            k, nm = C.c_char_p(), C.c_char_p()
+            self._lib.gk_constraint_info(self._e, i, C.byref(k), C.byref(nm))
+            out.append((k.value.decode(), nm.value.decode()))
+        return out

@@ -1,0 +1,449 @@
+"""BASELINE workloads: ConstraintTemplates, Constraints and seeded synthetic resources.
+
+Templates are the demo policies BASELINE.json names, written out here in the
+form the driver receives them (OPA-formatted module text; client.go:332-339
+re-prints sources with format.Ast), so tests and the bench run where the
+reference tree is absent:
+
+* K8sRequiredLabels (basic)   — demo/basic/templates/k8srequiredlabels_template.yaml
+* K8sRequiredLabels (regex)   — demo/agilebank/templates/k8srequiredlabels_template.yaml
+* K8sAllowedRepos             — demo/agilebank/templates/k8sallowedrepos_template.yaml
+* K8sContainerLimits          — demo/agilebank/templates/k8scontainterlimits_template.yaml
+* K8sRequiredProbes           — demo/agilebank/templates/k8srequiredprobes_template.yaml
+* K8sAllowedLabelRegex / K8sAllowedAnnotationRegex — build-authored allowedRegex
+  variants for config 3, same Rego subset.
+
+Generators follow SURVEY 8(d)'s synthetic-input spec with the seeds given there.
+"""
+from __future__ import annotations
+
+import json
+import random
+
+TARGET = "admission.k8s.gatekeeper.sh"
+
+
+def _tmpl(kind, rego, schema=None):
+    return {
+        "apiVersion": "templates.gatekeeper.sh/v1beta1",
+        "kind": "ConstraintTemplate",
+        "metadata": {"name": kind.lower()},
+        "spec": {"crd": {"spec": {"names": {"kind": kind}, "validation": {"openAPIV3Schema": schema or {}}}},
+                 "targets": [{"target": TARGET, "rego": rego}]},
+    }
+
+
+REQUIRED_LABELS_BASIC = _tmpl("K8sRequiredLabels", """package k8srequiredlabels
+
+violation[{"msg": msg, "details": {"missing_labels": missing}}] {
+	provided := {label | input.review.object.metadata.labels[label]}
+	required := {label | label := input.parameters.labels[_]}
+	missing := required - provided
+	count(missing) > 0
+	msg := sprintf("you must provide labels: %v", [missing])
+}
+""")
+
+REQUIRED_LABELS = _tmpl("K8sRequiredLabels", """package k8srequiredlabels
+
+get_message(parameters, _default) = msg {
+	not parameters.message
+	msg := _default
+}
+
+get_message(parameters, _default) = msg {
+	msg := parameters.message
+}
+
+violation[{"msg": msg, "details": {"missing_labels": missing}}] {
+	provided := {label | input.review.object.metadata.labels[label]}
+	required := {label | label := input.parameters.labels[_].key}
+	missing := required - provided
+	count(missing) > 0
+	def_msg := sprintf("you must provide labels: %v", [missing])
+	msg := get_message(input.parameters, def_msg)
+}
+
+violation[{"msg": msg}] {
+	value := input.review.object.metadata.labels[key]
+	expected := input.parameters.labels[_]
+	expected.key == key
+
+	# do not match if allowedRegex is not defined, or is an empty string
+	expected.allowedRegex != ""
+	not re_match(expected.allowedRegex, value)
+	def_msg := sprintf("Label <%v: %v> does not satisfy allowed regex: %v", [key, value, expected.allowedRegex])
+	msg := get_message(input.parameters, def_msg)
+}
+""")
+
+ALLOWED_REPOS = _tmpl("K8sAllowedRepos", """package k8sallowedrepos
+
+violation[{"msg": msg}] {
+	container := input.review.object.spec.containers[_]
+	satisfied := [good | repo = input.parameters.repos[_]; good = startswith(container.image, repo)]
+	not any(satisfied)
+	msg := sprintf("container <%v> has an invalid image repo <%v>, allowed repos are %v", [container.name, container.image, input.parameters.repos])
+}
+
+violation[{"msg": msg}] {
+	container := input.review.object.spec.initContainers[_]
+	satisfied := [good | repo = input.parameters.repos[_]; good = startswith(container.image, repo)]
+	not any(satisfied)
+	msg := sprintf("container <%v> has an invalid image repo <%v>, allowed repos are %v", [container.name, container.image, input.parameters.repos])
+}
+""")
+
+_MEM = [("E", "1000000000000000000000"), ("P", "1000000000000000000"), ("T", "1000000000000000"),
+        ("G", "1000000000000"), ("M", "1000000000"), ("k", "1000000"), ("", "1000"), ("m", "1"),
+        ("Ki", "1024000"), ("Mi", "1048576000"), ("Gi", "1073741824000"), ("Ti", "1099511627776000"),
+        ("Pi", "1125899906842624000"), ("Ei", "1152921504606846976000")]
+
+CONTAINER_LIMITS = _tmpl("K8sContainerLimits", """package k8scontainerlimits
+
+missing(obj, field) = true {
+	not obj[field]
+}
+
+missing(obj, field) = true {
+	obj[field] == ""
+}
+
+canonify_cpu(orig) = new {
+	is_number(orig)
+	new := orig * 1000
+}
+
+canonify_cpu(orig) = new {
+	not is_number(orig)
+	endswith(orig, "m")
+	new := to_number(replace(orig, "m", ""))
+}
+
+canonify_cpu(orig) = new {
+	not is_number(orig)
+	not endswith(orig, "m")
+	re_match("^[0-9]+$", orig)
+	new := to_number(orig) * 1000
+}
+""" + "".join('\nmem_multiple("%s") = %s {\n\ttrue\n}\n' % (s, v) for s, v in _MEM) + """
+get_suffix(mem) = suffix {
+	not is_string(mem)
+	suffix := ""
+}
+
+get_suffix(mem) = suffix {
+	is_string(mem)
+	count(mem) > 0
+	suffix := substring(mem, count(mem) - 1, -1)
+	mem_multiple(suffix)
+}
+
+get_suffix(mem) = suffix {
+	is_string(mem)
+	count(mem) > 1
+	suffix := substring(mem, count(mem) - 2, -1)
+	mem_multiple(suffix)
+}
+
+get_suffix(mem) = suffix {
+	is_string(mem)
+	count(mem) > 1
+	not mem_multiple(substring(mem, count(mem) - 1, -1))
+	not mem_multiple(substring(mem, count(mem) - 2, -1))
+	suffix := ""
+}
+
+get_suffix(mem) = suffix {
+	is_string(mem)
+	count(mem) == 1
+	not mem_multiple(substring(mem, count(mem) - 1, -1))
+	suffix := ""
+}
+
+get_suffix(mem) = suffix {
+	is_string(mem)
+	count(mem) == 0
+	suffix := ""
+}
+
+canonify_mem(orig) = new {
+	is_number(orig)
+	new := orig * 1000
+}
+
+canonify_mem(orig) = new {
+	not is_number(orig)
+	suffix := get_suffix(orig)
+	raw := replace(orig, suffix, "")
+	re_match("^[0-9]+$", raw)
+	new := to_number(raw) * mem_multiple(suffix)
+}
+
+violation[{"msg": msg}] {
+	general_violation[{"msg": msg, "field": "containers"}]
+}
+
+violation[{"msg": msg}] {
+	general_violation[{"msg": msg, "field": "initContainers"}]
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	cpu_orig := container.resources.limits.cpu
+	not canonify_cpu(cpu_orig)
+	msg := sprintf("container <%v> cpu limit <%v> could not be parsed", [container.name, cpu_orig])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	mem_orig := container.resources.limits.memory
+	not canonify_mem(mem_orig)
+	msg := sprintf("container <%v> memory limit <%v> could not be parsed", [container.name, mem_orig])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	not container.resources
+	msg := sprintf("container <%v> has no resource limits", [container.name])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	not container.resources.limits
+	msg := sprintf("container <%v> has no resource limits", [container.name])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	missing(container.resources.limits, "cpu")
+	msg := sprintf("container <%v> has no cpu limit", [container.name])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	missing(container.resources.limits, "memory")
+	msg := sprintf("container <%v> has no memory limit", [container.name])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	cpu_orig := container.resources.limits.cpu
+	cpu := canonify_cpu(cpu_orig)
+	max_cpu_orig := input.parameters.cpu
+	max_cpu := canonify_cpu(max_cpu_orig)
+	cpu > max_cpu
+	msg := sprintf("container <%v> cpu limit <%v> is higher than the maximum allowed of <%v>", [container.name, cpu_orig, max_cpu_orig])
+}
+
+general_violation[{"msg": msg, "field": field}] {
+	container := input.review.object.spec[field][_]
+	mem_orig := container.resources.limits.memory
+	mem := canonify_mem(mem_orig)
+	max_mem_orig := input.parameters.memory
+	max_mem := canonify_mem(max_mem_orig)
+	mem > max_mem
+	msg := sprintf("container <%v> memory limit <%v> is higher than the maximum allowed of <%v>", [container.name, mem_orig, max_mem_orig])
+}
+""")
+
+REQUIRED_PROBES = _tmpl("K8sRequiredProbes", """package k8srequiredprobes
+
+probe_type_set = probe_types {
+	probe_types := {type | type := input.parameters.probeTypes[_]}
+}
+
+violation[{"msg": msg}] {
+	container := input.review.object.spec.containers[_]
+	probe := input.parameters.probes[_]
+	probe_is_missing(container, probe)
+	msg := get_violation_message(container, input.review, probe)
+}
+
+probe_is_missing(ctr, probe) = true {
+	not ctr[probe]
+}
+
+probe_is_missing(ctr, probe) = true {
+	probe_field_empty(ctr, probe)
+}
+
+probe_field_empty(ctr, probe) = true {
+	probe_fields := {field | ctr[probe][field]}
+	diff_fields := probe_type_set - probe_fields
+	count(diff_fields) == count(probe_type_set)
+}
+
+get_violation_message(container, review, probe) = msg {
+	msg := sprintf("Container <%v> in your <%v> <%v> has no <%v>", [container.name, review.kind.kind, review.object.metadata.name, probe])
+}
+""")
+
+ALLOWED_LABEL_REGEX = _tmpl("K8sAllowedLabelRegex", """package k8sallowedlabelregex
+
+violation[{"msg": msg, "details": {"label": key}}] {
+	value := input.review.object.metadata.labels[key]
+	rule := input.parameters.rules[_]
+	rule.key == key
+	not re_match(rule.allowedRegex, value)
+	msg := sprintf("label <%v: %v> does not match allowed regex %v", [key, value, rule.allowedRegex])
+}
+""")
+
+ALLOWED_ANNOTATION_REGEX = _tmpl("K8sAllowedAnnotationRegex", """package k8sallowedannotationregex
+
+violation[{"msg": msg, "details": {"annotation": key}}] {
+	value := input.review.object.metadata.annotations[key]
+	rule := input.parameters.rules[_]
+	rule.key == key
+	not re_match(rule.allowedRegex, value)
+	msg := sprintf("annotation <%v: %v> does not match allowed regex %v", [key, value, rule.allowedRegex])
+}
+""")
+
+
+def constraint(kind, name, match=None, parameters=None, enforcement_action=None):
+    spec = {}
+    if match is not None:
+        spec["match"] = match
+    if parameters is not None:
+        spec["parameters"] = parameters
+    if enforcement_action is not None:
+        spec["enforcementAction"] = enforcement_action
+    c = {"apiVersion": "constraints.gatekeeper.sh/v1beta1", "kind": kind, "metadata": {"name": name}}
+    if spec:
+        c["spec"] = spec
+    return c
+
+
+# -- config 1: demo/basic all_ns_must_have_gatekeeper.yaml over namespaces
+def config1():
+    templates = [REQUIRED_LABELS_BASIC]
+    constraints = [constraint("K8sRequiredLabels", "ns-must-have-gk",
+                              match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
+                              parameters={"labels": ["gatekeeper"]})]
+    return templates, constraints
+
+
+# -- config 2: demo/agilebank constraints over Pods
+def config2():
+    templates = [REQUIRED_LABELS, ALLOWED_REPOS, CONTAINER_LIMITS, REQUIRED_PROBES]
+    constraints = [
+        constraint("K8sRequiredLabels", "all-must-have-owner",
+                   match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
+                   parameters={"message": "All namespaces must have an `owner` label that points to your company username",
+                               "labels": [{"key": "owner", "allowedRegex": "^[a-zA-Z]+.agilebank.demo$"}]}),
+        constraint("K8sAllowedRepos", "prod-repo-is-openpolicyagent",
+                   match={"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}], "namespaces": ["production"]},
+                   parameters={"repos": ["openpolicyagent"]}),
+        constraint("K8sContainerLimits", "container-must-have-limits",
+                   match={"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}]},
+                   parameters={"cpu": "200m", "memory": "1Gi"}),
+        constraint("K8sRequiredProbes", "must-have-probes",
+                   match={"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}]},
+                   parameters={"probes": ["readinessProbe", "livenessProbe"], "probeTypes": ["tcpSocket", "httpGet", "exec"]}),
+    ]
+    return templates, constraints
+
+
+_ALNUM = "abcdefghijklmnopqrstuvwxyz0123456789"
+
+
+def _word(rng, lo=1, hi=16, alphabet=_ALNUM + "-"):
+    n = rng.randint(lo, hi)
+    s = "".join(rng.choice(alphabet) for _ in range(n))
+    return s
+
+
+def namespace_obj(name, labels=None):
+    md = {"name": name, "creationTimestamp": None}
+    if labels:
+        md["labels"] = labels
+    return {"apiVersion": "v1", "kind": "Namespace", "metadata": md, "spec": {"finalizers": ["kubernetes"]},
+            "status": {"phase": "Active"}}
+
+
+def gen_namespaces(n, seed=1):
+    """Config 1: `ns-%05d`, P(gatekeeper label)=0.5, plus 0-3 labels from a 64-key vocabulary."""
+    rng = random.Random(seed)
+    vocab = ["k%02d-%s" % (i, _word(rng, 3, 8, _ALNUM)) for i in range(64)]
+    out = []
+    for i in range(n):
+        labels = {}
+        if rng.random() < 0.5:
+            labels["gatekeeper"] = _word(rng, 1, 16)
+        for _ in range(rng.randint(0, 3)):
+            labels[rng.choice(vocab)] = _word(rng, 1, 16)
+        if rng.random() < 0.3:
+            labels["owner"] = rng.choice(["alice.agilebank.demo", "bob", "x.agilebank.demo", "Carol1.agilebank.demo"])
+        out.append(namespace_obj("ns-%05d" % i, labels or None))
+    return out
+
+
+_CPU = ["100m", "200m", "300m", "1", "0.5", "2000m", None]
+_MEMV = ["30Mi", "1Gi", "4000Mi", "2G", "512Ki", None]
+
+
+def gen_pods(n, seed=42, n_namespaces=1000):
+    """Config 2: Pods over 1,000 namespaces (10% named `production`), 1-4 containers +
+    0-1 initContainers, images from {openpolicyagent/opa 60%, gcr.io/x/opa 20%, nginx 20%},
+    cpu/memory limits from SURVEY 8(d)'s value sets, probes P=0.5, `owner` label P=0.7."""
+    rng = random.Random(seed)
+    nss = []
+    for i in range(n_namespaces):
+        name = "production" if i < n_namespaces // 10 else "team-%04d" % i
+        if name == "production" and i > 0:
+            name = "production-%03d" % i
+        nss.append(name)
+    # 10% of namespaces are "production": only one literal name can equal it, so
+    # route 10% of pods there explicitly
+    objs, ns_of = [], []
+    ns_objs = {}
+    for i in range(n):
+        ns = "production" if rng.random() < 0.10 else rng.choice(nss[n_namespaces // 10:] or ["default"])
+        conts = []
+        for c in range(rng.randint(1, 4)):
+            conts.append(_container(rng, "c%d" % c))
+        pod_spec = {"containers": conts}
+        if rng.random() < 0.5:
+            pod_spec["initContainers"] = [_container(rng, "init")]
+        labels = {"app": "app-%d" % rng.randint(0, 99)}
+        if rng.random() < 0.7:
+            labels["owner"] = rng.choice(["alice", "bob.agilebank.demo"])
+        obj = {"apiVersion": "v1", "kind": "Pod",
+               "metadata": {"name": "pod-%07d" % i, "namespace": ns, "labels": labels}, "spec": pod_spec}
+        objs.append(obj)
+        if ns not in ns_objs:
+            ns_objs[ns] = namespace_obj(ns, {"env": "prod" if ns == "production" else "dev"})
+        ns_of.append(ns)
+    return objs, ns_of, ns_objs
+
+
+def _container(rng, name):
+    r = rng.random()
+    tag = "0.%d.%d" % (rng.randint(1, 30), rng.randint(0, 9))
+    if r < 0.6:
+        image = "openpolicyagent/opa:" + tag
+    elif r < 0.8:
+        image = "gcr.io/x/opa:" + tag
+    else:
+        image = "nginx"
+    c = {"name": name, "image": image}
+    cpu = rng.choice(_CPU)
+    mem = rng.choice(_MEMV)
+    if cpu is not None or mem is not None or rng.random() < 0.5:
+        lim = {}
+        if cpu is not None:
+            lim["cpu"] = cpu
+        if mem is not None:
+            lim["memory"] = mem
+        c["resources"] = {"limits": lim}
+    for probe in ("readinessProbe", "livenessProbe"):
+        if rng.random() < 0.5:
+            kind = rng.choice(["tcpSocket", "httpGet", "exec", "other"])
+            c[probe] = {kind: {"port": 8080}} if kind != "other" else {"initialDelaySeconds": 3}
+    return c
+
+
+def dumps(x) -> str:
+    return json.dumps(x, separators=(",", ":"))

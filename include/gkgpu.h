@@ -1,0 +1,136 @@
+/*
+ * gkgpu — MI355X batch policy-evaluation engine for Gatekeeper's audit sweep.
+ *
+ * C ABI of libgkgpu.so.  The first block mirrors the constraint framework's
+ * plugin boundary one-for-one, so a cgo shim can implement drivers.Driver on
+ * top of it:
+ *
+ *   vendor/github.com/open-policy-agent/frameworks/constraint/pkg/client/
+ *     drivers/interface.go:21-39   type Driver interface { Init; PutModule;
+ *     PutModules; DeleteModule; DeleteModules; PutData; DeleteData; Query; Dump }
+ *
+ * replacing the local OPA driver selected at main.go:223-229
+ * (local.New(local.Tracing(false))).  The second block adds the batch entry
+ * points the audit loop (pkg/audit/manager.go:333-398) and the webhook
+ * micro-batch use.  Ownership: every input buffer is borrowed for the
+ * duration of the call only (the engine copies/flattens it); results are
+ * engine-allocated and released with gk_results_free.  Every function
+ * returns 0 on success or a GK_E* code; gk_last_error() holds the message.
+ * Calls on one engine are serialized internally (mutations vs evaluation).
+ */
+#ifndef GKGPU_H
+#define GKGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GK_OK 0
+#define GK_EINVAL 1      /* bad argument / malformed JSON / bad path        */
+#define GK_EPARSE 2      /* Rego parse / compile error (PutModule(s))      */
+#define GK_EQUERY 3      /* unsupported query path                          */
+#define GK_EDEVICE 4     /* HIP runtime failure / no MI355X visible         */
+#define GK_ENOTFOUND 5
+
+/* per-review status in gk_results (bit set) */
+#define GK_REVIEW_ERROR 1u     /* reference Query would return an error    */
+#define GK_REVIEW_FALLBACK 2u  /* route this review to the CPU OPA driver  */
+
+typedef struct gk_engine gk_engine;
+typedef struct gk_results gk_results;
+typedef struct gk_batch gk_batch;
+
+/* opts_json: {"device": 0, "max_violations": N} (may be NULL) */
+int gk_engine_create(const char* opts_json, gk_engine** out);
+void gk_engine_destroy(gk_engine* e);
+const char* gk_last_error(gk_engine* e);
+/* 1 if a HIP device is usable by this engine */
+int gk_device_available(void);
+
+/* ---- drivers.Driver (interface.go:21-39) -------------------------------- */
+/* Driver.Init — interface.go:22 */
+int gk_init(gk_engine* e);
+/* Driver.PutModule(ctx, name, src string) error — interface.go:24; the hooks
+ * and target-library modules (client.go:667-722) are recognized and served
+ * natively; template modules compile to GPU bytecode or are marked FALLBACK. */
+int gk_put_module(gk_engine* e, const char* name, const char* src, size_t len);
+/* Driver.PutModules(ctx, namePrefix string, srcs []string) error — interface.go:26 */
+int gk_put_modules(gk_engine* e, const char* prefix, const char* const* srcs, const size_t* lens, size_t n);
+/* Driver.DeleteModule(ctx, name) (bool, error) — interface.go:28 */
+int gk_delete_module(gk_engine* e, const char* name, int* deleted);
+/* Driver.DeleteModules(ctx, namePrefix) (int, error) — interface.go:30 */
+int gk_delete_modules(gk_engine* e, const char* prefix, int* count);
+/* Driver.PutData(ctx, path string, data interface{}) error — interface.go:32;
+ * data passed as JSON text (constraints under /constraints/<target>/...,
+ * synced inventory under /external/<target>/...; client.go:79-113, 498-510) */
+int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len);
+/* Driver.DeleteData(ctx, path) (bool, error) — interface.go:34 */
+int gk_delete_data(gk_engine* e, const char* path, int* deleted);
+/* Driver.Query(ctx, path, input, opts...) (*types.Response, error) —
+ * interface.go:36.  path: `hooks["admission.k8s.gatekeeper.sh"].violation`
+ * (input = {"review": ...}) or `hooks["admission.k8s.gatekeeper.sh"].audit`
+ * (input ignored).  Results carry (review index, constraint, msg, details,
+ * enforcementAction) per types.Result (types/validation.go:11-29). */
+int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len, gk_results** out);
+/* Driver.Dump(ctx) (string, error) — interface.go:38; caller frees with gk_free_string */
+int gk_dump(gk_engine* e, char** out);
+void gk_free_string(char* s);
+
+/* ---- batch extensions ----------------------------------------------------- */
+/* n independent Query(violation, inputs[i]) calls in one launch (webhook micro-batch) */
+int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n, gk_results** out);
+/* audit discovery mode: Review(AugmentedUnstructured{objs[i], ns(objs[i])}) for
+ * every object (pkg/audit/manager.go:361-389, pkg/target/target.go:129-163).
+ * ns_json[i] is the JSON of the object's corev1.Namespace (NULL / len 0 for
+ * cluster-scoped objects, which the reference reviews with an empty Namespace{}). */
+int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                      const size_t* ns_lens, size_t n, gk_results** out);
+
+/* staged (device-resident) batches for the audit sweep: flatten + upload once,
+ * evaluate many times.  stage_objects has gk_review_objects' semantics. */
+int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                           const size_t* ns_lens, size_t n, gk_batch** out);
+/* evaluate a staged batch; decode=0 keeps results on the device (counts only) */
+int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out);
+void gk_batch_free(gk_batch* b);
+/* bytes of review documents + match columns resident in HBM for the batch */
+uint64_t gk_batch_device_bytes(const gk_batch* b);
+
+/* ---- results ------------------------------------------------------------- */
+typedef struct {
+  uint32_t review;          /* index of the input / object in the call */
+  uint32_t constraint;      /* engine constraint index */
+  const char* constraint_kind;
+  const char* constraint_name;
+  const char* msg;          /* UTF-8, not NUL-terminated */
+  size_t msg_len;
+  const char* details_json; /* json.Marshal of Result.Metadata["details"] */
+  size_t details_len;
+  const char* enforcement_action;
+} gk_result_view;
+
+size_t gk_results_count(const gk_results* r);
+int gk_results_get(const gk_results* r, size_t i, gk_result_view* out);
+size_t gk_results_reviews(const gk_results* r);
+uint32_t gk_results_review_status(const gk_results* r, size_t review);
+uint32_t gk_results_review_reason(const gk_results* r, size_t review);
+/* per-constraint violation totals (device-side counters), length = constraints */
+size_t gk_results_constraints(const gk_results* r);
+uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
+/* timings of the call in milliseconds: [flatten, upload, kernel, download, decode] */
+int gk_results_timing(const gk_results* r, double* ms5);
+void gk_results_free(gk_results* r);
+
+/* ---- introspection --------------------------------------------------------- */
+/* template status: 1 = compiled to GPU bytecode, 0 = CPU fallback, -1 unknown kind */
+int gk_template_status(gk_engine* e, const char* kind, const char** reason);
+size_t gk_constraint_count(gk_engine* e);
+int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GKGPU_H */

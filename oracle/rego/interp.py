@@ -938,7 +938,13 @@ def _expr_needs_outputs(e: Expr, safe, is_global):
     if e.kind == "term":
         t = e.terms[0]
         it = its(t) - safe
-        return (vs(t) - it) | wvars, it
+        needs, outs = (vs(t) - it), set(it)
+        # hoisted call with a generated output variable (RewriteExprTerms)
+        if isinstance(t, Call) and t.args and isinstance(t.args[-1], Var) and t.args[-1].name.startswith("$l") \
+                and t.args[-1].name not in safe:
+            needs.discard(t.args[-1].name)
+            outs.add(t.args[-1].name)
+        return needs | wvars, outs
     l, r = e.terms
     rn = vs(r) - its(r)
     if rn - safe == set():

@@ -1,0 +1,92 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports
+every symbol include/gkgpu.h declares, templates compile (or are explicitly
+marked for CPU fallback), driver bookkeeping mirrors drivers.Driver."""
+import os
+import re
+
+import pytest
+
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, template_modules
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gkgpu.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    decl = r"^\s*(?:int|void|const char\s*\*|size_t|uint32_t|uint64_t)\s+\**(gk_\w+)\s*\("
+    return sorted(set(re.findall(decl, txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = gkgpu.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(gkgpu.driver.EXPORTS) <= set(syms)
+
+
+def test_subset_templates_compile_to_gpu_bytecode():
+    d = gkgpu.Driver()
+    cl = Client(d)
+    for t in [W.REQUIRED_LABELS_BASIC, W.REQUIRED_LABELS, W.ALLOWED_REPOS, W.CONTAINER_LIMITS, W.REQUIRED_PROBES,
+              W.ALLOWED_LABEL_REGEX, W.ALLOWED_ANNOTATION_REGEX]:
+        kind = cl.add_template(t)
+        st, why = d.template_status(kind)
+        assert st == 1, (kind, why)
+
+
+def test_out_of_subset_template_is_explicit_fallback():
+    d = gkgpu.Driver()
+    cl = Client(d)
+    t = W._tmpl("K8sUniqueServiceSelector", """package k8suniqueserviceselector
+
+violation[{"msg": msg}] {
+	other := data.inventory.namespace[namespace][_][_][name]
+	msg := sprintf("same selector as service <%v> in namespace <%v>", [name, namespace])
+}
+""")
+    kind = cl.add_template(t)
+    st, why = d.template_status(kind)
+    assert st == 0 and "inventory" in why
+
+
+def test_put_modules_replaces_and_delete_modules_counts():
+    d = gkgpu.Driver()
+    prefix, mods = template_modules(W.ALLOWED_REPOS)
+    d.put_modules(prefix, mods)
+    d.put_modules(prefix, mods)
+    assert d.delete_modules(prefix) == 1
+    assert d.delete_modules(prefix) == 0
+
+
+def test_bad_rego_is_a_put_error():
+    d = gkgpu.Driver()
+    with pytest.raises(RuntimeError):
+        d.put_module("x", "package p\n\nviolation[{\"msg\": msg}] {\n\tmsg := \n}\n")
+
+
+def test_constraints_and_delete_data():
+    d = gkgpu.Driver()
+    cl = Client(d)
+    ts, cs = W.config2()
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    assert len(d.constraints()) == 4
+    assert cl.remove_constraint(cs[0]) is True
+    assert len(d.constraints()) == 3
+    cl.reset()
+    assert d.constraints() == []
+
+
+def test_dump_lists_modules():
+    d = gkgpu.Driver()
+    cl = Client(d)
+    cl.add_template(W.REQUIRED_LABELS_BASIC)
+    s = d.dump()
+    assert "K8sRequiredLabels" in s

@@ -1,0 +1,208 @@
+"""GPU parity: the HIP engine vs the CPU oracle on the same driver calls and inputs.
+
+Bar: bit-exact (constraint, msg, details, enforcementAction) multisets per
+review; the engine's CPU-fallback reviews are excluded and counted (they would
+be evaluated by CPU OPA), and must stay a small fraction on these workloads.
+"""
+import json
+import os
+
+import pytest
+
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+
+from parity import Report, compare, oracle_for, run_objects
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_device():
+    if not gkgpu.Driver.device_available():
+        pytest.fail("no HIP device visible: GPU parity tests must run on an MI355X")
+
+
+def _assert_clean(rep, max_fallback_frac=0.0):
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.compared > 0
+    total = rep.compared + rep.fallback + rep.errors
+    assert rep.fallback <= max_fallback_frac * total, rep
+
+
+def test_config1_namespaces_required_labels():
+    ts, cs = W.config1()
+    nss = W.gen_namespaces(3000, seed=1)
+    rep, res = run_objects(gkgpu.Driver(), ts, cs, nss, [None] * len(nss))
+    _assert_clean(rep)
+    assert rep.violations > 1000
+    # README.md:313-327 message shape
+    assert any(r.msg == 'you must provide labels: {"gatekeeper"}' for r in res.results)
+    assert all(r.details_json == '{"missing_labels":["gatekeeper"]}' for r in res.results)
+
+
+def test_config2_agilebank_pods():
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(1500, seed=42, n_namespaces=100)
+    nss = [ns_objs[n] for n in ns_of]
+    rep, res = run_objects(gkgpu.Driver(), ts, cs, pods, nss)
+    _assert_clean(rep)
+    assert rep.violations > 5000
+
+
+def test_config2_agilebank_namespaces_regex():
+    ts, cs = W.config2()
+    nss = W.gen_namespaces(2000, seed=7)
+    rep, res = run_objects(gkgpu.Driver(), ts, cs, nss, [None] * len(nss))
+    _assert_clean(rep)
+    msgs = {r.msg for r in res.results}
+    assert "All namespaces must have an `owner` label that points to your company username" in msgs
+
+
+def test_demo_agilebank_resources():
+    """Shapes of demo/agilebank/{bad,good}_resources."""
+    ts, cs = W.config2()
+    pods = [
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "opa", "namespace": "production"},
+         "spec": {"containers": [{"name": "opa", "image": "openpolicyagent/opa:0.9.2",
+                                  "args": ["run", "--server", "--addr=localhost:8080"],
+                                  "resources": {"limits": {"cpu": "300m", "memory": "4000Mi"}}}]}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "opa", "namespace": "production"},
+         "spec": {"containers": [{"name": "opa", "image": "openpolicyagent/opa:0.9.2"}]}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "opa", "namespace": "production"},
+         "spec": {"containers": [{"name": "opa", "image": "gcr.io/smythe-kpc/testbuilds/opa:0.9.2",
+                                  "resources": {"limits": {"cpu": "100m", "memory": "30Mi"}}}]}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "opa", "namespace": "production"},
+         "spec": {"containers": [{"name": "opa", "image": "openpolicyagent/opa:0.9.2",
+                                  "resources": {"limits": {"cpu": "100m", "memory": "30Mi"}},
+                                  "readinessProbe": {"httpGet": {"path": "/", "port": 8080}},
+                                  "livenessProbe": {"tcpSocket": {"port": 8080}}}]}},
+        W.namespace_obj("production", {"owner": "me"}),
+        W.namespace_obj("production", {"owner": "me.agilebank.demo"}),
+    ]
+    nss = [W.namespace_obj("production")] * 4 + [None, None]
+    rep, res = run_objects(gkgpu.Driver(), ts, cs, pods, nss)
+    _assert_clean(rep)
+    per = [[r.msg for r in res.results if r.review == i] for i in range(len(pods))]
+    assert "container <opa> cpu limit <300m> is higher than the maximum allowed of <200m>" in per[0]
+    assert per[1].count("container <opa> has no resource limits") == 2  # two rules, no dedupe
+    assert any("invalid image repo" in m for m in per[2])
+    assert per[3] == []
+    assert per[5] == []
+
+
+def _integration_reviews(case):
+    o = case["object"]
+    obj = {"apiVersion": "%s/v1" % o["group"], "kind": o["kind"]}
+    if o.get("labels"):
+        obj["metadata"] = {"labels": o["labels"]}
+    ns = case["namespace"]
+    nsobj = None
+    if ns is not None:
+        md = {"name": ns["name"], "creationTimestamp": None}
+        if ns.get("labels"):
+            md["labels"] = ns["labels"]
+        nsobj = {"metadata": md, "spec": {}, "status": {}}
+    kind = {"group": o["group"], "version": "v1", "kind": o["kind"]}
+    base = {"uid": "", "kind": kind, "resource": {"group": "", "version": "", "resource": ""}}
+    if ns is not None:
+        base["namespace"] = ns["name"]
+    tail = {"operation": "", "userInfo": {}}
+    unstable = {"namespace": nsobj} if nsobj is not None else {}
+    r1 = dict(base, **tail, object=obj, oldObject=None, options=None, _unstable=unstable)
+    r2 = dict(base, **tail, object=None, oldObject=obj, options=None, _unstable=unstable)
+    r3 = dict(base, **tail, object=obj, oldObject=None, options=None, _unstable=unstable)
+    return [r1, r2, r3]
+
+
+def test_target_integration_cases():
+    """pkg/target/target_integration_test.go:141-363, three review forms each."""
+    cases = json.load(open(os.path.join(HERE, "golden", "integration_cases.json")))
+    deny_all = W._tmpl("DenyAll", 'package denyall\n\nviolation[{"msg": msg}] {\n\tmsg := "denyall constraint installed"\n}\n')
+    rep = Report()
+    for case in cases:
+        c = W.constraint("DenyAll", "my-constraint", match=case["match"])
+        drv = gkgpu.Driver()
+        cl = Client(drv)
+        cl.add_template(deny_all)
+        cl.add_constraint(c)
+        od = oracle_for([deny_all], [c])
+        reviews = _integration_reviews(case)
+        res = drv.query_batch([{"review": r} for r in reviews])
+        compare(od, reviews, res, rep)
+        for i in range(3):
+            got_allowed = not any(r.review == i for r in res.results)
+            assert res.status[i] == 0, case["name"]
+            assert got_allowed == case["allowed"], (case["name"], i)
+    assert not rep.mismatches, rep.mismatches[:3]
+
+
+def test_label_and_annotation_regex_config3():
+    ts = [W.ALLOWED_LABEL_REGEX, W.ALLOWED_ANNOTATION_REGEX]
+    rules = [{"key": "env", "allowedRegex": "^(dev|stage|prod)-[0-9]{1,4}$"},
+             {"key": "owner", "allowedRegex": "^[a-zA-Z]+.agilebank.demo$"},
+             {"key": "app", "allowedRegex": "^[a-z0-9]([-a-z0-9]*[a-z0-9])?$"}]
+    cs = [W.constraint("K8sAllowedLabelRegex", "label-rules",
+                       match={"kinds": [{"apiGroups": ["apps", ""], "kinds": ["Deployment", "Service"]}]},
+                       parameters={"rules": rules}),
+          W.constraint("K8sAllowedAnnotationRegex", "annotation-rules",
+                       match={"kinds": [{"apiGroups": ["apps", ""], "kinds": ["Deployment", "Service"]}]},
+                       parameters={"rules": rules})]
+    import random
+    rng = random.Random(7)
+    vals = {"env": ["dev-1", "prod-9999", "prod-10000", "stage-", "dev-12\n", "qa-1", ""],
+            "owner": ["alice.agilebank.demo", "bob_agilebank.demo", "x.agilebank.demo\n", "9.agilebank.demo"],
+            "app": ["web", "-web", "web-", "a", "Web", "a-b-c", ""]}
+    objs = []
+    for i in range(1500):
+        kind = rng.choice(["Deployment", "Service"])
+        lab = {k: rng.choice(v) for k, v in vals.items() if rng.random() < 0.8}
+        ann = {k: rng.choice(v) for k, v in vals.items() if rng.random() < 0.5}
+        objs.append({"apiVersion": "apps/v1" if kind == "Deployment" else "v1", "kind": kind,
+                     "metadata": {"name": "o%d" % i, "namespace": "ns%d" % (i % 7), "labels": lab, "annotations": ann}})
+    nss = [W.namespace_obj("ns%d" % (i % 7)) for i in range(len(objs))]
+    rep, res = run_objects(gkgpu.Driver(), ts, cs, objs, nss)
+    _assert_clean(rep)
+    assert rep.violations > 500
+
+
+def test_query_single_review_and_batch_agree():
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(50, seed=3, n_namespaces=5)
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    reviews = [augmented_review(p, ns_objs[n]) for p, n in zip(pods, ns_of)]
+    batch = drv.query_batch([{"review": r} for r in reviews])
+    objs = drv.review_objects(pods, [ns_objs[n] for n in ns_of])
+    for i, r in enumerate(reviews):
+        single = cl.review(r)
+        a = sorted((x.constraint_name, x.msg) for x in single.results)
+        b = sorted((x.constraint_name, x.msg) for x in batch.results if x.review == i)
+        c = sorted((x.constraint_name, x.msg) for x in objs.results if x.review == i)
+        assert a == b == c
+
+
+def test_staged_batch_matches_direct_and_counts():
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(400, seed=5, n_namespaces=30)
+    nss = [ns_objs[n] for n in ns_of]
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    direct = drv.review_objects(pods, nss)
+    b = drv.stage_objects(pods, nss)
+    r1 = b.eval(decode=True)
+    r2 = b.eval(decode=False)
+    assert sorted((x.review, x.msg) for x in r1.results) == sorted((x.review, x.msg) for x in direct.results)
+    assert r2.totals == r1.totals
+    assert sum(r1.totals) == len(r1.results)
