@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Audit-sweep benchmark: resource x constraint evals/sec on MI355X.
+
+Workload (BASELINE.json configs[1]): demo/agilebank policies (required labels,
+allowed repos, container limits, required probes) over synthetic Pods,
+1,000,000 Pods per GPU (weak scaling: each rank audits its own shard; the only
+exchange step is the all-reduce of per-constraint violation totals the audit
+status write needs, pkg/audit/manager.go:462-508, over RCCL).
+
+A step = one audit sweep of the rank's staged (HBM-resident) batch: match +
+template predicates + GPU message formatting + tuple compaction + totals
+all-reduce.  Run as `python bench.py --gpus N --steps K --warmup W` (N>1 under
+torch.distributed.run).  Prints one JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gatekeeper-1_amd")]
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pods", type=int, default=1_000_000, help="Pods per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=1500, help="Pods timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per launch for this workload (rocprofv3 --pmc), if measured")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import gkgpu
+    from gkgpu import workloads as W
+    from gkgpu.client import Client
+
+    templates, constraints = W.config2()
+    drv = gkgpu.Driver(device=local)
+    cl = Client(drv)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    n_cons = len(constraints)
+
+    t0 = time.time()
+    objs, nss = W.gen_pods_json(args.pods, seed=42, n_namespaces=1000, start=rank * args.pods)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    batch = drv.stage_objects(objs, nss)
+    t_stage = time.time() - t0
+    nrev, nodes, str_bytes, col_bytes = batch.stats()
+
+    def sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+
+    def step():
+        res = batch.eval(decode=False, light=True)
+        if dist is not None:
+            import torch
+            tot = torch.tensor(res.totals, dtype=torch.int64, device="cuda")
+            dist.all_reduce(tot)
+        return res
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    last = None
+    for _ in range(args.steps):
+        last = step()
+        kernel_ms.append(last.timing_ms[2])
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1000.0
+    evals_per_step = nrev * n_cons * world
+    value = evals_per_step / (ms_per_step / 1000.0)
+
+    # roofline: algorithmic bytes of one sweep over the rank's batch (each staged
+    # document node / referenced string / match column read once, tuples and
+    # message bytes written once) / average kernel duration (HIP events)
+    k_avg_ms = sum(kernel_ms) / len(kernel_ms)
+    algo_bytes = nodes * 16 + str_bytes + col_bytes + last.device_tuples * 32 + last.device_bytes
+    achieved = algo_bytes / (k_avg_ms / 1000.0) / 1e9
+    fallback = last.n_fallbacks
+    errors = last.n_errors
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("pods") == args.pods and tj.get("constraints") == n_cons:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(templates, constraints, objs[: args.cpu_sample], nss[: args.cpu_sample])
+
+    if rank == 0:
+        out = {
+            "metric": "resource x constraint evals/sec (1/2/4/8 GPU) + % HBM roofline; vs host-CPU OPA",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded generator, SURVEY 8(d) config 2 distribution)",
+            "config": {
+                "workload": "config2: demo/agilebank policies over synthetic Pods (BASELINE configs[1])",
+                "pods_per_gpu": nrev,
+                "constraints": n_cons,
+                "templates": [t["spec"]["crd"]["spec"]["names"]["kind"] for t in templates],
+                "evals_per_step": evals_per_step,
+                "violations_per_step_rank0": last.device_tuples,
+                "fallback_reviews": fallback,
+                "error_reviews": errors,
+                "parallelism": "dp%d (resource shards, totals all-reduce over RCCL)" % world,
+                "stage_s": round(t_stage, 3),
+                "gen_s": round(t_gen, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algo_bytes_per_launch": algo_bytes,
+                "kernel_ms_avg": k_avg_ms,
+                "kernel": "audit_kernel",
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(templates, constraints, objs_json, nss_json):
+    """The oracle (CPU restatement of OPA topdown + the match library) timed on a
+    bounded sample of the same workload, one core."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import oracle_for, oracle_review
+    from gkgpu.client import augmented_review
+    od = oracle_for(templates, constraints)
+    objs = [json.loads(o) for o in objs_json]
+    nss = [json.loads(n) for n in nss_json]
+    t0 = time.perf_counter()
+    for o, n in zip(objs, nss):
+        oracle_review(od, augmented_review(o, n))
+    dt = time.perf_counter() - t0
+    return {"value": len(objs) * len(constraints) / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": "%d Pods x %d constraints (config2 distribution), oracle/ CPU restatement of OPA v0.21 "
+                      "topdown; Go/OPA not buildable offline" % (len(objs), len(constraints)),
+            "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

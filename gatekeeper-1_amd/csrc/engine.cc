@@ -125,9 +125,11 @@ struct gk_results {
   std::vector<uint64_t> totals;
   std::vector<std::string> ckind, cname, cea;
   double ms[5] = {0, 0, 0, 0, 0};
+  uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
 };
 
 struct gk_batch {
+  uint64_t node_count = 0, str_bytes = 0;  // algorithmic input bytes of the staged documents
   uint64_t gen = 0;
   uint32_t nrev = 0;
   uint32_t node_begin = 0, node_end = 0;
@@ -652,7 +654,8 @@ static ReviewCol review_columns(gk_engine* e, uint32_t root) {
 
 // Review(AugmentedUnstructured{obj, ns}) envelope (pkg/target/target.go:129-163,
 // admission/v1beta1 AdmissionRequest json field order).
-static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const JDoc& nd, int nj) {
+static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const JDoc& nd, int nj, uint32_t ns_root,
+                                    const std::string& nsname_in) {
   Store& st = e->st;
   std::string apiv, kind, name;
   int av = od.get(oj, "apiVersion");
@@ -665,9 +668,11 @@ static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const 
   size_t slash = apiv.find('/');
   if (slash == std::string::npos) version = apiv;
   else if (apiv.find('/', slash + 1) == std::string::npos) { group = apiv.substr(0, slash); version = apiv.substr(slash + 1); }
-  std::string nsname;
-  int nmd = nd.get(nj, "metadata");
-  if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
+  std::string nsname = nsname_in;
+  if (ns_root == NO_ID) {
+    int nmd = nd.get(nj, "metadata");
+    if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
+  }
   // children: uid kind resource [name] [namespace] operation userInfo object oldObject options _unstable
   uint32_t nch = 9 + (name.empty() ? 0 : 1) + (nsname.empty() ? 0 : 1);
   uint32_t root = st.add_node(Node{});
@@ -718,7 +723,7 @@ static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const 
     st.nodes()[objslot] = n;
   }
   // _unstable: {"namespace": <ns>}
-  uint32_t nsroot = st.add_doc(nd, nj);
+  uint32_t nsroot = ns_root != NO_ID ? ns_root : st.add_doc(nd, nj);
   uint32_t uf = st.reserve(1);
   {
     Node n = st.nodes()[nsroot];
@@ -866,6 +871,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
         return fail(e, GK_EDEVICE, "device allocation failed");
       continue;
     }
+    res->dev_tuples = counters[0];
+    res->dev_bytes = counters[1];
     std::vector<uint32_t> tot(ncons);
     hipMemcpy(tot.data(), e->d_totals.p, ncons * 4, hipMemcpyDeviceToHost);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
@@ -1189,7 +1196,9 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
                            const size_t* ns_lens, size_t n, std::vector<ReviewCol>& cols) {
   JDoc od, nd;
   std::string empty_ns = EMPTY_NS_JSON;
-  // namespace docs are shared by all objects of a namespace: parse each distinct text once
+  // a namespace document is shared by all objects of the namespace: flatten each
+  // distinct namespace text once and point every review's _unstable.namespace at it
+  std::unordered_map<std::string, std::pair<uint32_t, std::string>> ns_nodes;
   for (size_t i = 0; i < n; ++i) {
     JsonReader ro(objs[i], obj_lens ? obj_lens[i] : strlen(objs[i]), &od);
     int oj = ro.parse();
@@ -1197,10 +1206,24 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
     const char* ns = (ns_json && ns_json[i]) ? ns_json[i] : nullptr;
     size_t nl = ns ? (ns_lens ? ns_lens[i] : strlen(ns)) : 0;
     if (!ns || nl == 0) { ns = empty_ns.data(); nl = empty_ns.size(); }
-    JsonReader rn(ns, nl, &nd);
-    int nj = rn.parse();
-    if (nj < 0) return fail(e, GK_EINVAL, "invalid namespace JSON at " + std::to_string(i) + ": " + nd.err);
-    uint32_t root = build_object_review(e, od, oj, nd, nj);
+    std::string key(ns, nl);
+    auto it = ns_nodes.find(key);
+    uint32_t nsroot = NO_ID;
+    std::string nsname;
+    int nj = 0;
+    if (it != ns_nodes.end()) {
+      nsroot = it->second.first;
+      nsname = it->second.second;
+    } else {
+      JsonReader rn(ns, nl, &nd);
+      nj = rn.parse();
+      if (nj < 0) return fail(e, GK_EINVAL, "invalid namespace JSON at " + std::to_string(i) + ": " + nd.err);
+      int nmd = nd.get(nj, "metadata");
+      if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
+      nsroot = e->st.add_doc(nd, nj);
+      ns_nodes[key] = {nsroot, nsname};
+    }
+    uint32_t root = build_object_review(e, od, oj, nd, nj, nsroot, nsname);
     cols.push_back(review_columns(e, root));
   }
   return GK_OK;
@@ -1252,6 +1275,15 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
   if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
   if (!sync_tables(e) || !up(b->d_revs, b->cols, false)) { delete b; return fail(e, GK_EDEVICE, "upload failed"); }
   b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
+  {
+    // one pass over every staged document node and each distinct string value it references
+    std::vector<uint8_t> seen(e->st.nstrings(), 0);
+    b->node_count = b->node_end - b->node_begin;
+    for (uint32_t k = b->node_begin; k < b->node_end; ++k) {
+      const Node& nd = e->st.nodes()[k];
+      if (nd.type == NT_STR && !seen[nd.val]) { seen[nd.val] = 1; b->str_bytes += e->st.strings()[nd.val].len; }
+    }
+  }
   *out = b;
   return GK_OK;
 }
@@ -1274,6 +1306,38 @@ void gk_batch_free(gk_batch* b) {
 }
 
 uint64_t gk_batch_device_bytes(const gk_batch* b) { return b ? b->dev_bytes : 0; }
+
+int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes) {
+  if (!b) return GK_EINVAL;
+  if (reviews) *reviews = b->nrev;
+  if (nodes) *nodes = b->node_count;
+  if (str_bytes) *str_bytes = b->str_bytes;
+  if (col_bytes) *col_bytes = (uint64_t)b->cols.size() * sizeof(ReviewCol);
+  return GK_OK;
+}
+
+int gk_results_flag_counts(const gk_results* r, uint64_t* errors, uint64_t* fallbacks) {
+  if (!r) return GK_EINVAL;
+  uint64_t ne = 0, nf = 0;
+  for (uint32_t s : r->status) { ne += (s & GK_REVIEW_ERROR) != 0; nf += (s & GK_REVIEW_FALLBACK) != 0; }
+  if (errors) *errors = ne;
+  if (fallbacks) *fallbacks = nf;
+  return GK_OK;
+}
+
+int gk_results_copy_status(const gk_results* r, uint32_t* status, uint32_t* reason) {
+  if (!r) return GK_EINVAL;
+  if (status && !r->status.empty()) memcpy(status, r->status.data(), r->status.size() * 4);
+  if (reason && !r->reason.empty()) memcpy(reason, r->reason.data(), r->reason.size() * 4);
+  return GK_OK;
+}
+
+int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes) {
+  if (!r) return GK_EINVAL;
+  if (tuples) *tuples = r->dev_tuples;
+  if (bytes) *bytes = r->dev_bytes;
+  return GK_OK;
+}
 
 int gk_dump(gk_engine* e, char** out) {
   if (!e || !out) return GK_EINVAL;

@@ -26,6 +26,7 @@ EXPORTS = [
     "gk_batch_free", "gk_batch_device_bytes", "gk_results_count", "gk_results_get", "gk_results_reviews",
     "gk_results_review_status", "gk_results_review_reason", "gk_results_constraints", "gk_results_constraint_total",
     "gk_results_timing", "gk_results_free", "gk_template_status", "gk_constraint_count", "gk_constraint_info",
+    "gk_batch_stats", "gk_results_device_counts", "gk_results_copy_status", "gk_results_flag_counts",
 ]
 
 
@@ -99,6 +100,11 @@ def load_library():
     lib.gk_results_constraint_total.restype = C.c_uint64
     lib.gk_results_timing.argtypes = [vp, C.POINTER(C.c_double)]
     lib.gk_results_free.argtypes = [vp]
+    pu64 = C.POINTER(C.c_uint64)
+    lib.gk_batch_stats.argtypes = [vp, pu64, pu64, pu64, pu64]
+    lib.gk_results_device_counts.argtypes = [vp, pu64, pu64]
+    lib.gk_results_copy_status.argtypes = [vp, C.c_void_p, C.c_void_p]
+    lib.gk_results_flag_counts.argtypes = [vp, pu64, pu64]
     lib.gk_template_status.argtypes = [vp, cp, C.POINTER(cp)]
     lib.gk_template_status.restype = C.c_int
     lib.gk_constraint_count.argtypes = [vp]
@@ -131,9 +137,29 @@ class Results:
     reason: List[int]
     totals: List[int]          # per constraint (device counters)
     timing_ms: List[float] = field(default_factory=list)  # flatten, upload, kernel, download, decode
+    device_tuples: int = 0      # violation tuples the kernel wrote (32 B each)
+    device_bytes: int = 0       # message/details bytes the kernel wrote
+    n_errors: int = 0
+    n_fallbacks: int = 0
 
     def for_review(self, i):
         return [r for r in self.results if r.review == i]
+
+
+def _collect_light(lib, h) -> Results:
+    """totals, counters and flag counts only (no per-review arrays)."""
+    try:
+        nc = lib.gk_results_constraints(h)
+        totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
+        t = (C.c_double * 5)()
+        lib.gk_results_timing(h, t)
+        dt, db = C.c_uint64(), C.c_uint64()
+        lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
+        ne, nf = C.c_uint64(), C.c_uint64()
+        lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
+        return Results([], [], [], totals, list(t), dt.value, db.value, ne.value, nf.value)
+    finally:
+        lib.gk_results_free(h)
 
 
 def _collect(lib, h, decode=True) -> Results:
@@ -148,13 +174,19 @@ def _collect(lib, h, decode=True) -> Results:
             out.append(Result(v.review, v.constraint, v.constraint_kind.decode(), v.constraint_name.decode(), msg, det,
                               v.enforcement_action.decode()))
         nr = lib.gk_results_reviews(h)
-        status = [lib.gk_results_review_status(h, i) for i in range(nr)]
-        reason = [lib.gk_results_review_reason(h, i) for i in range(nr)]
+        st = (C.c_uint32 * nr)()
+        rs = (C.c_uint32 * nr)()
+        lib.gk_results_copy_status(h, st, rs)
+        status = list(st)
+        reason = list(rs)
         nc = lib.gk_results_constraints(h)
         totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
         t = (C.c_double * 5)()
         lib.gk_results_timing(h, t)
-        return Results(out, status, reason, totals, list(t))
+        dt, db = C.c_uint64(), C.c_uint64()
+        lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
+        return Results(out, status, reason, totals, list(t), dt.value, db.value,
+                       sum(1 for x in status if x & 1), sum(1 for x in status if x & 2))
     finally:
         lib.gk_results_free(h)
 
@@ -174,15 +206,21 @@ class Batch:
         self._h = handle
         self.n = n
 
-    def eval(self, decode=True) -> Results:
+    def eval(self, decode=True, light=False) -> Results:
         lib = self._drv._lib
         out = C.c_void_p()
         rc = lib.gk_batch_eval(self._drv._e, self._h, 1 if decode else 0, C.byref(out))
         self._drv._check(rc)
-        return _collect(lib, out)
+        return _collect_light(lib, out) if light else _collect(lib, out)
 
     def device_bytes(self) -> int:
         return self._drv._lib.gk_batch_device_bytes(self._h)
+
+    def stats(self):
+        """(reviews, document nodes, distinct string-value bytes, match-column bytes)."""
+        v = [C.c_uint64() for _ in range(4)]
+        self._drv._lib.gk_batch_stats(self._h, *[C.byref(x) for x in v])
+        return tuple(x.value for x in v)
 
     def free(self):
         if self._h:

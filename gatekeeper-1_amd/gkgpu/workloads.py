@@ -447,3 +447,31 @@ def _container(rng, name):
 
 def dumps(x) -> str:
     return json.dumps(x, separators=(",", ":"))
+
+
+def gen_pods_json(n, seed=42, n_namespaces=1000, start=0):
+    """Fast JSON-text generator with gen_pods' distribution (config 2 at scale).
+
+    Returns (object JSON strings, namespace JSON strings aligned with objects);
+    namespace strings are shared objects per namespace.  Containers are drawn
+    from seeded pools of pre-serialized variants (2,048 per slot)."""
+    rng = random.Random(seed)
+    pools = [[json.dumps(_container(rng, "c%d" % slot), separators=(",", ":")) for _ in range(2048)] for slot in range(4)]
+    init_pool = [json.dumps(_container(rng, "init"), separators=(",", ":")) for _ in range(2048)]
+    names = ["team-%04d" % i for i in range(n_namespaces - 1)]
+    ns_json = {nm: dumps(namespace_obj(nm, {"env": "dev"})) for nm in names}
+    ns_json["production"] = dumps(namespace_obj("production", {"env": "prod"}))
+    objs, nss = [], []
+    r = random.Random(seed * 7919 + start)
+    rand = r.random
+    rbits = r.getrandbits
+    for i in range(start, start + n):
+        ns = "production" if rand() < 0.10 else names[rbits(16) % len(names)]
+        k = 1 + (rbits(2))
+        conts = ",".join(pools[s][rbits(11)] for s in range(k))
+        init = (',"initContainers":[' + init_pool[rbits(11)] + "]") if rand() < 0.5 else ""
+        owner = (',"owner":"alice"' if rand() < 0.5 else ',"owner":"bob.agilebank.demo"') if rand() < 0.7 else ""
+        objs.append('{"apiVersion":"v1","kind":"Pod","metadata":{"name":"pod-%08d","namespace":"%s","labels":{"app":"app-%d"%s}},'
+                    '"spec":{"containers":[%s]%s}}' % (i, ns, rbits(7), owner, conts, init))
+        nss.append(ns_json[ns])
+    return objs, nss

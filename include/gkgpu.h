@@ -98,6 +98,9 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out);
 void gk_batch_free(gk_batch* b);
 /* bytes of review documents + match columns resident in HBM for the batch */
 uint64_t gk_batch_device_bytes(const gk_batch* b);
+/* algorithmic input of one sweep over the batch: reviews, document nodes (16 B
+ * each), bytes of the distinct string values they reference, match-column bytes */
+int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes);
 
 /* ---- results ------------------------------------------------------------- */
 typedef struct {
@@ -117,11 +120,17 @@ int gk_results_get(const gk_results* r, size_t i, gk_result_view* out);
 size_t gk_results_reviews(const gk_results* r);
 uint32_t gk_results_review_status(const gk_results* r, size_t review);
 uint32_t gk_results_review_reason(const gk_results* r, size_t review);
+/* bulk copy of the per-review status / reason arrays (length gk_results_reviews) */
+int gk_results_copy_status(const gk_results* r, uint32_t* status, uint32_t* reason);
+/* number of reviews flagged GK_REVIEW_ERROR / GK_REVIEW_FALLBACK */
+int gk_results_flag_counts(const gk_results* r, uint64_t* errors, uint64_t* fallbacks);
 /* per-constraint violation totals (device-side counters), length = constraints */
 size_t gk_results_constraints(const gk_results* r);
 uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
 /* timings of the call in milliseconds: [flatten, upload, kernel, download, decode] */
 int gk_results_timing(const gk_results* r, double* ms5);
+/* violation tuples (32 B each) and message/details bytes the kernel wrote */
+int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes);
 void gk_results_free(gk_results* r);
 
 /* ---- introspection --------------------------------------------------------- */
