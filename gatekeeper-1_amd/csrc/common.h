@@ -10,7 +10,19 @@
 //                 selectors / scope), evaluated by the match stage;
 //   * ReviewCol — per-review match columns extracted by the host flattener.
 #pragma once
+#ifdef __HIPCC_RTC__
+// runtime-compiled template kernels (jit.cc): hipRTC supplies the fixed-width types
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int8_t int8_t;
+typedef __hip_internal::int16_t int16_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::int64_t int64_t;
+#else
 #include <stdint.h>
+#endif
 
 namespace gk {
 
@@ -88,6 +100,7 @@ enum Op : uint16_t {
   OP_EMIT,         // a(msg), b(details), y=rule index
   OP_LEN_EQ,       // a(dst bool), b(value), y=n : collection length test (array patterns)
   OP_FAIL_FALLBACK,// y=reason : unsupported construct reached at run time
+  OP_TABLE,        // a = lookup(K[x..]: n, (key, value) x n ; R[b]) — constant-table function call
   OP_COUNT_
 };
 
@@ -184,5 +197,43 @@ struct Viol {
 static_assert(sizeof(Viol) == 32, "Viol layout");
 
 constexpr uint32_t RULE_AUTOREJECT = 0xffffu;
+
+// ------------------------------------------------------------------ launch
+// Kernel arguments of one audit launch (passed by value; shared by the bytecode
+// VM kernel in kernels.hip and the per-template kernels jit.cc compiles).
+struct DevArgs {
+  const Node* nodes;
+  const StrEnt* strs;
+  const uint8_t* pool;
+  const uint8_t* sflags;
+  const NumEnt* nums;
+  const Ins* code;
+  const uint64_t* K;
+  const uint32_t* fmt;
+  const MatchSpec* cons;
+  const uint32_t* mwords;
+  const uint32_t* prog_off;
+  const ReviewCol* revs;
+  const uint32_t* dfa_keys;   // sorted pattern string ids
+  const uint32_t* dfa_meta;   // per entry: word offset into dfa_words | status<<30
+  const uint32_t* dfa_words;
+  uint32_t ndfa;
+  uint32_t ncode;
+  uint32_t ncons;
+  uint32_t nrev;
+  uint32_t ntiles;            // ceil(nrev / 64)
+  const uint32_t* clist;      // constraints this launch evaluates (wave -> tile x clist[j])
+  uint32_t nclist;
+  Viol* out;
+  uint32_t out_cap;
+  uint32_t* counters;         // [0] = tuples, [1] = bytes
+  char* bytes;
+  uint32_t bytes_cap;
+  uint32_t* rflags;
+  uint32_t* totals;           // per constraint violation count
+  uint32_t* rreason;          // per review fallback reason (diagnostic)
+  unsigned int* pchist;       // optional (GKGPU_PROFILE=2): executions per bytecode pc
+  unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]
+};
 
 }  // namespace gk

@@ -707,11 +707,18 @@ class Comp {
       bool has_out = t->items.size() == nargs + 1;
       if (!has_out && t->items.size() != nargs) throw Unsupported("arity mismatch " + name);
       std::vector<TermP> args(t->items.begin(), t->items.begin() + nargs);
-      items_k(args, 0, {}, env, fail, [&, has_out](const std::vector<int>& regs, int f) {
-        int out = loadk(tag_val(V_UNDEF, 0));
-        if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
-        for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
-        --inline_depth_;
+      int tab = table_func(rules, stmt && !has_out);
+      items_k(args, 0, {}, env, fail, [&, has_out, tab](const std::vector<int>& regs, int f) {
+        int out;
+        if (tab >= 0) {
+          out = alloc();
+          emit(OP_TABLE, (uint16_t)out, (uint16_t)regs[0], 0, (uint32_t)tab);
+        } else {
+          out = loadk(tag_val(V_UNDEF, 0));
+          if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
+          for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
+          --inline_depth_;
+        }
         emit_jmp(OP_JUNDEF, out, f);
         if (has_out) {
           unify_value(t->items.back(), out, env, f, [&](int f2) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f2); });
@@ -774,6 +781,42 @@ class Comp {
     } else {
       k(d, f);
     }
+  }
+
+  // A one-argument function whose every definition is `f("key") = scalar { true }`
+  // is a constant table: the argument unifies with at most one distinct key, so
+  // evaluating all bodies (topdown evalFunc) reduces to one lookup.  Duplicate
+  // keys must carry the same value text (else the general path reports the
+  // conflict at run time).  As a statement (`f(x)` without output) a `false`
+  // value makes the call undefined, so such entries are left out.  Returns the
+  // table's offset in the constant bank, or -1.
+  int table_func(const std::vector<std::shared_ptr<Rule>>& rules, bool stmt) {
+    std::vector<std::pair<uint64_t, uint64_t>> ents;
+    std::map<std::string, std::string> seen;
+    for (auto& r : rules) {
+      if (r->kind != Rule::FUNC || r->is_else || r->is_default || r->args.size() != 1) return -1;
+      const TermP& a = r->args[0];
+      if (a->k != T_SCALAR || a->stype != S_STR) return -1;
+      if (!r->value || r->value->k != T_SCALAR) return -1;
+      for (auto& e : r->body) {
+        if (e->kind != Expr::TERM || e->negated || !e->withs.empty() || e->terms.size() != 1) return -1;
+        if (e->terms[0]->k != T_SCALAR || e->terms[0]->stype != S_TRUE) return -1;
+      }
+      std::string vt = std::to_string(r->value->stype) + ":" + r->value->s;
+      auto it = seen.find(a->s);
+      if (it != seen.end()) {
+        if (it->second != vt) return -1;
+        continue;
+      }
+      seen[a->s] = vt;
+      if (stmt && r->value->stype == S_FALSE) continue;
+      ents.push_back({scalar_val(a), scalar_val(r->value)});
+    }
+    if (rules.empty()) return -1;
+    uint32_t off = (uint32_t)bank_.consts.size();
+    bank_.consts.push_back(ents.size());
+    for (auto& e : ents) { bank_.consts.push_back(e.first); bank_.consts.push_back(e.second); }
+    return (int)off;
   }
 
   void inline_func(const std::shared_ptr<Rule>& r, const std::vector<int>& args, int out, bool stmt) {
@@ -850,11 +893,11 @@ class Comp {
         term(msg, env, f, [&](int mr, int f2) {
           if (det) {
             term(det, env, f2, [&](int dr, int f3) {
-              emit(OP_EMIT, (uint16_t)mr, (uint16_t)dr, 0, 0, (uint32_t)idx);
+              emit(OP_EMIT, (uint16_t)mr, (uint16_t)dr, (uint16_t)depth(), 0, (uint32_t)idx);
               emit_jmp(OP_JMP, 0, f3);
             });
           } else {
-            emit(OP_EMIT, (uint16_t)mr, NOREG, 0, 0, (uint32_t)idx);
+            emit(OP_EMIT, (uint16_t)mr, NOREG, (uint16_t)depth(), 0, (uint32_t)idx);
             emit_jmp(OP_JMP, 0, f2);
           }
         });
@@ -866,7 +909,7 @@ class Comp {
       emit(OP_GETK, (uint16_t)m, (uint16_t)kv, 0, kconst(tag_val(V_STR, st_.s_msg)));
       emit_jmp(OP_JUNDEF, m, f2);
       emit(OP_GETK, (uint16_t)d, (uint16_t)kv, 0, kconst(tag_val(V_STR, st_.s_details)));
-      emit(OP_EMIT, (uint16_t)m, (uint16_t)d, 0, 0, (uint32_t)idx);
+      emit(OP_EMIT, (uint16_t)m, (uint16_t)d, (uint16_t)depth(), 0, (uint32_t)idx);
       emit_jmp(OP_JMP, 0, f2);
     });
   }

@@ -1,0 +1,1225 @@
+// Device runtime of the MI355X audit engine: value model, document access,
+// comparisons, builtins, printing, regex DFA, match stage, staged emission and
+// the per-instruction semantics of the predicate bytecode.
+//
+// Shared verbatim by the two evaluation back ends so they cannot drift apart:
+//   * kernels.hip  — the bytecode VM kernel (any compiled template), and
+//   * jit.cc       — per-template kernels: the template's bytecode translated to
+//                    straight-line HIP (registers become VGPR locals, constants
+//                    become immediates) and compiled with hipRTC for gfx950; this
+//                    header is embedded into the library and handed to hipRTC.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#endif
+
+#include "common.h"
+
+namespace gk {
+
+constexpr int HCAP = 128;   // heap words per lane (lists, big floats)
+constexpr int MAXLOOP = 16; // loop nesting levels with per-iteration heap reclamation
+constexpr int BCAP = 4096;  // byte buffer per lane (computed strings, staged messages)
+constexpr int EMCAP = 32;   // staged violation tuples per lane
+
+
+
+// ------------------------------------------------------------------ values
+__device__ __forceinline__ uint32_t vtag(uint64_t v) { return (uint32_t)(v >> 60); }
+__device__ __forceinline__ uint64_t vpay(uint64_t v) { return v & 0x0fffffffffffffffull; }
+__device__ __forceinline__ uint64_t mkv(uint32_t t, uint64_t p) { return ((uint64_t)t << 60) | (p & 0x0fffffffffffffffull); }
+__device__ __forceinline__ uint64_t mkint(int64_t i) { return mkv(V_INT, (uint64_t)i & 0x0000ffffffffffffull); }
+__device__ __forceinline__ int64_t intof(uint64_t v) {
+  uint64_t p = vpay(v) & 0x0000ffffffffffffull;
+  return (p & 0x0000800000000000ull) ? (int64_t)(p | 0xffff000000000000ull) : (int64_t)p;
+}
+__device__ __forceinline__ uint32_t list_kind(uint64_t v) { return (uint32_t)((v >> 56) & 0xf); }
+__device__ __forceinline__ uint64_t mklist(uint32_t kind, uint32_t off) { return mkv(V_LIST, ((uint64_t)kind << 56) | off); }
+__device__ __forceinline__ uint32_t list_off(uint64_t v) { return (uint32_t)(v & 0xffffffffu); }
+__device__ __forceinline__ uint64_t mkhstr(uint32_t off, uint32_t len) { return mkv(V_HSTR, ((uint64_t)off << 16) | len); }
+__device__ __forceinline__ uint64_t mkslice(uint32_t sid, uint32_t st, uint32_t len) {
+  return mkv(V_SLICE, ((uint64_t)sid << 28) | ((uint64_t)st << 14) | len);
+}
+__device__ __forceinline__ bool is_strv(uint64_t v) { uint32_t t = vtag(v); return t == V_STR || t == V_HSTR || t == V_SLICE; }
+__device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); return t == V_NUM || t == V_INT || t == V_BFN; }
+
+struct Lane {
+  uint64_t H[HCAP];
+  char B[BCAP];
+  uint32_t hp, bp, seq, fail;  // fail: 0 ok, RF_ERROR, RF_FALLBACK
+  uint32_t reason;
+  // per loop depth: heap / byte watermarks that values escaping the loop pinned
+  uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
+  // staged emissions: msg bytes then details JSON at B[off..off+mlen+dlen)
+  uint32_t en, steps;
+  uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP];
+};
+
+// a heap-resident value (must survive a loop's per-iteration heap reset when it
+// escapes to a register that outlives the iteration)
+__device__ __forceinline__ bool heap_val(uint64_t v) {
+  uint32_t t = v >> 60;
+  return t == V_LIST || t == V_BFN || t == V_HSTR;
+}
+__device__ __forceinline__ void pin_escape(Lane& L, uint32_t range) {
+  uint32_t lo = range & 0xff, hi = (range >> 8) & 0xff;
+  for (uint32_t d = lo; d <= hi && d < MAXLOOP; ++d) {
+    if (L.keepH[d] < L.hp) L.keepH[d] = (uint16_t)L.hp;
+    if (L.keepB[d] < L.bp) L.keepB[d] = (uint16_t)L.bp;
+  }
+}
+
+__device__ __forceinline__ void lane_fallback(Lane& L, uint32_t reason) {
+  if (!L.fail) { L.fail = RF_FALLBACK; L.reason = reason; }
+}
+__device__ __forceinline__ void lane_error(Lane& L) {
+  if (!L.fail) { L.fail = RF_ERROR; L.reason = 0; }
+}
+
+__device__ __forceinline__ uint64_t nodeval(const DevArgs& A, uint32_t idx) {
+  const Node& n = A.nodes[idx];
+  switch (n.type) {
+    case NT_NULL: return mkv(V_NULL, 0);
+    case NT_FALSE: return mkv(V_BOOL, 0);
+    case NT_TRUE: return mkv(V_BOOL, 1);
+    case NT_NUM: return mkv(V_NUM, n.val);
+    case NT_STR: return mkv(V_STR, n.val);
+    case NT_ARR: case NT_OBJ: return mkv(V_NODE, idx);
+  }
+  return mkv(V_UNDEF, 0);
+}
+
+// string bytes of a string value
+struct SView { const char* p; uint32_t n; };
+__device__ __forceinline__ SView sview(const DevArgs& A, const Lane& L, uint64_t v) {
+  uint32_t t = vtag(v);
+  if (t == V_STR) { const StrEnt& s = A.strs[(uint32_t)vpay(v)]; return SView{(const char*)A.pool + s.off, s.len}; }
+  if (t == V_HSTR) { uint64_t p = vpay(v); return SView{L.B + (uint32_t)(p >> 16), (uint32_t)(p & 0xffff)}; }
+  if (t == V_SLICE) {
+    uint64_t p = vpay(v);
+    const StrEnt& s = A.strs[(uint32_t)(p >> 28)];
+    return SView{(const char*)A.pool + s.off + (uint32_t)((p >> 14) & 0x3fff), (uint32_t)(p & 0x3fff)};
+  }
+  return SView{nullptr, 0};
+}
+__device__ __forceinline__ int bytes_cmp(SView a, SView b) {
+  uint32_t n = a.n < b.n ? a.n : b.n;
+  for (uint32_t i = 0; i < n; ++i) {
+    unsigned char x = (unsigned char)a.p[i], y = (unsigned char)b.p[i];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return a.n == b.n ? 0 : (a.n < b.n ? -1 : 1);
+}
+
+// ------------------------------------------------------------------ numbers
+// exact 64-bit-mantissa big-float view of a numeric value; returns false if unavailable
+struct BF { uint64_t m; int32_t e; bool neg; bool zero; };
+__device__ bool num_bf(const DevArgs& A, const Lane& L, uint64_t v, BF& out) {
+  uint32_t t = vtag(v);
+  if (t == V_NUM) {
+    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    if (!(n.flags & NF_BF_OK)) return false;
+    out.m = n.mant; out.e = n.exp; out.neg = n.neg != 0; out.zero = n.mant == 0;
+    return true;
+  }
+  if (t == V_INT) {
+    int64_t i = intof(v);
+    out.neg = i < 0;
+    uint64_t a = out.neg ? (uint64_t)(-i) : (uint64_t)i;
+    out.zero = a == 0;
+    if (out.zero) { out.m = 0; out.e = 0; return true; }
+    int lz = __builtin_clzll(a);
+    out.m = a << lz;
+    out.e = -lz;
+    return true;
+  }
+  if (t == V_BFN) {
+    uint32_t o = (uint32_t)vpay(v);
+    out.m = L.H[o];
+    uint64_t w = L.H[o + 1];
+    out.e = (int32_t)(uint32_t)w;
+    out.neg = (w >> 32) & 1;
+    out.zero = out.m == 0;
+    return true;
+  }
+  return false;
+}
+__device__ int bf_cmp(const BF& a, const BF& b) {
+  if (a.zero && b.zero) return 0;
+  if (a.zero) return b.neg ? 1 : -1;
+  if (b.zero) return a.neg ? -1 : 1;
+  if (a.neg != b.neg) return a.neg ? -1 : 1;
+  int mag;
+  if (a.e != b.e) mag = a.e < b.e ? -1 : 1;
+  else mag = a.m == b.m ? 0 : (a.m < b.m ? -1 : 1);
+  return a.neg ? -mag : mag;
+}
+// integer view: true if the value is an exact integer representable in int64
+__device__ bool num_int(const DevArgs& A, const Lane& L, uint64_t v, int64_t& out) {
+  uint32_t t = vtag(v);
+  if (t == V_INT) { out = intof(v); return true; }
+  if (t == V_NUM) {
+    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    if (n.flags & NF_INT64) { out = n.i; return true; }
+    BF b;
+    if (!num_bf(A, L, v, b)) return false;
+    if (b.zero) { out = 0; return true; }
+    if (b.e >= 0 || b.e < -63) return false;
+    uint64_t sh = (uint64_t)(-b.e);
+    if (b.m & ((1ull << sh) - 1)) return false;
+    uint64_t mag = b.m >> sh;
+    if (mag > (1ull << 62)) return false;
+    out = b.neg ? -(int64_t)mag : (int64_t)mag;
+    return true;
+  }
+  if (t == V_BFN) {
+    BF b;
+    num_bf(A, L, v, b);
+    if (b.zero) { out = 0; return true; }
+    if (b.e >= 0 || b.e < -63) return false;
+    uint64_t sh = (uint64_t)(-b.e);
+    if (b.m & ((1ull << sh) - 1)) return false;
+    uint64_t mag = b.m >> sh;
+    if (mag > (1ull << 62)) return false;
+    out = b.neg ? -(int64_t)mag : (int64_t)mag;
+    return true;
+  }
+  return false;
+}
+__device__ uint64_t heap_bf(Lane& L, const BF& b) {
+  if (L.hp + 2 > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
+  uint32_t o = L.hp;
+  L.hp += 2;
+  L.H[o] = b.zero ? 0 : b.m;
+  L.H[o + 1] = (uint64_t)(uint32_t)b.e | ((uint64_t)(b.neg ? 1 : 0) << 32);
+  return mkv(V_BFN, o);
+}
+// big.Float Mul at prec 64, ToNearestEven
+__device__ BF bf_mul(const BF& a, const BF& b) {
+  BF r;
+  r.neg = a.neg != b.neg;
+  if (a.zero || b.zero) { r.zero = true; r.m = 0; r.e = 0; r.neg = false; return r; }
+  r.zero = false;
+  uint64_t lo = a.m * b.m;
+  uint64_t hi = __umul64hi(a.m, b.m);
+  int32_t e = a.e + b.e;
+  // product in [2^126, 2^128): normalize hi to have top bit set
+  uint64_t m;
+  uint64_t rest;  // bits shifted out (as a 64-bit fraction, msb = half)
+  if (hi >> 63) { m = hi; rest = lo; e += 64; }
+  else { m = (hi << 1) | (lo >> 63); rest = lo << 1; e += 63; }
+  bool half = rest >> 63;
+  bool sticky = (rest << 1) != 0;
+  if (half && (sticky || (m & 1))) {
+    ++m;
+    if (m == 0) { m = 1ull << 63; ++e; }
+  }
+  r.m = m;
+  r.e = e;
+  return r;
+}
+
+// ------------------------------------------------------------------ lists
+__device__ __forceinline__ uint32_t list_len(const Lane& L, uint64_t v) { return (uint32_t)L.H[list_off(v)]; }
+__device__ __forceinline__ uint64_t list_at(const Lane& L, uint64_t v, uint32_t i) { return L.H[list_off(v) + 2 + i]; }
+
+__device__ uint64_t list_new(Lane& L, uint32_t kind, uint32_t cap) {
+  if (L.hp + 2 + cap > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
+  uint32_t o = L.hp;
+  L.H[o] = 0;
+  L.H[o + 1] = cap;
+  L.hp += 2 + cap;
+  return mklist(kind, o);
+}
+
+// value type ordering class (ast/compare.go sortOrder)
+__device__ __forceinline__ int tclass(const DevArgs& A, uint64_t v) {
+  switch (vtag(v)) {
+    case V_NULL: return 1;
+    case V_BOOL: return 2;
+    case V_NUM: case V_INT: case V_BFN: return 3;
+    case V_STR: case V_HSTR: case V_SLICE: return 4;
+    case V_NODE: return A.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
+    case V_LIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
+  }
+  return 0;
+}
+
+// collection view helpers (NODE arrays/objects and heap lists)
+__device__ uint32_t coll_len(const DevArgs& A, const Lane& L, uint64_t v) {
+  if (vtag(v) == V_NODE) return A.nodes[(uint32_t)vpay(v)].n;
+  if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
+  return 0;
+}
+// i-th (key, value) of a collection
+__device__ void coll_at(const DevArgs& A, const Lane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
+  if (vtag(v) == V_NODE) {
+    const Node& n = A.nodes[(uint32_t)vpay(v)];
+    uint32_t c = n.first + i;
+    val = nodeval(A, c);
+    k = n.type == NT_OBJ ? mkv(V_STR, A.nodes[c].key) : mkint(i);
+    return;
+  }
+  uint32_t kind = list_kind(v);
+  if (kind == LK_OBJ) { k = list_at(L, v, 2 * i); val = list_at(L, v, 2 * i + 1); return; }
+  val = list_at(L, v, i);
+  k = kind == LK_SET ? val : mkint(i);
+}
+
+// scalar compare within one type class (1..4); 2 = undecidable (fallback set)
+__device__ int scmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b, int cls) {
+  switch (cls) {
+    case 1: return 0;
+    case 2: { uint64_t x = vpay(a), y = vpay(b); return x == y ? 0 : (x < y ? -1 : 1); }
+    case 3: {
+      if (vtag(a) == V_NUM && vtag(b) == V_NUM && vpay(a) == vpay(b)) return 0;
+      BF x, y;
+      if (!num_bf(A, L, a, x) || !num_bf(A, L, b, y)) { lane_fallback(L, FB_NUMBER); return 2; }
+      return bf_cmp(x, y);
+    }
+    case 4: {
+      if (vtag(a) == V_STR && vtag(b) == V_STR && vpay(a) == vpay(b)) return 0;
+      return bytes_cmp(sview(A, L, a), sview(A, L, b));
+    }
+  }
+  return 2;
+}
+
+// element comparison inside a composite: scalars, or identical document nodes;
+// anything deeper is served by the CPU fallback
+__device__ int ecmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
+  int ca = tclass(A, a), cb = tclass(A, b);
+  if (ca != cb) return ca < cb ? -1 : 1;
+  if (ca <= 4) return scmp(A, L, a, b, ca);
+  if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
+  if (coll_len(A, L, a) == 0 && coll_len(A, L, b) == 0) return 0;
+  lane_fallback(L, FB_DEEP_EQ);
+  return 2;
+}
+
+// ast.Compare: -1/0/1; 3 = "not equal, order undefined here"; 2 = undecidable
+__device__ int vcmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
+  int ca = tclass(A, a), cb = tclass(A, b);
+  if (ca != cb) return ca < cb ? -1 : 1;
+  if (ca <= 4) return scmp(A, L, a, b, ca);
+  if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
+  uint32_t na = coll_len(A, L, a), nb = coll_len(A, L, b);
+  if (ca == 7) {
+    uint32_t n = na < nb ? na : nb;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint64_t k1, v1, k2, v2;
+      coll_at(A, L, a, i, k1, v1);
+      coll_at(A, L, b, i, k2, v2);
+      int c = ecmp(A, L, v1, v2);
+      if (c != 0) return c;
+    }
+    return na == nb ? 0 : (na < nb ? -1 : 1);
+  }
+  if (na != nb) return 3;
+  // objects / sets of equal size: equal iff every member of a is in b
+  for (uint32_t i = 0; i < na; ++i) {
+    uint64_t k1, v1;
+    coll_at(A, L, a, i, k1, v1);
+    bool found = false;
+    for (uint32_t j = 0; j < nb && !found; ++j) {
+      uint64_t k2, v2;
+      coll_at(A, L, b, j, k2, v2);
+      int c = ecmp(A, L, k1, k2);
+      if (c == 2) return 2;
+      if (c != 0) continue;
+      if (ca == 9) { found = true; break; }
+      int d = ecmp(A, L, v1, v2);
+      if (d == 2) return 2;
+      if (d != 0) return 3;
+      found = true;
+    }
+    if (!found) return 3;
+  }
+  return 0;
+}
+
+__device__ bool veq(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
+  if (a == b) {
+    uint32_t t = vtag(a);
+    if (t != V_HSTR && t != V_BFN) return true;
+  }
+  int c = vcmp(A, L, a, b);
+  return c == 0;
+}
+
+__device__ bool list_contains(const DevArgs& A, Lane& L, uint64_t l, uint64_t v) {
+  uint32_t n = list_len(L, l);
+  for (uint32_t i = 0; i < n; ++i) if (veq(A, L, list_at(L, l, i), v)) return true;
+  return false;
+}
+// append (sets dedupe); may relocate the list to the heap top when full
+__device__ uint64_t list_add(const DevArgs& A, Lane& L, uint64_t l, uint64_t v) {
+  if (vtag(l) != V_LIST) return l;
+  if (list_kind(l) == LK_SET && list_contains(A, L, l, v)) return l;
+  uint32_t o = list_off(l);
+  uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
+  if (n == cap) {
+    // grow: move to top of heap if this list is the last allocation, else copy
+    uint32_t ncap = cap < 4 ? 8 : cap * 2;
+    if (o + 2 + cap == L.hp) {
+      if (o + 2 + ncap > HCAP) { lane_fallback(L, FB_HEAP); return l; }
+      L.hp = o + 2 + ncap;
+      L.H[o + 1] = ncap;
+    } else {
+      if (L.hp + 2 + ncap > HCAP) { lane_fallback(L, FB_HEAP); return l; }
+      uint32_t no = L.hp;
+      L.hp += 2 + ncap;
+      for (uint32_t i = 0; i < n + 2; ++i) L.H[no + i] = L.H[o + i];
+      L.H[no + 1] = ncap;
+      o = no;
+      l = mklist(list_kind(l), o);
+    }
+  }
+  L.H[o + 2 + n] = v;
+  L.H[o] = n + 1;
+  return l;
+}
+
+// ------------------------------------------------------------------ get
+__device__ uint64_t vget(const DevArgs& A, Lane& L, uint64_t c, uint64_t key) {
+  uint32_t t = vtag(c);
+  if (t == V_NODE) {
+    const Node& n = A.nodes[(uint32_t)vpay(c)];
+    if (n.flags & 1) { lane_fallback(L, FB_UNSUPPORTED); return mkv(V_UNDEF, 0); }
+    if (n.type == NT_OBJ) {
+      uint32_t kt = vtag(key);
+      if (kt == V_STR) {
+        uint32_t id = (uint32_t)vpay(key);
+        for (uint32_t i = 0; i < n.n; ++i) if (A.nodes[n.first + i].key == id) return nodeval(A, n.first + i);
+        return mkv(V_UNDEF, 0);
+      }
+      if (kt == V_HSTR || kt == V_SLICE) {
+        SView kv = sview(A, L, key);
+        for (uint32_t i = 0; i < n.n; ++i) {
+          const StrEnt& s = A.strs[A.nodes[n.first + i].key];
+          if (bytes_cmp(kv, SView{(const char*)A.pool + s.off, s.len}) == 0) return nodeval(A, n.first + i);
+        }
+      }
+      return mkv(V_UNDEF, 0);
+    }
+    if (n.type == NT_ARR) {
+      if (!is_numv(key)) return mkv(V_UNDEF, 0);
+      int64_t i;
+      if (!num_int(A, L, key, i)) return mkv(V_UNDEF, 0);
+      if (i < 0 || i >= n.n) return mkv(V_UNDEF, 0);
+      return nodeval(A, n.first + (uint32_t)i);
+    }
+    return mkv(V_UNDEF, 0);
+  }
+  if (t == V_LIST) {
+    uint32_t kind = list_kind(c);
+    uint32_t n = list_len(L, c);
+    if (kind == LK_SET) return list_contains(A, L, c, key) ? key : mkv(V_UNDEF, 0);
+    if (kind == LK_ARR) {
+      if (!is_numv(key)) return mkv(V_UNDEF, 0);
+      int64_t i;
+      if (!num_int(A, L, key, i) || i < 0 || i >= n) return mkv(V_UNDEF, 0);
+      return list_at(L, c, (uint32_t)i);
+    }
+    for (uint32_t i = 0; i + 1 < n; i += 2) if (veq(A, L, list_at(L, c, i), key)) return list_at(L, c, i + 1);
+    return mkv(V_UNDEF, 0);
+  }
+  return mkv(V_UNDEF, 0);
+}
+
+// ------------------------------------------------------------------ printing
+struct Out {
+  char* p;
+  uint32_t n, cap;
+  bool ovf;
+};
+__device__ __forceinline__ void put(Out& o, char c) { if (o.n < o.cap) o.p[o.n++] = c; else o.ovf = true; }
+__device__ __forceinline__ void puts_(Out& o, const char* s, uint32_t n) { for (uint32_t i = 0; i < n; ++i) put(o, s[i]); }
+__device__ void put_cstr(Out& o, const char* s) { while (*s) put(o, *s++); }
+__device__ void put_int(Out& o, int64_t v) {
+  char t[24];
+  int n = 0;
+  uint64_t a = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+  do { t[n++] = (char)('0' + a % 10); a /= 10; } while (a);
+  if (v < 0) put(o, '-');
+  while (n) put(o, t[--n]);
+}
+__device__ void put_sid(const DevArgs& A, Out& o, uint32_t sid) {
+  const StrEnt& s = A.strs[sid];
+  puts_(o, (const char*)A.pool + s.off, s.len);
+}
+__device__ const char* hexd = "0123456789abcdef";
+
+// strconv.Quote; returns false if a non-ASCII byte needs unicode.IsPrint
+__device__ bool put_quoted(Out& o, SView s) {
+  put(o, '"');
+  for (uint32_t i = 0; i < s.n; ++i) {
+    unsigned char c = (unsigned char)s.p[i];
+    if (c >= 0x80) return false;
+    if (c == '"' || c == '\\') { put(o, '\\'); put(o, (char)c); continue; }
+    if (c >= 0x20 && c < 0x7f) { put(o, (char)c); continue; }
+    switch (c) {
+      case '\a': put_cstr(o, "\\a"); break;
+      case '\b': put_cstr(o, "\\b"); break;
+      case '\f': put_cstr(o, "\\f"); break;
+      case '\n': put_cstr(o, "\\n"); break;
+      case '\r': put_cstr(o, "\\r"); break;
+      case '\t': put_cstr(o, "\\t"); break;
+      case '\v': put_cstr(o, "\\v"); break;
+      default: put_cstr(o, "\\x"); put(o, hexd[c >> 4]); put(o, hexd[c & 15]); break;
+    }
+  }
+  put(o, '"');
+  return true;
+}
+
+// encoding/json string (HTMLEscape); false on non-ASCII
+__device__ bool put_json_str(Out& o, SView s) {
+  put(o, '"');
+  for (uint32_t i = 0; i < s.n; ++i) {
+    unsigned char c = (unsigned char)s.p[i];
+    if (c >= 0x80) return false;
+    if (c == '"') { put_cstr(o, "\\\""); continue; }
+    if (c == '\\') { put_cstr(o, "\\\\"); continue; }
+    if (c == '\n') { put_cstr(o, "\\n"); continue; }
+    if (c == '\r') { put_cstr(o, "\\r"); continue; }
+    if (c == '\t') { put_cstr(o, "\\t"); continue; }
+    if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+      put_cstr(o, "\\u00"); put(o, hexd[c >> 4]); put(o, hexd[c & 15]);
+      continue;
+    }
+    put(o, (char)c);
+  }
+  put(o, '"');
+  return true;
+}
+
+// scalar Term.String()/JSON; returns 0 not-scalar, 1 ok, -1 fallback
+__device__ int put_scalar(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool json) {
+  switch (vtag(v)) {
+    case V_UNDEF: if (json) { put_cstr(o, "{}"); return 1; } return -1;
+    case V_NULL: put_cstr(o, "null"); return 1;
+    case V_BOOL: put_cstr(o, vpay(v) ? "true" : "false"); return 1;
+    case V_NUM: put_sid(A, o, A.nums[(uint32_t)vpay(v)].text); return 1;
+    case V_INT: put_int(o, intof(v)); return 1;
+    case V_BFN: return -1;
+    case V_STR: case V_HSTR: case V_SLICE:
+      return (json ? put_json_str(o, sview(A, L, v)) : put_quoted(o, sview(A, L, v))) ? 1 : -1;
+    default: return 0;
+  }
+}
+
+struct PFrame { uint64_t v; uint32_t i, n; uint64_t last; int cls; };
+
+// ast.Term.String() (json=false) or encoding/json of ast.JSON (json=true, map
+// keys in byte order), iterative with an explicit stack; false => fallback
+__device__ bool put_value(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool json) {
+  int r = put_scalar(A, L, o, v, json);
+  if (r != 0) return r > 0;
+  PFrame st[8];
+  int sp = 0;
+  st[0] = PFrame{v, 0, coll_len(A, L, v), 0, tclass(A, v)};
+  if (!json && st[0].cls == 9 && st[0].n == 0) { put_cstr(o, "set()"); return true; }
+  put(o, (st[0].cls == 7 || (json && st[0].cls == 9)) ? '[' : '{');
+  while (sp >= 0) {
+    PFrame& f = st[sp];
+    if (f.i >= f.n) {
+      put(o, (f.cls == 7 || (json && f.cls == 9)) ? ']' : '}');
+      --sp;
+      continue;
+    }
+    if (f.i) { put(o, ','); if (!json) put(o, ' '); }
+    uint64_t k, val;
+    if (json && f.cls == 8) {
+      // next key in byte order after f.last
+      int best = -1;
+      uint64_t bk = 0;
+      for (uint32_t j = 0; j < f.n; ++j) {
+        uint64_t kk, vv;
+        coll_at(A, L, f.v, j, kk, vv);
+        if (!is_strv(kk)) return false;
+        if (f.i && bytes_cmp(sview(A, L, kk), sview(A, L, f.last)) <= 0) continue;
+        if (best < 0 || bytes_cmp(sview(A, L, kk), sview(A, L, bk)) < 0) { best = (int)j; bk = kk; }
+      }
+      if (best < 0) return false;
+      coll_at(A, L, f.v, (uint32_t)best, k, val);
+      f.last = k;
+    } else {
+      coll_at(A, L, f.v, f.i, k, val);
+    }
+    f.i++;
+    if (f.cls == 8) {
+      if (put_scalar(A, L, o, k, json) <= 0) return false;
+      put(o, ':');
+      if (!json) put(o, ' ');
+    }
+    int rs = put_scalar(A, L, o, val, json);
+    if (rs < 0) return false;
+    if (rs == 0) {
+      if (sp + 1 >= 8) return false;
+      int cls = tclass(A, val);
+      uint32_t n = coll_len(A, L, val);
+      if (!json && cls == 9 && n == 0) { put_cstr(o, "set()"); continue; }
+      st[++sp] = PFrame{val, 0, n, 0, cls};
+      put(o, (cls == 7 || (json && cls == 9)) ? '[' : '{');
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool put_term(const DevArgs& A, Lane& L, Out& o, uint64_t v) { return put_value(A, L, o, v, false); }
+__device__ __forceinline__ bool put_json(const DevArgs& A, Lane& L, Out& o, uint64_t v) { return put_value(A, L, o, v, true); }
+
+// Go fmt conversion of one sprintf argument (topdown/strings.go:355-367)
+__device__ bool put_fmt_arg(const DevArgs& A, Lane& L, Out& o, uint64_t v, uint32_t verb) {
+  uint32_t t = vtag(v);
+  if (t == V_STR || t == V_HSTR || t == V_SLICE) {
+    SView s = sview(A, L, v);
+    if (verb == 'd') { put_cstr(o, "%!d(string="); puts_(o, s.p, s.n); put(o, ')'); return true; }
+    puts_(o, s.p, s.n);
+    return true;
+  }
+  if (t == V_NUM) {
+    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    if (n.flags & NF_INT64) {
+      if (verb == 's') { put_cstr(o, "%!s(int="); put_int(o, n.i); put(o, ')'); return true; }
+      put_int(o, n.i);
+      return true;
+    }
+    if (verb != 'v') return false;
+    put_sid(A, o, n.print);
+    return true;
+  }
+  if (t == V_INT) {
+    if (verb == 's') { put_cstr(o, "%!s(int="); put_int(o, intof(v)); put(o, ')'); return true; }
+    put_int(o, intof(v));
+    return true;
+  }
+  if (t == V_BFN) return false;
+  // everything else is formatted as Term.String() (a Go string)
+  if (verb == 'd') return false;
+  return put_term(A, L, o, v);
+}
+
+// ------------------------------------------------------------------ regex
+// DFA layout at dfa_words[off]: [nstates, start, then per state: accept flags
+// word, 256 transitions (u16 packed 2 per word)]; accept flags: bit0 = match
+// already found (sticky), bit1 = accepting at end of text.
+__device__ int re_lookup(const DevArgs& A, uint32_t sid) {
+  int lo = 0, hi = (int)A.ndfa - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) >> 1;
+    uint32_t k = A.dfa_keys[mid];
+    if (k == sid) return mid;
+    if (k < sid) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
+// returns 1 match, 0 no match, -1 error (invalid pattern), -2 fallback
+__device__ int re_run(const DevArgs& A, const Lane& L, uint64_t pat, uint64_t val) {
+  if (vtag(pat) != V_STR) return -2;
+  int e = re_lookup(A, (uint32_t)vpay(pat));
+  if (e < 0) return -2;
+  uint32_t meta = A.dfa_meta[e];
+  uint32_t status = meta >> 30;
+  if (status == 1) return -1;
+  if (status == 2) return -2;
+  const uint32_t* d = A.dfa_words + (meta & 0x3fffffffu);
+  uint32_t nst = d[0];
+  uint32_t s = d[1];
+  uint32_t utf8_sensitive = d[2];
+  const uint32_t* st = d + 3;
+  SView v = sview(A, L, val);
+  const uint32_t stride = 1 + 128;
+  for (uint32_t i = 0; i < v.n; ++i) {
+    unsigned char c = (unsigned char)v.p[i];
+    if (c >= 0x80 && utf8_sensitive) return -2;
+    const uint32_t* row = st + s * stride;
+    if (row[0] & 1) return 1;
+    uint32_t w = row[1 + (c >> 1)];
+    s = (c & 1) ? (w >> 16) : (w & 0xffff);
+    if (s >= nst) return 0;  // dead state
+  }
+  const uint32_t* row = st + s * stride;
+  return (row[0] & 3) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ match
+__device__ __forceinline__ bool label_lookup(const DevArgs& A, uint32_t labels, uint32_t key, uint32_t& val) {
+  if (labels == NO_ID) return false;
+  const Node& n = A.nodes[labels];
+  for (uint32_t i = 0; i < n.n; ++i) {
+    const Node& c = A.nodes[n.first + i];
+    if (c.key == key) { val = c.val; return true; }
+  }
+  return false;
+}
+
+// matches_label_selector (target_template_source.go:185-230) over a labels node
+// whose values are all strings (validated by the host).  Returns 1/0, or -1 error.
+__device__ int sel_match(const DevArgs& A, const uint32_t* w, uint32_t labels) {
+  uint32_t flags = w[0];
+  if (flags & 2) return -1;         // count() of a non-collection
+  if (flags & 1) return 0;          // never satisfiable
+  uint32_t nml = w[1];
+  const uint32_t* p = w + 2;
+  bool ok = true;
+  for (uint32_t i = 0; i < nml; ++i) {
+    uint32_t k = p[2 * i], v = p[2 * i + 1], lv;
+    if (!(label_lookup(A, labels, k, lv) && lv == v)) ok = false;
+  }
+  p += 2 * nml;
+  if (!ok) return 0;
+  uint32_t nex = *p++;
+  bool violated = false;
+  for (uint32_t e = 0; e < nex; ++e) {
+    uint32_t op = p[0], key = p[1], vflags = p[2], nv = p[3];
+    const uint32_t* vals = p + 4;
+    p += 4 + nv;
+    uint32_t lv = 0;
+    bool has = key != NO_ID && label_lookup(A, labels, key, lv);
+    if (op == SO_IN || op == SO_NOTIN) {
+      if (vflags & 2) return -1;      // count(values) type error
+      bool nonempty = vflags & 1;
+      bool inset = false;
+      if (has) for (uint32_t j = 0; j < nv; ++j) if (vals[j] == lv) inset = true;
+      if (op == SO_IN) {
+        if (!has) violated = true;
+        if (nonempty && has && !inset) violated = true;
+      } else {
+        if (nonempty && has && inset) violated = true;
+      }
+    } else if (op == SO_EXISTS) {
+      if (!has) violated = true;
+    } else if (op == SO_DOESNOTEXIST) {
+      if (has) violated = true;
+    }
+  }
+  return violated ? 0 : 1;
+}
+
+// any_labelselector_match over the review's object / oldObject labels
+__device__ int any_sel(const DevArgs& A, const uint32_t* w, const ReviewCol& rc) {
+  bool uo = rc.flags & RC_LABELS_OBJ, ul = rc.flags & RC_LABELS_OLD;
+  if (!uo && !ul) return sel_match(A, w, NO_ID);
+  int r = 0;
+  if (uo) { int x = sel_match(A, w, rc.labels); if (x < 0) return -1; r |= x; }
+  if (ul) { int x = sel_match(A, w, rc.old_labels); if (x < 0) return -1; r |= x; }
+  return r;
+}
+
+// 1 = match, 0 = no match, -1 = error (query fails), -2 = fallback
+__device__ int match_constraint(const DevArgs& A, const MatchSpec& m, const ReviewCol& rc) {
+  if (m.flags & MF_FALLBACK) return -2;
+  if (!(rc.flags & RC_REVIEW_DEF)) return 0;
+  const uint32_t* W = A.mwords;
+  // kinds
+  {
+    const uint32_t* k = W + m.kinds_off;
+    uint32_t nsel = *k++;
+    bool any = false;
+    for (uint32_t s = 0; s < nsel; ++s) {
+      uint32_t ng = *k++;
+      bool gm = false;
+      for (uint32_t i = 0; i < ng; ++i) { uint32_t g = k[i]; if (g == 0xfffffffeu || (g == rc.group && g != NO_ID)) gm = true; }
+      k += ng;
+      uint32_t nk = *k++;
+      bool km = false;
+      for (uint32_t i = 0; i < nk; ++i) { uint32_t x = k[i]; if (x == 0xfffffffeu || (x == rc.kind && x != NO_ID)) km = true; }
+      k += nk;
+      if (gm && km) any = true;
+    }
+    if (!any) return 0;
+  }
+  bool kind_def = rc.flags & RC_KIND_OK;
+  bool is_ns = rc.flags & RC_IS_NS;
+  bool always = kind_def && !is_ns && (rc.flags & RC_NS_EMPTY);
+  // namespaces / excludedNamespaces
+  if (m.flags & MF_HAS_NAMESPACES) {
+    if (!always) {
+      if (!kind_def || rc.nsname == NO_ID) return 0;
+      const uint32_t* l = W + m.ns_off;
+      bool in = false;
+      for (uint32_t i = 0; i < l[0]; ++i) if (l[1 + i] == rc.nsname) in = true;
+      if (!in) return 0;
+    }
+  }
+  if (m.flags & MF_HAS_EXCLUDED) {
+    if (!always) {
+      if (!kind_def || rc.nsname == NO_ID) return 0;
+      const uint32_t* l = W + m.exns_off;
+      for (uint32_t i = 0; i < l[0]; ++i) if (l[1 + i] == rc.nsname) return 0;
+    }
+  }
+  // namespaceSelector
+  if (m.flags & MF_HAS_NSSEL) {
+    if (!always) {
+      if (!kind_def) return 0;
+      const uint32_t* w = W + m.nssel_off;
+      int r;
+      if (is_ns) r = any_sel(A, w, rc);
+      else {
+        if (rc.ns_labels == NO_ID && !(rc.flags & (RC_UNSTABLE_NS | RC_NS_CACHED))) return 0;
+        r = sel_match(A, w, rc.ns_labels);
+      }
+      if (r < 0) return -1;
+      if (!r) return 0;
+    }
+  }
+  // scope
+  if (m.flags & MF_SCOPE_PRESENT) {
+    bool ok = (m.flags & MF_SCOPE_ANY) || ((m.flags & MF_SCOPE_NS) && !(rc.flags & RC_NS_EMPTY)) ||
+              ((m.flags & MF_SCOPE_CLUSTER) && (rc.flags & RC_NS_EMPTY));
+    if (!ok) return 0;
+  }
+  // labelSelector
+  {
+    int r = any_sel(A, W + m.labelsel_off, rc);
+    if (r < 0) return -1;
+    if (!r) return 0;
+  }
+  return 1;
+}
+
+// ------------------------------------------------------------------ emit
+// A violation is staged in the lane (bytes pinned in L.B against every
+// enclosing loop's per-iteration reset); output space is reserved once per
+// wavefront at the end of the kernel (flush_wave), so the global tuple/byte
+// cursors see one atomic per wave instead of one per violation.
+__device__ void stage_tuple(Lane& L, uint32_t rule, const char* msg, uint32_t mlen, const char* det, uint32_t dlen,
+                            uint32_t depth) {
+  if (L.en >= EMCAP || L.bp + mlen + dlen > BCAP) { lane_fallback(L, FB_MSG_LEN); return; }
+  uint32_t off = L.bp;
+  // det may already sit at B[bp + ...] (formatted in place): move it up first
+  char* B = L.B;
+  if (det == B + off) {
+    for (uint32_t i = dlen; i-- > 0;) B[off + mlen + i] = det[i];
+  } else {
+    for (uint32_t i = 0; i < dlen; ++i) B[off + mlen + i] = det[i];
+  }
+  for (uint32_t i = 0; i < mlen; ++i) B[off + i] = msg[i];
+  L.bp = off + mlen + dlen;
+  L.em_rule[L.en] = (uint16_t)rule;
+  L.em_off[L.en] = (uint16_t)off;
+  L.em_mlen[L.en] = (uint16_t)mlen;
+  L.em_dlen[L.en] = (uint16_t)dlen;
+  ++L.en;
+  // only the staged bytes escape: the iteration's list heap stays reclaimable
+  for (uint32_t d = 1; d <= depth && d < MAXLOOP; ++d)
+    if (L.keepB[d] < L.bp) L.keepB[d] = (uint16_t)L.bp;
+}
+
+// wave-wide exclusive prefix sum (all 64 lanes must be active)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t& total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+__device__ void flush_wave(const DevArgs& A, Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
+  uint32_t nt = keep ? L.en : 0, nb = 0;
+  if (keep)
+    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + L.em_dlen[i];
+  uint32_t tt, tb;
+  uint32_t pt = wave_excl_scan(nt, lane, tt);
+  uint32_t pb = wave_excl_scan(nb, lane, tb);
+  uint32_t bt = 0, bb = 0;
+  if (lane == 63 && tt) {
+    bt = atomicAdd(&A.counters[0], tt);
+    bb = atomicAdd(&A.counters[1], tb);
+    atomicAdd(&A.totals[c], tt);
+  }
+  if (!tt) return;
+  bt = __shfl(bt, 63, 64) + pt;
+  bb = __shfl(bb, 63, 64) + pb;
+  if (!nt) return;
+  if (bt + nt > A.out_cap || bb + nb > A.bytes_cap) {
+    atomicOr(&A.rflags[r], (uint32_t)RF_OVERFLOW);
+    return;
+  }
+  for (uint32_t i = 0; i < nt; ++i) {
+    uint32_t ml = L.em_mlen[i], dl = L.em_dlen[i], o = L.em_off[i];
+    for (uint32_t j = 0; j < ml + dl; ++j) A.bytes[bb + j] = L.B[o + j];
+    Viol v;
+    v.review = r;
+    v.constraint = c;
+    v.seq = i;
+    v.rule = L.em_rule[i];
+    v.msg_off = bb;
+    v.msg_len = ml;
+    v.det_off = bb + ml;
+    v.det_len = dl;
+    A.out[bt + i] = v;
+    bb += ml + dl;
+  }
+}
+
+// ------------------------------------------------------------------ builtins
+__device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const uint64_t* a) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  switch (id) {
+    case BI_COUNT: {
+      uint32_t t = vtag(a[0]);
+      if (t == V_NODE || t == V_LIST) return mkint(coll_len(A, L, a[0]));
+      if (is_strv(a[0])) return mkint(sview(A, L, a[0]).n);
+      lane_error(L);
+      return UND;
+    }
+    case BI_ANY: case BI_ALL: {
+      int cls = tclass(A, a[0]);
+      if (cls != 7 && cls != 9) { lane_error(L); return UND; }
+      uint32_t n = coll_len(A, L, a[0]);
+      bool any = false, all = true;
+      for (uint32_t i = 0; i < n; ++i) {
+        uint64_t k, v;
+        coll_at(A, L, a[0], i, k, v);
+        bool t = vtag(v) == V_BOOL && vpay(v) == 1;
+        any |= t;
+        all &= t;
+      }
+      return mkv(V_BOOL, id == BI_ANY ? any : all);
+    }
+    case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS: {
+      if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
+      SView s = sview(A, L, a[0]), p = sview(A, L, a[1]);
+      if (p.n > s.n) return mkv(V_BOOL, 0);
+      if (id == BI_STARTSWITH) { for (uint32_t i = 0; i < p.n; ++i) if (s.p[i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
+      if (id == BI_ENDSWITH) { uint32_t o = s.n - p.n; for (uint32_t i = 0; i < p.n; ++i) if (s.p[o + i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
+      for (uint32_t o = 0; o + p.n <= s.n; ++o) {
+        bool m = true;
+        for (uint32_t i = 0; i < p.n && m; ++i) if (s.p[o + i] != p.p[i]) m = false;
+        if (m) return mkv(V_BOOL, 1);
+      }
+      return mkv(V_BOOL, 0);
+    }
+    case BI_RE_MATCH: {
+      if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
+      int r = re_run(A, L, a[0], a[1]);
+      if (r == -1) { lane_error(L); return UND; }
+      if (r == -2) { lane_fallback(L, FB_REGEX); return UND; }
+      return mkv(V_BOOL, r);
+    }
+    case BI_TO_NUMBER: {
+      uint32_t t = vtag(a[0]);
+      if (t == V_NULL) return mkint(0);
+      if (t == V_BOOL) return mkint((int64_t)vpay(a[0]));
+      if (is_numv(a[0])) return a[0];
+      if (!is_strv(a[0])) { lane_error(L); return UND; }
+      SView s = sview(A, L, a[0]);
+      // strconv.ParseFloat: plain decimal integers are exact; other valid
+      // forms are served by the CPU fallback; invalid syntax is an error.
+      uint32_t i = 0;
+      bool neg = false;
+      if (i < s.n && (s.p[i] == '+' || s.p[i] == '-')) { neg = s.p[i] == '-'; ++i; }
+      if (i >= s.n) { lane_error(L); return UND; }
+      bool digits_only = true, any_digit = false, dot = false, ex = false, bad = false;
+      for (uint32_t j = i; j < s.n; ++j) {
+        char c = s.p[j];
+        if (c >= '0' && c <= '9') { any_digit = true; continue; }
+        digits_only = false;
+        if (c == '.' && !dot && !ex) { dot = true; continue; }
+        if ((c == 'e' || c == 'E') && any_digit && !ex) { ex = true; if (j + 1 < s.n && (s.p[j + 1] == '+' || s.p[j + 1] == '-')) ++j; continue; }
+        if (c == 'i' || c == 'I' || c == 'n' || c == 'N' || c == 'x' || c == 'X' || c == '_' || c == 'p' || c == 'P') { lane_fallback(L, FB_NUMBER); return UND; }
+        bad = true;
+      }
+      if (bad || !any_digit) { lane_error(L); return UND; }
+      if (!digits_only || s.n - i > 15) { lane_fallback(L, FB_NUMBER); return UND; }
+      int64_t v = 0;
+      for (uint32_t j = i; j < s.n; ++j) v = v * 10 + (s.p[j] - '0');
+      return mkint(neg ? -v : v);
+    }
+    case BI_REPLACE: {
+      if (!is_strv(a[0]) || !is_strv(a[1]) || !is_strv(a[2])) { lane_error(L); return UND; }
+      SView s = sview(A, L, a[0]), old = sview(A, L, a[1]), nw = sview(A, L, a[2]);
+      if (old.n == 0) { lane_fallback(L, FB_STRING); return UND; }
+      uint32_t start = L.bp;
+      for (uint32_t i = 0; i < s.n;) {
+        bool m = i + old.n <= s.n;
+        for (uint32_t j = 0; j < old.n && m; ++j) if (s.p[i + j] != old.p[j]) m = false;
+        if (m) {
+          for (uint32_t j = 0; j < nw.n; ++j) { if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; } L.B[L.bp++] = nw.p[j]; }
+          i += old.n;
+        } else {
+          if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; }
+          L.B[L.bp++] = s.p[i++];
+        }
+      }
+      return mkhstr(start, L.bp - start);
+    }
+    case BI_SUBSTRING: {
+      if (!is_strv(a[0])) { lane_error(L); return UND; }
+      int64_t st, ln;
+      if (!is_numv(a[1]) || !num_int(A, L, a[1], st)) { lane_error(L); return UND; }
+      SView s = sview(A, L, a[0]);
+      if (st >= (int64_t)s.n) return mkv(V_STR, 0);  // "" is string id 0
+      if (st < 0) { lane_error(L); return UND; }
+      if (!is_numv(a[2]) || !num_int(A, L, a[2], ln)) { lane_error(L); return UND; }
+      uint32_t end = ln < 0 ? s.n : (uint32_t)((st + ln) < (int64_t)s.n ? (st + ln) : s.n);
+      uint32_t len = end - (uint32_t)st;
+      if (vtag(a[0]) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a[0]), (uint32_t)st, len);
+      if (vtag(a[0]) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + (uint32_t)st, len);
+      if (vtag(a[0]) == V_SLICE) {
+        uint64_t p = vpay(a[0]);
+        return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + (uint32_t)st, len);
+      }
+      lane_fallback(L, FB_STRING);
+      return UND;
+    }
+    case BI_IS_NUMBER: return mkv(V_BOOL, is_numv(a[0]));
+    case BI_IS_STRING: return mkv(V_BOOL, is_strv(a[0]));
+    case BI_IS_BOOLEAN: return mkv(V_BOOL, vtag(a[0]) == V_BOOL);
+    case BI_IS_NULL: return mkv(V_BOOL, vtag(a[0]) == V_NULL);
+    case BI_IS_ARRAY: return mkv(V_BOOL, tclass(A, a[0]) == 7);
+    case BI_IS_OBJECT: return mkv(V_BOOL, tclass(A, a[0]) == 8);
+    case BI_IS_SET: return mkv(V_BOOL, tclass(A, a[0]) == 9);
+    default: break;
+  }
+  lane_fallback(L, FB_UNSUPPORTED);
+  return UND;
+}
+
+__device__ uint64_t arith(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  if (kind == AR_MINUS && tclass(A, x) == 9 && tclass(A, y) == 9) {
+    uint64_t out = list_new(L, LK_SET, coll_len(A, L, x));
+    if (vtag(out) == V_UNDEF) return UND;
+    uint32_t n = coll_len(A, L, x);
+    for (uint32_t i = 0; i < n; ++i) {
+      uint64_t k, v;
+      coll_at(A, L, x, i, k, v);
+      if (!list_contains(A, L, y, v)) out = list_add(A, L, out, v);
+    }
+    return out;
+  }
+  if ((kind == AR_OR || kind == AR_AND)) {
+    if (tclass(A, x) != 9 || tclass(A, y) != 9) { lane_error(L); return UND; }
+    uint32_t nx = coll_len(A, L, x), ny = coll_len(A, L, y);
+    uint64_t out = list_new(L, LK_SET, nx + ny);
+    if (vtag(out) == V_UNDEF) return UND;
+    for (uint32_t i = 0; i < nx; ++i) {
+      uint64_t k, v;
+      coll_at(A, L, x, i, k, v);
+      if (kind == AR_OR || list_contains(A, L, y, v)) out = list_add(A, L, out, v);
+    }
+    if (kind == AR_OR)
+      for (uint32_t i = 0; i < ny; ++i) { uint64_t k, v; coll_at(A, L, y, i, k, v); out = list_add(A, L, out, v); }
+    return out;
+  }
+  if (!is_numv(x) || !is_numv(y)) { lane_error(L); return UND; }
+  int64_t a, b;
+  bool ints = num_int(A, L, x, a) && num_int(A, L, y, b);
+  const int64_t LIM = (1ll << 46);
+  switch (kind) {
+    case AR_PLUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint(a + b); break;
+    case AR_MINUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint(a - b); break;
+    case AR_MUL: {
+      if (ints && a < (1ll << 23) && a > -(1ll << 23) && b < (1ll << 23) && b > -(1ll << 23)) return mkint(a * b);
+      BF p, q;
+      if (!num_bf(A, L, x, p) || !num_bf(A, L, y, q)) { lane_fallback(L, FB_NUMBER); return UND; }
+      return heap_bf(L, bf_mul(p, q));
+    }
+    case AR_REM: {
+      if (!ints) { lane_error(L); return UND; }
+      if (b == 0) { lane_error(L); return UND; }
+      return mkint(a % b);
+    }
+    default: break;
+  }
+  lane_fallback(L, FB_NUMBER);
+  return UND;
+}
+
+// ------------------------------------------------------------------ sprintf
+__device__ uint64_t do_sprintf(const DevArgs& A, Lane& L, uint32_t fidx, uint64_t args) {
+  const uint32_t* f = A.fmt + fidx;
+  uint32_t nseg = f[0], want = f[1];
+  if (tclass(A, args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
+  uint32_t nargs = coll_len(A, L, args);
+  if (nargs != want) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
+  Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
+  for (uint32_t s = 0; s < nseg; ++s) {
+    uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
+    if (kind == 0) { put_sid(A, o, a); continue; }
+    uint64_t k, v;
+    coll_at(A, L, args, a & 0xffff, k, v);
+    if (!put_fmt_arg(A, L, o, v, a >> 16)) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
+  }
+  if (o.ovf) { lane_fallback(L, FB_MSG_LEN); return mkv(V_UNDEF, 0); }
+  uint32_t start = L.bp;
+  L.bp += o.n;
+  return mkhstr(start, o.n);
+}
+
+// ------------------------------------------------------------------ ops
+// Per-instruction semantics (OP_* in common.h).  The VM dispatches to these
+// from its switch; the JIT emits one call per instruction with register
+// operands bound to locals.  A `false` return means "leave the program".
+__device__ __forceinline__ void op_iter_init(Lane& L, uint64_t& it, uint64_t& st, uint64_t coll, uint32_t y) {
+  it = coll;
+  st = ((uint64_t)L.hp << 32) | ((uint64_t)L.bp << 48);
+  uint32_t d = y < MAXLOOP ? y : 0;
+  L.keepH[d] = 0;
+  L.keepB[d] = 0;
+}
+
+// advances the iterator; false when exhausted (jump to the loop exit)
+__device__ __forceinline__ bool op_iter_next(const DevArgs& A, Lane& L, uint64_t coll, uint64_t& st, uint32_t y,
+                                             uint64_t& k, uint64_t& v) {
+  uint32_t pos = (uint32_t)st;
+  // per-iteration reclamation: everything allocated by the previous
+  // iteration is dead unless it escaped this loop
+  uint32_t d = y < MAXLOOP ? y : 0;
+  uint32_t mh = (uint32_t)((st >> 32) & 0xffff), mb = (uint32_t)(st >> 48);
+  L.hp = mh > L.keepH[d] ? mh : L.keepH[d];
+  L.bp = mb > L.keepB[d] ? mb : L.keepB[d];
+  uint32_t t = vtag(coll);
+  if ((t != V_NODE && t != V_LIST) || pos >= coll_len(A, L, coll)) return false;
+  coll_at(A, L, coll, pos, k, v);
+  st = (st & 0xffffffff00000000ull) | (pos + 1);
+  return true;
+}
+
+__device__ __forceinline__ bool op_cmp(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
+  if (vtag(x) == V_UNDEF || vtag(y) == V_UNDEF) { out = mkv(V_UNDEF, 0); return true; }
+  int cr = vcmp(A, L, x, y);
+  if (cr == 2) return false;
+  if (cr == 3 && kind != CMP_EQ && kind != CMP_NE) { lane_fallback(L, FB_DEEP_EQ); return false; }
+  bool res = false;
+  switch (kind) {
+    case CMP_EQ: res = cr == 0; break;
+    case CMP_NE: res = cr != 0; break;
+    case CMP_LT: res = cr < 0; break;
+    case CMP_LE: res = cr <= 0; break;
+    case CMP_GT: res = cr > 0; break;
+    case CMP_GE: res = cr >= 0; break;
+  }
+  out = mkv(V_BOOL, res);
+  return true;
+}
+
+__device__ __forceinline__ bool op_list_add(const DevArgs& A, Lane& L, uint64_t& l, uint64_t v, uint32_t y) {
+  l = list_add(A, L, l, v);
+  if (L.fail) return false;
+  if (y) pin_escape(L, y);
+  return true;
+}
+
+__device__ __forceinline__ bool op_obj_put(const DevArgs& A, Lane& L, uint64_t& o, uint64_t k, uint64_t v, uint32_t y) {
+  uint32_t n = list_len(L, o);
+  bool found = false;
+  for (uint32_t i = 0; i + 1 < n; i += 2) {
+    if (veq(A, L, list_at(L, o, i), k)) {
+      found = true;
+      if (!veq(A, L, list_at(L, o, i + 1), v)) { lane_error(L); return false; }
+    }
+  }
+  if (!found) { o = list_add(A, L, o, k); o = list_add(A, L, o, v); }
+  if (L.fail) return false;
+  if (y) pin_escape(L, y);
+  return true;
+}
+
+__device__ __forceinline__ bool op_yield(const DevArgs& A, Lane& L, uint64_t& out, uint64_t v, uint32_t y) {
+  if (vtag(out) != V_UNDEF) {
+    if (!veq(A, L, out, v)) { lane_error(L); return false; }  // conflicting function/rule outputs
+    if (L.fail) return false;
+  } else {
+    out = v;
+    if (y && heap_val(v)) pin_escape(L, y);
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint64_t op_len_eq(const DevArgs& A, Lane& L, uint64_t v, uint32_t y) {
+  uint32_t want = y & 0xffffff, kind = y >> 24;
+  int cls = tclass(A, v);
+  bool ok = (kind == LK_ARR ? cls == 7 : cls == 8) && coll_len(A, L, v) == want;
+  return mkv(V_BOOL, ok);
+}
+
+// f("k1") = v1 {true} ... compiled to a table (compiler.cc table_func): the
+// value of the (at most one) entry whose key equals the argument, else undefined
+__device__ __forceinline__ uint64_t op_table(const DevArgs& A, Lane& L, const uint64_t* T, uint64_t arg) {
+  if (vtag(arg) == V_UNDEF) return mkv(V_UNDEF, 0);
+  uint32_t n = (uint32_t)T[0];
+  for (uint32_t i = 0; i < n; ++i)
+    if (veq(A, L, T[1 + 2 * i], arg)) return T[2 + 2 * i];
+  return mkv(V_UNDEF, 0);
+}
+
+// m: message register, d: details register (undefined when absent)
+__device__ __forceinline__ bool op_emit(const DevArgs& A, Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+  if (!is_strv(m)) { lane_error(L); return false; }  // types.Result.msg must unmarshal as a string
+  SView ms = sview(A, L, m);
+  char* dbuf = L.B + L.bp;
+  Out o{dbuf, 0, (uint32_t)(BCAP - L.bp), false};
+  if (!put_json(A, L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
+  stage_tuple(L, rule, ms.p, ms.n, dbuf, o.n, depth);
+  return !L.fail;
+}
+
+// ------------------------------------------------------------------ kernel body
+// lane -> (review tile, constraint): a wave = 64 consecutive reviews x ONE
+// constraint of the launch's list, so every lane runs the same predicate and
+// the constraint's MatchSpec loads are wave-uniform.  `run(L, rc, m, r, c)`
+// evaluates the template predicate for a matched lane.
+template <typename Run>
+__device__ __forceinline__ void audit_body(const DevArgs& A, Run run) {
+  uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t wave = (uint32_t)(gid >> 6);
+  uint32_t lane = (uint32_t)(gid & 63);
+  uint32_t c = A.clist[wave % A.nclist];
+  uint32_t tile = wave / A.nclist;
+  if (tile >= A.ntiles) return;  // wave-uniform
+  uint32_t r = tile * 64 + lane;
+  Lane L;
+  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0;
+  for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+  bool live = r < A.nrev;
+  if (live) {
+    const ReviewCol rc = A.revs[r];
+    const MatchSpec m = A.cons[c];
+    if (rc.flags & RC_FALLBACK) {
+      L.fail = RF_FALLBACK;
+    } else {
+      // autoreject_review (target_template_source.go:12-25)
+      if ((m.flags & MF_HAS_NSSEL) && !(m.flags & MF_FALLBACK) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID &&
+          !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS)) {
+        const char* msg = "Namespace is not cached in OPA.";
+        stage_tuple(L, RULE_AUTOREJECT, msg, 31, "{}", 2, 0);
+      }
+      int mr = match_constraint(A, m, rc);
+      if (mr == -1) L.fail = RF_ERROR;
+      else if (mr == -2) L.fail = RF_FALLBACK;
+      else if (mr == 1 && m.prog != NO_ID) {
+        uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(A, m.params);
+        run(L, mkv(V_NODE, rc.root), params, m.prog, r, c);
+      }
+    }
+    if (L.fail) {
+      atomicOr(&A.rflags[r], L.fail);
+      if (A.rreason) atomicMax(&A.rreason[r], L.reason);
+    }
+  }
+  // every lane of the wave reaches here (reconverged): reserve + write output
+  flush_wave(A, L, lane, r, c, live && !L.fail);
+  if (A.prof) {
+    uint32_t mx = L.steps;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { uint32_t o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+    if (L.steps) {
+      atomicAdd(&A.prof[c * 4 + 0], (unsigned long long)L.steps);
+      atomicMax(&A.prof[c * 4 + 1], (unsigned long long)L.steps);
+      atomicAdd(&A.prof[c * 4 + 2], 1ull);
+    }
+    if (lane == 0) atomicAdd(&A.prof[c * 4 + 3], (unsigned long long)mx);
+  }
+}
+
+}  // namespace gk

@@ -10,20 +10,21 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../../include/gkgpu.h"
 #include "common.h"
 #include "compiler.h"
+#include "jit.h"
 #include "json.h"
 #include "rego.h"
 #include "regex.h"
 #include "store.h"
 
 namespace gk {
-struct DevArgs;
 }
-extern "C" int gk_launch_audit(const void* args, hipStream_t stream);
+extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
 extern "C" size_t gk_devargs_size();
 
 namespace gk {
@@ -35,37 +36,6 @@ static const char* EMPTY_NS_JSON = "{\"metadata\":{\"creationTimestamp\":null},\
 using Clock = std::chrono::steady_clock;
 static double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
 
-// mirror of kernels.hip DevArgs (kept in sync; size checked at runtime)
-struct HostDevArgs {
-  const Node* nodes;
-  const StrEnt* strs;
-  const uint8_t* pool;
-  const uint8_t* sflags;
-  const NumEnt* nums;
-  const Ins* code;
-  const uint64_t* K;
-  const uint32_t* fmt;
-  const MatchSpec* cons;
-  const uint32_t* mwords;
-  const uint32_t* prog_off;
-  const ReviewCol* revs;
-  const uint32_t* dfa_keys;
-  const uint32_t* dfa_meta;
-  const uint32_t* dfa_words;
-  uint32_t ndfa;
-  uint32_t ncode;
-  uint32_t ncons;
-  uint32_t nrev;
-  uint32_t ntiles;
-  Viol* out;
-  uint32_t out_cap;
-  uint32_t* counters;
-  char* bytes;
-  uint32_t bytes_cap;
-  uint32_t* rflags;
-  uint32_t* totals;
-  uint32_t* rreason;
-};
 
 // ------------------------------------------------------------------ device buffers
 struct DBuf {
@@ -126,6 +96,9 @@ struct gk_results {
   std::vector<std::string> ckind, cname, cea;
   double ms[5] = {0, 0, 0, 0, 0};
   uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
+  std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
+  struct Launch { std::string kernel; double ms; uint32_t nconstraints; };
+  std::vector<Launch> launches;            // kernels of the last attempt, in launch order
 };
 
 struct gk_batch {
@@ -143,6 +116,8 @@ struct gk_engine {
   std::string err;
   int device = 0;
   bool dev_ok = false;
+  std::vector<uint32_t> pchist;  // last launch's per-pc execution counts (GKGPU_PROFILE=2)
+  int profile = 0;  // GKGPU_PROFILE=1: VM step statistics per launch; 2: + per-pc histogram
   hipStream_t stream = nullptr;
   gk::Store st;
   // modules
@@ -150,6 +125,15 @@ struct gk_engine {
   gk::ModuleSet mods;
   gk::CodeBank bank;
   std::vector<gk::Program> progs;
+  // per-template kernels (jit.cc), parallel to progs
+  struct Jit {
+    std::string name, src, code, log;
+    int state = 0;  // 0 not compiled, 1 code ready, -1 compile failed
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+  };
+  std::vector<Jit> jits;
+  bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
   std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
   bool modules_dirty = true;
   // data
@@ -168,7 +152,7 @@ struct gk_engine {
   std::vector<uint32_t> dfa_keys, dfa_meta;
   // device mirrors
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
-      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason;
+      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
 };
 
@@ -263,6 +247,8 @@ static void rebuild_modules(gk_engine* e) {
   e->mods.clear();
   e->bank.clear();
   e->progs.clear();
+  for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
+  e->jits.clear();
   e->templates.clear();
   // drop the transient region before appending new permanent constant nodes
   e->st.nodes().resize(e->perm_nodes);
@@ -288,17 +274,23 @@ static void rebuild_modules(gk_engine* e) {
         const Ins& in = e->bank.code[p.code_off + k];
         auto reg_ok = [&](uint16_t r) { return r < p.nregs || r == 0xffff; };
         if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
-        if (!reg_ok(in.a) || !reg_ok(in.b) || !reg_ok(in.c)) throw std::runtime_error("internal: register out of range");
+        if (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))) throw std::runtime_error("internal: register out of range");
         if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
         if (in.op == OP_CALL && in.b + (uint32_t)in.c > p.nregs) throw std::runtime_error("internal: call args");
         bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || in.op == OP_ITER_NEXT;
         if (jmp && (in.x < p.code_off || in.x >= p.code_off + p.code_len)) throw std::runtime_error("internal: jump target");
         if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x >= e->bank.consts.size()) throw std::runtime_error("internal: constant index");
         if (in.op == OP_SPRINTF && in.x >= e->bank.fmt.size()) throw std::runtime_error("internal: format index");
+        if (in.op == OP_TABLE && (in.x >= e->bank.consts.size() || in.x + 1 + 2 * e->bank.consts[in.x] > e->bank.consts.size()))
+          throw std::runtime_error("internal: table bounds");
       }
       te.prog = (int)e->progs.size();
       te.supported = true;
       e->progs.push_back(p);
+      gk_engine::Jit j;
+      j.name = jit_name(p, e->bank);
+      j.src = jit_source(p, e->bank, j.name);
+      e->jits.push_back(std::move(j));
     } catch (const std::exception& ex) {
       te.supported = false;
       te.reason = ex.what();
@@ -788,6 +780,31 @@ static bool sync_tables(gk_engine* e) {
   return ok;
 }
 
+// Compiles (hipRTC, in parallel) every template kernel not yet built; with a
+// device, loads the code objects.  A template whose kernel fails to compile
+// stays on the bytecode VM kernel (same semantics, slower).
+static void ensure_jit(gk_engine* e, bool load) {
+  if (!e->jit_enabled) return;
+  std::vector<std::thread> th;
+  for (auto& j : e->jits) {
+    if (j.state != 0) continue;
+    th.emplace_back([&j] { j.state = jit_compile(j.src, j.code, j.log) ? 1 : -1; });
+  }
+  for (auto& t : th) t.join();
+  if (!load) return;
+  for (auto& j : e->jits) {
+    if (j.state != 1 || j.fn) continue;
+    if (hipModuleLoadData(&j.mod, j.code.data()) != hipSuccess ||
+        hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess) {
+      if (j.mod) hipModuleUnload(j.mod);
+      j.mod = nullptr;
+      j.fn = nullptr;
+      j.state = -1;
+      j.log = "module load failed";
+    }
+  }
+}
+
 // runs the kernel over `cols` (already resident in d_revs when `resident`)
 static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, DBuf* revbuf, bool decode,
                               gk_results* res) {
@@ -813,13 +830,42 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
   ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 4) &&
         e->d_counters.reserve(64) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
+  // launch plan: constraints grouped by template kernel (jit.cc); the bytecode
+  // VM kernel takes every constraint whose template has no kernel / program
+  ensure_jit(e, true);
+  struct Step { hipFunction_t fn; std::string name; uint32_t off, n; };
+  std::vector<Step> plan;
+  {
+    std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
+    for (uint32_t c = 0; c < ncons; ++c) {
+      uint32_t p = e->corder[c]->spec.prog;
+      bool jit = p != NO_ID && p < e->jits.size() && e->jits[p].fn;
+      groups[jit ? p : e->progs.size()].push_back(c);
+    }
+    std::vector<uint32_t> clist;
+    for (size_t g = 0; g < groups.size(); ++g) {
+      if (groups[g].empty()) continue;
+      bool vm = g == e->progs.size();
+      plan.push_back({vm ? nullptr : e->jits[g].fn, vm ? std::string("audit_kernel") : e->jits[g].name,
+                      (uint32_t)clist.size(), (uint32_t)groups[g].size()});
+      clist.insert(clist.end(), groups[g].begin(), groups[g].end());
+    }
+    if (!up(e->d_clist, clist, false)) return fail(e, GK_EDEVICE, "device upload failed");
+  }
   res->ms[1] = ms_since(t0);
   for (int attempt = 0; attempt < 4; ++attempt) {
     hipMemsetAsync(e->d_rflags.p, 0, nrev * 4, e->stream);
     hipMemsetAsync(e->d_rreason.p, 0, nrev * 4, e->stream);
     hipMemsetAsync(e->d_totals.p, 0, ncons * 4, e->stream);
     hipMemsetAsync(e->d_counters.p, 0, 64, e->stream);
-    HostDevArgs a{};
+    bool prof = e->profile && e->d_prof.reserve(ncons * 32);
+    if (prof) hipMemsetAsync(e->d_prof.p, 0, ncons * 32, e->stream);
+    DevArgs a{};
+    a.prof = prof ? (unsigned long long*)e->d_prof.p : nullptr;
+    uint32_t ncode = (uint32_t)e->bank.code.size();
+    bool hist = e->profile >= 2 && e->d_pchist.reserve(ncode * 4);
+    if (hist) hipMemsetAsync(e->d_pchist.p, 0, ncode * 4, e->stream);
+    a.pchist = hist ? (unsigned int*)e->d_pchist.p : nullptr;
     a.nodes = (const Node*)e->d_nodes.p;
     a.strs = (const StrEnt*)e->d_strs.p;
     a.pool = (const uint8_t*)e->d_pool.p;
@@ -848,19 +894,39 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     a.rflags = (uint32_t*)e->d_rflags.p;
     a.totals = (uint32_t*)e->d_totals.p;
     a.rreason = (uint32_t*)e->d_rreason.p;
-    hipEvent_t ev0, ev1;
-    hipEventCreate(&ev0);
-    hipEventCreate(&ev1);
-    hipEventRecord(ev0, e->stream);
-    int lr = gk_launch_audit(&a, e->stream);
-    hipEventRecord(ev1, e->stream);
-    if (lr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed: ") + hipGetErrorString((hipError_t)lr));
-    if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
-    float kms = 0;
-    hipEventElapsedTime(&kms, ev0, ev1);
-    hipEventDestroy(ev0);
-    hipEventDestroy(ev1);
-    res->ms[2] += kms;
+    std::vector<hipEvent_t> ev(plan.size() + 1);
+    for (auto& x : ev) hipEventCreate(&x);
+    hipEventRecord(ev[0], e->stream);
+    for (size_t i = 0; i < plan.size(); ++i) {
+      a.clist = (const uint32_t*)e->d_clist.p + plan[i].off;
+      a.nclist = plan[i].n;
+      int lr;
+      if (plan[i].fn) {
+        uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
+        uint32_t blocks = (uint32_t)((threads + 255) / 256);
+        void* params[] = {&a};
+        lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, e->stream, params, nullptr);
+      } else {
+        lr = gk_launch_audit(&a, e->stream);
+      }
+      hipEventRecord(ev[i + 1], e->stream);
+      if (lr != 0) {
+        for (auto& x : ev) hipEventDestroy(x);
+        return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
+      }
+    }
+    if (hipStreamSynchronize(e->stream) != hipSuccess) {
+      for (auto& x : ev) hipEventDestroy(x);
+      return fail(e, GK_EDEVICE, "kernel execution failed");
+    }
+    res->launches.clear();
+    for (size_t i = 0; i < plan.size(); ++i) {
+      float kms = 0;
+      hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
+      res->ms[2] += kms;
+      res->launches.push_back({plan[i].name, (double)kms, plan[i].n});
+    }
+    for (auto& x : ev) hipEventDestroy(x);
     auto t1 = Clock::now();
     uint32_t counters[2];
     hipMemcpy(counters, e->d_counters.p, 8, hipMemcpyDeviceToHost);
@@ -878,6 +944,14 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
     hipMemcpy(res->status.data(), e->d_rflags.p, nrev * 4, hipMemcpyDeviceToHost);
     hipMemcpy(res->reason.data(), e->d_rreason.p, nrev * 4, hipMemcpyDeviceToHost);
+    if (hist) {
+      e->pchist.assign(ncode, 0);
+      hipMemcpy(e->pchist.data(), e->d_pchist.p, ncode * 4, hipMemcpyDeviceToHost);
+    }
+    if (prof) {
+      res->prof.assign(ncons * 4, 0);
+      hipMemcpy(res->prof.data(), e->d_prof.p, ncons * 32, hipMemcpyDeviceToHost);
+    }
     bool flagged = false;
     for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
     bool ea_err = false;
@@ -942,7 +1016,7 @@ int gk_device_available(void) {
 
 int gk_engine_create(const char* opts_json, gk_engine** out) {
   if (!out) return GK_EINVAL;
-  if (gk_devargs_size() != sizeof(HostDevArgs)) return GK_EINVAL;
+  if (gk_devargs_size() != sizeof(DevArgs)) return GK_EINVAL;
   auto* e = new gk_engine();
   if (opts_json && *opts_json) {
     JDoc d;
@@ -951,9 +1025,17 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
     if (r >= 0) {
       int dv = d.get(r, "device");
       if (dv >= 0 && d.nodes[dv].type == NT_NUM) e->device = atoi(d.str(d.nodes[dv]));
+      int jv = d.get(r, "jit");
+      if (jv >= 0 && d.nodes[jv].type == NT_FALSE) e->jit_enabled = false;
       int mv = d.get(r, "max_violations");
       if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap = (size_t)atoll(d.str(d.nodes[mv]));
     }
+  }
+  {
+    const char* pe = getenv("GKGPU_PROFILE");
+    e->profile = pe ? atoi(pe) : 0;
+    const char* je = getenv("GKGPU_JIT");
+    if (je && *je == '0') e->jit_enabled = false;
   }
   e->perm_nodes = (uint32_t)e->st.nodes().size();
   *out = e;
@@ -964,8 +1046,9 @@ void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
                   &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
-                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason})
+                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist})
     b->free_();
+  for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1332,6 +1415,43 @@ int gk_results_copy_status(const gk_results* r, uint32_t* status, uint32_t* reas
   return GK_OK;
 }
 
+// diagnostics (GKGPU_PROFILE=1): per constraint [sum VM steps, max lane steps,
+// lanes that ran a program, sum over waves of the wave's max lane steps]
+extern "C" size_t gk_results_vm_profile(const gk_results* r, uint64_t* out, size_t n) {
+  if (!r) return 0;
+  if (out) for (size_t i = 0; i < n && i < r->prof.size(); ++i) out[i] = r->prof[i];
+  return r->prof.size();
+}
+
+size_t gk_results_launches(const gk_results* r) { return r ? r->launches.size() : 0; }
+
+int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints) {
+  if (!r || i >= r->launches.size()) return GK_EINVAL;
+  if (kernel) *kernel = r->launches[i].kernel.c_str();
+  if (ms) *ms = r->launches[i].ms;
+  if (nconstraints) *nconstraints = r->launches[i].nconstraints;
+  return GK_OK;
+}
+
+int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail) {
+  if (!e || !kind) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  rebuild_modules(e);
+  auto it = e->templates.find(kind);
+  if (it == e->templates.end()) return GK_ENOTFOUND;
+  int b = 0;
+  const char* d = it->second.reason.c_str();
+  if (it->second.supported) {
+    ensure_jit(e, false);
+    auto& j = e->jits[it->second.prog];
+    b = j.state == 1 ? 2 : 1;
+    d = j.state == 1 ? j.name.c_str() : (e->jit_enabled ? j.log.c_str() : "jit disabled");
+  }
+  if (backend) *backend = b;
+  if (detail) *detail = d;
+  return GK_OK;
+}
+
 int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes) {
   if (!r) return GK_EINVAL;
   if (tuples) *tuples = r->dev_tuples;
@@ -1438,14 +1558,22 @@ extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   const Program& p = e->progs[it->second.prog];
   static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
                                 "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",
-                                "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK"};
+                                "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK", "TABLE"};
   std::string s = "nregs=" + std::to_string(p.nregs) + " len=" + std::to_string(p.code_len) + "\n";
   for (uint32_t i = 0; i < p.code_len; ++i) {
     const Ins& in = e->bank.code[p.code_off + i];
     char buf[160];
-    snprintf(buf, sizeof buf, "%5u %-10s a=%u b=%u c=%u x=%u y=%u\n", p.code_off + i,
+    uint32_t pc = p.code_off + i;
+    snprintf(buf, sizeof buf, "%10u %5u %-10s a=%u b=%u c=%u x=%u y=%u", pc < e->pchist.size() ? e->pchist[pc] : 0u, pc,
              in.op < OP_COUNT_ ? names[in.op] : "?", in.a, in.b, in.c, in.x, in.y);
     s += buf;
+    if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x < e->bank.consts.size()) {
+      uint64_t k = e->bank.consts[in.x];
+      uint32_t tag = (uint32_t)(k >> 60);
+      if (tag == V_STR) s += "  ; \"" + std::string(e->st.str((uint32_t)(k & 0xffffffffu))) + "\"";
+      else { char kb[48]; snprintf(kb, sizeof kb, "  ; tag=%u pay=%llu", tag, (unsigned long long)(k & 0x0fffffffffffffffull)); s += kb; }
+    }
+    s += "\n";
   }
   *out = strdup(s.c_str());
   return GK_OK;

@@ -27,6 +27,7 @@ EXPORTS = [
     "gk_results_review_status", "gk_results_review_reason", "gk_results_constraints", "gk_results_constraint_total",
     "gk_results_timing", "gk_results_free", "gk_template_status", "gk_constraint_count", "gk_constraint_info",
     "gk_batch_stats", "gk_results_device_counts", "gk_results_copy_status", "gk_results_flag_counts",
+    "gk_results_launches", "gk_results_launch", "gk_template_backend",
 ]
 
 
@@ -105,6 +106,12 @@ def load_library():
     lib.gk_results_device_counts.argtypes = [vp, pu64, pu64]
     lib.gk_results_copy_status.argtypes = [vp, C.c_void_p, C.c_void_p]
     lib.gk_results_flag_counts.argtypes = [vp, pu64, pu64]
+    lib.gk_results_launches.argtypes = [vp]
+    lib.gk_results_launches.restype = sz
+    lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+    lib.gk_template_backend.argtypes = [vp, cp, C.POINTER(C.c_int), C.POINTER(cp)]
+    lib.gk_results_vm_profile.argtypes = [vp, C.c_void_p, sz]
+    lib.gk_results_vm_profile.restype = sz
     lib.gk_template_status.argtypes = [vp, cp, C.POINTER(cp)]
     lib.gk_template_status.restype = C.c_int
     lib.gk_constraint_count.argtypes = [vp]
@@ -141,9 +148,34 @@ class Results:
     device_bytes: int = 0       # message/details bytes the kernel wrote
     n_errors: int = 0
     n_fallbacks: int = 0
+    vm_profile: List[int] = field(default_factory=list)  # GKGPU_PROFILE=1 diagnostics
+    launches: List[tuple] = field(default_factory=list)  # (kernel, ms, n constraints) per launch
+
+    def vm_stats(self):
+        """per constraint: (sum VM steps, max lane steps, lanes run, sum of per-wave max steps)"""
+        p = self.vm_profile
+        return [tuple(p[i:i + 4]) for i in range(0, len(p), 4)]
 
     def for_review(self, i):
         return [r for r in self.results if r.review == i]
+
+
+def _vm_profile(lib, h):
+    n = lib.gk_results_vm_profile(h, None, 0)
+    if not n:
+        return []
+    buf = (C.c_uint64 * n)()
+    lib.gk_results_vm_profile(h, buf, n)
+    return list(buf)
+
+
+def _launches(lib, h):
+    out = []
+    for i in range(lib.gk_results_launches(h)):
+        k, ms, n = C.c_char_p(), C.c_double(), C.c_uint32()
+        lib.gk_results_launch(h, i, C.byref(k), C.byref(ms), C.byref(n))
+        out.append((k.value.decode(), ms.value, n.value))
+    return out
 
 
 def _collect_light(lib, h) -> Results:
@@ -157,7 +189,8 @@ def _collect_light(lib, h) -> Results:
         lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
         ne, nf = C.c_uint64(), C.c_uint64()
         lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
-        return Results([], [], [], totals, list(t), dt.value, db.value, ne.value, nf.value)
+        return Results([], [], [], totals, list(t), dt.value, db.value, ne.value, nf.value, _vm_profile(lib, h),
+                       _launches(lib, h))
     finally:
         lib.gk_results_free(h)
 
@@ -186,7 +219,8 @@ def _collect(lib, h, decode=True) -> Results:
         dt, db = C.c_uint64(), C.c_uint64()
         lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
         return Results(out, status, reason, totals, list(t), dt.value, db.value,
-                       sum(1 for x in status if x & 1), sum(1 for x in status if x & 2))
+                       sum(1 for x in status if x & 1), sum(1 for x in status if x & 2), _vm_profile(lib, h),
+                       _launches(lib, h))
     finally:
         lib.gk_results_free(h)
 
@@ -237,10 +271,11 @@ class Batch:
 class Driver:
     """drivers.Driver over libgkgpu (interface.go:21-39)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, jit: bool = True):
+        """jit=False pins every template to the bytecode VM kernel (A/B parity)."""
         self._lib = load_library()
         e = C.c_void_p()
-        rc = self._lib.gk_engine_create(_b(json.dumps({"device": device})), C.byref(e))
+        rc = self._lib.gk_engine_create(_b(json.dumps({"device": device, "jit": jit})), C.byref(e))
         if rc != 0:
             raise EngineUnavailable("gk_engine_create failed (%d)" % rc)
         self._e = e
@@ -348,6 +383,22 @@ class Driver:
         return Batch(self, out, len(o))
 
     # -- introspection
+    def debug_disasm(self, kind: str) -> str:
+        """bytecode listing of a compiled template (diagnostics; with GKGPU_PROFILE=2
+        the first column is the last launch's per-instruction execution count)"""
+        p = C.c_void_p()
+        self._lib.gk_debug_disasm.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]
+        self._check(self._lib.gk_debug_disasm(self._e, _b(kind), C.byref(p)))
+        s = C.string_at(p).decode()
+        self._lib.gk_free_string(p)
+        return s
+
+    def template_backend(self, kind: str):
+        """(backend, detail): 2 template kernel (hipRTC), 1 bytecode VM, 0 CPU fallback"""
+        b, d = C.c_int(), C.c_char_p()
+        self._check(self._lib.gk_template_backend(self._e, _b(kind), C.byref(b), C.byref(d)))
+        return b.value, (d.value or b"").decode("utf-8", "replace")
+
     def template_status(self, kind: str):
         r = C.c_char_p()
         st = self._lib.gk_template_status(self._e, _b(kind), C.byref(r))

@@ -131,11 +131,20 @@ uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
 int gk_results_timing(const gk_results* r, double* ms5);
 /* violation tuples (32 B each) and message/details bytes the kernel wrote */
 int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes);
+/* kernels of the call in launch order: kernel name ("audit_kernel" = bytecode
+ * VM, "gk_t_<hash>" = a template kernel), duration (HIP events) and how many
+ * constraints it evaluated */
+size_t gk_results_launches(const gk_results* r);
+int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints);
 void gk_results_free(gk_results* r);
 
 /* ---- introspection --------------------------------------------------------- */
 /* template status: 1 = compiled to GPU bytecode, 0 = CPU fallback, -1 unknown kind */
 int gk_template_status(gk_engine* e, const char* kind, const char** reason);
+/* evaluation back end of a template: 2 = template kernel (hipRTC-compiled for
+ * gfx950; detail = kernel name), 1 = bytecode VM kernel (detail = why not
+ * compiled), 0 = CPU fallback (detail = reason).  Compiles on demand. */
+int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail);
 size_t gk_constraint_count(gk_engine* e);
 int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name);
 

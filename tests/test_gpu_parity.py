@@ -26,6 +26,29 @@ def _need_device():
         pytest.fail("no HIP device visible: GPU parity tests must run on an MI355X")
 
 
+_BACKEND = {"jit": True}
+
+
+@pytest.fixture(autouse=True, params=["jit", "vm"])
+def backend(request):
+    """every parity test runs on both device back ends: the per-template
+    hipRTC kernels (jit.cc) and the bytecode VM kernel (kernels.hip)"""
+    _BACKEND["jit"] = request.param == "jit"
+    yield request.param
+
+
+def Driver():
+    d = gkgpu.Driver(jit=_BACKEND["jit"])
+    return d
+
+
+def _assert_backend(drv, kinds):
+    want = 2 if _BACKEND["jit"] else 1
+    for k in kinds:
+        b, detail = drv.template_backend(k)
+        assert b == want, (k, b, detail)
+
+
 def _assert_clean(rep, max_fallback_frac=0.0):
     assert not rep.mismatches, rep.mismatches[:3]
     assert rep.compared > 0
@@ -36,7 +59,7 @@ def _assert_clean(rep, max_fallback_frac=0.0):
 def test_config1_namespaces_required_labels():
     ts, cs = W.config1()
     nss = W.gen_namespaces(3000, seed=1)
-    rep, res = run_objects(gkgpu.Driver(), ts, cs, nss, [None] * len(nss))
+    rep, res = run_objects(Driver(), ts, cs, nss, [None] * len(nss))
     _assert_clean(rep)
     assert rep.violations > 1000
     # README.md:313-327 message shape
@@ -48,15 +71,22 @@ def test_config2_agilebank_pods():
     ts, cs = W.config2()
     pods, ns_of, ns_objs = W.gen_pods(1500, seed=42, n_namespaces=100)
     nss = [ns_objs[n] for n in ns_of]
-    rep, res = run_objects(gkgpu.Driver(), ts, cs, pods, nss)
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, pods, nss)
     _assert_clean(rep)
     assert rep.violations > 5000
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
+    kernels = {k for k, _, _ in res.launches}
+    if _BACKEND["jit"]:
+        assert kernels and all(k.startswith("gk_t_") for k in kernels), res.launches
+    else:
+        assert kernels == {"audit_kernel"}, res.launches
 
 
 def test_config2_agilebank_namespaces_regex():
     ts, cs = W.config2()
     nss = W.gen_namespaces(2000, seed=7)
-    rep, res = run_objects(gkgpu.Driver(), ts, cs, nss, [None] * len(nss))
+    rep, res = run_objects(Driver(), ts, cs, nss, [None] * len(nss))
     _assert_clean(rep)
     msgs = {r.msg for r in res.results}
     assert "All namespaces must have an `owner` label that points to your company username" in msgs
@@ -84,7 +114,7 @@ def test_demo_agilebank_resources():
         W.namespace_obj("production", {"owner": "me.agilebank.demo"}),
     ]
     nss = [W.namespace_obj("production")] * 4 + [None, None]
-    rep, res = run_objects(gkgpu.Driver(), ts, cs, pods, nss)
+    rep, res = run_objects(Driver(), ts, cs, pods, nss)
     _assert_clean(rep)
     per = [[r.msg for r in res.results if r.review == i] for i in range(len(pods))]
     assert "container <opa> cpu limit <300m> is higher than the maximum allowed of <200m>" in per[0]
@@ -125,7 +155,7 @@ def test_target_integration_cases():
     rep = Report()
     for case in cases:
         c = W.constraint("DenyAll", "my-constraint", match=case["match"])
-        drv = gkgpu.Driver()
+        drv = Driver()
         cl = Client(drv)
         cl.add_template(deny_all)
         cl.add_constraint(c)
@@ -164,7 +194,7 @@ def test_label_and_annotation_regex_config3():
         objs.append({"apiVersion": "apps/v1" if kind == "Deployment" else "v1", "kind": kind,
                      "metadata": {"name": "o%d" % i, "namespace": "ns%d" % (i % 7), "labels": lab, "annotations": ann}})
     nss = [W.namespace_obj("ns%d" % (i % 7)) for i in range(len(objs))]
-    rep, res = run_objects(gkgpu.Driver(), ts, cs, objs, nss)
+    rep, res = run_objects(Driver(), ts, cs, objs, nss)
     _assert_clean(rep)
     assert rep.violations > 500
 
@@ -172,7 +202,7 @@ def test_label_and_annotation_regex_config3():
 def test_query_single_review_and_batch_agree():
     ts, cs = W.config2()
     pods, ns_of, ns_objs = W.gen_pods(50, seed=3, n_namespaces=5)
-    drv = gkgpu.Driver()
+    drv = Driver()
     cl = Client(drv)
     for t in ts:
         cl.add_template(t)
@@ -193,7 +223,7 @@ def test_staged_batch_matches_direct_and_counts():
     ts, cs = W.config2()
     pods, ns_of, ns_objs = W.gen_pods(400, seed=5, n_namespaces=30)
     nss = [ns_objs[n] for n in ns_of]
-    drv = gkgpu.Driver()
+    drv = Driver()
     cl = Client(drv)
     for t in ts:
         cl.add_template(t)
