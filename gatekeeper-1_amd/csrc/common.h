@@ -101,6 +101,8 @@ enum Op : uint16_t {
   OP_LEN_EQ,       // a(dst bool), b(value), y=n : collection length test (array patterns)
   OP_FAIL_FALLBACK,// y=reason : unsupported construct reached at run time
   OP_TABLE,        // a = lookup(K[x..]: n, (key, value) x n ; R[b]) — constant-table function call
+  OP_MEMO_GET,     // memo slot y holds (R[b], R[c]) -> R[a] = cached value, jump x   (c = 0xffff: one arg)
+  OP_MEMO_PUT,     // memo slot y := (R[b], R[c]) -> R[a] when arguments and value are heap-free
   OP_COUNT_
 };
 
@@ -197,6 +199,7 @@ struct Viol {
 static_assert(sizeof(Viol) == 32, "Viol layout");
 
 constexpr uint32_t RULE_AUTOREJECT = 0xffffu;
+constexpr uint32_t MEMO_SLOTS = 16;  // memoized function call sites per template (per lane)
 
 // ------------------------------------------------------------------ launch
 // Kernel arguments of one audit launch (passed by value; shared by the bytecode

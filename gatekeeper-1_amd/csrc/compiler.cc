@@ -102,6 +102,7 @@ class Comp {
   std::map<uint64_t, uint32_t> kidx_;
   int reg_top_ = 0, max_reg_ = 0;
   int inline_depth_ = 0;
+  std::map<std::pair<const void*, bool>, int> memo_;  // memo slot per (function, statement form)
   std::vector<int> loop_base_;  // register base of each enclosing ITER loop (innermost last)
   Program prog_;
 
@@ -158,7 +159,7 @@ class Comp {
     prog_.code_len = (uint32_t)code_.size();
     for (auto& in : code_) {
       switch (in.op) {
-        case OP_JMP: case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT:
+        case OP_JMP: case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT: case OP_MEMO_GET:
           if (labels_[in.x] < 0) throw std::runtime_error("unplaced label");
           in.x = prog_.code_off + (uint32_t)labels_[in.x];
           break;
@@ -715,9 +716,15 @@ class Comp {
           emit(OP_TABLE, (uint16_t)out, (uint16_t)regs[0], 0, (uint32_t)tab);
         } else {
           out = loadk(tag_val(V_UNDEF, 0));
+          int slot = nargs >= 1 && nargs <= 2 ? memo_slot(rules, stmt && !has_out) : -1;
+          int Lhit = label();
+          uint16_t k1 = nargs == 2 ? (uint16_t)regs[1] : NOREG;
+          if (slot >= 0) emit(OP_MEMO_GET, (uint16_t)out, (uint16_t)regs[0], k1, (uint32_t)Lhit, (uint32_t)slot);
           if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
           for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
           --inline_depth_;
+          if (slot >= 0) emit(OP_MEMO_PUT, (uint16_t)out, (uint16_t)regs[0], k1, 0, (uint32_t)slot);
+          place(Lhit);
         }
         emit_jmp(OP_JUNDEF, out, f);
         if (has_out) {
@@ -781,6 +788,18 @@ class Comp {
     } else {
       k(d, f);
     }
+  }
+
+  // One memo slot per (function, statement-form) per template; see devrt.h
+  // memo_stable for which values are cached.  -1 once the slots run out.
+  int memo_slot(const std::vector<std::shared_ptr<Rule>>& rules, bool stmt) {
+    auto key = std::make_pair((const void*)rules[0].get(), stmt);
+    auto it = memo_.find(key);
+    if (it != memo_.end()) return it->second;
+    if (memo_.size() >= MEMO_SLOTS) return -1;
+    int s = (int)memo_.size();
+    memo_[key] = s;
+    return s;
   }
 
   // A one-argument function whose every definition is `f("key") = scalar { true }`

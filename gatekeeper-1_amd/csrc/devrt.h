@@ -16,6 +16,14 @@
 
 #include "common.h"
 
+// Launch arguments: ONE copy in constant memory, set before every launch
+// (hipMemcpyToSymbolAsync for the VM kernel, hipModuleGetGlobal + copy for a
+// template kernel) and read with wave-uniform scalar loads.  Passing them by
+// reference to non-inlined helpers would copy them into every lane's scratch.
+extern "C" {
+__constant__ gk::DevArgs gk_args;
+}
+
 namespace gk {
 
 constexpr int HCAP = 128;   // heap words per lane (lists, big floats)
@@ -53,6 +61,8 @@ struct Lane {
   uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
   // staged emissions: msg bytes then details JSON at B[off..off+mlen+dlen)
   uint32_t en, steps;
+  uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
+  uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
   uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP];
 };
 
@@ -77,8 +87,8 @@ __device__ __forceinline__ void lane_error(Lane& L) {
   if (!L.fail) { L.fail = RF_ERROR; L.reason = 0; }
 }
 
-__device__ __forceinline__ uint64_t nodeval(const DevArgs& A, uint32_t idx) {
-  const Node& n = A.nodes[idx];
+__device__ __forceinline__ uint64_t nodeval(uint32_t idx) {
+  const Node& n = gk_args.nodes[idx];
   switch (n.type) {
     case NT_NULL: return mkv(V_NULL, 0);
     case NT_FALSE: return mkv(V_BOOL, 0);
@@ -92,14 +102,14 @@ __device__ __forceinline__ uint64_t nodeval(const DevArgs& A, uint32_t idx) {
 
 // string bytes of a string value
 struct SView { const char* p; uint32_t n; };
-__device__ __forceinline__ SView sview(const DevArgs& A, const Lane& L, uint64_t v) {
+__device__ __forceinline__ SView sview(const Lane& L, uint64_t v) {
   uint32_t t = vtag(v);
-  if (t == V_STR) { const StrEnt& s = A.strs[(uint32_t)vpay(v)]; return SView{(const char*)A.pool + s.off, s.len}; }
+  if (t == V_STR) { const StrEnt& s = gk_args.strs[(uint32_t)vpay(v)]; return SView{(const char*)gk_args.pool + s.off, s.len}; }
   if (t == V_HSTR) { uint64_t p = vpay(v); return SView{L.B + (uint32_t)(p >> 16), (uint32_t)(p & 0xffff)}; }
   if (t == V_SLICE) {
     uint64_t p = vpay(v);
-    const StrEnt& s = A.strs[(uint32_t)(p >> 28)];
-    return SView{(const char*)A.pool + s.off + (uint32_t)((p >> 14) & 0x3fff), (uint32_t)(p & 0x3fff)};
+    const StrEnt& s = gk_args.strs[(uint32_t)(p >> 28)];
+    return SView{(const char*)gk_args.pool + s.off + (uint32_t)((p >> 14) & 0x3fff), (uint32_t)(p & 0x3fff)};
   }
   return SView{nullptr, 0};
 }
@@ -115,10 +125,10 @@ __device__ __forceinline__ int bytes_cmp(SView a, SView b) {
 // ------------------------------------------------------------------ numbers
 // exact 64-bit-mantissa big-float view of a numeric value; returns false if unavailable
 struct BF { uint64_t m; int32_t e; bool neg; bool zero; };
-__device__ bool num_bf(const DevArgs& A, const Lane& L, uint64_t v, BF& out) {
+__device__ bool num_bf(const Lane& L, uint64_t v, BF& out) {
   uint32_t t = vtag(v);
   if (t == V_NUM) {
-    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    const NumEnt& n = gk_args.nums[(uint32_t)vpay(v)];
     if (!(n.flags & NF_BF_OK)) return false;
     out.m = n.mant; out.e = n.exp; out.neg = n.neg != 0; out.zero = n.mant == 0;
     return true;
@@ -156,14 +166,14 @@ __device__ int bf_cmp(const BF& a, const BF& b) {
   return a.neg ? -mag : mag;
 }
 // integer view: true if the value is an exact integer representable in int64
-__device__ bool num_int(const DevArgs& A, const Lane& L, uint64_t v, int64_t& out) {
+__device__ bool num_int(const Lane& L, uint64_t v, int64_t& out) {
   uint32_t t = vtag(v);
   if (t == V_INT) { out = intof(v); return true; }
   if (t == V_NUM) {
-    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    const NumEnt& n = gk_args.nums[(uint32_t)vpay(v)];
     if (n.flags & NF_INT64) { out = n.i; return true; }
     BF b;
-    if (!num_bf(A, L, v, b)) return false;
+    if (!num_bf(L, v, b)) return false;
     if (b.zero) { out = 0; return true; }
     if (b.e >= 0 || b.e < -63) return false;
     uint64_t sh = (uint64_t)(-b.e);
@@ -175,7 +185,7 @@ __device__ bool num_int(const DevArgs& A, const Lane& L, uint64_t v, int64_t& ou
   }
   if (t == V_BFN) {
     BF b;
-    num_bf(A, L, v, b);
+    num_bf(L, v, b);
     if (b.zero) { out = 0; return true; }
     if (b.e >= 0 || b.e < -63) return false;
     uint64_t sh = (uint64_t)(-b.e);
@@ -234,31 +244,31 @@ __device__ uint64_t list_new(Lane& L, uint32_t kind, uint32_t cap) {
 }
 
 // value type ordering class (ast/compare.go sortOrder)
-__device__ __forceinline__ int tclass(const DevArgs& A, uint64_t v) {
+__device__ __forceinline__ int tclass(uint64_t v) {
   switch (vtag(v)) {
     case V_NULL: return 1;
     case V_BOOL: return 2;
     case V_NUM: case V_INT: case V_BFN: return 3;
     case V_STR: case V_HSTR: case V_SLICE: return 4;
-    case V_NODE: return A.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
+    case V_NODE: return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
     case V_LIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
   }
   return 0;
 }
 
 // collection view helpers (NODE arrays/objects and heap lists)
-__device__ uint32_t coll_len(const DevArgs& A, const Lane& L, uint64_t v) {
-  if (vtag(v) == V_NODE) return A.nodes[(uint32_t)vpay(v)].n;
+__device__ uint32_t coll_len(const Lane& L, uint64_t v) {
+  if (vtag(v) == V_NODE) return gk_args.nodes[(uint32_t)vpay(v)].n;
   if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
   return 0;
 }
 // i-th (key, value) of a collection
-__device__ void coll_at(const DevArgs& A, const Lane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
+__device__ void coll_at(const Lane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
   if (vtag(v) == V_NODE) {
-    const Node& n = A.nodes[(uint32_t)vpay(v)];
+    const Node& n = gk_args.nodes[(uint32_t)vpay(v)];
     uint32_t c = n.first + i;
-    val = nodeval(A, c);
-    k = n.type == NT_OBJ ? mkv(V_STR, A.nodes[c].key) : mkint(i);
+    val = nodeval(c);
+    k = n.type == NT_OBJ ? mkv(V_STR, gk_args.nodes[c].key) : mkint(i);
     return;
   }
   uint32_t kind = list_kind(v);
@@ -268,19 +278,19 @@ __device__ void coll_at(const DevArgs& A, const Lane& L, uint64_t v, uint32_t i,
 }
 
 // scalar compare within one type class (1..4); 2 = undecidable (fallback set)
-__device__ int scmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b, int cls) {
+__device__ int scmp(Lane& L, uint64_t a, uint64_t b, int cls) {
   switch (cls) {
     case 1: return 0;
     case 2: { uint64_t x = vpay(a), y = vpay(b); return x == y ? 0 : (x < y ? -1 : 1); }
     case 3: {
       if (vtag(a) == V_NUM && vtag(b) == V_NUM && vpay(a) == vpay(b)) return 0;
       BF x, y;
-      if (!num_bf(A, L, a, x) || !num_bf(A, L, b, y)) { lane_fallback(L, FB_NUMBER); return 2; }
+      if (!num_bf(L, a, x) || !num_bf(L, b, y)) { lane_fallback(L, FB_NUMBER); return 2; }
       return bf_cmp(x, y);
     }
     case 4: {
       if (vtag(a) == V_STR && vtag(b) == V_STR && vpay(a) == vpay(b)) return 0;
-      return bytes_cmp(sview(A, L, a), sview(A, L, b));
+      return bytes_cmp(sview(L, a), sview(L, b));
     }
   }
   return 2;
@@ -288,30 +298,30 @@ __device__ int scmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b, int cls) 
 
 // element comparison inside a composite: scalars, or identical document nodes;
 // anything deeper is served by the CPU fallback
-__device__ int ecmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
-  int ca = tclass(A, a), cb = tclass(A, b);
+__device__ int ecmp(Lane& L, uint64_t a, uint64_t b) {
+  int ca = tclass(a), cb = tclass(b);
   if (ca != cb) return ca < cb ? -1 : 1;
-  if (ca <= 4) return scmp(A, L, a, b, ca);
+  if (ca <= 4) return scmp(L, a, b, ca);
   if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
-  if (coll_len(A, L, a) == 0 && coll_len(A, L, b) == 0) return 0;
+  if (coll_len(L, a) == 0 && coll_len(L, b) == 0) return 0;
   lane_fallback(L, FB_DEEP_EQ);
   return 2;
 }
 
 // ast.Compare: -1/0/1; 3 = "not equal, order undefined here"; 2 = undecidable
-__device__ int vcmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
-  int ca = tclass(A, a), cb = tclass(A, b);
+__device__ int vcmp(Lane& L, uint64_t a, uint64_t b) {
+  int ca = tclass(a), cb = tclass(b);
   if (ca != cb) return ca < cb ? -1 : 1;
-  if (ca <= 4) return scmp(A, L, a, b, ca);
+  if (ca <= 4) return scmp(L, a, b, ca);
   if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
-  uint32_t na = coll_len(A, L, a), nb = coll_len(A, L, b);
+  uint32_t na = coll_len(L, a), nb = coll_len(L, b);
   if (ca == 7) {
     uint32_t n = na < nb ? na : nb;
     for (uint32_t i = 0; i < n; ++i) {
       uint64_t k1, v1, k2, v2;
-      coll_at(A, L, a, i, k1, v1);
-      coll_at(A, L, b, i, k2, v2);
-      int c = ecmp(A, L, v1, v2);
+      coll_at(L, a, i, k1, v1);
+      coll_at(L, b, i, k2, v2);
+      int c = ecmp(L, v1, v2);
       if (c != 0) return c;
     }
     return na == nb ? 0 : (na < nb ? -1 : 1);
@@ -320,16 +330,16 @@ __device__ int vcmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
   // objects / sets of equal size: equal iff every member of a is in b
   for (uint32_t i = 0; i < na; ++i) {
     uint64_t k1, v1;
-    coll_at(A, L, a, i, k1, v1);
+    coll_at(L, a, i, k1, v1);
     bool found = false;
     for (uint32_t j = 0; j < nb && !found; ++j) {
       uint64_t k2, v2;
-      coll_at(A, L, b, j, k2, v2);
-      int c = ecmp(A, L, k1, k2);
+      coll_at(L, b, j, k2, v2);
+      int c = ecmp(L, k1, k2);
       if (c == 2) return 2;
       if (c != 0) continue;
       if (ca == 9) { found = true; break; }
-      int d = ecmp(A, L, v1, v2);
+      int d = ecmp(L, v1, v2);
       if (d == 2) return 2;
       if (d != 0) return 3;
       found = true;
@@ -339,24 +349,24 @@ __device__ int vcmp(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
   return 0;
 }
 
-__device__ bool veq(const DevArgs& A, Lane& L, uint64_t a, uint64_t b) {
+__device__ bool veq(Lane& L, uint64_t a, uint64_t b) {
   if (a == b) {
     uint32_t t = vtag(a);
     if (t != V_HSTR && t != V_BFN) return true;
   }
-  int c = vcmp(A, L, a, b);
+  int c = vcmp(L, a, b);
   return c == 0;
 }
 
-__device__ bool list_contains(const DevArgs& A, Lane& L, uint64_t l, uint64_t v) {
+__device__ bool list_contains(Lane& L, uint64_t l, uint64_t v) {
   uint32_t n = list_len(L, l);
-  for (uint32_t i = 0; i < n; ++i) if (veq(A, L, list_at(L, l, i), v)) return true;
+  for (uint32_t i = 0; i < n; ++i) if (veq(L, list_at(L, l, i), v)) return true;
   return false;
 }
 // append (sets dedupe); may relocate the list to the heap top when full
-__device__ uint64_t list_add(const DevArgs& A, Lane& L, uint64_t l, uint64_t v) {
+__device__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
   if (vtag(l) != V_LIST) return l;
-  if (list_kind(l) == LK_SET && list_contains(A, L, l, v)) return l;
+  if (list_kind(l) == LK_SET && list_contains(L, l, v)) return l;
   uint32_t o = list_off(l);
   uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
   if (n == cap) {
@@ -382,23 +392,23 @@ __device__ uint64_t list_add(const DevArgs& A, Lane& L, uint64_t l, uint64_t v) 
 }
 
 // ------------------------------------------------------------------ get
-__device__ uint64_t vget(const DevArgs& A, Lane& L, uint64_t c, uint64_t key) {
+__device__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
   uint32_t t = vtag(c);
   if (t == V_NODE) {
-    const Node& n = A.nodes[(uint32_t)vpay(c)];
+    const Node& n = gk_args.nodes[(uint32_t)vpay(c)];
     if (n.flags & 1) { lane_fallback(L, FB_UNSUPPORTED); return mkv(V_UNDEF, 0); }
     if (n.type == NT_OBJ) {
       uint32_t kt = vtag(key);
       if (kt == V_STR) {
         uint32_t id = (uint32_t)vpay(key);
-        for (uint32_t i = 0; i < n.n; ++i) if (A.nodes[n.first + i].key == id) return nodeval(A, n.first + i);
+        for (uint32_t i = 0; i < n.n; ++i) if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
         return mkv(V_UNDEF, 0);
       }
       if (kt == V_HSTR || kt == V_SLICE) {
-        SView kv = sview(A, L, key);
+        SView kv = sview(L, key);
         for (uint32_t i = 0; i < n.n; ++i) {
-          const StrEnt& s = A.strs[A.nodes[n.first + i].key];
-          if (bytes_cmp(kv, SView{(const char*)A.pool + s.off, s.len}) == 0) return nodeval(A, n.first + i);
+          const StrEnt& s = gk_args.strs[gk_args.nodes[n.first + i].key];
+          if (bytes_cmp(kv, SView{(const char*)gk_args.pool + s.off, s.len}) == 0) return nodeval(n.first + i);
         }
       }
       return mkv(V_UNDEF, 0);
@@ -406,23 +416,23 @@ __device__ uint64_t vget(const DevArgs& A, Lane& L, uint64_t c, uint64_t key) {
     if (n.type == NT_ARR) {
       if (!is_numv(key)) return mkv(V_UNDEF, 0);
       int64_t i;
-      if (!num_int(A, L, key, i)) return mkv(V_UNDEF, 0);
+      if (!num_int(L, key, i)) return mkv(V_UNDEF, 0);
       if (i < 0 || i >= n.n) return mkv(V_UNDEF, 0);
-      return nodeval(A, n.first + (uint32_t)i);
+      return nodeval(n.first + (uint32_t)i);
     }
     return mkv(V_UNDEF, 0);
   }
   if (t == V_LIST) {
     uint32_t kind = list_kind(c);
     uint32_t n = list_len(L, c);
-    if (kind == LK_SET) return list_contains(A, L, c, key) ? key : mkv(V_UNDEF, 0);
+    if (kind == LK_SET) return list_contains(L, c, key) ? key : mkv(V_UNDEF, 0);
     if (kind == LK_ARR) {
       if (!is_numv(key)) return mkv(V_UNDEF, 0);
       int64_t i;
-      if (!num_int(A, L, key, i) || i < 0 || i >= n) return mkv(V_UNDEF, 0);
+      if (!num_int(L, key, i) || i < 0 || i >= n) return mkv(V_UNDEF, 0);
       return list_at(L, c, (uint32_t)i);
     }
-    for (uint32_t i = 0; i + 1 < n; i += 2) if (veq(A, L, list_at(L, c, i), key)) return list_at(L, c, i + 1);
+    for (uint32_t i = 0; i + 1 < n; i += 2) if (veq(L, list_at(L, c, i), key)) return list_at(L, c, i + 1);
     return mkv(V_UNDEF, 0);
   }
   return mkv(V_UNDEF, 0);
@@ -445,9 +455,9 @@ __device__ void put_int(Out& o, int64_t v) {
   if (v < 0) put(o, '-');
   while (n) put(o, t[--n]);
 }
-__device__ void put_sid(const DevArgs& A, Out& o, uint32_t sid) {
-  const StrEnt& s = A.strs[sid];
-  puts_(o, (const char*)A.pool + s.off, s.len);
+__device__ void put_sid(Out& o, uint32_t sid) {
+  const StrEnt& s = gk_args.strs[sid];
+  puts_(o, (const char*)gk_args.pool + s.off, s.len);
 }
 __device__ const char* hexd = "0123456789abcdef";
 
@@ -496,16 +506,16 @@ __device__ bool put_json_str(Out& o, SView s) {
 }
 
 // scalar Term.String()/JSON; returns 0 not-scalar, 1 ok, -1 fallback
-__device__ int put_scalar(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool json) {
+__device__ int put_scalar(Lane& L, Out& o, uint64_t v, bool json) {
   switch (vtag(v)) {
     case V_UNDEF: if (json) { put_cstr(o, "{}"); return 1; } return -1;
     case V_NULL: put_cstr(o, "null"); return 1;
     case V_BOOL: put_cstr(o, vpay(v) ? "true" : "false"); return 1;
-    case V_NUM: put_sid(A, o, A.nums[(uint32_t)vpay(v)].text); return 1;
+    case V_NUM: put_sid(o, gk_args.nums[(uint32_t)vpay(v)].text); return 1;
     case V_INT: put_int(o, intof(v)); return 1;
     case V_BFN: return -1;
     case V_STR: case V_HSTR: case V_SLICE:
-      return (json ? put_json_str(o, sview(A, L, v)) : put_quoted(o, sview(A, L, v))) ? 1 : -1;
+      return (json ? put_json_str(o, sview(L, v)) : put_quoted(o, sview(L, v))) ? 1 : -1;
     default: return 0;
   }
 }
@@ -514,12 +524,12 @@ struct PFrame { uint64_t v; uint32_t i, n; uint64_t last; int cls; };
 
 // ast.Term.String() (json=false) or encoding/json of ast.JSON (json=true, map
 // keys in byte order), iterative with an explicit stack; false => fallback
-__device__ bool put_value(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool json) {
-  int r = put_scalar(A, L, o, v, json);
+__device__ bool put_value(Lane& L, Out& o, uint64_t v, bool json) {
+  int r = put_scalar(L, o, v, json);
   if (r != 0) return r > 0;
   PFrame st[8];
   int sp = 0;
-  st[0] = PFrame{v, 0, coll_len(A, L, v), 0, tclass(A, v)};
+  st[0] = PFrame{v, 0, coll_len(L, v), 0, tclass(v)};
   if (!json && st[0].cls == 9 && st[0].n == 0) { put_cstr(o, "set()"); return true; }
   put(o, (st[0].cls == 7 || (json && st[0].cls == 9)) ? '[' : '{');
   while (sp >= 0) {
@@ -537,29 +547,29 @@ __device__ bool put_value(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool js
       uint64_t bk = 0;
       for (uint32_t j = 0; j < f.n; ++j) {
         uint64_t kk, vv;
-        coll_at(A, L, f.v, j, kk, vv);
+        coll_at(L, f.v, j, kk, vv);
         if (!is_strv(kk)) return false;
-        if (f.i && bytes_cmp(sview(A, L, kk), sview(A, L, f.last)) <= 0) continue;
-        if (best < 0 || bytes_cmp(sview(A, L, kk), sview(A, L, bk)) < 0) { best = (int)j; bk = kk; }
+        if (f.i && bytes_cmp(sview(L, kk), sview(L, f.last)) <= 0) continue;
+        if (best < 0 || bytes_cmp(sview(L, kk), sview(L, bk)) < 0) { best = (int)j; bk = kk; }
       }
       if (best < 0) return false;
-      coll_at(A, L, f.v, (uint32_t)best, k, val);
+      coll_at(L, f.v, (uint32_t)best, k, val);
       f.last = k;
     } else {
-      coll_at(A, L, f.v, f.i, k, val);
+      coll_at(L, f.v, f.i, k, val);
     }
     f.i++;
     if (f.cls == 8) {
-      if (put_scalar(A, L, o, k, json) <= 0) return false;
+      if (put_scalar(L, o, k, json) <= 0) return false;
       put(o, ':');
       if (!json) put(o, ' ');
     }
-    int rs = put_scalar(A, L, o, val, json);
+    int rs = put_scalar(L, o, val, json);
     if (rs < 0) return false;
     if (rs == 0) {
       if (sp + 1 >= 8) return false;
-      int cls = tclass(A, val);
-      uint32_t n = coll_len(A, L, val);
+      int cls = tclass(val);
+      uint32_t n = coll_len(L, val);
       if (!json && cls == 9 && n == 0) { put_cstr(o, "set()"); continue; }
       st[++sp] = PFrame{val, 0, n, 0, cls};
       put(o, (cls == 7 || (json && cls == 9)) ? '[' : '{');
@@ -568,27 +578,27 @@ __device__ bool put_value(const DevArgs& A, Lane& L, Out& o, uint64_t v, bool js
   return true;
 }
 
-__device__ __forceinline__ bool put_term(const DevArgs& A, Lane& L, Out& o, uint64_t v) { return put_value(A, L, o, v, false); }
-__device__ __forceinline__ bool put_json(const DevArgs& A, Lane& L, Out& o, uint64_t v) { return put_value(A, L, o, v, true); }
+__device__ __forceinline__ bool put_term(Lane& L, Out& o, uint64_t v) { return put_value(L, o, v, false); }
+__device__ __forceinline__ bool put_json(Lane& L, Out& o, uint64_t v) { return put_value(L, o, v, true); }
 
 // Go fmt conversion of one sprintf argument (topdown/strings.go:355-367)
-__device__ bool put_fmt_arg(const DevArgs& A, Lane& L, Out& o, uint64_t v, uint32_t verb) {
+__device__ bool put_fmt_arg(Lane& L, Out& o, uint64_t v, uint32_t verb) {
   uint32_t t = vtag(v);
   if (t == V_STR || t == V_HSTR || t == V_SLICE) {
-    SView s = sview(A, L, v);
+    SView s = sview(L, v);
     if (verb == 'd') { put_cstr(o, "%!d(string="); puts_(o, s.p, s.n); put(o, ')'); return true; }
     puts_(o, s.p, s.n);
     return true;
   }
   if (t == V_NUM) {
-    const NumEnt& n = A.nums[(uint32_t)vpay(v)];
+    const NumEnt& n = gk_args.nums[(uint32_t)vpay(v)];
     if (n.flags & NF_INT64) {
       if (verb == 's') { put_cstr(o, "%!s(int="); put_int(o, n.i); put(o, ')'); return true; }
       put_int(o, n.i);
       return true;
     }
     if (verb != 'v') return false;
-    put_sid(A, o, n.print);
+    put_sid(o, n.print);
     return true;
   }
   if (t == V_INT) {
@@ -599,38 +609,38 @@ __device__ bool put_fmt_arg(const DevArgs& A, Lane& L, Out& o, uint64_t v, uint3
   if (t == V_BFN) return false;
   // everything else is formatted as Term.String() (a Go string)
   if (verb == 'd') return false;
-  return put_term(A, L, o, v);
+  return put_term(L, o, v);
 }
 
 // ------------------------------------------------------------------ regex
 // DFA layout at dfa_words[off]: [nstates, start, then per state: accept flags
 // word, 256 transitions (u16 packed 2 per word)]; accept flags: bit0 = match
 // already found (sticky), bit1 = accepting at end of text.
-__device__ int re_lookup(const DevArgs& A, uint32_t sid) {
-  int lo = 0, hi = (int)A.ndfa - 1;
+__device__ int re_lookup(uint32_t sid) {
+  int lo = 0, hi = (int)gk_args.ndfa - 1;
   while (lo <= hi) {
     int mid = (lo + hi) >> 1;
-    uint32_t k = A.dfa_keys[mid];
+    uint32_t k = gk_args.dfa_keys[mid];
     if (k == sid) return mid;
     if (k < sid) lo = mid + 1; else hi = mid - 1;
   }
   return -1;
 }
 // returns 1 match, 0 no match, -1 error (invalid pattern), -2 fallback
-__device__ int re_run(const DevArgs& A, const Lane& L, uint64_t pat, uint64_t val) {
+__device__ int re_run(const Lane& L, uint64_t pat, uint64_t val) {
   if (vtag(pat) != V_STR) return -2;
-  int e = re_lookup(A, (uint32_t)vpay(pat));
+  int e = re_lookup((uint32_t)vpay(pat));
   if (e < 0) return -2;
-  uint32_t meta = A.dfa_meta[e];
+  uint32_t meta = gk_args.dfa_meta[e];
   uint32_t status = meta >> 30;
   if (status == 1) return -1;
   if (status == 2) return -2;
-  const uint32_t* d = A.dfa_words + (meta & 0x3fffffffu);
+  const uint32_t* d = gk_args.dfa_words + (meta & 0x3fffffffu);
   uint32_t nst = d[0];
   uint32_t s = d[1];
   uint32_t utf8_sensitive = d[2];
   const uint32_t* st = d + 3;
-  SView v = sview(A, L, val);
+  SView v = sview(L, val);
   const uint32_t stride = 1 + 128;
   for (uint32_t i = 0; i < v.n; ++i) {
     unsigned char c = (unsigned char)v.p[i];
@@ -646,11 +656,11 @@ __device__ int re_run(const DevArgs& A, const Lane& L, uint64_t pat, uint64_t va
 }
 
 // ------------------------------------------------------------------ match
-__device__ __forceinline__ bool label_lookup(const DevArgs& A, uint32_t labels, uint32_t key, uint32_t& val) {
+__device__ __forceinline__ bool label_lookup(uint32_t labels, uint32_t key, uint32_t& val) {
   if (labels == NO_ID) return false;
-  const Node& n = A.nodes[labels];
+  const Node& n = gk_args.nodes[labels];
   for (uint32_t i = 0; i < n.n; ++i) {
-    const Node& c = A.nodes[n.first + i];
+    const Node& c = gk_args.nodes[n.first + i];
     if (c.key == key) { val = c.val; return true; }
   }
   return false;
@@ -658,7 +668,7 @@ __device__ __forceinline__ bool label_lookup(const DevArgs& A, uint32_t labels, 
 
 // matches_label_selector (target_template_source.go:185-230) over a labels node
 // whose values are all strings (validated by the host).  Returns 1/0, or -1 error.
-__device__ int sel_match(const DevArgs& A, const uint32_t* w, uint32_t labels) {
+__device__ int sel_match(const uint32_t* w, uint32_t labels) {
   uint32_t flags = w[0];
   if (flags & 2) return -1;         // count() of a non-collection
   if (flags & 1) return 0;          // never satisfiable
@@ -667,7 +677,7 @@ __device__ int sel_match(const DevArgs& A, const uint32_t* w, uint32_t labels) {
   bool ok = true;
   for (uint32_t i = 0; i < nml; ++i) {
     uint32_t k = p[2 * i], v = p[2 * i + 1], lv;
-    if (!(label_lookup(A, labels, k, lv) && lv == v)) ok = false;
+    if (!(label_lookup(labels, k, lv) && lv == v)) ok = false;
   }
   p += 2 * nml;
   if (!ok) return 0;
@@ -678,7 +688,7 @@ __device__ int sel_match(const DevArgs& A, const uint32_t* w, uint32_t labels) {
     const uint32_t* vals = p + 4;
     p += 4 + nv;
     uint32_t lv = 0;
-    bool has = key != NO_ID && label_lookup(A, labels, key, lv);
+    bool has = key != NO_ID && label_lookup(labels, key, lv);
     if (op == SO_IN || op == SO_NOTIN) {
       if (vflags & 2) return -1;      // count(values) type error
       bool nonempty = vflags & 1;
@@ -700,20 +710,20 @@ __device__ int sel_match(const DevArgs& A, const uint32_t* w, uint32_t labels) {
 }
 
 // any_labelselector_match over the review's object / oldObject labels
-__device__ int any_sel(const DevArgs& A, const uint32_t* w, const ReviewCol& rc) {
+__device__ int any_sel(const uint32_t* w, const ReviewCol& rc) {
   bool uo = rc.flags & RC_LABELS_OBJ, ul = rc.flags & RC_LABELS_OLD;
-  if (!uo && !ul) return sel_match(A, w, NO_ID);
+  if (!uo && !ul) return sel_match(w, NO_ID);
   int r = 0;
-  if (uo) { int x = sel_match(A, w, rc.labels); if (x < 0) return -1; r |= x; }
-  if (ul) { int x = sel_match(A, w, rc.old_labels); if (x < 0) return -1; r |= x; }
+  if (uo) { int x = sel_match(w, rc.labels); if (x < 0) return -1; r |= x; }
+  if (ul) { int x = sel_match(w, rc.old_labels); if (x < 0) return -1; r |= x; }
   return r;
 }
 
 // 1 = match, 0 = no match, -1 = error (query fails), -2 = fallback
-__device__ int match_constraint(const DevArgs& A, const MatchSpec& m, const ReviewCol& rc) {
+__device__ int match_constraint(const MatchSpec& m, const ReviewCol& rc) {
   if (m.flags & MF_FALLBACK) return -2;
   if (!(rc.flags & RC_REVIEW_DEF)) return 0;
-  const uint32_t* W = A.mwords;
+  const uint32_t* W = gk_args.mwords;
   // kinds
   {
     const uint32_t* k = W + m.kinds_off;
@@ -758,10 +768,10 @@ __device__ int match_constraint(const DevArgs& A, const MatchSpec& m, const Revi
       if (!kind_def) return 0;
       const uint32_t* w = W + m.nssel_off;
       int r;
-      if (is_ns) r = any_sel(A, w, rc);
+      if (is_ns) r = any_sel(w, rc);
       else {
         if (rc.ns_labels == NO_ID && !(rc.flags & (RC_UNSTABLE_NS | RC_NS_CACHED))) return 0;
-        r = sel_match(A, w, rc.ns_labels);
+        r = sel_match(w, rc.ns_labels);
       }
       if (r < 0) return -1;
       if (!r) return 0;
@@ -775,7 +785,7 @@ __device__ int match_constraint(const DevArgs& A, const MatchSpec& m, const Revi
   }
   // labelSelector
   {
-    int r = any_sel(A, W + m.labelsel_off, rc);
+    int r = any_sel(W + m.labelsel_off, rc);
     if (r < 0) return -1;
     if (!r) return 0;
   }
@@ -822,7 +832,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-__device__ void flush_wave(const DevArgs& A, Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
+__device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
   uint32_t nt = keep ? L.en : 0, nb = 0;
   if (keep)
     for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + L.em_dlen[i];
@@ -831,21 +841,21 @@ __device__ void flush_wave(const DevArgs& A, Lane& L, uint32_t lane, uint32_t r,
   uint32_t pb = wave_excl_scan(nb, lane, tb);
   uint32_t bt = 0, bb = 0;
   if (lane == 63 && tt) {
-    bt = atomicAdd(&A.counters[0], tt);
-    bb = atomicAdd(&A.counters[1], tb);
-    atomicAdd(&A.totals[c], tt);
+    bt = atomicAdd(&gk_args.counters[0], tt);
+    bb = atomicAdd(&gk_args.counters[1], tb);
+    atomicAdd(&gk_args.totals[c], tt);
   }
   if (!tt) return;
   bt = __shfl(bt, 63, 64) + pt;
   bb = __shfl(bb, 63, 64) + pb;
   if (!nt) return;
-  if (bt + nt > A.out_cap || bb + nb > A.bytes_cap) {
-    atomicOr(&A.rflags[r], (uint32_t)RF_OVERFLOW);
+  if (bt + nt > gk_args.out_cap || bb + nb > gk_args.bytes_cap) {
+    atomicOr(&gk_args.rflags[r], (uint32_t)RF_OVERFLOW);
     return;
   }
   for (uint32_t i = 0; i < nt; ++i) {
     uint32_t ml = L.em_mlen[i], dl = L.em_dlen[i], o = L.em_off[i];
-    for (uint32_t j = 0; j < ml + dl; ++j) A.bytes[bb + j] = L.B[o + j];
+    for (uint32_t j = 0; j < ml + dl; ++j) gk_args.bytes[bb + j] = L.B[o + j];
     Viol v;
     v.review = r;
     v.constraint = c;
@@ -855,30 +865,30 @@ __device__ void flush_wave(const DevArgs& A, Lane& L, uint32_t lane, uint32_t r,
     v.msg_len = ml;
     v.det_off = bb + ml;
     v.det_len = dl;
-    A.out[bt + i] = v;
+    gk_args.out[bt + i] = v;
     bb += ml + dl;
   }
 }
 
 // ------------------------------------------------------------------ builtins
-__device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const uint64_t* a) {
+__device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   switch (id) {
     case BI_COUNT: {
       uint32_t t = vtag(a[0]);
-      if (t == V_NODE || t == V_LIST) return mkint(coll_len(A, L, a[0]));
-      if (is_strv(a[0])) return mkint(sview(A, L, a[0]).n);
+      if (t == V_NODE || t == V_LIST) return mkint(coll_len(L, a[0]));
+      if (is_strv(a[0])) return mkint(sview(L, a[0]).n);
       lane_error(L);
       return UND;
     }
     case BI_ANY: case BI_ALL: {
-      int cls = tclass(A, a[0]);
+      int cls = tclass(a[0]);
       if (cls != 7 && cls != 9) { lane_error(L); return UND; }
-      uint32_t n = coll_len(A, L, a[0]);
+      uint32_t n = coll_len(L, a[0]);
       bool any = false, all = true;
       for (uint32_t i = 0; i < n; ++i) {
         uint64_t k, v;
-        coll_at(A, L, a[0], i, k, v);
+        coll_at(L, a[0], i, k, v);
         bool t = vtag(v) == V_BOOL && vpay(v) == 1;
         any |= t;
         all &= t;
@@ -887,7 +897,7 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
     }
     case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS: {
       if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
-      SView s = sview(A, L, a[0]), p = sview(A, L, a[1]);
+      SView s = sview(L, a[0]), p = sview(L, a[1]);
       if (p.n > s.n) return mkv(V_BOOL, 0);
       if (id == BI_STARTSWITH) { for (uint32_t i = 0; i < p.n; ++i) if (s.p[i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
       if (id == BI_ENDSWITH) { uint32_t o = s.n - p.n; for (uint32_t i = 0; i < p.n; ++i) if (s.p[o + i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
@@ -900,7 +910,7 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
     }
     case BI_RE_MATCH: {
       if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
-      int r = re_run(A, L, a[0], a[1]);
+      int r = re_run(L, a[0], a[1]);
       if (r == -1) { lane_error(L); return UND; }
       if (r == -2) { lane_fallback(L, FB_REGEX); return UND; }
       return mkv(V_BOOL, r);
@@ -911,7 +921,7 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
       if (t == V_BOOL) return mkint((int64_t)vpay(a[0]));
       if (is_numv(a[0])) return a[0];
       if (!is_strv(a[0])) { lane_error(L); return UND; }
-      SView s = sview(A, L, a[0]);
+      SView s = sview(L, a[0]);
       // strconv.ParseFloat: plain decimal integers are exact; other valid
       // forms are served by the CPU fallback; invalid syntax is an error.
       uint32_t i = 0;
@@ -936,7 +946,7 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
     }
     case BI_REPLACE: {
       if (!is_strv(a[0]) || !is_strv(a[1]) || !is_strv(a[2])) { lane_error(L); return UND; }
-      SView s = sview(A, L, a[0]), old = sview(A, L, a[1]), nw = sview(A, L, a[2]);
+      SView s = sview(L, a[0]), old = sview(L, a[1]), nw = sview(L, a[2]);
       if (old.n == 0) { lane_fallback(L, FB_STRING); return UND; }
       uint32_t start = L.bp;
       for (uint32_t i = 0; i < s.n;) {
@@ -955,11 +965,11 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
     case BI_SUBSTRING: {
       if (!is_strv(a[0])) { lane_error(L); return UND; }
       int64_t st, ln;
-      if (!is_numv(a[1]) || !num_int(A, L, a[1], st)) { lane_error(L); return UND; }
-      SView s = sview(A, L, a[0]);
+      if (!is_numv(a[1]) || !num_int(L, a[1], st)) { lane_error(L); return UND; }
+      SView s = sview(L, a[0]);
       if (st >= (int64_t)s.n) return mkv(V_STR, 0);  // "" is string id 0
       if (st < 0) { lane_error(L); return UND; }
-      if (!is_numv(a[2]) || !num_int(A, L, a[2], ln)) { lane_error(L); return UND; }
+      if (!is_numv(a[2]) || !num_int(L, a[2], ln)) { lane_error(L); return UND; }
       uint32_t end = ln < 0 ? s.n : (uint32_t)((st + ln) < (int64_t)s.n ? (st + ln) : s.n);
       uint32_t len = end - (uint32_t)st;
       if (vtag(a[0]) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a[0]), (uint32_t)st, len);
@@ -975,45 +985,45 @@ __device__ uint64_t call_builtin(const DevArgs& A, Lane& L, uint32_t id, const u
     case BI_IS_STRING: return mkv(V_BOOL, is_strv(a[0]));
     case BI_IS_BOOLEAN: return mkv(V_BOOL, vtag(a[0]) == V_BOOL);
     case BI_IS_NULL: return mkv(V_BOOL, vtag(a[0]) == V_NULL);
-    case BI_IS_ARRAY: return mkv(V_BOOL, tclass(A, a[0]) == 7);
-    case BI_IS_OBJECT: return mkv(V_BOOL, tclass(A, a[0]) == 8);
-    case BI_IS_SET: return mkv(V_BOOL, tclass(A, a[0]) == 9);
+    case BI_IS_ARRAY: return mkv(V_BOOL, tclass(a[0]) == 7);
+    case BI_IS_OBJECT: return mkv(V_BOOL, tclass(a[0]) == 8);
+    case BI_IS_SET: return mkv(V_BOOL, tclass(a[0]) == 9);
     default: break;
   }
   lane_fallback(L, FB_UNSUPPORTED);
   return UND;
 }
 
-__device__ uint64_t arith(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+__device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
   const uint64_t UND = mkv(V_UNDEF, 0);
-  if (kind == AR_MINUS && tclass(A, x) == 9 && tclass(A, y) == 9) {
-    uint64_t out = list_new(L, LK_SET, coll_len(A, L, x));
+  if (kind == AR_MINUS && tclass(x) == 9 && tclass(y) == 9) {
+    uint64_t out = list_new(L, LK_SET, coll_len(L, x));
     if (vtag(out) == V_UNDEF) return UND;
-    uint32_t n = coll_len(A, L, x);
+    uint32_t n = coll_len(L, x);
     for (uint32_t i = 0; i < n; ++i) {
       uint64_t k, v;
-      coll_at(A, L, x, i, k, v);
-      if (!list_contains(A, L, y, v)) out = list_add(A, L, out, v);
+      coll_at(L, x, i, k, v);
+      if (!list_contains(L, y, v)) out = list_add(L, out, v);
     }
     return out;
   }
   if ((kind == AR_OR || kind == AR_AND)) {
-    if (tclass(A, x) != 9 || tclass(A, y) != 9) { lane_error(L); return UND; }
-    uint32_t nx = coll_len(A, L, x), ny = coll_len(A, L, y);
+    if (tclass(x) != 9 || tclass(y) != 9) { lane_error(L); return UND; }
+    uint32_t nx = coll_len(L, x), ny = coll_len(L, y);
     uint64_t out = list_new(L, LK_SET, nx + ny);
     if (vtag(out) == V_UNDEF) return UND;
     for (uint32_t i = 0; i < nx; ++i) {
       uint64_t k, v;
-      coll_at(A, L, x, i, k, v);
-      if (kind == AR_OR || list_contains(A, L, y, v)) out = list_add(A, L, out, v);
+      coll_at(L, x, i, k, v);
+      if (kind == AR_OR || list_contains(L, y, v)) out = list_add(L, out, v);
     }
     if (kind == AR_OR)
-      for (uint32_t i = 0; i < ny; ++i) { uint64_t k, v; coll_at(A, L, y, i, k, v); out = list_add(A, L, out, v); }
+      for (uint32_t i = 0; i < ny; ++i) { uint64_t k, v; coll_at(L, y, i, k, v); out = list_add(L, out, v); }
     return out;
   }
   if (!is_numv(x) || !is_numv(y)) { lane_error(L); return UND; }
   int64_t a, b;
-  bool ints = num_int(A, L, x, a) && num_int(A, L, y, b);
+  bool ints = num_int(L, x, a) && num_int(L, y, b);
   const int64_t LIM = (1ll << 46);
   switch (kind) {
     case AR_PLUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint(a + b); break;
@@ -1021,7 +1031,7 @@ __device__ uint64_t arith(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, 
     case AR_MUL: {
       if (ints && a < (1ll << 23) && a > -(1ll << 23) && b < (1ll << 23) && b > -(1ll << 23)) return mkint(a * b);
       BF p, q;
-      if (!num_bf(A, L, x, p) || !num_bf(A, L, y, q)) { lane_fallback(L, FB_NUMBER); return UND; }
+      if (!num_bf(L, x, p) || !num_bf(L, y, q)) { lane_fallback(L, FB_NUMBER); return UND; }
       return heap_bf(L, bf_mul(p, q));
     }
     case AR_REM: {
@@ -1036,19 +1046,19 @@ __device__ uint64_t arith(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, 
 }
 
 // ------------------------------------------------------------------ sprintf
-__device__ uint64_t do_sprintf(const DevArgs& A, Lane& L, uint32_t fidx, uint64_t args) {
-  const uint32_t* f = A.fmt + fidx;
+__device__ uint64_t do_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+  const uint32_t* f = gk_args.fmt + fidx;
   uint32_t nseg = f[0], want = f[1];
-  if (tclass(A, args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
-  uint32_t nargs = coll_len(A, L, args);
+  if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
+  uint32_t nargs = coll_len(L, args);
   if (nargs != want) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
   Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
   for (uint32_t s = 0; s < nseg; ++s) {
     uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
-    if (kind == 0) { put_sid(A, o, a); continue; }
+    if (kind == 0) { put_sid(o, a); continue; }
     uint64_t k, v;
-    coll_at(A, L, args, a & 0xffff, k, v);
-    if (!put_fmt_arg(A, L, o, v, a >> 16)) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
+    coll_at(L, args, a & 0xffff, k, v);
+    if (!put_fmt_arg(L, o, v, a >> 16)) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
   }
   if (o.ovf) { lane_fallback(L, FB_MSG_LEN); return mkv(V_UNDEF, 0); }
   uint32_t start = L.bp;
@@ -1069,7 +1079,7 @@ __device__ __forceinline__ void op_iter_init(Lane& L, uint64_t& it, uint64_t& st
 }
 
 // advances the iterator; false when exhausted (jump to the loop exit)
-__device__ __forceinline__ bool op_iter_next(const DevArgs& A, Lane& L, uint64_t coll, uint64_t& st, uint32_t y,
+__device__ __forceinline__ bool op_iter_next(Lane& L, uint64_t coll, uint64_t& st, uint32_t y,
                                              uint64_t& k, uint64_t& v) {
   uint32_t pos = (uint32_t)st;
   // per-iteration reclamation: everything allocated by the previous
@@ -1079,15 +1089,15 @@ __device__ __forceinline__ bool op_iter_next(const DevArgs& A, Lane& L, uint64_t
   L.hp = mh > L.keepH[d] ? mh : L.keepH[d];
   L.bp = mb > L.keepB[d] ? mb : L.keepB[d];
   uint32_t t = vtag(coll);
-  if ((t != V_NODE && t != V_LIST) || pos >= coll_len(A, L, coll)) return false;
-  coll_at(A, L, coll, pos, k, v);
+  if ((t != V_NODE && t != V_LIST) || pos >= coll_len(L, coll)) return false;
+  coll_at(L, coll, pos, k, v);
   st = (st & 0xffffffff00000000ull) | (pos + 1);
   return true;
 }
 
-__device__ __forceinline__ bool op_cmp(const DevArgs& A, Lane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
+__device__ __forceinline__ bool op_cmp(Lane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
   if (vtag(x) == V_UNDEF || vtag(y) == V_UNDEF) { out = mkv(V_UNDEF, 0); return true; }
-  int cr = vcmp(A, L, x, y);
+  int cr = vcmp(L, x, y);
   if (cr == 2) return false;
   if (cr == 3 && kind != CMP_EQ && kind != CMP_NE) { lane_fallback(L, FB_DEEP_EQ); return false; }
   bool res = false;
@@ -1103,31 +1113,31 @@ __device__ __forceinline__ bool op_cmp(const DevArgs& A, Lane& L, uint32_t kind,
   return true;
 }
 
-__device__ __forceinline__ bool op_list_add(const DevArgs& A, Lane& L, uint64_t& l, uint64_t v, uint32_t y) {
-  l = list_add(A, L, l, v);
+__device__ __forceinline__ bool op_list_add(Lane& L, uint64_t& l, uint64_t v, uint32_t y) {
+  l = list_add(L, l, v);
   if (L.fail) return false;
   if (y) pin_escape(L, y);
   return true;
 }
 
-__device__ __forceinline__ bool op_obj_put(const DevArgs& A, Lane& L, uint64_t& o, uint64_t k, uint64_t v, uint32_t y) {
+__device__ __forceinline__ bool op_obj_put(Lane& L, uint64_t& o, uint64_t k, uint64_t v, uint32_t y) {
   uint32_t n = list_len(L, o);
   bool found = false;
   for (uint32_t i = 0; i + 1 < n; i += 2) {
-    if (veq(A, L, list_at(L, o, i), k)) {
+    if (veq(L, list_at(L, o, i), k)) {
       found = true;
-      if (!veq(A, L, list_at(L, o, i + 1), v)) { lane_error(L); return false; }
+      if (!veq(L, list_at(L, o, i + 1), v)) { lane_error(L); return false; }
     }
   }
-  if (!found) { o = list_add(A, L, o, k); o = list_add(A, L, o, v); }
+  if (!found) { o = list_add(L, o, k); o = list_add(L, o, v); }
   if (L.fail) return false;
   if (y) pin_escape(L, y);
   return true;
 }
 
-__device__ __forceinline__ bool op_yield(const DevArgs& A, Lane& L, uint64_t& out, uint64_t v, uint32_t y) {
+__device__ __forceinline__ bool op_yield(Lane& L, uint64_t& out, uint64_t v, uint32_t y) {
   if (vtag(out) != V_UNDEF) {
-    if (!veq(A, L, out, v)) { lane_error(L); return false; }  // conflicting function/rule outputs
+    if (!veq(L, out, v)) { lane_error(L); return false; }  // conflicting function/rule outputs
     if (L.fail) return false;
   } else {
     out = v;
@@ -1136,30 +1146,40 @@ __device__ __forceinline__ bool op_yield(const DevArgs& A, Lane& L, uint64_t& ou
   return true;
 }
 
-__device__ __forceinline__ uint64_t op_len_eq(const DevArgs& A, Lane& L, uint64_t v, uint32_t y) {
+__device__ __forceinline__ uint64_t op_len_eq(Lane& L, uint64_t v, uint32_t y) {
   uint32_t want = y & 0xffffff, kind = y >> 24;
-  int cls = tclass(A, v);
-  bool ok = (kind == LK_ARR ? cls == 7 : cls == 8) && coll_len(A, L, v) == want;
+  int cls = tclass(v);
+  bool ok = (kind == LK_ARR ? cls == 7 : cls == 8) && coll_len(L, v) == want;
   return mkv(V_BOOL, ok);
 }
 
 // f("k1") = v1 {true} ... compiled to a table (compiler.cc table_func): the
 // value of the (at most one) entry whose key equals the argument, else undefined
-__device__ __forceinline__ uint64_t op_table(const DevArgs& A, Lane& L, const uint64_t* T, uint64_t arg) {
+__device__ __forceinline__ uint64_t op_table(Lane& L, const uint64_t* T, uint64_t arg) {
   if (vtag(arg) == V_UNDEF) return mkv(V_UNDEF, 0);
   uint32_t n = (uint32_t)T[0];
   for (uint32_t i = 0; i < n; ++i)
-    if (veq(A, L, T[1 + 2 * i], arg)) return T[2 + 2 * i];
+    if (veq(L, T[1 + 2 * i], arg)) return T[2 + 2 * i];
   return mkv(V_UNDEF, 0);
 }
 
+// Function-call memo (compiler.cc memo_slot): within one lane a Rego function's
+// value depends only on its arguments (templates with `with` fall back), so a
+// call with the same arguments may reuse the last value.  Only heap-free values
+// are keys or results: lane-heap lists / computed strings / big floats can be
+// reclaimed and their handles reused by different contents.
+__device__ __forceinline__ bool memo_stable(uint64_t v) {
+  uint32_t t = vtag(v);
+  return t != V_LIST && t != V_HSTR && t != V_BFN;
+}
+
 // m: message register, d: details register (undefined when absent)
-__device__ __forceinline__ bool op_emit(const DevArgs& A, Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+__device__ __forceinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   if (!is_strv(m)) { lane_error(L); return false; }  // types.Result.msg must unmarshal as a string
-  SView ms = sview(A, L, m);
+  SView ms = sview(L, m);
   char* dbuf = L.B + L.bp;
   Out o{dbuf, 0, (uint32_t)(BCAP - L.bp), false};
-  if (!put_json(A, L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
+  if (!put_json(L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
   stage_tuple(L, rule, ms.p, ms.n, dbuf, o.n, depth);
   return !L.fail;
 }
@@ -1170,21 +1190,21 @@ __device__ __forceinline__ bool op_emit(const DevArgs& A, Lane& L, uint64_t m, u
 // the constraint's MatchSpec loads are wave-uniform.  `run(L, rc, m, r, c)`
 // evaluates the template predicate for a matched lane.
 template <typename Run>
-__device__ __forceinline__ void audit_body(const DevArgs& A, Run run) {
+__device__ __forceinline__ void audit_body(Run run) {
   uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t wave = (uint32_t)(gid >> 6);
   uint32_t lane = (uint32_t)(gid & 63);
-  uint32_t c = A.clist[wave % A.nclist];
-  uint32_t tile = wave / A.nclist;
-  if (tile >= A.ntiles) return;  // wave-uniform
+  uint32_t c = gk_args.clist[wave % gk_args.nclist];
+  uint32_t tile = wave / gk_args.nclist;
+  if (tile >= gk_args.ntiles) return;  // wave-uniform
   uint32_t r = tile * 64 + lane;
   Lane L;
-  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0;
+  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
-  bool live = r < A.nrev;
+  bool live = r < gk_args.nrev;
   if (live) {
-    const ReviewCol rc = A.revs[r];
-    const MatchSpec m = A.cons[c];
+    const ReviewCol rc = gk_args.revs[r];
+    const MatchSpec m = gk_args.cons[c];
     if (rc.flags & RC_FALLBACK) {
       L.fail = RF_FALLBACK;
     } else {
@@ -1194,31 +1214,31 @@ __device__ __forceinline__ void audit_body(const DevArgs& A, Run run) {
         const char* msg = "Namespace is not cached in OPA.";
         stage_tuple(L, RULE_AUTOREJECT, msg, 31, "{}", 2, 0);
       }
-      int mr = match_constraint(A, m, rc);
+      int mr = match_constraint(m, rc);
       if (mr == -1) L.fail = RF_ERROR;
       else if (mr == -2) L.fail = RF_FALLBACK;
       else if (mr == 1 && m.prog != NO_ID) {
-        uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(A, m.params);
+        uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
         run(L, mkv(V_NODE, rc.root), params, m.prog, r, c);
       }
     }
     if (L.fail) {
-      atomicOr(&A.rflags[r], L.fail);
-      if (A.rreason) atomicMax(&A.rreason[r], L.reason);
+      atomicOr(&gk_args.rflags[r], L.fail);
+      if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
     }
   }
   // every lane of the wave reaches here (reconverged): reserve + write output
-  flush_wave(A, L, lane, r, c, live && !L.fail);
-  if (A.prof) {
+  flush_wave(L, lane, r, c, live && !L.fail);
+  if (gk_args.prof) {
     uint32_t mx = L.steps;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) { uint32_t o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
     if (L.steps) {
-      atomicAdd(&A.prof[c * 4 + 0], (unsigned long long)L.steps);
-      atomicMax(&A.prof[c * 4 + 1], (unsigned long long)L.steps);
-      atomicAdd(&A.prof[c * 4 + 2], 1ull);
+      atomicAdd(&gk_args.prof[c * 4 + 0], (unsigned long long)L.steps);
+      atomicMax(&gk_args.prof[c * 4 + 1], (unsigned long long)L.steps);
+      atomicAdd(&gk_args.prof[c * 4 + 2], 1ull);
     }
-    if (lane == 0) atomicAdd(&A.prof[c * 4 + 3], (unsigned long long)mx);
+    if (lane == 0) atomicAdd(&gk_args.prof[c * 4 + 3], (unsigned long long)mx);
   }
 }
 

@@ -97,7 +97,7 @@ struct gk_results {
   double ms[5] = {0, 0, 0, 0, 0};
   uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
   std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
-  struct Launch { std::string kernel; double ms; uint32_t nconstraints; };
+  struct Launch { std::string kernel; double ms; uint32_t nconstraints; uint64_t tuples, bytes; };
   std::vector<Launch> launches;            // kernels of the last attempt, in launch order
 };
 
@@ -131,6 +131,7 @@ struct gk_engine {
     int state = 0;  // 0 not compiled, 1 code ready, -1 compile failed
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    hipDeviceptr_t args = nullptr;  // the module's gk_args (constant memory)
   };
   std::vector<Jit> jits;
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
@@ -277,7 +278,9 @@ static void rebuild_modules(gk_engine* e) {
         if (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))) throw std::runtime_error("internal: register out of range");
         if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
         if (in.op == OP_CALL && in.b + (uint32_t)in.c > p.nregs) throw std::runtime_error("internal: call args");
-        bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || in.op == OP_ITER_NEXT;
+        bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE ||
+                   in.op == OP_ITER_NEXT || in.op == OP_MEMO_GET;
+        if ((in.op == OP_MEMO_GET || in.op == OP_MEMO_PUT) && in.y >= MEMO_SLOTS) throw std::runtime_error("internal: memo slot");
         if (jmp && (in.x < p.code_off || in.x >= p.code_off + p.code_len)) throw std::runtime_error("internal: jump target");
         if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x >= e->bank.consts.size()) throw std::runtime_error("internal: constant index");
         if (in.op == OP_SPRINTF && in.x >= e->bank.fmt.size()) throw std::runtime_error("internal: format index");
@@ -794,11 +797,14 @@ static void ensure_jit(gk_engine* e, bool load) {
   if (!load) return;
   for (auto& j : e->jits) {
     if (j.state != 1 || j.fn) continue;
+    size_t asz = 0;
     if (hipModuleLoadData(&j.mod, j.code.data()) != hipSuccess ||
-        hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess) {
+        hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess ||
+        hipModuleGetGlobal(&j.args, &asz, j.mod, "gk_args") != hipSuccess || asz != sizeof(DevArgs)) {
       if (j.mod) hipModuleUnload(j.mod);
       j.mod = nullptr;
       j.fn = nullptr;
+      j.args = nullptr;
       j.state = -1;
       j.log = "module load failed";
     }
@@ -828,12 +834,12 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
   }
   bool ok = true;
   ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 4) &&
-        e->d_counters.reserve(64) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
+        e->d_counters.reserve(64 + 8 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
   // launch plan: constraints grouped by template kernel (jit.cc); the bytecode
   // VM kernel takes every constraint whose template has no kernel / program
   ensure_jit(e, true);
-  struct Step { hipFunction_t fn; std::string name; uint32_t off, n; };
+  struct Step { hipFunction_t fn; hipDeviceptr_t args; std::string name; uint32_t off, n; };
   std::vector<Step> plan;
   {
     std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
@@ -846,7 +852,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     for (size_t g = 0; g < groups.size(); ++g) {
       if (groups[g].empty()) continue;
       bool vm = g == e->progs.size();
-      plan.push_back({vm ? nullptr : e->jits[g].fn, vm ? std::string("audit_kernel") : e->jits[g].name,
+      plan.push_back({vm ? nullptr : e->jits[g].fn, vm ? nullptr : e->jits[g].args,
+                      vm ? std::string("audit_kernel") : e->jits[g].name,
                       (uint32_t)clist.size(), (uint32_t)groups[g].size()});
       clist.insert(clist.end(), groups[g].begin(), groups[g].end());
     }
@@ -857,7 +864,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     hipMemsetAsync(e->d_rflags.p, 0, nrev * 4, e->stream);
     hipMemsetAsync(e->d_rreason.p, 0, nrev * 4, e->stream);
     hipMemsetAsync(e->d_totals.p, 0, ncons * 4, e->stream);
-    hipMemsetAsync(e->d_counters.p, 0, 64, e->stream);
+    hipMemsetAsync(e->d_counters.p, 0, 64 + 8 * plan.size(), e->stream);
     bool prof = e->profile && e->d_prof.reserve(ncons * 32);
     if (prof) hipMemsetAsync(e->d_prof.p, 0, ncons * 32, e->stream);
     DevArgs a{};
@@ -897,19 +904,24 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     std::vector<hipEvent_t> ev(plan.size() + 1);
     for (auto& x : ev) hipEventCreate(&x);
     hipEventRecord(ev[0], e->stream);
+    std::vector<DevArgs> argv(plan.size(), a);  // live until the stream sync below
     for (size_t i = 0; i < plan.size(); ++i) {
-      a.clist = (const uint32_t*)e->d_clist.p + plan[i].off;
-      a.nclist = plan[i].n;
+      argv[i].clist = (const uint32_t*)e->d_clist.p + plan[i].off;
+      argv[i].nclist = plan[i].n;
+      const DevArgs& a = argv[i];
       int lr;
       if (plan[i].fn) {
         uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
         uint32_t blocks = (uint32_t)((threads + 255) / 256);
-        void* params[] = {&a};
-        lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, e->stream, params, nullptr);
+        lr = (int)hipMemcpyHtoDAsync(plan[i].args, (void*)&a, sizeof(a), e->stream);
+        if (lr == 0)
+          lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, e->stream, nullptr, nullptr);
       } else {
         lr = gk_launch_audit(&a, e->stream);
       }
       hipEventRecord(ev[i + 1], e->stream);
+      // cumulative (tuples, bytes) after this launch -> per-launch output counts
+      hipMemcpyAsync((char*)e->d_counters.p + 64 + 8 * i, e->d_counters.p, 8, hipMemcpyDeviceToDevice, e->stream);
       if (lr != 0) {
         for (auto& x : ev) hipEventDestroy(x);
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
@@ -920,11 +932,14 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       return fail(e, GK_EDEVICE, "kernel execution failed");
     }
     res->launches.clear();
+    std::vector<uint32_t> snap(2 * plan.size());
+    hipMemcpy(snap.data(), (char*)e->d_counters.p + 64, 8 * plan.size(), hipMemcpyDeviceToHost);
     for (size_t i = 0; i < plan.size(); ++i) {
       float kms = 0;
       hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
       res->ms[2] += kms;
-      res->launches.push_back({plan[i].name, (double)kms, plan[i].n});
+      uint32_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
+      res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
     for (auto& x : ev) hipEventDestroy(x);
     auto t1 = Clock::now();
@@ -1425,11 +1440,14 @@ extern "C" size_t gk_results_vm_profile(const gk_results* r, uint64_t* out, size
 
 size_t gk_results_launches(const gk_results* r) { return r ? r->launches.size() : 0; }
 
-int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints) {
+int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints,
+                      uint64_t* tuples, uint64_t* bytes) {
   if (!r || i >= r->launches.size()) return GK_EINVAL;
   if (kernel) *kernel = r->launches[i].kernel.c_str();
   if (ms) *ms = r->launches[i].ms;
   if (nconstraints) *nconstraints = r->launches[i].nconstraints;
+  if (tuples) *tuples = r->launches[i].tuples;
+  if (bytes) *bytes = r->launches[i].bytes;
   return GK_OK;
 }
 
@@ -1558,7 +1576,8 @@ extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   const Program& p = e->progs[it->second.prog];
   static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
                                 "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",
-                                "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK", "TABLE"};
+                                "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK", "TABLE",
+                                "MEMO_GET", "MEMO_PUT"};
   std::string s = "nregs=" + std::to_string(p.nregs) + " len=" + std::to_string(p.code_len) + "\n";
   for (uint32_t i = 0; i < p.code_len; ++i) {
     const Ins& in = e->bank.code[p.code_off + i];

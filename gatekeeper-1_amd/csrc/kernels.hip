@@ -17,46 +17,64 @@ namespace gk {
 
 constexpr int NREG = 192;
 
-__device__ void run_program(const DevArgs& A, Lane& L, uint32_t pc, uint64_t review, uint64_t params) {
+__device__ void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   uint64_t R[NREG];
   for (int guard = 0; guard < (1 << 22); ++guard) {
-    if (pc >= A.ncode) { lane_fallback(L, FB_UNSUPPORTED); return; }
-    const Ins in = A.code[pc];
+    if (pc >= gk_args.ncode) { lane_fallback(L, FB_UNSUPPORTED); return; }
+    const Ins in = gk_args.code[pc];
     ++pc;
     ++L.steps;
-    if (A.pchist) atomicAdd(&A.pchist[pc - 1], 1u);
+    if (gk_args.pchist) atomicAdd(&gk_args.pchist[pc - 1], 1u);
     switch (in.op) {
       case OP_END: return;
       case OP_JMP: pc = in.x; break;
       case OP_JUNDEF: if (vtag(R[in.a]) == V_UNDEF) pc = in.x; break;
       case OP_JFALSE: if (vtag(R[in.a]) == V_BOOL && vpay(R[in.a]) == 0) pc = in.x; break;
       case OP_JTRUE: if (vtag(R[in.a]) == V_BOOL && vpay(R[in.a]) == 1) pc = in.x; break;
-      case OP_LOADK: R[in.a] = A.K[in.x]; break;
+      case OP_LOADK: R[in.a] = gk_args.K[in.x]; break;
       case OP_LOADREV: R[in.a] = review; break;
       case OP_LOADPARAM: R[in.a] = params; break;
       case OP_MOV: R[in.a] = R[in.b]; break;
-      case OP_GET: R[in.a] = vget(A, L, R[in.b], R[in.c]); break;
-      case OP_GETK: R[in.a] = vget(A, L, R[in.b], A.K[in.x]); break;
+      case OP_GET: R[in.a] = vget(L, R[in.b], R[in.c]); break;
+      case OP_GETK: R[in.a] = vget(L, R[in.b], gk_args.K[in.x]); break;
       case OP_ITER_INIT: op_iter_init(L, R[in.a], R[in.a + 1], R[in.b], in.y); break;
       case OP_ITER_NEXT: {
         uint64_t k = UND, v = UND;
-        if (!op_iter_next(A, L, R[in.a], R[in.a + 1], in.y, k, v)) { pc = in.x; break; }
+        if (!op_iter_next(L, R[in.a], R[in.a + 1], in.y, k, v)) { pc = in.x; break; }
         if (in.b != 0xffff) R[in.b] = k;
         if (in.c != 0xffff) R[in.c] = v;
         break;
       }
-      case OP_CMP: if (!op_cmp(A, L, in.y, R[in.b], R[in.c], R[in.a])) return; break;
-      case OP_ARITH: R[in.a] = arith(A, L, in.y, R[in.b], R[in.c]); if (L.fail) return; break;
+      case OP_CMP: if (!op_cmp(L, in.y, R[in.b], R[in.c], R[in.a])) return; break;
+      case OP_ARITH: R[in.a] = arith(L, in.y, R[in.b], R[in.c]); if (L.fail) return; break;
       case OP_LIST_NEW: R[in.a] = list_new(L, in.y, 4); if (L.fail) return; break;
-      case OP_LIST_ADD: if (!op_list_add(A, L, R[in.a], R[in.b], in.y)) return; break;
-      case OP_OBJ_PUT: if (!op_obj_put(A, L, R[in.a], R[in.b], R[in.c], in.y)) return; break;
-      case OP_YIELD: if (!op_yield(A, L, R[in.a], R[in.b], in.y)) return; break;
-      case OP_CALL: R[in.a] = call_builtin(A, L, in.y, &R[in.b]); if (L.fail) return; break;
-      case OP_SPRINTF: R[in.a] = do_sprintf(A, L, in.x, R[in.b]); if (L.fail) return; break;
-      case OP_LEN_EQ: R[in.a] = op_len_eq(A, L, R[in.b], in.y); break;
-      case OP_EMIT: if (!op_emit(A, L, R[in.a], in.b == 0xffff ? UND : R[in.b], in.c, in.y)) return; break;
-      case OP_TABLE: R[in.a] = op_table(A, L, A.K + in.x, R[in.b]); break;
+      case OP_LIST_ADD: if (!op_list_add(L, R[in.a], R[in.b], in.y)) return; break;
+      case OP_OBJ_PUT: if (!op_obj_put(L, R[in.a], R[in.b], R[in.c], in.y)) return; break;
+      case OP_YIELD: if (!op_yield(L, R[in.a], R[in.b], in.y)) return; break;
+      case OP_CALL: R[in.a] = call_builtin(L, in.y, &R[in.b]); if (L.fail) return; break;
+      case OP_SPRINTF: R[in.a] = do_sprintf(L, in.x, R[in.b]); if (L.fail) return; break;
+      case OP_LEN_EQ: R[in.a] = op_len_eq(L, R[in.b], in.y); break;
+      case OP_EMIT: if (!op_emit(L, R[in.a], in.b == 0xffff ? UND : R[in.b], in.c, in.y)) return; break;
+      case OP_TABLE: R[in.a] = op_table(L, gk_args.K + in.x, R[in.b]); break;
+      case OP_MEMO_GET: {
+        uint64_t k1 = in.c == 0xffff ? 0 : R[in.c];
+        if (((L.memo_ok >> in.y) & 1) && L.memo_k0[in.y] == R[in.b] && L.memo_k1[in.y] == k1) {
+          R[in.a] = L.memo_v[in.y];
+          pc = in.x;
+        }
+        break;
+      }
+      case OP_MEMO_PUT: {
+        uint64_t k1 = in.c == 0xffff ? 0 : R[in.c];
+        if (memo_stable(R[in.b]) && memo_stable(k1) && memo_stable(R[in.a])) {
+          L.memo_k0[in.y] = R[in.b];
+          L.memo_k1[in.y] = k1;
+          L.memo_v[in.y] = R[in.a];
+          L.memo_ok |= 1u << in.y;
+        }
+        break;
+      }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
@@ -64,9 +82,9 @@ __device__ void run_program(const DevArgs& A, Lane& L, uint32_t pc, uint64_t rev
   lane_fallback(L, FB_UNSUPPORTED);
 }
 
-__global__ void __launch_bounds__(256) audit_kernel(DevArgs A) {
-  audit_body(A, [&](Lane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
-    run_program(A, L, A.prog_off[prog], review, params);
+__global__ void __launch_bounds__(256) audit_kernel() {
+  audit_body([&](Lane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
+    run_program(L, gk_args.prog_off[prog], review, params);
   });
 }
 
@@ -78,7 +96,9 @@ extern "C" int gk_launch_audit(const gk::DevArgs* a, hipStream_t stream) {
   uint64_t threads = waves * 64;
   uint32_t blocks = (uint32_t)((threads + 255) / 256);
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(gk::audit_kernel, dim3(blocks), dim3(256), 0, stream, *a);
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gk_args), a, sizeof(*a), 0, hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gk::audit_kernel, dim3(blocks), dim3(256), 0, stream);
   return (int)hipGetLastError();
 }
 

@@ -108,7 +108,7 @@ def load_library():
     lib.gk_results_flag_counts.argtypes = [vp, pu64, pu64]
     lib.gk_results_launches.argtypes = [vp]
     lib.gk_results_launches.restype = sz
-    lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+    lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32), pu64, pu64]
     lib.gk_template_backend.argtypes = [vp, cp, C.POINTER(C.c_int), C.POINTER(cp)]
     lib.gk_results_vm_profile.argtypes = [vp, C.c_void_p, sz]
     lib.gk_results_vm_profile.restype = sz
@@ -138,6 +138,18 @@ class Result:
 
 
 @dataclass
+class Launch:
+    kernel: str        # "audit_kernel" (bytecode VM) or "gk_t_<hash>" (template kernel)
+    ms: float          # HIP-event duration
+    constraints: int   # constraints the launch evaluated
+    tuples: int        # violation tuples it wrote
+    bytes: int         # message/details bytes it wrote
+
+    def __iter__(self):  # (kernel, ms, constraints) unpacking
+        return iter((self.kernel, self.ms, self.constraints))
+
+
+@dataclass
 class Results:
     results: List[Result]
     status: List[int]          # per review: GK_REVIEW_ERROR / GK_REVIEW_FALLBACK bits
@@ -149,7 +161,7 @@ class Results:
     n_errors: int = 0
     n_fallbacks: int = 0
     vm_profile: List[int] = field(default_factory=list)  # GKGPU_PROFILE=1 diagnostics
-    launches: List[tuple] = field(default_factory=list)  # (kernel, ms, n constraints) per launch
+    launches: List["Launch"] = field(default_factory=list)  # per kernel launch, in order
 
     def vm_stats(self):
         """per constraint: (sum VM steps, max lane steps, lanes run, sum of per-wave max steps)"""
@@ -172,9 +184,9 @@ def _vm_profile(lib, h):
 def _launches(lib, h):
     out = []
     for i in range(lib.gk_results_launches(h)):
-        k, ms, n = C.c_char_p(), C.c_double(), C.c_uint32()
-        lib.gk_results_launch(h, i, C.byref(k), C.byref(ms), C.byref(n))
-        out.append((k.value.decode(), ms.value, n.value))
+        k, ms, n, t, b = C.c_char_p(), C.c_double(), C.c_uint32(), C.c_uint64(), C.c_uint64()
+        lib.gk_results_launch(h, i, C.byref(k), C.byref(ms), C.byref(n), C.byref(t), C.byref(b))
+        out.append(Launch(k.value.decode(), ms.value, n.value, t.value, b.value))
     return out
 
 

@@ -132,10 +132,11 @@ int gk_results_timing(const gk_results* r, double* ms5);
 /* violation tuples (32 B each) and message/details bytes the kernel wrote */
 int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes);
 /* kernels of the call in launch order: kernel name ("audit_kernel" = bytecode
- * VM, "gk_t_<hash>" = a template kernel), duration (HIP events) and how many
- * constraints it evaluated */
+ * VM, "gk_t_<hash>" = a template kernel), duration (HIP events), how many
+ * constraints it evaluated and the violation tuples / message bytes it wrote */
 size_t gk_results_launches(const gk_results* r);
-int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints);
+int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double* ms, uint32_t* nconstraints,
+                      uint64_t* tuples, uint64_t* bytes);
 void gk_results_free(gk_results* r);
 
 /* ---- introspection --------------------------------------------------------- */

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summaries of a profiles/run_profile.sh run (rocprofv3 rocpd SQLite output).
+
+usage: summarize.py gpurun_out/prof_<round> <round>
+writes profiles/<round>_kernel_stats.txt   (--kernel-trace --stats: per-kernel calls / total / avg)
+       profiles/<round>_traffic.json       (PMC passes: HBM bytes per launch per template kernel)
+       profiles/<round>_bench.json         (the bench line of the same run)
+       profiles/traffic_latest.json        (read by bench.py for roofline.traffic)
+
+HBM bytes (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE come from
+separate passes (they do not share a TCC pass), both in KiB per dispatch; gfx950
+tallies 128-B read requests at 64 B, so FETCH_SIZE is doubled.  The guide
+calibrates only 16-B/lane streaming reads, so this is an estimate for the
+gather-heavy template kernels.  Per kernel, the median over its dispatches.
+"""
+import json
+import os
+import sqlite3
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    lines = ["%-40s %7s %14s %12s %7s" % ("kernel", "calls", "total_us", "avg_us", "pct")]
+    for n, calls, tot, avg, pct in rows:
+        lines.append("%-40s %7d %14.0f %12.0f %7.2f" % (n[:40], calls, tot, avg, pct))
+    return "\n".join(lines) + "\n", {r[0]: r[3] for r in rows}
+
+
+def counter(db, name):
+    c = sqlite3.connect(db)
+    vals = {}
+    for k, v in c.execute("select kernel_name, value from counters_collection where counter_name = ?", (name,)):
+        vals.setdefault(k.split("(")[0].strip(), []).append(float(v) * 1024.0)
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def bench_line(path):
+    return json.loads(open(path).read().strip().splitlines()[-1])
+
+
+def main():
+    d, rnd = sys.argv[1], sys.argv[2]
+    txt, avg = kernel_stats(os.path.join(d, "trace", "run_results.db"))
+    bench = bench_line(os.path.join(d, "bench.json"))
+    tb = bench_line(os.path.join(d, "bench_trace.json"))
+    kt = bench["config"]["kernel_templates"]
+    hdr = ("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0\n"
+           "# (config2, %d pods, %d constraints); bench HIP-event avg of the dominant kernel %s: %.3f ms\n"
+           % (tb["config"]["pods_per_gpu"], tb["config"]["constraints"], tb["roofline"]["kernel"],
+              tb["roofline"]["kernel_ms_avg"]))
+    for k, kind in kt.items():
+        hdr += "# %s = %s\n" % (k, kind)
+    open(os.path.join(HERE, "%s_kernel_stats.txt" % rnd), "w").write(hdr + txt)
+    fetch = counter(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
+    write = counter(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
+    out = {"pods": bench["config"]["pods_per_gpu"], "constraints": bench["config"]["constraints"],
+           "note": "FETCH_SIZE x2 (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE, median per dispatch",
+           "hbm_bytes_per_launch": {}, "fetch_bytes_x2": {}, "write_bytes": {}}
+    for k, kind in kt.items():
+        if k in fetch and k in write:
+            out["fetch_bytes_x2"][kind] = 2 * fetch[k]
+            out["write_bytes"][kind] = write[k]
+            out["hbm_bytes_per_launch"][kind] = 2 * fetch[k] + write[k]
+    for name in ("%s_traffic.json" % rnd, "traffic_latest.json"):
+        json.dump(out, open(os.path.join(HERE, name), "w"), indent=1)
+    open(os.path.join(HERE, "%s_bench.json" % rnd), "w").write(json.dumps(bench) + "\n")
+    print(hdr + txt)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
