@@ -71,6 +71,7 @@ enum Tag : uint32_t {
   V_HSTR = 8,                                      // HSTR: lane byte-buffer string (off:16 | len:16)
   V_LIST = 9,                                      // LIST: heap list (set/array/object); kind in bits 56..59
   V_SLICE = 10,                                    // SLICE: string id:32 | start:14 | len:14
+  V_FMT = 11,                                      // FMT: deferred sprintf (template kernels only): fidx:24 <<32 | args (bit31: node, else heap list offset)
 };
 enum ListKind : uint32_t { LK_SET = 1, LK_ARR = 2, LK_OBJ = 3 };
 

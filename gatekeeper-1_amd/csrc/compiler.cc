@@ -101,6 +101,7 @@ class Comp {
   std::vector<int> labels_;
   std::map<uint64_t, uint32_t> kidx_;
   int reg_top_ = 0, max_reg_ = 0;
+  const Term* stmt_key_ = nullptr;  // last selector of the statement-level ref being compiled
   int inline_depth_ = 0;
   std::map<std::pair<const void*, bool>, int> memo_;  // memo slot per (function, statement form)
   std::vector<int> loop_base_;  // register base of each enclosing ITER loop (innermost last)
@@ -294,7 +295,11 @@ class Comp {
       if (t->k == T_CALL) {
         call(t, env, fail, true, [&](int r, int f) { emit_jmp(OP_JFALSE, r, f); k(f); });
       } else {
+        // a statement-level ref: only its definedness/truthiness is observed
+        // (rule_ref may then unify an object-pattern key member by member)
+        stmt_key_ = (t->k == T_REF && !t->items.empty()) ? t->items.back().get() : nullptr;
         term(t, env, fail, [&](int r, int f) { emit_jmp(OP_JFALSE, r, f); k(f); });
+        stmt_key_ = nullptr;
       }
       return;
     }
@@ -576,6 +581,8 @@ class Comp {
     }
     if (kind == Rule::POBJ) throw Unsupported("partial object rule");
     // partial set
+    bool stmt = i + 1 == path.size() && path[i].get() == stmt_key_;
+    stmt_key_ = nullptr;
     if (i == path.size()) { full_set(rules, fail, k); return; }
     const TermP& key = path[i];
     for (auto& r : rules) {
@@ -604,6 +611,13 @@ class Comp {
         for (auto& pt : pre_terms) safe.push_back(pt.first);
         const auto& body = cbody(r, safe);
         body_k(body, 0, &renv, f, [&](int f2) {
+          if (stmt && same_object_keys(key, r->key)) {
+            // `s[{"msg": msg, "field": "x"}]` as a statement against a rule head
+            // `s[{"msg": m, "field": f}]`: object unification is member-wise
+            // unification over equal key sets, so the head object is never built
+            unify_members(key, r->key, 0, env, &renv, f2, [&](int f4) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f4); });
+            return;
+          }
           term(r->key, &renv, f2, [&](int kv, int f3) {
             unify_value(key, kv, env, f3, [&](int f4) { walk(kv, path, i + 1, env, f4, k); });
           });
@@ -613,6 +627,35 @@ class Comp {
       reg_top_ = save;
     }
     emit_jmp(OP_JMP, 0, fail);
+  }
+
+  // both object literals with scalar keys, the same key set, no duplicates
+  static bool same_object_keys(const TermP& a, const TermP& b) {
+    if (a->k != T_OBJECT || b->k != T_OBJECT || a->items.size() != b->items.size()) return false;
+    for (size_t x = 0; x < a->items.size(); x += 2) {
+      const TermP& ka = a->items[x];
+      if (ka->k != T_SCALAR) return false;
+      int found = 0;
+      for (size_t y = 0; y < b->items.size(); y += 2) {
+        const TermP& kb = b->items[y];
+        if (kb->k != T_SCALAR) return false;
+        if (kb->stype == ka->stype && kb->s == ka->s) ++found;
+      }
+      if (found != 1) return false;
+      for (size_t z = x + 2; z < a->items.size(); z += 2)
+        if (a->items[z]->k == T_SCALAR && a->items[z]->stype == ka->stype && a->items[z]->s == ka->s) return false;
+    }
+    return true;
+  }
+
+  void unify_members(const TermP& pat, const TermP& head, size_t x, Env* env, Env* renv, int fail, const KE& k) {
+    if (x == pat->items.size()) { k(fail); return; }
+    const TermP& ka = pat->items[x];
+    size_t y = 0;
+    while (!(head->items[y]->stype == ka->stype && head->items[y]->s == ka->s)) y += 2;
+    term(head->items[y + 1], renv, fail, [&, x](int hv, int f) {
+      unify_value(pat->items[x + 1], hv, env, f, [&, x](int f2) { unify_members(pat, head, x + 2, env, renv, f2, k); });
+    });
   }
 
   void prebind(const std::vector<std::pair<std::string, TermP>>& pts, size_t i, Env* caller, Env* renv, int fail,

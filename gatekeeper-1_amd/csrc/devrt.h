@@ -38,6 +38,11 @@ __device__ __forceinline__ uint32_t vtag(uint64_t v) { return (uint32_t)(v >> 60
 __device__ __forceinline__ uint64_t vpay(uint64_t v) { return v & 0x0fffffffffffffffull; }
 __device__ __forceinline__ uint64_t mkv(uint32_t t, uint64_t p) { return ((uint64_t)t << 60) | (p & 0x0fffffffffffffffull); }
 __device__ __forceinline__ uint64_t mkint(int64_t i) { return mkv(V_INT, (uint64_t)i & 0x0000ffffffffffffull); }
+// an int that came out of arithmetic: OPA turns big.Float results back into
+// numbers with Text('g', -1), so from 1e6 up they print in exponent form
+// (put_intv); comparisons and intof ignore the flag
+constexpr uint64_t INT_G = 1ull << 48;
+__device__ __forceinline__ uint64_t mkint_g(int64_t i) { return mkint(i) | INT_G; }
 __device__ __forceinline__ int64_t intof(uint64_t v) {
   uint64_t p = vpay(v) & 0x0000ffffffffffffull;
   return (p & 0x0000800000000000ull) ? (int64_t)(p | 0xffff000000000000ull) : (int64_t)p;
@@ -70,7 +75,7 @@ struct Lane {
 // escapes to a register that outlives the iteration)
 __device__ __forceinline__ bool heap_val(uint64_t v) {
   uint32_t t = v >> 60;
-  return t == V_LIST || t == V_BFN || t == V_HSTR;
+  return t == V_LIST || t == V_BFN || t == V_HSTR || t == V_FMT;
 }
 __device__ __forceinline__ void pin_escape(Lane& L, uint32_t range) {
   uint32_t lo = range & 0xff, hi = (range >> 8) & 0xff;
@@ -354,6 +359,14 @@ __device__ bool veq(Lane& L, uint64_t a, uint64_t b) {
     uint32_t t = vtag(a);
     if (t != V_HSTR && t != V_BFN) return true;
   }
+  if (is_strv(a) && is_strv(b)) {
+    // interned strings: equal bytes <=> equal id; otherwise lengths first
+    if (vtag(a) == V_STR && vtag(b) == V_STR) return false;
+    SView x = sview(L, a), y = sview(L, b);
+    if (x.n != y.n) return false;
+    for (uint32_t i = 0; i < x.n; ++i) if (x.p[i] != y.p[i]) return false;
+    return true;
+  }
   int c = vcmp(L, a, b);
   return c == 0;
 }
@@ -439,30 +452,106 @@ __device__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
 }
 
 // ------------------------------------------------------------------ printing
+// Output sinks of the printers below (each has put(c); puts_/put_* dispatch on it):
+//   Out  — the lane byte buffer (eagerly formatted strings, details JSON);
+//   Cnt  — length only (sizing a deferred message before the wave reservation);
+//   GOut — the global output bytes at a reserved offset, packed into dword
+//          stores (byte stores only for the partial dwords at either end, which
+//          neighbouring tuples share).
 struct Out {
   char* p;
   uint32_t n, cap;
   bool ovf;
+  __device__ __forceinline__ void put(char c) { if (n < cap) p[n++] = c; else ovf = true; }
 };
-__device__ __forceinline__ void put(Out& o, char c) { if (o.n < o.cap) o.p[o.n++] = c; else o.ovf = true; }
-__device__ __forceinline__ void puts_(Out& o, const char* s, uint32_t n) { for (uint32_t i = 0; i < n; ++i) put(o, s[i]); }
-__device__ void put_cstr(Out& o, const char* s) { while (*s) put(o, *s++); }
-__device__ void put_int(Out& o, int64_t v) {
-  char t[24];
-  int n = 0;
-  uint64_t a = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
-  do { t[n++] = (char)('0' + a % 10); a /= 10; } while (a);
-  if (v < 0) put(o, '-');
-  while (n) put(o, t[--n]);
+struct Cnt {
+  uint32_t n;
+  bool ovf;
+  __device__ __forceinline__ void put(char) { ++n; }
+};
+struct GOut {
+  uint8_t* base;
+  uint32_t start, pos, acc;
+  bool ovf;
+  __device__ __forceinline__ void word(uint32_t w) {
+    if (w >= start) *(uint32_t*)(base + w) = acc;
+    else for (uint32_t i = start - w; i < 4; ++i) base[w + i] = (uint8_t)(acc >> (8 * i));
+  }
+  __device__ __forceinline__ void put(char c) {
+    acc |= (uint32_t)(uint8_t)c << ((pos & 3) * 8);
+    if ((++pos & 3) == 0) { word(pos - 4); acc = 0; }
+  }
+  __device__ __forceinline__ void finish() {
+    if (pos & 3) {
+      uint32_t w = pos & ~3u, lo = w > start ? w : start;
+      for (uint32_t i = lo; i < pos; ++i) base[i] = (uint8_t)(acc >> (8 * (i - w)));
+    }
+  }
+};
+template <class O> __device__ __forceinline__ void put(O& o, char c) { o.put(c); }
+// n bytes at s, read a dword at a time (the device string pool is padded past
+// its end; lane buffers are dword-aligned arrays)
+template <class O> __device__ __forceinline__ void puts_(O& o, const char* s, uint32_t n) {
+  if (!n) return;
+  uint64_t a = (uint64_t)s;
+  const uint32_t* w = (const uint32_t*)(a & ~(uint64_t)3);
+  uint32_t sh = (uint32_t)(a & 3);
+  uint32_t cur = *w;
+  for (uint32_t i = 0; i < n; ++i) {
+    o.put((char)(cur >> (8 * sh)));
+    if (++sh == 4 && i + 1 < n) { sh = 0; cur = *++w; }
+  }
 }
-__device__ void put_sid(Out& o, uint32_t sid) {
+__device__ __forceinline__ void puts_(Cnt& o, const char*, uint32_t n) { o.n += n; }
+template <class O> __device__ void put_cstr(O& o, const char* s) { while (*s) put(o, *s++); }
+template <class O> __device__ void put_int(O& o, int64_t v) {
+  uint64_t a = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+  if (v < 0) put(o, '-');
+  uint64_t p = 1;
+  while (p <= a / 10) p *= 10;
+  for (;;) {
+    put(o, (char)('0' + (a / p) % 10));
+    if (p == 1) break;
+    p /= 10;
+  }
+}
+// V_INT text: plain for counts and parsed integers; arithmetic results
+// (INT_G) as big.Float.Text('g', -1) -- exponent form from 1e6 up, digits
+// without trailing zeros (31457280 -> 3.145728e+07)
+__device__ __forceinline__ bool intv_gform(uint64_t v) {
+  int64_t i = intof(v);
+  return (v & INT_G) && (i >= 1000000 || i <= -1000000);
+}
+template <class O> __device__ void put_intv(O& o, uint64_t v) {
+  int64_t i = intof(v);
+  if (!intv_gform(v)) { put_int(o, i); return; }
+  uint64_t a = i < 0 ? (uint64_t)(-i) : (uint64_t)i;
+  if (i < 0) put(o, '-');
+  uint32_t e = 0;
+  while (a % 10 == 0) { a /= 10; ++e; }
+  uint64_t p = 1;
+  uint32_t d = 1;
+  while (p <= a / 10) { p *= 10; ++d; }
+  e += d - 1;
+  put(o, (char)('0' + a / p));
+  a %= p;
+  if (d > 1) {
+    put(o, '.');
+    for (p /= 10; p; p /= 10) { put(o, (char)('0' + a / p)); a %= p; }
+  }
+  put(o, 'e');
+  put(o, '+');
+  put(o, (char)('0' + e / 10));
+  put(o, (char)('0' + e % 10));
+}
+template <class O> __device__ void put_sid(O& o, uint32_t sid) {
   const StrEnt& s = gk_args.strs[sid];
   puts_(o, (const char*)gk_args.pool + s.off, s.len);
 }
 __device__ const char* hexd = "0123456789abcdef";
 
 // strconv.Quote; returns false if a non-ASCII byte needs unicode.IsPrint
-__device__ bool put_quoted(Out& o, SView s) {
+template <class O> __device__ bool put_quoted(O& o, SView s) {
   put(o, '"');
   for (uint32_t i = 0; i < s.n; ++i) {
     unsigned char c = (unsigned char)s.p[i];
@@ -485,7 +574,7 @@ __device__ bool put_quoted(Out& o, SView s) {
 }
 
 // encoding/json string (HTMLEscape); false on non-ASCII
-__device__ bool put_json_str(Out& o, SView s) {
+template <class O> __device__ bool put_json_str(O& o, SView s) {
   put(o, '"');
   for (uint32_t i = 0; i < s.n; ++i) {
     unsigned char c = (unsigned char)s.p[i];
@@ -506,16 +595,17 @@ __device__ bool put_json_str(Out& o, SView s) {
 }
 
 // scalar Term.String()/JSON; returns 0 not-scalar, 1 ok, -1 fallback
-__device__ int put_scalar(Lane& L, Out& o, uint64_t v, bool json) {
+template <class O> __device__ int put_scalar(Lane& L, O& o, uint64_t v, bool json) {
   switch (vtag(v)) {
     case V_UNDEF: if (json) { put_cstr(o, "{}"); return 1; } return -1;
     case V_NULL: put_cstr(o, "null"); return 1;
     case V_BOOL: put_cstr(o, vpay(v) ? "true" : "false"); return 1;
     case V_NUM: put_sid(o, gk_args.nums[(uint32_t)vpay(v)].text); return 1;
-    case V_INT: put_int(o, intof(v)); return 1;
+    case V_INT: put_intv(o, v); return 1;
     case V_BFN: return -1;
     case V_STR: case V_HSTR: case V_SLICE:
       return (json ? put_json_str(o, sview(L, v)) : put_quoted(o, sview(L, v))) ? 1 : -1;
+    case V_FMT: return -1;  // forced before any printing (jit.cc)
     default: return 0;
   }
 }
@@ -524,7 +614,7 @@ struct PFrame { uint64_t v; uint32_t i, n; uint64_t last; int cls; };
 
 // ast.Term.String() (json=false) or encoding/json of ast.JSON (json=true, map
 // keys in byte order), iterative with an explicit stack; false => fallback
-__device__ bool put_value(Lane& L, Out& o, uint64_t v, bool json) {
+template <class O> __device__ bool put_value(Lane& L, O& o, uint64_t v, bool json) {
   int r = put_scalar(L, o, v, json);
   if (r != 0) return r > 0;
   PFrame st[8];
@@ -578,11 +668,11 @@ __device__ bool put_value(Lane& L, Out& o, uint64_t v, bool json) {
   return true;
 }
 
-__device__ __forceinline__ bool put_term(Lane& L, Out& o, uint64_t v) { return put_value(L, o, v, false); }
-__device__ __forceinline__ bool put_json(Lane& L, Out& o, uint64_t v) { return put_value(L, o, v, true); }
+template <class O> __device__ __forceinline__ bool put_term(Lane& L, O& o, uint64_t v) { return put_value(L, o, v, false); }
+template <class O> __device__ __forceinline__ bool put_json(Lane& L, O& o, uint64_t v) { return put_value(L, o, v, true); }
 
 // Go fmt conversion of one sprintf argument (topdown/strings.go:355-367)
-__device__ bool put_fmt_arg(Lane& L, Out& o, uint64_t v, uint32_t verb) {
+template <class O> __device__ bool put_fmt_arg(Lane& L, O& o, uint64_t v, uint32_t verb) {
   uint32_t t = vtag(v);
   if (t == V_STR || t == V_HSTR || t == V_SLICE) {
     SView s = sview(L, v);
@@ -602,14 +692,31 @@ __device__ bool put_fmt_arg(Lane& L, Out& o, uint64_t v, uint32_t verb) {
     return true;
   }
   if (t == V_INT) {
+    if (intv_gform(v)) {  // a float64 to Go fmt
+      if (verb != 'v') return false;
+      put_intv(o, v);
+      return true;
+    }
     if (verb == 's') { put_cstr(o, "%!s(int="); put_int(o, intof(v)); put(o, ')'); return true; }
     put_int(o, intof(v));
     return true;
   }
-  if (t == V_BFN) return false;
+  if (t == V_BFN || t == V_FMT) return false;
   // everything else is formatted as Term.String() (a Go string)
   if (verb == 'd') return false;
   return put_term(L, o, v);
+}
+
+// the segments of format fidx (compiler.cc parse_format) with argument i = arg(i)
+template <class O, class A> __device__ bool fmt_run(Lane& L, O& o, uint32_t fidx, A arg) {
+  const uint32_t* f = gk_args.fmt + fidx;
+  uint32_t nseg = f[0];
+  for (uint32_t s = 0; s < nseg; ++s) {
+    uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
+    if (kind == 0) { put_sid(o, a); continue; }
+    if (!put_fmt_arg(L, o, arg(a & 0xffff), a >> 16)) return false;
+  }
+  return true;
 }
 
 // ------------------------------------------------------------------ regex
@@ -835,7 +942,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
   uint32_t nt = keep ? L.en : 0, nb = 0;
   if (keep)
-    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + L.em_dlen[i];
+    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + (L.em_dlen[i] & 0x7fffu);
   uint32_t tt, tb;
   uint32_t pt = wave_excl_scan(nt, lane, tt);
   uint32_t pb = wave_excl_scan(nb, lane, tb);
@@ -854,8 +961,18 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
     return;
   }
   for (uint32_t i = 0; i < nt; ++i) {
-    uint32_t ml = L.em_mlen[i], dl = L.em_dlen[i], o = L.em_off[i];
-    for (uint32_t j = 0; j < ml + dl; ++j) gk_args.bytes[bb + j] = L.B[o + j];
+    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = dw & 0x7fffu, o = L.em_off[i];
+    GOut g{(uint8_t*)gk_args.bytes, bb, bb, 0, false};
+    if (dw & 0x8000u) {
+      // deferred message (op_emit): record [fidx | nargs << 24, args...], then details
+      const uint64_t* rec = (const uint64_t*)(L.B + o);
+      uint32_t h = (uint32_t)rec[0], na = h >> 24;
+      fmt_run(L, g, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
+      puts_(g, L.B + o + 8 * (1 + na), dl);
+    } else {
+      puts_(g, L.B + o, ml + dl);
+    }
+    g.finish();
     Viol v;
     v.review = r;
     v.constraint = c;
@@ -871,116 +988,151 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
 }
 
 // ------------------------------------------------------------------ builtins
-__device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
+// One device function per builtin: template kernels call them directly with
+// register operands (jit.cc); the VM dispatches through call_builtin.
+__device__ __forceinline__ uint64_t bi_count(Lane& L, uint64_t a) {
+  uint32_t t = vtag(a);
+  if (t == V_NODE || t == V_LIST) return mkint(coll_len(L, a));
+  if (is_strv(a)) return mkint(sview(L, a).n);
+  lane_error(L);
+  return mkv(V_UNDEF, 0);
+}
+
+__device__ uint64_t bi_anyall(Lane& L, uint32_t id, uint64_t a) {
+  int cls = tclass(a);
+  if (cls != 7 && cls != 9) { lane_error(L); return mkv(V_UNDEF, 0); }
+  uint32_t n = coll_len(L, a);
+  bool any = false, all = true;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t k, v;
+    coll_at(L, a, i, k, v);
+    bool t = vtag(v) == V_BOOL && vpay(v) == 1;
+    any |= t;
+    all &= t;
+  }
+  return mkv(V_BOOL, id == BI_ANY ? any : all);
+}
+
+// startswith / endswith / contains (topdown/strings.go:135-175, byte-wise)
+__device__ uint64_t bi_strpred(Lane& L, uint32_t id, uint64_t a, uint64_t b) {
+  if (!is_strv(a) || !is_strv(b)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  SView s = sview(L, a), p = sview(L, b);
+  if (p.n > s.n) return mkv(V_BOOL, 0);
+  if (id == BI_STARTSWITH) { for (uint32_t i = 0; i < p.n; ++i) if (s.p[i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
+  if (id == BI_ENDSWITH) { uint32_t o = s.n - p.n; for (uint32_t i = 0; i < p.n; ++i) if (s.p[o + i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
+  for (uint32_t o = 0; o + p.n <= s.n; ++o) {
+    bool m = true;
+    for (uint32_t i = 0; i < p.n && m; ++i) if (s.p[o + i] != p.p[i]) m = false;
+    if (m) return mkv(V_BOOL, 1);
+  }
+  return mkv(V_BOOL, 0);
+}
+
+// re_run / a literal pattern's compiled DFA (jit.cc) -> value: 1/0 match,
+// -1 invalid pattern (builtin error), -2 CPU fallback
+__device__ __forceinline__ uint64_t re_result(Lane& L, int r) {
+  if (r == -1) { lane_error(L); return mkv(V_UNDEF, 0); }
+  if (r == -2) { lane_fallback(L, FB_REGEX); return mkv(V_UNDEF, 0); }
+  return mkv(V_BOOL, r);
+}
+__device__ __forceinline__ uint64_t bi_re_match(Lane& L, uint64_t a, uint64_t b) {
+  if (!is_strv(a) || !is_strv(b)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  return re_result(L, re_run(L, a, b));
+}
+
+// to_number (topdown/casts.go:14-33).  The number keeps the string's text, so
+// only canonical integer texts become V_INT (no '+', no leading zero, no "-0":
+// those print differently); other valid forms go to the CPU fallback.
+__device__ uint64_t bi_to_number(Lane& L, uint64_t a) {
   const uint64_t UND = mkv(V_UNDEF, 0);
+  uint32_t t = vtag(a);
+  if (t == V_NULL) return mkint(0);
+  if (t == V_BOOL) return mkint((int64_t)vpay(a));
+  if (is_numv(a)) return a;
+  if (!is_strv(a)) { lane_error(L); return UND; }
+  SView s = sview(L, a);
+  uint32_t i = 0;
+  bool neg = false;
+  if (i < s.n && (s.p[i] == '+' || s.p[i] == '-')) { neg = s.p[i] == '-'; ++i; }
+  if (i >= s.n) { lane_error(L); return UND; }
+  bool digits_only = true, any_digit = false, dot = false, ex = false, bad = false;
+  for (uint32_t j = i; j < s.n; ++j) {
+    char c = s.p[j];
+    if (c >= '0' && c <= '9') { any_digit = true; continue; }
+    digits_only = false;
+    if (c == '.' && !dot && !ex) { dot = true; continue; }
+    if ((c == 'e' || c == 'E') && any_digit && !ex) { ex = true; if (j + 1 < s.n && (s.p[j + 1] == '+' || s.p[j + 1] == '-')) ++j; continue; }
+    if (c == 'i' || c == 'I' || c == 'n' || c == 'N' || c == 'x' || c == 'X' || c == '_' || c == 'p' || c == 'P') { lane_fallback(L, FB_NUMBER); return UND; }
+    bad = true;
+  }
+  if (bad || !any_digit) { lane_error(L); return UND; }
+  if (!digits_only || s.n - i > 15 || s.p[0] == '+' || (s.n - i > 1 && s.p[i] == '0')) { lane_fallback(L, FB_NUMBER); return UND; }
+  int64_t v = 0;
+  for (uint32_t j = i; j < s.n; ++j) v = v * 10 + (s.p[j] - '0');
+  if (neg && v == 0) { lane_fallback(L, FB_NUMBER); return UND; }
+  return mkint(neg ? -v : v);
+}
+
+// replace = strings.Replace(s, old, new, -1) (topdown/strings.go:212-229)
+__device__ uint64_t bi_replace(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  if (!is_strv(a0) || !is_strv(a1) || !is_strv(a2)) { lane_error(L); return UND; }
+  SView s = sview(L, a0), old = sview(L, a1), nw = sview(L, a2);
+  if (old.n == 0) { lane_fallback(L, FB_STRING); return UND; }
+  // no occurrence: the result is the subject itself (no lane-buffer copy)
+  bool any = false;
+  for (uint32_t i = 0; i + old.n <= s.n && !any; ++i) {
+    bool m = true;
+    for (uint32_t j = 0; j < old.n && m; ++j) if (s.p[i + j] != old.p[j]) m = false;
+    any = m;
+  }
+  if (!any) return a0;
+  uint32_t start = L.bp;
+  for (uint32_t i = 0; i < s.n;) {
+    bool m = i + old.n <= s.n;
+    for (uint32_t j = 0; j < old.n && m; ++j) if (s.p[i + j] != old.p[j]) m = false;
+    if (m) {
+      for (uint32_t j = 0; j < nw.n; ++j) { if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; } L.B[L.bp++] = nw.p[j]; }
+      i += old.n;
+    } else {
+      if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; }
+      L.B[L.bp++] = s.p[i++];
+    }
+  }
+  return mkhstr(start, L.bp - start);
+}
+
+// substring(s, start, length), byte-indexed (topdown/strings.go:100-133)
+__device__ uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  if (!is_strv(a0)) { lane_error(L); return UND; }
+  int64_t st, ln;
+  if (!is_numv(a1) || !num_int(L, a1, st)) { lane_error(L); return UND; }
+  SView s = sview(L, a0);
+  if (st >= (int64_t)s.n) return mkv(V_STR, 0);  // "" is string id 0
+  if (st < 0) { lane_error(L); return UND; }
+  if (!is_numv(a2) || !num_int(L, a2, ln)) { lane_error(L); return UND; }
+  uint32_t end = ln < 0 ? s.n : (uint32_t)((st + ln) < (int64_t)s.n ? (st + ln) : s.n);
+  uint32_t len = end - (uint32_t)st;
+  if (vtag(a0) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a0), (uint32_t)st, len);
+  if (vtag(a0) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + (uint32_t)st, len);
+  if (vtag(a0) == V_SLICE) {
+    uint64_t p = vpay(a0);
+    return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + (uint32_t)st, len);
+  }
+  lane_fallback(L, FB_STRING);
+  return UND;
+}
+
+__device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
   switch (id) {
-    case BI_COUNT: {
-      uint32_t t = vtag(a[0]);
-      if (t == V_NODE || t == V_LIST) return mkint(coll_len(L, a[0]));
-      if (is_strv(a[0])) return mkint(sview(L, a[0]).n);
-      lane_error(L);
-      return UND;
-    }
-    case BI_ANY: case BI_ALL: {
-      int cls = tclass(a[0]);
-      if (cls != 7 && cls != 9) { lane_error(L); return UND; }
-      uint32_t n = coll_len(L, a[0]);
-      bool any = false, all = true;
-      for (uint32_t i = 0; i < n; ++i) {
-        uint64_t k, v;
-        coll_at(L, a[0], i, k, v);
-        bool t = vtag(v) == V_BOOL && vpay(v) == 1;
-        any |= t;
-        all &= t;
-      }
-      return mkv(V_BOOL, id == BI_ANY ? any : all);
-    }
-    case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS: {
-      if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
-      SView s = sview(L, a[0]), p = sview(L, a[1]);
-      if (p.n > s.n) return mkv(V_BOOL, 0);
-      if (id == BI_STARTSWITH) { for (uint32_t i = 0; i < p.n; ++i) if (s.p[i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
-      if (id == BI_ENDSWITH) { uint32_t o = s.n - p.n; for (uint32_t i = 0; i < p.n; ++i) if (s.p[o + i] != p.p[i]) return mkv(V_BOOL, 0); return mkv(V_BOOL, 1); }
-      for (uint32_t o = 0; o + p.n <= s.n; ++o) {
-        bool m = true;
-        for (uint32_t i = 0; i < p.n && m; ++i) if (s.p[o + i] != p.p[i]) m = false;
-        if (m) return mkv(V_BOOL, 1);
-      }
-      return mkv(V_BOOL, 0);
-    }
-    case BI_RE_MATCH: {
-      if (!is_strv(a[0]) || !is_strv(a[1])) { lane_error(L); return UND; }
-      int r = re_run(L, a[0], a[1]);
-      if (r == -1) { lane_error(L); return UND; }
-      if (r == -2) { lane_fallback(L, FB_REGEX); return UND; }
-      return mkv(V_BOOL, r);
-    }
-    case BI_TO_NUMBER: {
-      uint32_t t = vtag(a[0]);
-      if (t == V_NULL) return mkint(0);
-      if (t == V_BOOL) return mkint((int64_t)vpay(a[0]));
-      if (is_numv(a[0])) return a[0];
-      if (!is_strv(a[0])) { lane_error(L); return UND; }
-      SView s = sview(L, a[0]);
-      // strconv.ParseFloat: plain decimal integers are exact; other valid
-      // forms are served by the CPU fallback; invalid syntax is an error.
-      uint32_t i = 0;
-      bool neg = false;
-      if (i < s.n && (s.p[i] == '+' || s.p[i] == '-')) { neg = s.p[i] == '-'; ++i; }
-      if (i >= s.n) { lane_error(L); return UND; }
-      bool digits_only = true, any_digit = false, dot = false, ex = false, bad = false;
-      for (uint32_t j = i; j < s.n; ++j) {
-        char c = s.p[j];
-        if (c >= '0' && c <= '9') { any_digit = true; continue; }
-        digits_only = false;
-        if (c == '.' && !dot && !ex) { dot = true; continue; }
-        if ((c == 'e' || c == 'E') && any_digit && !ex) { ex = true; if (j + 1 < s.n && (s.p[j + 1] == '+' || s.p[j + 1] == '-')) ++j; continue; }
-        if (c == 'i' || c == 'I' || c == 'n' || c == 'N' || c == 'x' || c == 'X' || c == '_' || c == 'p' || c == 'P') { lane_fallback(L, FB_NUMBER); return UND; }
-        bad = true;
-      }
-      if (bad || !any_digit) { lane_error(L); return UND; }
-      if (!digits_only || s.n - i > 15) { lane_fallback(L, FB_NUMBER); return UND; }
-      int64_t v = 0;
-      for (uint32_t j = i; j < s.n; ++j) v = v * 10 + (s.p[j] - '0');
-      return mkint(neg ? -v : v);
-    }
-    case BI_REPLACE: {
-      if (!is_strv(a[0]) || !is_strv(a[1]) || !is_strv(a[2])) { lane_error(L); return UND; }
-      SView s = sview(L, a[0]), old = sview(L, a[1]), nw = sview(L, a[2]);
-      if (old.n == 0) { lane_fallback(L, FB_STRING); return UND; }
-      uint32_t start = L.bp;
-      for (uint32_t i = 0; i < s.n;) {
-        bool m = i + old.n <= s.n;
-        for (uint32_t j = 0; j < old.n && m; ++j) if (s.p[i + j] != old.p[j]) m = false;
-        if (m) {
-          for (uint32_t j = 0; j < nw.n; ++j) { if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; } L.B[L.bp++] = nw.p[j]; }
-          i += old.n;
-        } else {
-          if (L.bp >= BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; }
-          L.B[L.bp++] = s.p[i++];
-        }
-      }
-      return mkhstr(start, L.bp - start);
-    }
-    case BI_SUBSTRING: {
-      if (!is_strv(a[0])) { lane_error(L); return UND; }
-      int64_t st, ln;
-      if (!is_numv(a[1]) || !num_int(L, a[1], st)) { lane_error(L); return UND; }
-      SView s = sview(L, a[0]);
-      if (st >= (int64_t)s.n) return mkv(V_STR, 0);  // "" is string id 0
-      if (st < 0) { lane_error(L); return UND; }
-      if (!is_numv(a[2]) || !num_int(L, a[2], ln)) { lane_error(L); return UND; }
-      uint32_t end = ln < 0 ? s.n : (uint32_t)((st + ln) < (int64_t)s.n ? (st + ln) : s.n);
-      uint32_t len = end - (uint32_t)st;
-      if (vtag(a[0]) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a[0]), (uint32_t)st, len);
-      if (vtag(a[0]) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + (uint32_t)st, len);
-      if (vtag(a[0]) == V_SLICE) {
-        uint64_t p = vpay(a[0]);
-        return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + (uint32_t)st, len);
-      }
-      lane_fallback(L, FB_STRING);
-      return UND;
-    }
+    case BI_COUNT: return bi_count(L, a[0]);
+    case BI_ANY: case BI_ALL: return bi_anyall(L, id, a[0]);
+    case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS: return bi_strpred(L, id, a[0], a[1]);
+    case BI_RE_MATCH: return bi_re_match(L, a[0], a[1]);
+    case BI_TO_NUMBER: return bi_to_number(L, a[0]);
+    case BI_REPLACE: return bi_replace(L, a[0], a[1], a[2]);
+    case BI_SUBSTRING: return bi_substring(L, a[0], a[1], a[2]);
     case BI_IS_NUMBER: return mkv(V_BOOL, is_numv(a[0]));
     case BI_IS_STRING: return mkv(V_BOOL, is_strv(a[0]));
     case BI_IS_BOOLEAN: return mkv(V_BOOL, vtag(a[0]) == V_BOOL);
@@ -991,7 +1143,7 @@ __device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
     default: break;
   }
   lane_fallback(L, FB_UNSUPPORTED);
-  return UND;
+  return mkv(V_UNDEF, 0);
 }
 
 __device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
@@ -1026,10 +1178,16 @@ __device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
   bool ints = num_int(L, x, a) && num_int(L, y, b);
   const int64_t LIM = (1ll << 46);
   switch (kind) {
-    case AR_PLUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint(a + b); break;
-    case AR_MINUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint(a - b); break;
+    case AR_PLUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint_g(a + b); break;
+    case AR_MINUS: if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) return mkint_g(a - b); break;
     case AR_MUL: {
-      if (ints && a < (1ll << 23) && a > -(1ll << 23) && b < (1ll << 23) && b > -(1ll << 23)) return mkint(a * b);
+      // an integer product below 2^46 in magnitude is exact at any precision the
+      // big.Float Mul rounds to (64-bit mantissa), so it stays a heap-free V_INT
+      // (memoizable; e.g. to_number("1") * mem_multiple("Gi") = 2^30)
+      if (ints && a < LIM && a > -LIM && b < LIM && b > -LIM) {
+        uint64_t ua = a < 0 ? (uint64_t)(-a) : (uint64_t)a, ub = b < 0 ? (uint64_t)(-b) : (uint64_t)b;
+        if (__umul64hi(ua, ub) == 0 && ua * ub < (uint64_t)LIM) return mkint_g(a * b);
+      }
       BF p, q;
       if (!num_bf(L, x, p) || !num_bf(L, y, q)) { lane_fallback(L, FB_NUMBER); return UND; }
       return heap_bf(L, bf_mul(p, q));
@@ -1048,22 +1206,47 @@ __device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
 // ------------------------------------------------------------------ sprintf
 __device__ uint64_t do_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
   const uint32_t* f = gk_args.fmt + fidx;
-  uint32_t nseg = f[0], want = f[1];
+  uint32_t want = f[1];
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t nargs = coll_len(L, args);
   if (nargs != want) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
   Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
-  for (uint32_t s = 0; s < nseg; ++s) {
-    uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
-    if (kind == 0) { put_sid(o, a); continue; }
-    uint64_t k, v;
-    coll_at(L, args, a & 0xffff, k, v);
-    if (!put_fmt_arg(L, o, v, a >> 16)) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
-  }
+  bool ok = fmt_run(L, o, fidx, [&](uint32_t i) { uint64_t k, v; coll_at(L, args, i, k, v); return v; });
+  if (!ok) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
   if (o.ovf) { lane_fallback(L, FB_MSG_LEN); return mkv(V_UNDEF, 0); }
   uint32_t start = L.bp;
   L.bp += o.n;
   return mkhstr(start, o.n);
+}
+
+// Deferred sprintf (template kernels): the message is not built in the lane
+// buffer; the value records (format, argument array) and is formatted straight
+// into the output bytes when the violation is flushed (flush_wave), or forced
+// into the lane buffer where anything else reads it (jit.cc inserts force_fmt).
+// The argument array is the heap list / document array sprintf received, so a
+// V_FMT lives exactly as long as that array (heap_val: pinned like a list).
+constexpr uint32_t FMT_MAXARGS = 6;
+__device__ __forceinline__ uint64_t fmt_args(uint64_t f) {
+  uint64_t p = vpay(f);
+  uint32_t lo = (uint32_t)p;
+  return (lo >> 31) ? mkv(V_NODE, lo & 0x7fffffffu) : mklist(LK_ARR, lo);
+}
+__device__ __forceinline__ uint32_t fmt_fidx(uint64_t f) { return (uint32_t)(vpay(f) >> 32) & 0xffffffu; }
+
+__device__ uint64_t lazy_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+  if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
+  uint32_t t = vtag(args);
+  if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
+  uint32_t idx = t == V_NODE ? ((uint32_t)vpay(args) | 0x80000000u) : list_off(args);
+  if (t == V_NODE && (uint32_t)vpay(args) >= 0x80000000u) return do_sprintf(L, fidx, args);
+  if (coll_len(L, args) != gk_args.fmt[fidx + 1]) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
+  return mkv(V_FMT, ((uint64_t)fidx << 32) | idx);
+}
+
+// the string a deferred sprintf denotes, built in the lane buffer
+__device__ uint64_t force_fmt(Lane& L, uint64_t v) {
+  if (vtag(v) != V_FMT) return v;
+  return do_sprintf(L, fmt_fidx(v), fmt_args(v));
 }
 
 // ------------------------------------------------------------------ ops
@@ -1137,6 +1320,7 @@ __device__ __forceinline__ bool op_obj_put(Lane& L, uint64_t& o, uint64_t k, uin
 
 __device__ __forceinline__ bool op_yield(Lane& L, uint64_t& out, uint64_t v, uint32_t y) {
   if (vtag(out) != V_UNDEF) {
+    if (vtag(out) == V_FMT || vtag(v) == V_FMT) { out = force_fmt(L, out); v = force_fmt(L, v); if (L.fail) return false; }
     if (!veq(L, out, v)) { lane_error(L); return false; }  // conflicting function/rule outputs
     if (L.fail) return false;
   } else {
@@ -1170,11 +1354,43 @@ __device__ __forceinline__ uint64_t op_table(Lane& L, const uint64_t* T, uint64_
 // reclaimed and their handles reused by different contents.
 __device__ __forceinline__ bool memo_stable(uint64_t v) {
   uint32_t t = vtag(v);
-  return t != V_LIST && t != V_HSTR && t != V_BFN;
+  return t != V_LIST && t != V_HSTR && t != V_BFN && t != V_FMT;
 }
 
 // m: message register, d: details register (undefined when absent)
 __device__ __forceinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+  if (vtag(m) == V_FMT) {
+    // deferred message: size it now, format it into the output at flush_wave.
+    // Only heap-free arguments are recorded (the record outlives this
+    // iteration's heap); otherwise the message is built here as before.
+    uint64_t args = fmt_args(m);
+    uint32_t fidx = fmt_fidx(m), n = coll_len(L, args);
+    bool ok = n <= FMT_MAXARGS;
+    for (uint32_t i = 0; i < n && ok; ++i) { uint64_t k, v; coll_at(L, args, i, k, v); ok = memo_stable(v); }
+    if (ok) {
+      auto arg = [&](uint32_t i) { uint64_t k, v; coll_at(L, args, i, k, v); return v; };
+      Cnt cn{0, false};
+      if (!fmt_run(L, cn, fidx, arg)) { lane_fallback(L, FB_PRINT); return false; }
+      uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
+      if (cn.n > 0x7fffu || L.en >= EMCAP || off + rec > BCAP) { lane_fallback(L, FB_MSG_LEN); return false; }
+      Out o{L.B + off + rec, 0, (uint32_t)(BCAP - off - rec), false};
+      if (!put_json(L, o, d) || o.ovf || o.n > 0x7fffu) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
+      uint64_t* w = (uint64_t*)(L.B + off);
+      w[0] = fidx | (n << 24);
+      for (uint32_t i = 0; i < n; ++i) w[1 + i] = arg(i);
+      L.bp = off + rec + o.n;
+      L.em_rule[L.en] = (uint16_t)rule;
+      L.em_off[L.en] = (uint16_t)off;
+      L.em_mlen[L.en] = (uint16_t)cn.n;
+      L.em_dlen[L.en] = (uint16_t)(o.n | 0x8000u);
+      ++L.en;
+      for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
+        if (L.keepB[dd] < L.bp) L.keepB[dd] = (uint16_t)L.bp;
+      return !L.fail;
+    }
+    m = force_fmt(L, m);
+    if (L.fail) return false;
+  }
   if (!is_strv(m)) { lane_error(L); return false; }  // types.Result.msg must unmarshal as a string
   SView ms = sview(L, m);
   char* dbuf = L.B + L.bp;

@@ -291,8 +291,8 @@ static void rebuild_modules(gk_engine* e) {
       te.supported = true;
       e->progs.push_back(p);
       gk_engine::Jit j;
-      j.name = jit_name(p, e->bank);
-      j.src = jit_source(p, e->bank, j.name);
+      j.name = jit_name(p, e->bank, e->st);
+      j.src = jit_source(p, e->bank, e->st, j.name);
       e->jits.push_back(std::move(j));
     } catch (const std::exception& ex) {
       te.supported = false;
@@ -755,6 +755,9 @@ static bool sync_tables(gk_engine* e) {
   bool ok = true;
   ok &= up(e->d_nodes, st.nodes(), false);
   ok &= up(e->d_strs, st.strings(), true);
+  // +16: the device reads string bytes a dword at a time (devrt.h ByteRd) and may
+  // touch up to 3 bytes past the last string
+  ok &= e->d_pool.reserve(st.pool().size() + 16);
   ok &= e->d_pool.upload(st.pool().data(), st.pool().size(), true);
   ok &= up(e->d_sflags, st.str_flags(), true);
   ok &= up(e->d_nums, st.numbers(), true);

@@ -1,12 +1,15 @@
 // Template JIT (see jit.h).
 #include "jit.h"
 
+#include "regex.h"
+
 #include <hip/hiprtc.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -35,15 +38,190 @@ std::string hex16(uint64_t v) {
   return b;
 }
 
+// Registers an instruction reads as values that must be plain strings (a
+// deferred sprintf is forced into the lane buffer first).  Not listed: MOV and
+// YIELD (copy the deferred value; op_yield forces before a conflict check),
+// EMIT's message (formatted into the output at flush), jumps (a V_FMT is
+// neither undefined nor a boolean) and MEMO_PUT (never caches a V_FMT).
+std::vector<uint32_t> fmt_reads(const Ins& in) {
+  std::vector<uint32_t> rs;
+  auto add = [&](uint32_t r) { if (r != 0xffff) rs.push_back(r); };
+  switch (in.op) {
+    case OP_GET: case OP_CMP: case OP_ARITH: case OP_MEMO_GET: add(in.b); add(in.c); break;
+    case OP_GETK: case OP_ITER_INIT: case OP_SPRINTF: case OP_LEN_EQ: case OP_TABLE: case OP_EMIT: add(in.b); break;
+    case OP_LIST_ADD: add(in.a); add(in.b); break;
+    case OP_OBJ_PUT: add(in.a); add(in.b); add(in.c); break;
+    case OP_CALL: for (uint32_t i = 0; i < in.c; ++i) add(in.b + i); break;
+    default: break;
+  }
+  return rs;
+}
+
+bool lazy_fmt(const Ins& in) { return in.op == OP_SPRINTF && in.x < (1u << 24); }
+
+// Which registers may hold a deferred sprintf (V_FMT) on entry to each
+// instruction: forward data flow over the template's control-flow graph.  A
+// register becomes "maybe V_FMT" where a lazy sprintf (or a copy of such a
+// value) writes it, and stops being one at any other write or where it is forced.
+struct FmtFlow {
+  uint32_t nw = 1;
+  std::vector<std::vector<uint64_t>> in;
+  std::vector<char> reached;
+  bool has(uint32_t k, uint32_t r) const { return r < 64 * nw && ((in[k][r >> 6] >> (r & 63)) & 1); }
+};
+
+FmtFlow fmt_flow(const Program& p, const CodeBank& bank) {
+  const uint32_t b0 = p.code_off, n = p.code_len;
+  FmtFlow F;
+  F.nw = (p.nregs + 64) / 64;
+  F.in.assign(n, std::vector<uint64_t>(F.nw, 0));
+  F.reached.assign(n, 0);
+  auto has = [&](const std::vector<uint64_t>& s, uint32_t r) { return r < 64 * F.nw && ((s[r >> 6] >> (r & 63)) & 1); };
+  auto put = [&](std::vector<uint64_t>& s, uint32_t r, bool v) {
+    if (r >= 64 * F.nw) return;
+    if (v) s[r >> 6] |= 1ull << (r & 63);
+    else s[r >> 6] &= ~(1ull << (r & 63));
+  };
+  std::vector<uint32_t> work;
+  auto flow = [&](uint32_t to, const std::vector<uint64_t>& s) {
+    if (to < b0 || to >= b0 + n) return;
+    uint32_t k = to - b0;
+    bool ch = !F.reached[k];
+    F.reached[k] = 1;
+    for (uint32_t w = 0; w < F.nw; ++w) {
+      uint64_t nv = F.in[k][w] | s[w];
+      if (nv != F.in[k][w]) { F.in[k][w] = nv; ch = true; }
+    }
+    if (ch) work.push_back(k);
+  };
+  if (n) { F.reached[0] = 1; work.push_back(0); }
+  while (!work.empty()) {
+    uint32_t k = work.back();
+    work.pop_back();
+    const Ins& in = bank.code[b0 + k];
+    std::vector<uint64_t> s = F.in[k];
+    for (uint32_t r : fmt_reads(in)) put(s, r, false);  // forced here
+    uint32_t next = b0 + k + 1;
+    switch (in.op) {
+      case OP_END: case OP_FAIL_FALLBACK: continue;
+      case OP_JMP: flow(in.x, s); continue;
+      case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: flow(in.x, s); flow(next, s); continue;
+      case OP_ITER_NEXT:
+        flow(in.x, s);
+        if (in.b != 0xffff) put(s, in.b, false);
+        if (in.c != 0xffff) put(s, in.c, false);
+        flow(next, s);
+        continue;
+      case OP_MEMO_GET: {
+        std::vector<uint64_t> t = s;
+        put(t, in.a, false);
+        flow(in.x, t);
+        flow(next, s);
+        continue;
+      }
+      case OP_MOV: put(s, in.a, has(s, in.b)); break;
+      case OP_YIELD: if (has(s, in.b)) put(s, in.a, true); break;
+      case OP_ITER_INIT: put(s, in.a, false); put(s, in.a + 1u, false); break;
+      case OP_EMIT: case OP_MEMO_PUT: break;
+      default: put(s, in.a, lazy_fmt(in)); break;
+    }
+    flow(next, s);
+  }
+  return F;
+}
+
+// A literal re_match pattern's DFA (regex.cc layout; the semantics of re_run /
+// run_regex_dfa) as code: a switch over states with byte ranges as compares,
+// so matching loads only the subject's bytes.  "" when too large to inline.
+std::string regex_fn(const std::string& fn, const std::vector<uint32_t>& d) {
+  uint32_t nst = d[0], start = d[1], sens = d[2];
+  const uint32_t* st = d.data() + 3;
+  auto target = [&](uint32_t k, uint32_t c) -> uint32_t {
+    uint32_t w = st[k * 129 + 1 + (c >> 1)];
+    return (c & 1) ? (w >> 16) : (w & 0xffff);
+  };
+  if (nst > 64) return "";
+  std::ostringstream o;
+  size_t ranges = 0;
+  o << "__device__ int " << fn << "(SView v) {\n  uint32_t s = " << start << "u;\n"
+    << "  for (uint32_t i = 0; i < v.n; ++i) {\n    uint32_t c = (uint8_t)v.p[i];\n";
+  if (sens) o << "    if (c >= 0x80u) return -2;\n";
+  o << "    switch (s) {\n";
+  for (uint32_t k = 0; k < nst; ++k) {
+    o << "      case " << k << "u:";
+    if (st[k * 129] & 1) { o << " return 1;\n"; continue; }
+    for (uint32_t c = 0; c < 256;) {
+      uint32_t t = target(k, c), e = c;
+      while (e + 1 < 256 && target(k, e + 1) == t) ++e;
+      if (t < nst) {
+        ++ranges;
+        if (c == e) o << " if (c == " << c << "u) { s = " << t << "u; break; }";
+        else o << " if (c >= " << c << "u && c <= " << e << "u) { s = " << t << "u; break; }";
+      }
+      c = e + 1;
+    }
+    o << " return 0;\n";
+  }
+  o << "      default: return 0;\n    }\n  }\n";
+  std::vector<uint32_t> acc;
+  for (uint32_t k = 0; k < nst; ++k) if (st[k * 129] & 3) acc.push_back(k);
+  if (acc.empty()) {
+    o << "  return 0;\n";
+  } else {
+    o << "  switch (s) {";
+    for (uint32_t k : acc) o << " case " << k << "u:";
+    o << " return 1; default: return 0; }\n";
+  }
+  o << "}\n";
+  if (ranges > 1024) return "";
+  return o.str();
+}
+
+// OP_TABLE over string keys only (mem_multiple-style suffix tables) inlined:
+// the argument's bytes are compared with each key as immediates (a non-string
+// argument equals no key).  "" when the table is not of that shape.
+std::string table_inline(const CodeBank& bank, const Store& st, uint32_t off, const std::string& dst,
+                         const std::string& arg, const std::function<std::string(uint64_t)>& lit) {
+  const uint64_t* T = bank.consts.data() + off;
+  uint32_t n = (uint32_t)T[0];
+  size_t maxlen = 0;
+  std::vector<std::string> keys;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t kv = T[1 + 2 * i];
+    if ((kv >> 60) != V_STR) return "";
+    uint64_t sid = kv & 0x0fffffffffffffffull;
+    if (sid >= st.nstrings()) return "";
+    keys.emplace_back(st.str((uint32_t)sid));
+    maxlen = std::max(maxlen, keys.back().size());
+  }
+  if (n == 0 || n > 64 || maxlen > 8) return "";
+  std::ostringstream o;
+  o << "{ uint64_t t_ = 0x0000000000000000ull; if (is_strv(" << arg << ")) { SView s_ = sview(L, " << arg << ");";
+  for (size_t j = 0; j < maxlen; ++j) o << " uint32_t c" << j << "_ = s_.n > " << j << "u ? (uint8_t)s_.p[" << j << "] : 0u;";
+  for (uint32_t i = 0; i < n; ++i) {
+    o << (i ? " else if (" : " if (") << "s_.n == " << keys[i].size() << "u";
+    for (size_t j = 0; j < keys[i].size(); ++j) o << " && c" << j << "_ == " << (unsigned)(uint8_t)keys[i][j] << "u";
+    o << ") t_ = " << lit(T[2 + 2 * i]) << ";";
+  }
+  o << " } " << dst << " = t_; }";
+  return o.str();
+}
+
+struct Gen {
+  std::string pre;   // helper functions (literal regex DFAs)
+  std::string body;  // body of the predicate function
+};
+
 // Body of the predicate function: one statement per bytecode instruction.
 // Unlike the VM, the generated code does not test L.fail after every helper
 // call (a scratch load per call): the first failure recorded in the lane wins
 // either way, helpers return well-formed values (undefined) once it is set,
 // and a failed lane's staged tuples are discarded by flush_wave — so running
 // on to the end yields the same lane outcome at no cost to passing lanes.
-std::string body(const Program& p, const CodeBank& bank) {
+Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   const uint32_t b0 = p.code_off, b1 = p.code_off + p.code_len;
-  std::set<uint32_t> labels, memo;
+  std::set<uint32_t> labels, memo, memo2;
+  std::map<uint32_t, int> memo_sites;
   for (uint32_t pc = b0; pc < b1; ++pc) {
     const Ins& in = bank.code[pc];
     switch (in.op) {
@@ -53,6 +231,26 @@ std::string body(const Program& p, const CodeBank& bank) {
       default: break;
     }
     if (in.op == OP_MEMO_GET || in.op == OP_MEMO_PUT) memo.insert(in.y);
+    if (in.op == OP_MEMO_GET && ++memo_sites[in.y] == 2) memo2.insert(in.y);
+  }
+  FmtFlow F = fmt_flow(p, bank);
+  Gen g;
+  // literal re_match patterns compiled to code
+  std::vector<std::pair<uint64_t, std::string>> relits;  // (pattern value, function)
+  {
+    std::ostringstream pre;
+    std::set<uint32_t> seen;
+    for (uint32_t sid : p.regex_literals) {
+      if (!seen.insert(sid).second) continue;
+      std::vector<uint32_t> d;
+      if (compile_regex_dfa(std::string(st.str(sid)), d) != RX_OK) continue;
+      std::string fn = "re_lit_" + std::to_string(relits.size());
+      std::string code = regex_fn(fn, d);
+      if (code.empty()) continue;
+      pre << code;
+      relits.push_back({((uint64_t)V_STR << 60) | sid, fn});
+    }
+    g.pre = pre.str();
   }
   std::ostringstream o;
   auto R = [](uint32_t r) { return "r" + std::to_string(r); };
@@ -64,16 +262,26 @@ std::string body(const Program& p, const CodeBank& bank) {
   if (!p.nregs) o << "unused_";
   o << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)
-  for (uint32_t m : memo)
+  for (uint32_t m : memo) {
     o << "  uint64_t mk0_" << m << ", mk1_" << m << ", mv_" << m << "; bool mok_" << m << " = false;\n";
+    if (memo2.count(m))
+      o << "  uint64_t mkb0_" << m << ", mkb1_" << m << ", mvb_" << m << "; bool mokb_" << m << " = false;\n";
+  }
   const char* UND = "0x0000000000000000ull";
-  char kb[40];
-  auto lit = [&](uint64_t v) { snprintf(kb, sizeof kb, "0x%016llxull", (unsigned long long)v); return std::string(kb); };
+  std::function<std::string(uint64_t)> lit = [](uint64_t v) {
+    char kb[40];
+    snprintf(kb, sizeof kb, "0x%016llxull", (unsigned long long)v);
+    return std::string(kb);
+  };
   for (uint32_t pc = b0; pc < b1; ++pc) {
     const Ins& in = bank.code[pc];
+    const uint32_t k = pc - b0;
     if (labels.count(pc)) o << "L" << pc << ":;\n";
     std::string a = R(in.a), b = R(in.b), c = R(in.c), x = "L" + std::to_string(in.x);
     std::string y = std::to_string(in.y) + "u";
+    if (F.reached[k])
+      for (uint32_t r : fmt_reads(in))
+        if (F.has(k, r)) o << "  if (vtag(" << R(r) << ") == V_FMT) " << R(r) << " = force_fmt(L, " << R(r) << ");\n";
     o << "  ";
     switch (in.op) {
       case OP_END: o << "return;"; break;
@@ -102,39 +310,81 @@ std::string body(const Program& p, const CodeBank& bank) {
       case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) return;"; break;
       case OP_YIELD: o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) return;"; break;
       case OP_CALL: {
-        uint32_t n = in.c ? in.c : 1;
-        o << "{ uint64_t av_[" << n << "] = {";
-        for (uint32_t i = 0; i < in.c; ++i) o << (i ? ", " : "") << R(in.b + i);
-        if (!in.c) o << "0";
-        o << "}; " << a << " = call_builtin(L, " << y << ", av_); }";
+        // builtins are called directly with register operands (no argument
+        // array, no dispatch on the builtin id)
+        std::string A0 = R(in.b), A1 = R(in.b + 1), A2 = R(in.b + 2);
+        switch (in.y) {
+          case BI_COUNT: o << a << " = bi_count(L, " << A0 << ");"; break;
+          case BI_ANY: case BI_ALL: o << a << " = bi_anyall(L, " << in.y << "u, " << A0 << ");"; break;
+          case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS:
+            o << a << " = bi_strpred(L, " << in.y << "u, " << A0 << ", " << A1 << ");";
+            break;
+          case BI_RE_MATCH:
+            o << "{ uint64_t p_ = " << A0 << ", s_ = " << A1 << "; if (!is_strv(p_) || !is_strv(s_)) { lane_error(L); "
+              << a << " = " << UND << "; }";
+            for (auto& rl : relits)
+              o << " else if (p_ == " << lit(rl.first) << ") " << a << " = re_result(L, " << rl.second << "(sview(L, s_)));";
+            o << " else " << a << " = re_result(L, re_run(L, p_, s_)); }";
+            break;
+          case BI_TO_NUMBER: o << a << " = bi_to_number(L, " << A0 << ");"; break;
+          case BI_REPLACE: o << a << " = bi_replace(L, " << A0 << ", " << A1 << ", " << A2 << ");"; break;
+          case BI_SUBSTRING: o << a << " = bi_substring(L, " << A0 << ", " << A1 << ", " << A2 << ");"; break;
+          case BI_IS_NUMBER: o << a << " = mkv(V_BOOL, is_numv(" << A0 << "));"; break;
+          case BI_IS_STRING: o << a << " = mkv(V_BOOL, is_strv(" << A0 << "));"; break;
+          default: {
+            uint32_t n = in.c ? in.c : 1;
+            o << "{ uint64_t av_[" << n << "] = {";
+            for (uint32_t i = 0; i < in.c; ++i) o << (i ? ", " : "") << R(in.b + i);
+            if (!in.c) o << "0";
+            o << "}; " << a << " = call_builtin(L, " << y << ", av_); }";
+            break;
+          }
+        }
         break;
       }
-      case OP_SPRINTF: o << a << " = do_sprintf(L, " << in.x << "u, " << b << ");"; break;
+      case OP_SPRINTF:
+        o << a << " = " << (lazy_fmt(in) ? "lazy_sprintf" : "do_sprintf") << "(L, " << in.x << "u, " << b << ");";
+        break;
       case OP_LEN_EQ: o << a << " = op_len_eq(L, " << b << ", " << y << ");"; break;
       case OP_EMIT:
         o << "if (!op_emit(L, " << a << ", " << (in.b == 0xffff ? std::string(UND) : b) << ", " << in.c << "u, " << y
           << ")) return;";
         break;
       case OP_MEMO_GET: {
+        // two entries per slot (most recent first): call sites of one function
+        // with alternating arguments (canonify_mem(x) vs canonify_mem(max)) hit
         std::string m = std::to_string(in.y), k1 = in.c == 0xffff ? std::string("0ull") : c;
         o << "if (mok_" << m << " && mk0_" << m << " == " << b << " && mk1_" << m << " == " << k1 << ") { " << a
           << " = mv_" << m << "; goto " << x << "; }";
+        if (memo2.count(in.y))
+          o << " if (mokb_" << m << " && mkb0_" << m << " == " << b << " && mkb1_" << m << " == " << k1 << ") { " << a
+            << " = mvb_" << m << "; goto " << x << "; }";
         break;
       }
       case OP_MEMO_PUT: {
         std::string m = std::to_string(in.y), k1 = in.c == 0xffff ? std::string("0ull") : c;
-        o << "if (memo_stable(" << b << ") && memo_stable(" << k1 << ") && memo_stable(" << a << ")) { mk0_" << m
-          << " = " << b << "; mk1_" << m << " = " << k1 << "; mv_" << m << " = " << a << "; mok_" << m << " = true; }";
+        o << "if (memo_stable(" << b << ") && memo_stable(" << k1 << ") && memo_stable(" << a << ")) { ";
+        if (memo2.count(in.y))
+          o << "mkb0_" << m << " = mk0_" << m << "; mkb1_" << m << " = mk1_" << m << "; mvb_" << m << " = mv_" << m
+            << "; mokb_" << m << " = mok_" << m << "; ";
+        o << "mk0_" << m << " = " << b << "; mk1_" << m << " = " << k1 << "; mv_" << m << " = " << a << "; mok_" << m
+          << " = true; }";
         break;
       }
-      case OP_TABLE: o << a << " = op_table(L, gk_args.K + " << in.x << "u, " << b << ");"; break;
+      case OP_TABLE: {
+        std::string t = table_inline(bank, st, in.x, a, b, lit);
+        if (t.empty()) o << a << " = op_table(L, gk_args.K + " << in.x << "u, " << b << ");";
+        else o << t;
+        break;
+      }
       case OP_FAIL_FALLBACK: o << "lane_fallback(L, " << y << "); return;"; break;
       default: o << "lane_fallback(L, FB_UNSUPPORTED); return;"; break;
     }
     o << "\n";
   }
   o << "  lane_fallback(L, FB_UNSUPPORTED);\n";
-  return o.str();
+  g.body = o.str();
+  return g;
 }
 
 std::mutex g_mu;
@@ -185,17 +435,20 @@ static std::string wpe_suffix() {
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 
-std::string jit_name(const Program& p, const CodeBank& bank) {
-  return "gk_t_" + hex16(fnv1a(body(p, bank) + wpe_suffix()));
+std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
+  Gen g = generate(p, bank, st);
+  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix()));
 }
 
-std::string jit_source(const Program& p, const CodeBank& bank, const std::string& name) {
+std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
+  Gen g = generate(p, bank, st);
   std::ostringstream o;
   o << "// generated by jit.cc from template bytecode (" << p.code_len << " instructions)\n"
     << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
+    << g.pre
     << "__device__ void " << name << "_pred(Lane& L, uint64_t review, uint64_t params) {\n"
-    << body(p, bank) << "}\n"
+    << g.body << "}\n"
     << "}  // namespace gk\n"
     << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix() << ") " << name << "() {\n"
     << "  gk::audit_body([&](gk::Lane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"

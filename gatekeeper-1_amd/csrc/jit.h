@@ -11,11 +11,12 @@
 #include <string>
 
 #include "compiler.h"
+#include "store.h"
 
 namespace gk {
 
 // HIP source of one template kernel named `name` (extern "C" __global__).
-std::string jit_source(const Program& p, const CodeBank& bank, const std::string& name);
+std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name);
 
 // Compiles `src` for gfx950 (hipRTC).  Thread-safe; results are cached per
 // process by source text and, when GKGPU_JIT_CACHE names a directory (default
@@ -24,6 +25,6 @@ std::string jit_source(const Program& p, const CodeBank& bank, const std::string
 bool jit_compile(const std::string& src, std::string& code, std::string& log);
 
 // Kernel name for a source body: "gk_t_<16 hex digits of a content hash>".
-std::string jit_name(const Program& p, const CodeBank& bank);
+std::string jit_name(const Program& p, const CodeBank& bank, const Store& st);
 
 }  // namespace gk
