@@ -102,6 +102,14 @@ class Comp {
   std::map<uint64_t, uint32_t> kidx_;
   int reg_top_ = 0, max_reg_ = 0;
   const Term* stmt_key_ = nullptr;  // last selector of the statement-level ref being compiled
+  // Complete rules are evaluated once per lane: a lane's input (one review x one
+  // constraint's parameters) is fixed and `with` is outside the subset, so the
+  // value cannot change.  Each cached rule owns a (value, evaluated) register
+  // pair numbered from kVReg while compiling; finish() renumbers them above the
+  // scratch registers and clears the flags at program entry.
+  static constexpr int kVReg = 10000;
+  static constexpr size_t kMaxCachedRules = 16;
+  std::map<const Rule*, std::pair<int, int>> crule_;
   int inline_depth_ = 0;
   std::map<std::pair<const void*, bool>, int> memo_;  // memo slot per (function, statement form)
   std::vector<int> loop_base_;  // register base of each enclosing ITER loop (innermost last)
@@ -156,6 +164,17 @@ class Comp {
   }
 
   Program finish() {
+    if (!crule_.empty()) {
+      const int base = max_reg_;
+      auto remap = [&](uint16_t& r) { if (r != NOREG && r >= kVReg) r = (uint16_t)(base + (r - kVReg)); };
+      for (auto& in : code_) { remap(in.a); remap(in.b); remap(in.c); }
+      std::vector<Ins> pro;
+      uint32_t kf = kconst(tag_val(V_BOOL, 0));
+      for (auto& cr : crule_) pro.push_back(Ins{OP_LOADK, (uint16_t)(base + (cr.second.second - kVReg)), 0, 0, kf, 0});
+      code_.insert(code_.begin(), pro.begin(), pro.end());
+      for (auto& l : labels_) if (l >= 0) l += (int)pro.size();
+      max_reg_ = base + 2 * (int)crule_.size();
+    }
     prog_.code_off = (uint32_t)bank_.code.size();
     prog_.code_len = (uint32_t)code_.size();
     for (auto& in : code_) {
@@ -685,6 +704,60 @@ class Comp {
   }
 
   void complete_value(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    auto it = crule_.find(rules[0].get());
+    if (it == crule_.end() && crule_.size() < kMaxCachedRules) {
+      int n = (int)crule_.size();
+      it = crule_.emplace(rules[0].get(), std::make_pair(kVReg + 2 * n, kVReg + 2 * n + 1)).first;
+    }
+    if (it == crule_.end()) { complete_eval(rules, fail, k); return; }
+    int val = it->second.first, done = it->second.second;
+    int Lhave = label();
+    emit_jmp(OP_JTRUE, done, Lhave);
+    {
+      int save = reg_top_;
+      // the value outlives every enclosing loop's iteration heap: pin them all
+      uint32_t rng = depth() ? (1u | ((uint32_t)depth() << 8)) : 0u;
+      int u = loadk(tag_val(V_UNDEF, 0));
+      emit(OP_MOV, (uint16_t)val, (uint16_t)u);
+      complete_into(rules, val, rng);
+      int t = loadk(tag_val(V_BOOL, 1));
+      emit(OP_MOV, (uint16_t)done, (uint16_t)t);
+      reg_top_ = save;
+    }
+    place(Lhave);
+    emit_jmp(OP_JUNDEF, val, fail);
+    k(val, fail);
+  }
+
+  // all bodies of a complete rule yield into `out` (conflicting values are an
+  // error; a constant default applies when none is defined)
+  void complete_into(const std::vector<std::shared_ptr<Rule>>& rules, int out, uint32_t rng) {
+    TermP def;
+    for (auto& r : rules) {
+      if (r->is_else) throw Unsupported("else");
+      if (r->is_default) { def = r->value; continue; }
+      int Lr = label();
+      Env renv;
+      renv.mod = r->mod;
+      body_k(cbody(r, {}), 0, &renv, Lr, [&](int f) {
+        term(r->value, &renv, f, [&](int v, int f2) { emit(OP_YIELD, (uint16_t)out, (uint16_t)v, 0, 0, rng); emit_jmp(OP_JMP, 0, f2); });
+      });
+      place(Lr);
+    }
+    if (def) {
+      if (!is_const(def)) throw Unsupported("non-constant default");
+      int Lh = label();
+      int dv = loadk(const_value(def));
+      int Lskip = label();
+      emit_jmp(OP_JUNDEF, out, Lh);
+      emit_jmp(OP_JMP, 0, Lskip);
+      place(Lh);
+      emit(OP_MOV, (uint16_t)out, (uint16_t)dv);
+      place(Lskip);
+    }
+  }
+
+  void complete_eval(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
     int save = reg_top_;
     int out = loadk(tag_val(V_UNDEF, 0));
     TermP def;

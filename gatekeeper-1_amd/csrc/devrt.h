@@ -1439,6 +1439,7 @@ __device__ __forceinline__ void audit_body(Run run) {
       }
     }
     if (L.fail) {
+      atomicAdd(&gk_args.counters[2], 1u);
       atomicOr(&gk_args.rflags[r], L.fail);
       if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
     }

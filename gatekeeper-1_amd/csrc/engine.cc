@@ -91,7 +91,8 @@ struct ResultRow {
 
 struct gk_results {
   std::vector<gk::ResultRow> rows;
-  std::vector<uint32_t> status, reason;
+  std::vector<uint32_t> status, reason;  // empty when no review was flagged (all zero)
+  uint32_t nrev = 0;
   std::vector<uint64_t> totals;
   std::vector<std::string> ckind, cname, cea;
   double ms[5] = {0, 0, 0, 0, 0};
@@ -108,6 +109,7 @@ struct gk_batch {
   uint32_t node_begin = 0, node_end = 0;
   std::vector<gk::ReviewCol> cols;
   gk::DBuf d_revs;
+  gk::DBuf d_nodes;  // the batch's own device node array: permanent region + its documents
   uint64_t dev_bytes = 0;
 };
 
@@ -155,7 +157,16 @@ struct gk_engine {
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
       d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
+  std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
+  uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
 };
+
+// Drops the transient node region (review documents of the last call).  The
+// device mirror stays valid below the cut, so the next upload is incremental.
+static void reset_transient(gk_engine* e) {
+  e->st.nodes().resize(e->perm_nodes);
+  e->dev_nodes_ok = std::min<uint32_t>(e->dev_nodes_ok, e->perm_nodes);
+}
 
 namespace gk {
 
@@ -252,7 +263,7 @@ static void rebuild_modules(gk_engine* e) {
   e->jits.clear();
   e->templates.clear();
   // drop the transient region before appending new permanent constant nodes
-  e->st.nodes().resize(e->perm_nodes);
+  reset_transient(e);
   std::vector<std::shared_ptr<rego::Module>> parsed;
   for (auto& kv : e->modules) {
     auto m = rego::parse_module(kv.second);
@@ -750,10 +761,19 @@ static bool up(DBuf& b, const std::vector<T>& v, bool append_only) {
   return b.upload(v.data(), v.size() * sizeof(T), append_only);
 }
 
-static bool sync_tables(gk_engine* e) {
+static bool sync_tables(gk_engine* e, bool nodes = true) {
   Store& st = e->st;
   bool ok = true;
-  ok &= up(e->d_nodes, st.nodes(), false);
+  if (nodes) {
+    // only the nodes appended (or rewritten after a transient reset) since the
+    // last upload travel: a staged 1M-review batch is not re-sent per call
+    size_t n = st.nodes().size();
+    ok &= e->d_nodes.reserve(std::max<size_t>(n, 1) * sizeof(Node));
+    if (ok && n > e->dev_nodes_ok)
+      ok &= hipMemcpy((char*)e->d_nodes.p + (size_t)e->dev_nodes_ok * sizeof(Node), st.nodes().data() + e->dev_nodes_ok,
+                      (n - e->dev_nodes_ok) * sizeof(Node), hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) { e->dev_nodes_ok = (uint32_t)n; e->d_nodes.used = n * sizeof(Node); }
+  }
   ok &= up(e->d_strs, st.strings(), true);
   // +16: the device reads string bytes a dword at a time (devrt.h ByteRd) and may
   // touch up to 3 bytes past the last string
@@ -816,22 +836,23 @@ static void ensure_jit(gk_engine* e, bool load) {
 
 // runs the kernel over `cols` (already resident in d_revs when `resident`)
 static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, DBuf* revbuf, bool decode,
-                              gk_results* res) {
+                              gk_results* res, const void* nodes = nullptr) {
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
-  res->status.assign(nrev, 0);
-  res->reason.assign(nrev, 0);
+  res->nrev = nrev;
   res->totals.assign(ncons, 0);
   for (auto* c : e->corder) { res->ckind.push_back(c->kind); res->cname.push_back(c->name); res->cea.push_back(c->ea); }
   if (nrev == 0) return GK_OK;
   // reviews flagged for fallback on the host never reach the device when there are no constraints
   if (ncons == 0) {
+    res->status.assign(nrev, 0);
+    res->reason.assign(nrev, 0);
     for (uint32_t r = 0; r < nrev; ++r) if (cols[r].flags & RC_FALLBACK) res->status[r] = GK_REVIEW_FALLBACK;
     return GK_OK;
   }
   if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
   auto t0 = Clock::now();
-  if (!sync_tables(e)) return fail(e, GK_EDEVICE, "device upload failed");
+  if (!sync_tables(e, nodes == nullptr)) return fail(e, GK_EDEVICE, "device upload failed");
   if (revbuf == &e->d_revs || !revbuf->p || revbuf->used != cols.size() * sizeof(ReviewCol)) {
     if (!up(*revbuf, cols, false)) return fail(e, GK_EDEVICE, "device upload failed");
   }
@@ -876,7 +897,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     bool hist = e->profile >= 2 && e->d_pchist.reserve(ncode * 4);
     if (hist) hipMemsetAsync(e->d_pchist.p, 0, ncode * 4, e->stream);
     a.pchist = hist ? (unsigned int*)e->d_pchist.p : nullptr;
-    a.nodes = (const Node*)e->d_nodes.p;
+    a.nodes = (const Node*)(nodes ? nodes : e->d_nodes.p);
     a.strs = (const StrEnt*)e->d_strs.p;
     a.pool = (const uint8_t*)e->d_pool.p;
     a.sflags = (const uint8_t*)e->d_sflags.p;
@@ -904,8 +925,12 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     a.rflags = (uint32_t*)e->d_rflags.p;
     a.totals = (uint32_t*)e->d_totals.p;
     a.rreason = (uint32_t*)e->d_rreason.p;
-    std::vector<hipEvent_t> ev(plan.size() + 1);
-    for (auto& x : ev) hipEventCreate(&x);
+    while (e->events.size() < plan.size() + 1) {
+      hipEvent_t x;
+      if (hipEventCreate(&x) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
+      e->events.push_back(x);
+    }
+    const std::vector<hipEvent_t>& ev = e->events;
     hipEventRecord(ev[0], e->stream);
     std::vector<DevArgs> argv(plan.size(), a);  // live until the stream sync below
     for (size_t i = 0; i < plan.size(); ++i) {
@@ -926,14 +951,10 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       // cumulative (tuples, bytes) after this launch -> per-launch output counts
       hipMemcpyAsync((char*)e->d_counters.p + 64 + 8 * i, e->d_counters.p, 8, hipMemcpyDeviceToDevice, e->stream);
       if (lr != 0) {
-        for (auto& x : ev) hipEventDestroy(x);
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
     }
-    if (hipStreamSynchronize(e->stream) != hipSuccess) {
-      for (auto& x : ev) hipEventDestroy(x);
-      return fail(e, GK_EDEVICE, "kernel execution failed");
-    }
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
     res->launches.clear();
     std::vector<uint32_t> snap(2 * plan.size());
     hipMemcpy(snap.data(), (char*)e->d_counters.p + 64, 8 * plan.size(), hipMemcpyDeviceToHost);
@@ -944,10 +965,10 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       uint32_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
       res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
-    for (auto& x : ev) hipEventDestroy(x);
     auto t1 = Clock::now();
-    uint32_t counters[2];
-    hipMemcpy(counters, e->d_counters.p, 8, hipMemcpyDeviceToHost);
+    // [0] tuples, [1] message bytes, [2] lanes that flagged their review (error/fallback)
+    uint32_t counters[3];
+    hipMemcpy(counters, e->d_counters.p, 12, hipMemcpyDeviceToHost);
     if (counters[0] > e->out_cap || counters[1] > e->bytes_cap) {
       e->out_cap = std::max<size_t>(e->out_cap * 2, counters[0] + 1024);
       e->bytes_cap = std::max<size_t>(e->bytes_cap * 2, (size_t)counters[1] + 65536);
@@ -960,6 +981,16 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     std::vector<uint32_t> tot(ncons);
     hipMemcpy(tot.data(), e->d_totals.p, ncons * 4, hipMemcpyDeviceToHost);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
+    bool ea_err = false;
+    for (auto* c : e->corder) ea_err |= c->ea_error;
+    if (!decode && !ea_err && counters[2] == 0 && !hist && !prof) {
+      // nothing flagged: per-review status stays implicit (all zero), so the
+      // audit step downloads a few counters instead of 8 bytes per review
+      res->ms[3] = ms_since(t1);
+      return GK_OK;
+    }
+    res->status.assign(nrev, 0);
+    res->reason.assign(nrev, 0);
     hipMemcpy(res->status.data(), e->d_rflags.p, nrev * 4, hipMemcpyDeviceToHost);
     hipMemcpy(res->reason.data(), e->d_rreason.p, nrev * 4, hipMemcpyDeviceToHost);
     if (hist) {
@@ -972,8 +1003,6 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     bool flagged = false;
     for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
-    bool ea_err = false;
-    for (auto* c : e->corder) ea_err |= c->ea_error;
     if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); return GK_OK; }
     std::vector<Viol> vs(counters[0]);
     std::string bytes;
@@ -1067,6 +1096,7 @@ void gk_engine_destroy(gk_engine* e) {
                   &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist})
     b->free_();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
+  for (hipEvent_t x : e->events) hipEventDestroy(x);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1153,7 +1183,7 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
   e->gen++;
   if (p.size() == 6 && p[0] == "constraints" && p[1] == TARGET && p[2] == "cluster" && p[3] == CGROUP) {
     rebuild_modules(e);
-    e->st.nodes().resize(e->perm_nodes);
+    reset_transient(e);
     ConstraintEnt c;
     c.kind = p[4];
     c.name = p[5];
@@ -1168,7 +1198,7 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
     e->inventory[key] = std::string(json, len);
     if (p.size() == 6 && p[2] == "cluster" && p[3] == "v1" && p[4] == "Namespace") {
       rebuild_modules(e);
-      e->st.nodes().resize(e->perm_nodes);
+      reset_transient(e);
       e->ns_cache[p[5]] = e->st.add_doc(d, root);
       e->perm_nodes = (uint32_t)e->st.nodes().size();
     }
@@ -1222,7 +1252,7 @@ static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, si
     return fail(e, GK_EPARSE, ex.what());
   }
   auto t0 = Clock::now();
-  e->st.nodes().resize(e->perm_nodes);
+  reset_transient(e);
   std::vector<ReviewCol> cols;
   cols.reserve(inputs.size());
   JDoc d;
@@ -1343,7 +1373,7 @@ int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_l
     return fail(e, GK_EPARSE, ex.what());
   }
   auto t0 = Clock::now();
-  e->st.nodes().resize(e->perm_nodes);
+  reset_transient(e);
   std::vector<ReviewCol> cols;
   cols.reserve(n);
   int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, cols);
@@ -1366,7 +1396,7 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
     return fail(e, GK_EPARSE, ex.what());
   }
   auto* b = new gk_batch();
-  e->st.nodes().resize(e->perm_nodes);
+  reset_transient(e);
   b->node_begin = (uint32_t)e->st.nodes().size();
   int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols);
   if (rc != GK_OK) { delete b; return rc; }
@@ -1374,7 +1404,13 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
   b->nrev = (uint32_t)n;
   b->gen = e->gen;
   if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
-  if (!sync_tables(e) || !up(b->d_revs, b->cols, false)) { delete b; return fail(e, GK_EDEVICE, "upload failed"); }
+  if (!sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
+      !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
+    b->d_revs.free_();
+    b->d_nodes.free_();
+    delete b;
+    return fail(e, GK_EDEVICE, "upload failed");
+  }
   b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
   {
     // one pass over every staged document node and each distinct string value it references
@@ -1394,7 +1430,7 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   std::lock_guard<std::mutex> g(e->mu);
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
   auto* res = new gk_results();
-  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res);
+  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, b->d_nodes.p);
   if (rc != GK_OK) { delete res; return rc; }
   *out = res;
   return GK_OK;
@@ -1403,6 +1439,7 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
 void gk_batch_free(gk_batch* b) {
   if (!b) return;
   b->d_revs.free_();
+  b->d_nodes.free_();
   delete b;
 }
 
@@ -1420,7 +1457,7 @@ int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64
 int gk_results_flag_counts(const gk_results* r, uint64_t* errors, uint64_t* fallbacks) {
   if (!r) return GK_EINVAL;
   uint64_t ne = 0, nf = 0;
-  for (uint32_t s : r->status) { ne += (s & GK_REVIEW_ERROR) != 0; nf += (s & GK_REVIEW_FALLBACK) != 0; }
+  for (uint32_t s : r->status) { ne += (s & GK_REVIEW_ERROR) != 0; nf += (s & GK_REVIEW_FALLBACK) != 0; }  // empty: none
   if (errors) *errors = ne;
   if (fallbacks) *fallbacks = nf;
   return GK_OK;
@@ -1428,8 +1465,14 @@ int gk_results_flag_counts(const gk_results* r, uint64_t* errors, uint64_t* fall
 
 int gk_results_copy_status(const gk_results* r, uint32_t* status, uint32_t* reason) {
   if (!r) return GK_EINVAL;
-  if (status && !r->status.empty()) memcpy(status, r->status.data(), r->status.size() * 4);
-  if (reason && !r->reason.empty()) memcpy(reason, r->reason.data(), r->reason.size() * 4);
+  if (status) {
+    if (r->status.empty()) memset(status, 0, (size_t)r->nrev * 4);
+    else memcpy(status, r->status.data(), r->status.size() * 4);
+  }
+  if (reason) {
+    if (r->reason.empty()) memset(reason, 0, (size_t)r->nrev * 4);
+    else memcpy(reason, r->reason.data(), r->reason.size() * 4);
+  }
   return GK_OK;
 }
 
@@ -1523,7 +1566,7 @@ int gk_results_get(const gk_results* r, size_t i, gk_result_view* out) {
   return GK_OK;
 }
 
-size_t gk_results_reviews(const gk_results* r) { return r ? r->status.size() : 0; }
+size_t gk_results_reviews(const gk_results* r) { return r ? std::max<size_t>(r->nrev, r->status.size()) : 0; }
 uint32_t gk_results_review_status(const gk_results* r, size_t i) { return r && i < r->status.size() ? r->status[i] : 0; }
 uint32_t gk_results_review_reason(const gk_results* r, size_t i) { return r && i < r->reason.size() ? r->reason[i] : 0; }
 size_t gk_results_constraints(const gk_results* r) { return r ? r->totals.size() : 0; }

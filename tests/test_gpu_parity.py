@@ -236,3 +236,28 @@ def test_staged_batch_matches_direct_and_counts():
     assert sorted((x.review, x.msg) for x in r1.results) == sorted((x.review, x.msg) for x in direct.results)
     assert r2.totals == r1.totals
     assert sum(r1.totals) == len(r1.results)
+
+
+def test_staged_batches_are_independent():
+    """A staged batch keeps its own device documents: staging another batch or
+    serving a Query in between does not change its results."""
+    ts, cs = W.config2()
+    pods_a, ns_a, nso_a = W.gen_pods(300, seed=11, n_namespaces=20)
+    pods_b, ns_b, nso_b = W.gen_pods(200, seed=12, n_namespaces=20)
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    nss_a = [nso_a[n] for n in ns_a]
+    nss_b = [nso_b[n] for n in ns_b]
+    want_a = sorted((x.review, x.constraint, x.msg) for x in drv.review_objects(pods_a, nss_a).results)
+    want_b = sorted((x.review, x.constraint, x.msg) for x in drv.review_objects(pods_b, nss_b).results)
+    ba = drv.stage_objects(pods_a, nss_a)
+    bb = drv.stage_objects(pods_b, nss_b)
+    drv.review_objects(pods_b[:7], nss_b[:7])
+    got_a = sorted((x.review, x.constraint, x.msg) for x in ba.eval(decode=True).results)
+    got_b = sorted((x.review, x.constraint, x.msg) for x in bb.eval(decode=True).results)
+    assert got_a == want_a
+    assert got_b == want_b
