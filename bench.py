@@ -80,12 +80,27 @@ def main():
             import torch
             torch.cuda.synchronize()
 
+    gather = None
+    if dist is not None:
+        import torch
+        from gkgpu.parallel import DeviceOutput, Gatherer
+        dev_out = DeviceOutput(torch.device("cuda", local))
+        gatherer = Gatherer(dst=0)
+    gather_ms = []
+
     def step():
-        res = batch.eval(decode=False, light=True)
-        if dist is not None:
-            import torch
-            tot = torch.tensor(res.totals, dtype=torch.int64, device="cuda")
-            dist.all_reduce(tot)
+        if dist is None:
+            return batch.eval(decode=False, light=True)
+        # sweep the rank's shard, then the exchange the audit needs: totals
+        # all-reduce + every rank's compacted violations (tuples + message
+        # bytes) gathered to rank 0 over RCCL
+        res = batch.eval(decode=False, light=True, device_out=dev_out)
+        t0 = time.perf_counter()
+        tot = torch.tensor(res.totals, dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot)
+        gatherer.gather(dev_out.tuples(), dev_out.bytes(), review_base=rank * args.pods)
+        torch.cuda.synchronize()
+        gather_ms.append((time.perf_counter() - t0) * 1000.0)
         return res
 
     for _ in range(args.warmup):
@@ -163,7 +178,10 @@ def main():
                 "violations_per_step_rank0": last.device_tuples,
                 "fallback_reviews": fallback,
                 "error_reviews": errors,
-                "parallelism": "dp%d (resource shards, totals all-reduce over RCCL)" % world,
+                "parallelism": "dp%d (resource shards; totals all-reduce + violation gather to rank 0 over RCCL)" % world,
+                "gather_ms_avg_rank0": (sum(gather_ms[-args.steps:]) / args.steps) if gather_ms else 0.0,
+                "kernel_ms_per_step": sum(k["avg_ms"] for k in kernels),
+                "kernel_only_evals_per_s": evals_per_step / (sum(k["avg_ms"] for k in kernels) / 1000.0),
                 "backends": {k: ("template-kernel" if drv.template_backend(k)[0] == 2 else "bytecode-vm")
                              for k in kinds},
                 "kernel_templates": kinds_of,

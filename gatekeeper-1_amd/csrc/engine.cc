@@ -97,6 +97,9 @@ struct gk_results {
   std::vector<std::string> ckind, cname, cea;
   double ms[5] = {0, 0, 0, 0, 0};
   uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
+  const void* d_tuples = nullptr;          // engine-owned device output of this call (valid
+  const void* d_bytes = nullptr;           // until the engine's next evaluation)
+  uint64_t epoch = 0;
   std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
   struct Launch { std::string kernel; double ms; uint32_t nconstraints; uint64_t tuples, bytes; };
   std::vector<Launch> launches;            // kernels of the last attempt, in launch order
@@ -159,6 +162,7 @@ struct gk_engine {
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
   std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
   uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
+  uint64_t eval_epoch = 0;         // bumps on every evaluation (device output buffers reused)
 };
 
 // Drops the transient node region (review documents of the last call).  The
@@ -978,6 +982,9 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     res->dev_tuples = counters[0];
     res->dev_bytes = counters[1];
+    res->d_tuples = e->d_out.p;
+    res->d_bytes = e->d_bytes.p;
+    res->epoch = ++e->eval_epoch;
     std::vector<uint32_t> tot(ncons);
     hipMemcpy(tot.data(), e->d_totals.p, ncons * 4, hipMemcpyDeviceToHost);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
@@ -1513,6 +1520,19 @@ int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char
   }
   if (backend) *backend = b;
   if (detail) *detail = d;
+  return GK_OK;
+}
+
+int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst) {
+  if (!e || !r) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (r->epoch == 0 || r->epoch != e->eval_epoch)
+    return fail(e, GK_EINVAL, "device output was overwritten by a later evaluation on this engine");
+  if (tuples_dst && r->dev_tuples &&
+      hipMemcpy(tuples_dst, r->d_tuples, r->dev_tuples * sizeof(Viol), hipMemcpyDeviceToDevice) != hipSuccess)
+    return fail(e, GK_EDEVICE, "device copy failed");
+  if (bytes_dst && r->dev_bytes && hipMemcpy(bytes_dst, r->d_bytes, r->dev_bytes, hipMemcpyDeviceToDevice) != hipSuccess)
+    return fail(e, GK_EDEVICE, "device copy failed");
   return GK_OK;
 }
 

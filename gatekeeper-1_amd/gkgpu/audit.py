@@ -1,0 +1,106 @@
+"""Audit results writer: the consumer of the violation set.
+
+Restates pkg/audit/manager.go for the results of one sweep:
+  * addAuditResponsesToUpdateLists (:462-508) -- per-constraint totals, the
+    first `limit` results per constraint in evaluation order, per-action totals
+    keyed by the raw enforcementAction string (deny/dryrun/unrecognized
+    pre-zeroed, :190-193);
+  * updateConstraintStatus (:555-631) -- status.violations[] entries
+    {kind, name, namespace (omitempty), message, enforcementAction}, messages
+    over msgSize (256) bytes cut by truncateString (:623-631), plus
+    totalViolations; an empty list removes status.violations.
+The resource fields come from HandleViolation (pkg/target/target.go:193-244):
+the review's object (else oldObject) with kind = review.kind.kind.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+MSG_SIZE = 256                      # manager.go:41
+DEFAULT_LIMIT = 20                  # manager.go:43 (--constraint-violations-limit)
+KNOWN_ACTIONS = ("deny", "dryrun", "unrecognized")  # pkg/util/enforcement_action.go:11-17
+
+
+def truncate_string(msg: str, size: int = MSG_SIZE) -> str:
+    """truncateString (manager.go:623-631) on the message's bytes; the status
+    is JSON, so a cut inside a UTF-8 sequence marshals as U+FFFD."""
+    b = msg.encode("utf-8", "surrogateescape")
+    if len(b) <= size:
+        return msg
+    cut = size - 3 if size > 3 else size
+    return (b[:cut] + b"...").decode("utf-8", "replace")
+
+
+class AuditWriter:
+    """Accumulates one audit sweep's results (in evaluation order) per constraint."""
+
+    def __init__(self, constraints: Sequence[Tuple[str, str]], limit: int = DEFAULT_LIMIT):
+        self.constraints = list(constraints)        # engine constraint index -> (kind, name)
+        self.limit = limit
+        self.totals: Dict[int, int] = {}
+        self.samples: Dict[int, List[dict]] = {}
+        self.per_action: Dict[str, int] = {a: 0 for a in KNOWN_ACTIONS}
+
+    def add(self, constraint: int, resource: Tuple[str, str, str], msg: str, enforcement_action: str):
+        """one types.Result: resource = (kind, name, namespace)"""
+        self.totals[constraint] = self.totals.get(constraint, 0) + 1
+        lst = self.samples.setdefault(constraint, [])
+        if len(lst) < self.limit:
+            kind, name, ns = resource
+            lst.append({"kind": kind, "name": name, "namespace": ns, "message": msg,
+                        "enforcementAction": enforcement_action})
+        self.per_action[enforcement_action] = self.per_action.get(enforcement_action, 0) + 1
+
+    def add_results(self, results, resources: Sequence[Tuple[str, str, str]]):
+        """engine or oracle results, already in evaluation order (review, then
+        the per-review result order), each with .review/.constraint/.msg/
+        .enforcement_action; resources[review] = (kind, name, namespace)"""
+        for r in results:
+            self.add(r.constraint, resources[r.review], r.msg, r.enforcement_action)
+
+    def status(self, constraint: int) -> dict:
+        """the constraint's status fields written by updateConstraintStatus"""
+        out = {"totalViolations": self.totals.get(constraint, 0)}
+        vs = []
+        for ar in self.samples.get(constraint, [])[: self.limit]:
+            v = {"kind": ar["kind"], "name": ar["name"]}
+            if ar["namespace"]:
+                v["namespace"] = ar["namespace"]
+            v["message"] = truncate_string(ar["message"])
+            v["enforcementAction"] = ar["enforcementAction"]
+            vs.append(v)
+        if vs:
+            out["violations"] = vs
+        return out
+
+    def statuses(self) -> Dict[Tuple[str, str], dict]:
+        return {self.constraints[i]: self.status(i) for i in range(len(self.constraints))}
+
+    @staticmethod
+    def merge(writers: Sequence["AuditWriter"]) -> "AuditWriter":
+        """Rank-order merge of per-shard writers (contiguous resource shards,
+        rank r holding the r-th range): totals add, samples concatenate in rank
+        order up to the limit -- the single-process sweep's result."""
+        w0 = writers[0]
+        m = AuditWriter(w0.constraints, w0.limit)
+        for w in writers:
+            for c, n in w.totals.items():
+                m.totals[c] = m.totals.get(c, 0) + n
+            for c, lst in w.samples.items():
+                dst = m.samples.setdefault(c, [])
+                dst.extend(lst[: max(0, m.limit - len(dst))])
+            for a, n in w.per_action.items():
+                m.per_action[a] = m.per_action.get(a, 0) + n
+        return m
+
+
+def resource_of(review_or_object: dict, is_review: bool = False) -> Tuple[str, str, str]:
+    """(kind, name, namespace) of HandleViolation's Resource (target.go:193-244)."""
+    if is_review:
+        kind = (review_or_object.get("kind") or {}).get("kind", "")
+        obj = review_or_object.get("object") or review_or_object.get("oldObject") or {}
+    else:
+        obj = review_or_object
+        kind = obj.get("kind", "")
+    md = obj.get("metadata") or {}
+    return kind, md.get("name", "") or "", md.get("namespace", "") or ""

@@ -27,7 +27,7 @@ EXPORTS = [
     "gk_results_review_status", "gk_results_review_reason", "gk_results_constraints", "gk_results_constraint_total",
     "gk_results_timing", "gk_results_free", "gk_template_status", "gk_constraint_count", "gk_constraint_info",
     "gk_batch_stats", "gk_results_device_counts", "gk_results_copy_status", "gk_results_flag_counts",
-    "gk_results_launches", "gk_results_launch", "gk_template_backend",
+    "gk_results_launches", "gk_results_launch", "gk_template_backend", "gk_results_copy_device_output",
 ]
 
 
@@ -110,6 +110,7 @@ def load_library():
     lib.gk_results_launches.restype = sz
     lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32), pu64, pu64]
     lib.gk_template_backend.argtypes = [vp, cp, C.POINTER(C.c_int), C.POINTER(cp)]
+    lib.gk_results_copy_device_output.argtypes = [vp, vp, vp, vp]
     lib.gk_results_vm_profile.argtypes = [vp, C.c_void_p, sz]
     lib.gk_results_vm_profile.restype = sz
     lib.gk_template_status.argtypes = [vp, cp, C.POINTER(cp)]
@@ -252,11 +253,22 @@ class Batch:
         self._h = handle
         self.n = n
 
-    def eval(self, decode=True, light=False) -> Results:
+    def eval(self, decode=True, light=False, device_out=None) -> Results:
+        """device_out(n_tuples, n_bytes) -> (tuples_ptr, bytes_ptr): device
+        buffers (e.g. torch tensors' data_ptr()) that receive the call's raw
+        output (gk_viol records + message bytes) before the handle is freed."""
         lib = self._drv._lib
         out = C.c_void_p()
         rc = lib.gk_batch_eval(self._drv._e, self._h, 1 if decode else 0, C.byref(out))
         self._drv._check(rc)
+        if device_out is not None:
+            dt, db = C.c_uint64(), C.c_uint64()
+            lib.gk_results_device_counts(out, C.byref(dt), C.byref(db))
+            tp, bp = device_out(dt.value, db.value)
+            rc = lib.gk_results_copy_device_output(self._drv._e, out, tp, bp)
+            if rc != 0:
+                lib.gk_results_free(out)
+                self._drv._check(rc)
         return _collect_light(lib, out) if light else _collect(lib, out)
 
     def device_bytes(self) -> int:

@@ -1,0 +1,137 @@
+"""Multi-GPU audit sweep: resource shards per rank, violations gathered to rank 0.
+
+SURVEY 8(e): resources are independent units, so each rank (one process per
+GPU) audits a contiguous shard of the resources against every constraint with
+no data-path collective.  The exchange steps are the ones the audit needs
+downstream: the per-constraint totals (an all-reduce, the status write of
+pkg/audit/manager.go:462-508) and the compacted violation lists, gathered to
+rank 0 with exact-size point-to-point transfers over RCCL (xGMI) -- or gloo
+for the CPU tests.
+
+The violation records are the engine's gk_viol (include/gkgpu.h): 8 x u32
+(review, constraint, seq, rule, msg_off, msg_len, det_off, det_len).  A rank's
+review indices are rebased to global indices before sending; message offsets
+stay relative to that rank's byte buffer (a global buffer could pass 4 GiB),
+so rank 0 holds one (tuples, bytes) pair per source rank.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+VIOL_WORDS = 8
+VIOL_BYTES = 32
+
+
+def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous shard [start, stop) of n_total resources for `rank`: ceil(n/world) each."""
+    per = (n_total + world - 1) // world
+    start = min(n_total, rank * per)
+    return start, min(n_total, start + per)
+
+
+class DeviceOutput:
+    """Reusable device buffers receiving one evaluation's raw output
+    (Batch.eval(device_out=...)); grown on demand, kept across steps."""
+
+    def __init__(self, device):
+        import torch
+        self.torch = torch
+        self.device = device
+        self._t = None
+        self._b = None
+        self.n_tuples = 0
+        self.n_bytes = 0
+
+    def __call__(self, n_tuples: int, n_bytes: int):
+        torch = self.torch
+        if self._t is None or self._t.numel() < n_tuples * VIOL_BYTES:
+            self._t = torch.empty(max(n_tuples, 1) * VIOL_BYTES, dtype=torch.uint8, device=self.device)
+        if self._b is None or self._b.numel() < n_bytes:
+            self._b = torch.empty(max(n_bytes, 1), dtype=torch.uint8, device=self.device)
+        self.n_tuples, self.n_bytes = n_tuples, n_bytes
+        return self._t.data_ptr(), self._b.data_ptr()
+
+    def tuples(self):
+        """int32 [n, 8] view of the gk_viol records."""
+        return self._t[: self.n_tuples * VIOL_BYTES].view(self.torch.int32).view(-1, VIOL_WORDS)
+
+    def bytes(self):
+        return self._b[: self.n_bytes]
+
+
+class Gatherer:
+    """Gathers every rank's violation tuples and message bytes to `dst`.
+
+    Receive buffers on `dst` are kept across calls (an audit sweep repeats with
+    the same shapes), so a steady-state gather allocates nothing."""
+
+    def __init__(self, dst: int = 0, group=None):
+        self.dst = dst
+        self.group = group
+        self._recv = {}
+
+    def gather(self, tuples, bytes_, review_base: int):
+        """tuples: int32 [n, 8] (gk_viol) and bytes_: uint8 [m] on this rank's
+        device (CPU tensors under gloo).  Returns, on `dst`, a list with one
+        (tuples, bytes) pair per rank in rank order -- review indices global,
+        byte offsets relative to that pair's bytes -- and None elsewhere."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        dev = tuples.device
+        t = tuples
+        if review_base:
+            t = tuples.clone()
+            t[:, 0] += int(review_base)
+        counts = torch.tensor([t.shape[0], bytes_.numel()], dtype=torch.int64, device=dev)
+        allc = [torch.zeros_like(counts) for _ in range(world)]
+        dist.all_gather(allc, counts, group=self.group)
+        sizes = [(int(c[0]), int(c[1])) for c in allc]
+        ops = []
+        out: Optional[List] = None
+        if rank == self.dst:
+            out = []
+            for r in range(world):
+                nt, nb = sizes[r]
+                if r == rank:
+                    out.append((t, bytes_))
+                    continue
+                key = (r, nt, nb)
+                if key not in self._recv:
+                    self._recv = {k: v for k, v in self._recv.items() if k[0] != r}
+                    self._recv[key] = (torch.empty((nt, VIOL_WORDS), dtype=torch.int32, device=dev),
+                                       torch.empty(nb, dtype=torch.uint8, device=dev))
+                rt, rb = self._recv[key]
+                if nt:
+                    ops.append(dist.P2POp(dist.irecv, rt, r, self.group))
+                if nb:
+                    ops.append(dist.P2POp(dist.irecv, rb, r, self.group))
+                out.append((rt, rb))
+        else:
+            nt, nb = sizes[rank]
+            if nt:
+                ops.append(dist.P2POp(dist.isend, t.contiguous(), self.dst, self.group))
+            if nb:
+                ops.append(dist.P2POp(dist.isend, bytes_.contiguous(), self.dst, self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return out
+
+
+def decode(parts, limit: Optional[int] = None):
+    """(review, constraint, seq, rule, msg, details) rows from gathered parts,
+    in the reference's per-object order (review, autoreject first, constraint,
+    emission order).  Host-side; for tests and status samples."""
+    rows = []
+    for t, b in parts:
+        tt = t.cpu().numpy()
+        bb = b.cpu().numpy().tobytes()
+        for rec in tt:
+            rv, c, seq, rule, mo, ml, do, dl = (int(x) & 0xffffffff for x in rec)
+            rows.append((rv, 0 if rule == 0xffff else 1, c, seq, rule, bb[mo:mo + ml].decode("utf-8", "surrogateescape"),
+                         bb[do:do + dl].decode("utf-8", "surrogateescape")))
+    rows.sort(key=lambda r: (r[0], r[1], r[2], r[3]))
+    out = [(r[0], r[2], r[3], r[4], r[5], r[6]) for r in rows]
+    return out[:limit] if limit is not None else out

@@ -131,6 +131,16 @@ uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
 int gk_results_timing(const gk_results* r, double* ms5);
 /* violation tuples (32 B each) and message/details bytes the kernel wrote */
 int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* bytes);
+/* The device-resident output of the call: dev_tuples gk_viol records and
+ * dev_bytes message/details bytes (unordered: one reservation per wavefront).
+ * Copied device-to-device into caller buffers on the engine's device (e.g.
+ * tensors handed to an RCCL gather).  Valid until the engine's next
+ * evaluation; GK_EINVAL after that. */
+typedef struct {
+  uint32_t review, constraint, seq, rule; /* rule 0xffff = autoreject */
+  uint32_t msg_off, msg_len, det_off, det_len;
+} gk_viol;
+int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst);
 /* kernels of the call in launch order: kernel name ("audit_kernel" = bytecode
  * VM, "gk_t_<hash>" = a template kernel), duration (HIP events), how many
  * constraints it evaluated and the violation tuples / message bytes it wrote */

@@ -261,3 +261,56 @@ def test_staged_batches_are_independent():
     got_b = sorted((x.review, x.constraint, x.msg) for x in bb.eval(decode=True).results)
     assert got_a == want_a
     assert got_b == want_b
+
+
+def test_audit_writer_engine_matches_oracle():
+    """status.violations / totalViolations / per-action totals written from the
+    engine's results equal those written from the oracle's (manager.go:462-631)."""
+    from gkgpu.audit import AuditWriter, resource_of
+    from parity import engine_for, oracle_review
+    ts, cs = W.config2()
+    cs = [dict(c) for c in cs]
+    cs[3] = W.constraint("K8sRequiredProbes", "must-have-probes", match=cs[3]["spec"]["match"],
+                         parameters=cs[3]["spec"]["parameters"], enforcement_action="dryrun")
+    pods, ns_of, ns_objs = W.gen_pods(600, seed=21, n_namespaces=30)
+    nss = [ns_objs[n] for n in ns_of]
+    drv = Driver()
+    engine_for(drv, ts, cs)
+    od = oracle_for(ts, cs)
+    res = drv.review_objects(pods, nss)
+    assert not any(res.status)
+    resources = [resource_of(p) for p in pods]
+    cons = drv.constraints()
+    we = AuditWriter(cons)
+    we.add_results(res.results, resources)
+    wo = AuditWriter(cons)
+    cidx = {kc: i for i, kc in enumerate(cons)}
+    for i, p in enumerate(pods):
+        for kind, name, msg, _det, ea in oracle_review(od, augmented_review(p, nss[i])):
+            wo.add(cidx[(kind, name)], resources[i], msg, ea)
+    assert we.statuses() == wo.statuses()
+    assert we.per_action == wo.per_action
+    assert we.per_action["dryrun"] > 0 and we.per_action["deny"] > 0
+
+
+def test_device_output_copy_decodes_to_results():
+    """Batch.eval(device_out=...) hands the raw gk_viol records + message bytes
+    to caller device buffers (the tensors the multi-GPU gather sends)."""
+    import torch
+    from gkgpu.parallel import DeviceOutput, decode
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(300, seed=31, n_namespaces=20)
+    nss = [ns_objs[n] for n in ns_of]
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    b = drv.stage_objects(pods, nss)
+    out = DeviceOutput(torch.device("cuda", 0))
+    r = b.eval(decode=False, light=True, device_out=out)
+    assert out.n_tuples == r.device_tuples and out.n_bytes == r.device_bytes
+    rows = decode([(out.tuples(), out.bytes())])
+    full = b.eval(decode=True)
+    assert [(x[0], x[1], x[4]) for x in rows] == [(x.review, x.constraint, x.msg) for x in full.results]
