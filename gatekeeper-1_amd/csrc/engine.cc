@@ -1437,7 +1437,8 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   std::lock_guard<std::mutex> g(e->mu);
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
   auto* res = new gk_results();
-  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, b->d_nodes.p);
+  const void* nodes = b->d_nodes.p;
+  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, nodes);
   if (rc != GK_OK) { delete res; return rc; }
   *out = res;
   return GK_OK;
