@@ -29,15 +29,37 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pods", type=int, default=1_000_000, help="Pods per GPU")
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[n-1]: 2 = agilebank x Pods (the metric's config), "
+                         "3 = allowedRegex x Deployments+Services, 4 = mixed kinds x 50 constraints (per-GPU shard)")
+    ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=1500, help="Pods timed on the CPU oracle (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch for this workload (rocprofv3 --pmc), if measured")
     return ap.parse_args()
 
 
+# config -> (templates/constraints, JSON generator(n, start), default resources per GPU, description)
+def _configs():
+    from gkgpu import workloads as W
+    return {
+        "2": (W.config2, lambda n, start: W.gen_pods_json(n, seed=42, n_namespaces=1000, start=start), 1_000_000,
+              "config2: demo/agilebank policies over synthetic Pods (BASELINE configs[1])"),
+        "3": (W.config3, lambda n, start: W.gen_config3_json(n, seed=7, start=start), 1_000_000,
+              "config3: 10 allowedRegex label/annotation constraints over Deployments + Services (BASELINE configs[2])"),
+        "4": (W.config4, lambda n, start: W.gen_config4_json(n, seed=1234, start=start), 1_250_000,
+              "config4: mixed kinds x 50 randomized constraints, 1.25M resources per GPU = 10M over 8 (BASELINE configs[3])"),
+    }
+
+
+CONFIGS = ("2", "3", "4")
+
+
 def main():
     args = parse()
+    cfg_templates, cfg_gen, cfg_default_n, cfg_desc = _configs()[args.config]
+    if args.pods is None:
+        args.pods = cfg_default_n
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -52,7 +74,7 @@ def main():
     from gkgpu import workloads as W
     from gkgpu.client import Client
 
-    templates, constraints = W.config2()
+    templates, constraints = cfg_templates()
     drv = gkgpu.Driver(device=local)
     cl = Client(drv)
     for t in templates:
@@ -68,7 +90,7 @@ def main():
             kinds_of[detail] = k
 
     t0 = time.time()
-    objs, nss = W.gen_pods_json(args.pods, seed=42, n_namespaces=1000, start=rank * args.pods)
+    objs, nss = cfg_gen(args.pods, rank * args.pods)
     t_gen = time.time() - t0
     t0 = time.time()
     batch = drv.stage_objects(objs, nss)
@@ -146,7 +168,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("pods") == args.pods and tj.get("constraints") == n_cons:
+            if tj.get("pods") == args.pods and tj.get("constraints") == n_cons and tj.get("config", "2") == args.config:
                 traffic = tj.get("hbm_bytes_per_launch", {}).get(kinds_of.get(dom))
         except Exception:
             traffic = None
@@ -168,10 +190,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded generator, SURVEY 8(d) config 2 distribution)",
+            "data": "synthetic (seeded generator, SURVEY 8(d) config %s distribution)" % args.config,
             "config": {
-                "workload": "config2: demo/agilebank policies over synthetic Pods (BASELINE configs[1])",
-                "pods_per_gpu": nrev,
+                "workload": cfg_desc,
+                "resources_per_gpu": nrev,
                 "constraints": n_cons,
                 "templates": [t["spec"]["crd"]["spec"]["names"]["kind"] for t in templates],
                 "evals_per_step": evals_per_step,
@@ -216,13 +238,13 @@ def cpu_baseline(templates, constraints, objs_json, nss_json):
     from gkgpu.client import augmented_review
     od = oracle_for(templates, constraints)
     objs = [json.loads(o) for o in objs_json]
-    nss = [json.loads(n) for n in nss_json]
+    nss = [None if n is None else json.loads(n) for n in nss_json]
     t0 = time.perf_counter()
     for o, n in zip(objs, nss):
         oracle_review(od, augmented_review(o, n))
     dt = time.perf_counter() - t0
     return {"value": len(objs) * len(constraints) / dt, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": "%d Pods x %d constraints (config2 distribution), oracle/ CPU restatement of OPA v0.21 "
+            "sample": "%d resources x %d constraints (same workload), oracle/ CPU restatement of OPA v0.21 "
                       "topdown; Go/OPA not buildable offline" % (len(objs), len(constraints)),
             "seconds": dt}
 

@@ -475,3 +475,193 @@ def gen_pods_json(n, seed=42, n_namespaces=1000, start=0):
                     '"spec":{"containers":[%s]%s}}' % (i, ns, rbits(7), owner, conts, init))
         nss.append(ns_json[ns])
     return objs, nss
+
+
+# -- config 3: allowedRegex label / annotation templates over Deployments + Services
+_C3_RULES = {
+    "env": "^(dev|stage|prod)-[0-9]{1,4}$",
+    "owner": "^[a-zA-Z]+.agilebank.demo$",
+    "app": "^[a-z0-9]([-a-z0-9]*[a-z0-9])?$",
+    "tier": "^(frontend|backend|cache|db)$",
+    "team": "^team-[a-z]{2,8}$",
+    "version": "^v[0-9]+\\.[0-9]+\\.[0-9]+$",
+    "region": "^[a-z]{2}-[a-z]+-[0-9]$",
+    "component": "^[a-z]+(-[a-z]+)*$",
+}
+# values near each pattern's boundaries (~half match); ASCII only, so no review
+# needs the UTF-8 fallback (non-ASCII subjects are covered by the parity tests)
+_C3_VALUES = {
+    "env": ["dev-1", "prod-9999", "stage-42", "prod-10000", "stage-", "dev-12\n", "qa-1", "", "DEV-1", "prod-0001"],
+    "owner": ["alice.agilebank.demo", "Bob.agilebank.demo", "bob_agilebank.demo", "x.agilebank.demo\n",
+              "9.agilebank.demo", "carol-agilebank-demo", "dave.agilebank.demo.", "e.agilebankXdemo"],
+    "app": ["web", "-web", "web-", "a", "Web", "a-b-c", "", "api-7", "x" * 40, "db_1"],
+    "tier": ["frontend", "backend", "cache", "db", "Frontend", "frontend ", "web", ""],
+    "team": ["team-ab", "team-payments", "team-a", "team-abcdefghi", "Team-ab", "team-12", "team-ops"],
+    "version": ["v1.2.3", "v10.0.1", "1.2.3", "v1.2", "v1.2.3-rc1", "v01.2.3", "v1..3"],
+    "region": ["us-east-1", "eu-west-2", "us-east-12", "US-east-1", "ap-south", "eu-central-3"],
+    "component": ["api", "api-server", "-api", "api-", "API", "a-b-c-d", "api--server"],
+}
+
+
+def config3():
+    """10 allowedRegex constraints: 5 over labels, 5 over annotations, each a
+    different pair of key rules, all matching Deployments and Services."""
+    keys = list(_C3_RULES)
+    cs = []
+    for i in range(5):
+        sel = [keys[(2 * i + j) % len(keys)] for j in range(3)]
+        rules = [{"key": k, "allowedRegex": _C3_RULES[k]} for k in sel]
+        match = {"kinds": [{"apiGroups": ["apps", ""], "kinds": ["Deployment", "Service"]}]}
+        cs.append(constraint("K8sAllowedLabelRegex", "label-rules-%d" % i, match=match, parameters={"rules": rules}))
+        cs.append(constraint("K8sAllowedAnnotationRegex", "annotation-rules-%d" % i, match=match,
+                             parameters={"rules": rules}))
+    return [ALLOWED_LABEL_REGEX, ALLOWED_ANNOTATION_REGEX], cs
+
+
+def gen_config3_json(n, seed=7, start=0, n_namespaces=200):
+    """Config 3 at scale: 50% Deployments / 50% Services, 2-8 labels and 0-4
+    annotations drawn from _C3_VALUES (JSON text; pools of pre-serialized maps)."""
+    rng = random.Random(seed)
+    keys = list(_C3_VALUES)
+
+    def amap(lo, hi):
+        ks = rng.sample(keys, rng.randint(lo, hi))
+        return {k: rng.choice(_C3_VALUES[k]) for k in ks}
+
+    lab_pool = [dumps(amap(2, 8)) for _ in range(4096)]
+    ann_pool = [dumps(amap(0, 4)) for _ in range(4096)]
+    names = ["c3-ns-%03d" % i for i in range(n_namespaces)]
+    ns_json = {nm: dumps(namespace_obj(nm, {"env": "dev"})) for nm in names}
+    r = random.Random(seed * 7919 + start)
+    rb = r.getrandbits
+    objs, nss = [], []
+    for i in range(start, start + n):
+        ns = names[rb(16) % len(names)]
+        lab, ann = lab_pool[rb(12)], ann_pool[rb(12)]
+        if rb(1):
+            objs.append('{"apiVersion":"apps/v1","kind":"Deployment","metadata":{"name":"dep-%08d","namespace":"%s",'
+                        '"labels":%s,"annotations":%s},"spec":{"replicas":%d}}' % (i, ns, lab, ann, 1 + rb(3)))
+        else:
+            objs.append('{"apiVersion":"v1","kind":"Service","metadata":{"name":"svc-%08d","namespace":"%s",'
+                        '"labels":%s,"annotations":%s},"spec":{"ports":[{"port":%d}]}}' % (i, ns, lab, ann, 80 + rb(10)))
+        nss.append(ns_json[ns])
+    return objs, nss
+
+
+# -- config 4: 50 constraints cloned from the subset templates, randomized match
+_C4_KINDS = [("", "Pod"), ("apps", "Deployment"), ("", "Service"), ("", "ConfigMap"), ("", "Namespace")]
+
+
+def config4(seed=1234, n_namespaces=1000):
+    """50 constraints over the subset templates with randomized match (kinds,
+    namespaces, excludedNamespaces, labelSelector In/NotIn/Exists/DoesNotExist,
+    namespaceSelector, scope) and parameters."""
+    rng = random.Random(seed)
+    ns_names = ["team-%04d" % i for i in range(n_namespaces - 1)] + ["production"]
+    templates = [REQUIRED_LABELS, ALLOWED_REPOS, CONTAINER_LIMITS, REQUIRED_PROBES, ALLOWED_LABEL_REGEX,
+                 ALLOWED_ANNOTATION_REGEX]
+    cs = []
+    for i in range(50):
+        kind = ["K8sRequiredLabels", "K8sAllowedRepos", "K8sContainerLimits", "K8sRequiredProbes",
+                "K8sAllowedLabelRegex", "K8sAllowedAnnotationRegex"][i % 6]
+        match = {}
+        r = rng.random()
+        if r < 0.15:
+            pass  # default kinds: everything
+        else:
+            ks = rng.sample(_C4_KINDS, rng.randint(1, 3))
+            groups = sorted({g for g, _ in ks})
+            match["kinds"] = [{"apiGroups": groups if rng.random() < 0.7 else ["*"], "kinds": [k for _, k in ks]}]
+        if rng.random() < 0.2:
+            match["namespaces"] = rng.sample(ns_names, 3) + ["production"]
+        if rng.random() < 0.2:
+            match["excludedNamespaces"] = rng.sample(ns_names, 5)
+        if rng.random() < 0.3:
+            op = rng.choice(["In", "NotIn", "Exists", "DoesNotExist"])
+            e = {"key": rng.choice(["app", "owner", "tier"]), "operator": op}
+            if op in ("In", "NotIn"):
+                e["values"] = ["app-%d" % rng.randint(0, 99) for _ in range(3)] + ["alice", "frontend"]
+            sel = {"matchExpressions": [e]}
+            if rng.random() < 0.3:
+                sel["matchLabels"] = {"app": "app-%d" % rng.randint(0, 9)}
+            match["labelSelector"] = sel
+        if rng.random() < 0.25:
+            match["namespaceSelector"] = {"matchExpressions": [
+                {"key": "env", "operator": rng.choice(["In", "NotIn"]), "values": [rng.choice(["dev", "prod", "stage"])]}]}
+        if rng.random() < 0.15:
+            match["scope"] = rng.choice(["Namespaced", "Cluster", "*"])
+        if kind == "K8sRequiredLabels":
+            params = {"labels": [{"key": rng.choice(["owner", "app", "tier"]),
+                                  "allowedRegex": rng.choice(["^[a-zA-Z]+.agilebank.demo$", "^app-[0-9]+$", ""])}]}
+            if rng.random() < 0.5:
+                params["message"] = "constraint %d: required label missing" % i
+        elif kind == "K8sAllowedRepos":
+            params = {"repos": rng.sample(["openpolicyagent", "gcr.io/x", "nginx", "docker.io/library"], 2)}
+        elif kind == "K8sContainerLimits":
+            params = {"cpu": rng.choice(["100m", "200m", "1", "2"]), "memory": rng.choice(["512Mi", "1Gi", "2Gi", "1G"])}
+        elif kind == "K8sRequiredProbes":
+            params = {"probes": rng.sample(["readinessProbe", "livenessProbe"], rng.randint(1, 2)),
+                      "probeTypes": ["tcpSocket", "httpGet", "exec"]}
+        else:
+            keys = rng.sample(list(_C3_RULES), 2)
+            params = {"rules": [{"key": k, "allowedRegex": _C3_RULES[k]} for k in keys]}
+        ea = "dryrun" if rng.random() < 0.2 else None
+        cs.append(constraint(kind, "c4-%02d-%s" % (i, kind.lower()), match=match or None, parameters=params,
+                             enforcement_action=ea))
+    return templates, cs
+
+
+def gen_config4_json(n, seed=1234, start=0, n_namespaces=1000):
+    """Config 4 mix: Pods 60%, Deployments 15%, Services 10%, ConfigMaps 14%,
+    Namespaces 1% (cluster-scoped: no namespace object)."""
+    rng = random.Random(seed)
+    pools = [[dumps(_container(rng, "c%d" % slot)) for _ in range(1024)] for slot in range(4)]
+    init_pool = [dumps(_container(rng, "init")) for _ in range(1024)]
+    keys = list(_C3_VALUES)
+
+    def labels():
+        d = {"app": "app-%d" % rng.randint(0, 99)}
+        if rng.random() < 0.6:
+            d["owner"] = rng.choice(["alice", "bob.agilebank.demo", "Carol.agilebank.demo"])
+        if rng.random() < 0.5:
+            d["tier"] = rng.choice(_C3_VALUES["tier"])
+        for k in rng.sample(keys, rng.randint(0, 2)):
+            d[k] = rng.choice(_C3_VALUES[k])
+        return dumps(d)
+
+    lab_pool = [labels() for _ in range(4096)]
+    ann_pool = [dumps({k: rng.choice(_C3_VALUES[k]) for k in rng.sample(keys, rng.randint(0, 3))}) for _ in range(1024)]
+    names = ["team-%04d" % i for i in range(n_namespaces - 1)] + ["production"]
+    envs = ["dev", "prod", "stage"]
+    ns_json = {nm: dumps(namespace_obj(nm, {"env": "prod" if nm == "production" else envs[sum(map(ord, nm)) % 3]}))
+               for nm in names}
+    r = random.Random(seed * 7919 + start)
+    rand, rb = r.random, r.getrandbits
+    objs, nss = [], []
+    for i in range(start, start + n):
+        ns = names[rb(16) % len(names)]
+        lab, ann = lab_pool[rb(12)], ann_pool[rb(10)]
+        x = rand()
+        k = 1 + rb(2)
+        conts = ",".join(pools[s][rb(10)] for s in range(k))
+        if x < 0.60:
+            init = (',"initContainers":[' + init_pool[rb(10)] + "]") if rand() < 0.3 else ""
+            objs.append('{"apiVersion":"v1","kind":"Pod","metadata":{"name":"pod-%08d","namespace":"%s","labels":%s,'
+                        '"annotations":%s},"spec":{"containers":[%s]%s}}' % (i, ns, lab, ann, conts, init))
+        elif x < 0.75:
+            objs.append('{"apiVersion":"apps/v1","kind":"Deployment","metadata":{"name":"dep-%08d","namespace":"%s",'
+                        '"labels":%s,"annotations":%s},"spec":{"replicas":%d,"template":{"metadata":{"labels":%s},'
+                        '"spec":{"containers":[%s]}}}}' % (i, ns, lab, ann, 1 + rb(3), lab, conts))
+        elif x < 0.85:
+            objs.append('{"apiVersion":"v1","kind":"Service","metadata":{"name":"svc-%08d","namespace":"%s","labels":%s,'
+                        '"annotations":%s},"spec":{"selector":%s,"ports":[{"port":%d}]}}' % (i, ns, lab, ann, lab, 80 + rb(8)))
+        elif x < 0.99:
+            objs.append('{"apiVersion":"v1","kind":"ConfigMap","metadata":{"name":"cm-%08d","namespace":"%s","labels":%s},'
+                        '"data":{"k":"v%d"}}' % (i, ns, lab, rb(10)))
+        else:
+            objs.append('{"apiVersion":"v1","kind":"Namespace","metadata":{"name":"nsobj-%08d","labels":%s},'
+                        '"spec":{"finalizers":["kubernetes"]},"status":{"phase":"Active"}}' % (i, lab))
+            nss.append(None)
+            continue
+        nss.append(ns_json[ns])
+    return objs, nss

@@ -314,3 +314,39 @@ def test_device_output_copy_decodes_to_results():
     rows = decode([(out.tuples(), out.bytes())])
     full = b.eval(decode=True)
     assert [(x[0], x[1], x[4]) for x in rows] == [(x.review, x.constraint, x.msg) for x in full.results]
+
+
+def test_config3_generator_regex_constraints():
+    """Config 3's 10 allowedRegex constraints over its generator's Deployments
+    and Services, plus non-ASCII subjects: those under a UTF-8-sensitive
+    pattern (`.`) are routed to the CPU fallback, every other review is
+    bit-exact with the oracle."""
+    ts, cs = W.config3()
+    objs, nss = W.gen_config3_json(700, seed=7)
+    objs = [json.loads(o) for o in objs]
+    nss = [json.loads(n) for n in nss]
+    extra = [{"apiVersion": "v1", "kind": "Service",
+              "metadata": {"name": "u%d" % i, "namespace": "c3-ns-000", "labels": {"owner": v, "env": "dev-1"},
+                           "annotations": {"app": v}}}
+             for i, v in enumerate(["émile.agilebank.demo", "bob.agilebank.demo", "日本", "xé"])]
+    objs += extra
+    nss += [nss[0]] * len(extra)
+    rep, res = run_objects(Driver(), ts, cs, objs, nss)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.violations > 1000
+    assert rep.fallback <= len(extra)
+
+
+def test_config4_mixed_kinds_fifty_constraints():
+    """Config 4: mixed kinds (Pods, Deployments, Services, ConfigMaps,
+    Namespaces) x 50 constraints with randomized match blocks (namespaces,
+    excludedNamespaces, label/namespace selectors, scope) and parameters."""
+    ts, cs = W.config4()
+    objs, nss = W.gen_config4_json(400, seed=1234)
+    objs = [json.loads(o) for o in objs]
+    nss = [None if n is None else json.loads(n) for n in nss]
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, nss)
+    _assert_clean(rep)
+    assert rep.violations > 500
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
