@@ -27,11 +27,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; 1000 launches for config 5)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
                     help="BASELINE.json configs[n-1]: 2 = agilebank x Pods (the metric's config), "
-                         "3 = allowedRegex x Deployments+Services, 4 = mixed kinds x 50 constraints (per-GPU shard)")
+                         "3 = allowedRegex x Deployments+Services, 4 = mixed kinds x 50 constraints (per-GPU shard), "
+                         "5 = admission-webhook micro-batch (256 AdmissionReviews per launch, p50/p99 latency)")
+    ap.add_argument("--load", type=int, default=50, help="config 5: constraints loaded (policy_benchmark_test.go:268)")
+    ap.add_argument("--batch", type=int, default=256, help="config 5: AdmissionReviews per launch")
     ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=1500, help="Pods timed on the CPU oracle (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -52,11 +55,15 @@ def _configs():
     }
 
 
-CONFIGS = ("2", "3", "4")
+CONFIGS = ("2", "3", "4", "5")
 
 
 def main():
     args = parse()
+    if args.config == "5":
+        return webhook_main(args)
+    if args.steps is None:
+        args.steps = 20
     cfg_templates, cfg_gen, cfg_default_n, cfg_desc = _configs()[args.config]
     if args.pods is None:
         args.pods = cfg_default_n
@@ -247,6 +254,124 @@ def cpu_baseline(templates, constraints, objs_json, nss_json):
             "sample": "%d resources x %d constraints (same workload), oracle/ CPU restatement of OPA v0.21 "
                       "topdown; Go/OPA not buildable offline" % (len(objs), len(constraints)),
             "seconds": dt}
+
+
+def webhook_main(args):
+    """Config 5 (BASELINE configs[4]): admission-webhook micro-batch.  A step is
+    one gk_query_batch launch over `--batch` UPDATE AdmissionReviews (object +
+    oldObject, policy_benchmark_test.go:197-231) against the PSP policies at
+    constraint load `--load`, timed from the call's entry to decoded results
+    (messages, details, enforcementAction) back on the host.  Inputs are JSON
+    text (what the webhook receives), generated before the timed region."""
+    if args.steps is None:
+        args.steps = 1000
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import gkgpu
+    from gkgpu import workloads as W
+    from gkgpu.client import Client
+    from gkgpu.webhook import handle_batch  # noqa: F401  (the per-request decision path tests use)
+
+    templates, constraints = W.config5(args.load)
+    drv = gkgpu.Driver(device=local)
+    cl = Client(drv)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    nb = 16
+    batches = [W.gen_admission_inputs(args.batch, seed=99, start=(rank * nb + i) * args.batch) for i in range(nb)]
+    for i in range(args.warmup):
+        drv.query_batch(batches[i % nb])
+    if dist is not None:
+        dist.barrier()
+    lat = []
+    n_results = n_flagged = 0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ts = time.perf_counter()
+        res = drv.query_batch(batches[i % nb])
+        lat.append((time.perf_counter() - ts) * 1000.0)
+        n_results += len(res.results)
+        n_flagged += res.n_errors + res.n_fallbacks
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [ln.ms for ln in res.launches]
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lat.sort()
+
+    def pct(p):
+        return lat[min(len(lat) - 1, int(round(p / 100.0 * (len(lat) - 1))))]
+
+    n_cons = len(constraints)
+    evals = args.steps * args.batch * n_cons * world
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = webhook_cpu_baseline(templates, constraints, batches[0][: min(args.batch, args.cpu_sample)])
+    if rank == 0:
+        out = {
+            "metric": "resource x constraint evals/sec (1/2/4/8 GPU) + % HBM roofline; vs host-CPU OPA",
+            "value": evals / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1000.0,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (PSP pods of policy_benchmark_test.go as UPDATE AdmissionReviews, seed 99)",
+            "config": {
+                "workload": "config5: admission-webhook micro-batch, %d AdmissionReviews per launch x %d PSP "
+                            "constraints (BASELINE configs[4])" % (args.batch, n_cons),
+                "requests_per_launch": args.batch,
+                "constraints": n_cons,
+                "latency_ms": {"p50": pct(50), "p99": pct(99), "mean": sum(lat) / len(lat), "max": lat[-1]},
+                "requests_per_s": args.steps * args.batch * world / elapsed,
+                "results_per_launch": n_results / args.steps,
+                "flagged_reviews": n_flagged,
+                "kernel_ms_last_launch": kernel_ms,
+                "parallelism": "replicas%d (independent webhook replicas, no collective)" % world,
+            },
+            "roofline": None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def webhook_cpu_baseline(templates, constraints, inputs):
+    """The oracle on one host core over one micro-batch of the same requests:
+    per-request Query latency (the reference webhook evaluates one request per
+    Review call, policy.go:371-387)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import oracle_for, oracle_review
+    od = oracle_for(templates, constraints)
+    reviews = [json.loads(s)["review"] for s in inputs]
+    lat = []
+    for rv in reviews:
+        t0 = time.perf_counter()
+        oracle_review(od, rv)
+        lat.append((time.perf_counter() - t0) * 1000.0)
+    lat.sort()
+    tot = sum(lat) / 1000.0
+    return {"value": len(reviews) * len(constraints) / tot, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": "%d AdmissionReviews x %d constraints, one Query per request, oracle/ CPU restatement of "
+                      "OPA v0.21 topdown; Go/OPA not buildable offline" % (len(reviews), len(constraints)),
+            "latency_ms_per_request": {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(0.99 * len(lat)))]},
+            "batch_latency_ms": tot * 1000.0, "seconds": tot}
 
 
 if __name__ == "__main__":

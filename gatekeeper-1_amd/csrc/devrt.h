@@ -1124,6 +1124,131 @@ __device__ uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2)
   return UND;
 }
 
+// the byte range [st, st+len) of string value a0 (s = its view) as a value
+// that shares the bytes: a slice of an interned string or of the lane buffer
+__device__ uint64_t str_sub(Lane& L, uint64_t a0, SView s, uint32_t st, uint32_t len) {
+  if (st == 0 && len == s.n) return a0;
+  if (len == 0) return mkv(V_STR, 0);
+  if (vtag(a0) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a0), st, len);
+  if (vtag(a0) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + st, len);
+  if (vtag(a0) == V_SLICE) {
+    uint64_t p = vpay(a0);
+    return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + st, len);
+  }
+  lane_fallback(L, FB_STRING);
+  return mkv(V_UNDEF, 0);
+}
+
+__device__ __forceinline__ bool bytes_at(SView s, uint32_t o, SView p) {
+  if (o + p.n > s.n) return false;
+  for (uint32_t i = 0; i < p.n; ++i) if (s.p[o + i] != p.p[i]) return false;
+  return true;
+}
+
+// trim(s, cutset) = strings.Trim (topdown/strings.go:261-273).  The cutset is a
+// set of runes; for an ASCII cutset byte-wise trimming is exact (UTF-8 lead and
+// continuation bytes are >= 0x80), otherwise the review goes to the CPU.
+__device__ uint64_t bi_trim(Lane& L, uint64_t a0, uint64_t a1) {
+  if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  SView s = sview(L, a0), c = sview(L, a1);
+  for (uint32_t i = 0; i < c.n; ++i) if ((unsigned char)c.p[i] >= 0x80) { lane_fallback(L, FB_UNICODE); return mkv(V_UNDEF, 0); }
+  auto in_cut = [&](char ch) { for (uint32_t i = 0; i < c.n; ++i) if (c.p[i] == ch) return true; return false; };
+  uint32_t i = 0, j = s.n;
+  while (i < j && in_cut(s.p[i])) ++i;
+  while (j > i && in_cut(s.p[j - 1])) --j;
+  return str_sub(L, a0, s, i, j - i);
+}
+
+// trim_prefix / trim_suffix = strings.TrimPrefix / TrimSuffix (byte-wise)
+__device__ uint64_t bi_trim_fix(Lane& L, uint32_t id, uint64_t a0, uint64_t a1) {
+  if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  SView s = sview(L, a0), p = sview(L, a1);
+  if (p.n > s.n) return a0;
+  if (id == BI_TRIM_PREFIX) return bytes_at(s, 0, p) ? str_sub(L, a0, s, p.n, s.n - p.n) : a0;
+  return bytes_at(s, s.n - p.n, p) ? str_sub(L, a0, s, 0, s.n - p.n) : a0;
+}
+
+// split(s, sep) = strings.Split (topdown/strings.go:195-210): an array of the
+// pieces, each sharing the subject's bytes.  An empty separator splits into
+// runes (ASCII subjects only; others go to the CPU).
+__device__ uint64_t bi_split(Lane& L, uint64_t a0, uint64_t a1) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return UND; }
+  SView s = sview(L, a0), d = sview(L, a1);
+  uint32_t n = 1;
+  if (d.n == 0) {
+    for (uint32_t i = 0; i < s.n; ++i) if ((unsigned char)s.p[i] >= 0x80) { lane_fallback(L, FB_UNICODE); return UND; }
+    n = s.n;
+  } else {
+    for (uint32_t i = 0; i + d.n <= s.n;) { if (bytes_at(s, i, d)) { ++n; i += d.n; } else ++i; }
+  }
+  uint64_t l = list_new(L, LK_ARR, n);
+  if (vtag(l) != V_LIST) return UND;
+  uint32_t o = list_off(l);
+  if (d.n == 0) {
+    for (uint32_t i = 0; i < n; ++i) L.H[o + 2 + i] = str_sub(L, a0, s, i, 1);
+  } else {
+    uint32_t k = 0, st = 0;
+    for (uint32_t i = 0; i + d.n <= s.n;) {
+      if (bytes_at(s, i, d)) { L.H[o + 2 + k++] = str_sub(L, a0, s, st, i - st); i += d.n; st = i; } else ++i;
+    }
+    L.H[o + 2 + k++] = str_sub(L, a0, s, st, s.n - st);
+  }
+  L.H[o] = n;
+  return l;
+}
+
+// lower / upper = strings.ToLower / ToUpper: ASCII subjects on the GPU
+__device__ uint64_t bi_case(Lane& L, uint32_t id, uint64_t a0) {
+  if (!is_strv(a0)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  SView s = sview(L, a0);
+  bool change = false;
+  for (uint32_t i = 0; i < s.n; ++i) {
+    unsigned char ch = (unsigned char)s.p[i];
+    if (ch >= 0x80) { lane_fallback(L, FB_UNICODE); return mkv(V_UNDEF, 0); }
+    change |= id == BI_LOWER ? (ch >= 'A' && ch <= 'Z') : (ch >= 'a' && ch <= 'z');
+  }
+  if (!change) return a0;
+  if (L.bp + s.n > BCAP) { lane_fallback(L, FB_MSG_LEN); return mkv(V_UNDEF, 0); }
+  uint32_t st = L.bp;
+  for (uint32_t i = 0; i < s.n; ++i) {
+    char ch = s.p[i];
+    if (id == BI_LOWER && ch >= 'A' && ch <= 'Z') ch = (char)(ch + 32);
+    if (id == BI_UPPER && ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+    L.B[L.bp++] = ch;
+  }
+  return mkhstr(st, s.n);
+}
+
+// concat(delim, array|set) = strings.Join (topdown/strings.go:48-83); non-string
+// elements and other collections are operand errors
+__device__ uint64_t bi_concat(Lane& L, uint64_t a0, uint64_t a1) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  int cls = tclass(a1);
+  if (!is_strv(a0) || (cls != 7 && cls != 9)) { lane_error(L); return UND; }
+  SView d = sview(L, a0);
+  uint32_t n = coll_len(L, a1), st = L.bp;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t k, v;
+    coll_at(L, a1, i, k, v);
+    if (!is_strv(v)) { L.bp = st; lane_error(L); return UND; }
+    SView e = sview(L, v);
+    if (L.bp + e.n + d.n > BCAP) { lane_fallback(L, FB_MSG_LEN); return UND; }
+    if (i) for (uint32_t j = 0; j < d.n; ++j) L.B[L.bp++] = d.p[j];
+    for (uint32_t j = 0; j < e.n; ++j) L.B[L.bp++] = e.p[j];
+  }
+  if (L.bp == st) return mkv(V_STR, 0);
+  return mkhstr(st, L.bp - st);
+}
+
+// indexof(s, sub) = strings.Index: byte offset or -1 (topdown/strings.go:85-98)
+__device__ uint64_t bi_indexof(Lane& L, uint64_t a0, uint64_t a1) {
+  if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
+  SView s = sview(L, a0), p = sview(L, a1);
+  for (uint32_t o = 0; o + p.n <= s.n; ++o) if (bytes_at(s, o, p)) return mkint(o);
+  return mkint(-1);
+}
+
 __device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
   switch (id) {
     case BI_COUNT: return bi_count(L, a[0]);
@@ -1140,6 +1265,12 @@ __device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
     case BI_IS_ARRAY: return mkv(V_BOOL, tclass(a[0]) == 7);
     case BI_IS_OBJECT: return mkv(V_BOOL, tclass(a[0]) == 8);
     case BI_IS_SET: return mkv(V_BOOL, tclass(a[0]) == 9);
+    case BI_TRIM: return bi_trim(L, a[0], a[1]);
+    case BI_TRIM_PREFIX: case BI_TRIM_SUFFIX: return bi_trim_fix(L, id, a[0], a[1]);
+    case BI_SPLIT: return bi_split(L, a[0], a[1]);
+    case BI_LOWER: case BI_UPPER: return bi_case(L, id, a[0]);
+    case BI_CONCAT: return bi_concat(L, a[0], a[1]);
+    case BI_INDEXOF: return bi_indexof(L, a[0], a[1]);
     default: break;
   }
   lane_fallback(L, FB_UNSUPPORTED);

@@ -665,3 +665,245 @@ def gen_config4_json(n, seed=1234, start=0, n_namespaces=1000):
             continue
         nss.append(ns_json[ns])
     return objs, nss
+
+
+# -- config 5: admission-webhook micro-batch over the PSP policies of
+# BenchmarkValidationHandler (pkg/webhook/policy_benchmark_test.go:233-329;
+# templates/constraints/pods from pkg/webhook/testdata/psp-all-violations/)
+PSP_HOST_FILESYSTEM = _tmpl("K8sPSPHostFilesystem", """package k8spsphostfilesystem
+
+violation[{"msg": msg, "details": {}}] {
+	volume := input_hostpath_volumes[_]
+	not input_hostpath_allowed(volume)
+	msg := sprintf("HostPath volume %v is not allowed, pod: %v. Allowed path: %v", [volume, input.review.object.metadata.name, input.parameters.allowedHostPaths])
+}
+
+input_hostpath_allowed(volume) {
+	input.parameters.allowedHostPaths == []
+}
+
+input_hostpath_allowed(volume) {
+	allowedHostPath := input.parameters.allowedHostPaths[_]
+	path_matches(allowedHostPath.pathPrefix, volume.hostPath.path)
+	not allowedHostPath.readOnly == true
+}
+
+input_hostpath_allowed(volume) {
+	allowedHostPath := input.parameters.allowedHostPaths[_]
+	path_matches(allowedHostPath.pathPrefix, volume.hostPath.path)
+	allowedHostPath.readOnly
+	not writeable_input_volume_mounts(volume.name)
+}
+
+writeable_input_volume_mounts(volume_name) {
+	container := input_containers[_]
+	mount := container.volumeMounts[_]
+	mount.name == volume_name
+	not mount.readOnly
+}
+
+path_matches(prefix, path) {
+	a := split(trim(prefix, "/"), "/")
+	b := split(trim(path, "/"), "/")
+	prefix_matches(a, b)
+}
+
+prefix_matches(a, b) {
+	count(a) <= count(b)
+	not any_not_equal_upto(a, b, count(a))
+}
+
+any_not_equal_upto(a, b, n) {
+	a[i] != b[i]
+	i < n
+}
+
+input_hostpath_volumes[v] {
+	v := input.review.object.spec.volumes[_]
+	has_field(v, "hostPath")
+}
+
+has_field(object, field) = true {
+	object[field]
+}
+
+input_containers[c] {
+	c := input.review.object.spec.containers[_]
+}
+
+input_containers[c] {
+	c := input.review.object.spec.initContainers[_]
+}
+""")
+
+PSP_HOST_NAMESPACE = _tmpl("K8sPSPHostNamespace", """package k8spsphostnamespace
+
+violation[{"msg": msg, "details": {}}] {
+	input_share_hostnamespace(input.review.object)
+	msg := sprintf("Sharing the host namespace is not allowed: %v", [input.review.object.metadata.name])
+}
+
+input_share_hostnamespace(o) {
+	o.spec.hostPID
+}
+
+input_share_hostnamespace(o) {
+	o.spec.hostIPC
+}
+""")
+
+PSP_HOST_NETWORK_PORTS = _tmpl("K8sPSPHostNetworkingPorts", """package k8spsphostnetworkingports
+
+violation[{"msg": msg, "details": {}}] {
+	input_share_hostnetwork(input.review.object)
+	msg := sprintf("The specified hostNetwork and hostPort are not allowed, pod: %v. Allowed values: %v", [input.review.object.metadata.name, input.parameters])
+}
+
+input_share_hostnetwork(o) {
+	not input.parameters.hostNetwork
+	o.spec.hostNetwork
+}
+
+input_share_hostnetwork(o) {
+	hostPort := input_containers[_].ports[_].hostPort
+	hostPort < input.parameters.min
+}
+
+input_share_hostnetwork(o) {
+	hostPort := input_containers[_].ports[_].hostPort
+	hostPort > input.parameters.max
+}
+
+input_containers[c] {
+	c := input.review.object.spec.containers[_]
+}
+
+input_containers[c] {
+	c := input.review.object.spec.initContainers[_]
+}
+""")
+
+PSP_PRIVILEGED = _tmpl("K8sPSPPrivilegedContainer", """package k8spspprivileged
+
+violation[{"msg": msg, "details": {}}] {
+	c := input_containers[_]
+	c.securityContext.privileged
+	msg := sprintf("Privileged container is not allowed: %v, securityContext: %v", [c.name, c.securityContext])
+}
+
+input_containers[c] {
+	c := input.review.object.spec.containers[_]
+}
+
+input_containers[c] {
+	c := input.review.object.spec.initContainers[_]
+}
+""")
+
+PSP_VOLUME_TYPES = _tmpl("K8sPSPVolumeTypes", """package k8spspvolumetypes
+
+violation[{"msg": msg, "details": {}}] {
+	volume_fields := {x | input.review.object.spec.volumes[_][x]; x != "name"}
+	not input_volume_type_allowed(volume_fields)
+	msg := sprintf("One of the volume types %v is not allowed, pod: %v. Allowed volume types: %v", [volume_fields, input.review.object.metadata.name, input.parameters.volumes])
+}
+
+input_volume_type_allowed(volume_fields) {
+	input.parameters.volumes[_] == "*"
+}
+
+input_volume_type_allowed(volume_fields) {
+	allowed_set := {x | x = input.parameters.volumes[_]}
+	test := volume_fields - allowed_set
+	count(test) == 0
+}
+""")
+
+PSP_TEMPLATES = [PSP_HOST_FILESYSTEM, PSP_HOST_NAMESPACE, PSP_HOST_NETWORK_PORTS, PSP_PRIVILEGED, PSP_VOLUME_TYPES]
+
+_POD_MATCH = {"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}]}
+PSP_CONSTRAINTS = [
+    constraint("K8sPSPHostFilesystem", "psp-host-filesystem", match=_POD_MATCH,
+               parameters={"allowedHostPaths": [{"readOnly": True, "pathPrefix": "/foo"}]}),
+    constraint("K8sPSPHostNamespace", "psp-host-namespace", match=_POD_MATCH),
+    constraint("K8sPSPHostNetworkingPorts", "psp-host-network-ports", match=_POD_MATCH,
+               parameters={"hostNetwork": True, "min": 80, "max": 9000}),
+    constraint("K8sPSPPrivilegedContainer", "psp-privileged-container", match=_POD_MATCH),
+    constraint("K8sPSPVolumeTypes", "psp-volume-types", match=_POD_MATCH,
+               parameters={"volumes": ["configMap", "emptyDir", "projected", "secret", "downwardAPI",
+                                       "persistentVolumeClaim", "flexVolume"]}),
+]
+
+
+def _psp_pod(name, spec):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "labels": {"app": name}}, "spec": spec}
+
+
+PSP_PODS = [
+    _psp_pod("nginx-host-filesystem", {
+        "containers": [{"name": "nginx", "image": "nginx",
+                        "volumeMounts": [{"mountPath": "/cache", "name": "cache-volume", "readOnly": True}]}],
+        "volumes": [{"name": "cache-volume", "hostPath": {"path": "/tmp"}}]}),
+    _psp_pod("nginx-host-namespace", {"hostPID": True, "hostIPC": True,
+                                      "containers": [{"name": "nginx", "image": "nginx"}]}),
+    _psp_pod("nginx-host-networking-ports", {
+        "hostNetwork": True,
+        "containers": [{"name": "nginx", "image": "nginx", "ports": [{"containerPort": 9001, "hostPort": 9001}]}]}),
+    _psp_pod("nginx-privileged", {"containers": [{"name": "nginx", "image": "nginx",
+                                                  "securityContext": {"privileged": True}}]}),
+    _psp_pod("nginx-volume-types", {
+        "containers": [{"name": "nginx", "image": "nginx", "volumeMounts": [{"mountPath": "/cache", "name": "cache-volume"}]},
+                       {"name": "nginx2", "image": "nginx", "volumeMounts": [{"mountPath": "/cache2", "name": "demo-vol"}]}],
+        "volumes": [{"name": "cache-volume", "hostPath": {"path": "/tmp"}}, {"name": "demo-vol", "emptyDir": {}}]}),
+]
+
+
+def config5(load=5, seed=99):
+    """The PSP templates with `load` constraints: generateConstraints
+    (policy_benchmark_test.go:176-186) cycles through the 5 constraints, every
+    copy after the first round under a fresh random 10-letter name."""
+    rng = random.Random(seed)
+    cs = []
+    names = [c["metadata"]["name"] for c in PSP_CONSTRAINTS]
+    for i in range(load):
+        base = PSP_CONSTRAINTS[i % len(PSP_CONSTRAINTS)]
+        c = json.loads(json.dumps(base))
+        c["metadata"]["name"] = names[i % len(names)]
+        names[i % len(names)] = "".join(rng.choice("abcdefghijklmnopqrstuvwxyz") for _ in range(10))
+        cs.append(c)
+    return list(PSP_TEMPLATES), cs
+
+
+def admission_request(n, rng):
+    """createAdmissionRequests (policy_benchmark_test.go:197-231): the n-th
+    UPDATE request over PSP pod n % 5, object at resourceVersion 2 and
+    oldObject at 1, as admission/v1beta1 AdmissionRequest JSON (field order and
+    omitempty of k8s.io/api/admission/v1beta1/types.go:45-112)."""
+    pod = json.loads(json.dumps(PSP_PODS[n % len(PSP_PODS)]))
+    name, namespace = "res-name-%d" % n, "res-namespace-%d" % n
+    pod["metadata"]["name"] = name
+    pod["metadata"]["namespace"] = namespace
+    old = json.loads(json.dumps(pod))
+    pod["metadata"]["resourceVersion"] = "2"
+    old["metadata"]["resourceVersion"] = "1"
+    uid = "%08x-%04x-4%03x-%04x-%012x" % (rng.getrandbits(32), rng.getrandbits(16), rng.getrandbits(12),
+                                          0x8000 | rng.getrandbits(14), rng.getrandbits(48))
+    gvk = {"group": "", "version": "v1", "kind": "Pod"}
+    gvr = {"group": "", "version": "v1", "resource": "pods"}
+    return {"uid": uid, "kind": gvk, "resource": gvr, "requestKind": dict(gvk), "requestResource": dict(gvr),
+            "name": name, "namespace": namespace, "operation": "UPDATE",
+            "userInfo": {"username": "res-creator", "uid": "uid", "groups": ["res-creator-group"],
+                         "extra": {"extraKey": ["value1", "value2"]}},
+            "object": pod, "oldObject": old, "dryRun": False, "options": None}
+
+
+def gen_admission_inputs(n, seed=99, start=0):
+    """n Query inputs {"review": gkReview} for AugmentedReview{request, ns}
+    (policy.go:363-387 with the benchmark's fake namespace getter), JSON text."""
+    from .webhook import namespace_object, review_input
+    rng = random.Random(seed * 7919 + start)
+    out = []
+    for i in range(start, start + n):
+        req = admission_request(i, rng)
+        out.append(dumps(review_input(req, namespace_object(req["namespace"]))))
+    return out

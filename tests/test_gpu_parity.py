@@ -350,3 +350,62 @@ def test_config4_mixed_kinds_fifty_constraints():
     _assert_clean(rep)
     assert rep.violations > 500
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
+
+
+def test_config5_webhook_micro_batch():
+    """Config 5: 256 UPDATE AdmissionReviews (object + oldObject) per
+    gk_query_batch launch over the PSP policies at constraint load 50."""
+    from gkgpu.webhook import DENIED, handle_batch
+    ts, cs = W.config5(50)
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
+    od = oracle_for(ts, cs)
+    ins = W.gen_admission_inputs(256, seed=99)
+    res = drv.query_batch(ins)
+    rep = compare(od, [json.loads(s)["review"] for s in ins], res)
+    _assert_clean(rep)
+    assert rep.violations >= 256 * 10
+    resp = handle_batch(drv, ins)
+    assert all(r.code == DENIED for r in resp)
+
+
+STR_BUILTINS = W._tmpl("K8sStrBuiltins", """package k8sstrbuiltins
+
+violation[{"msg": msg}] {
+	v := input.review.object.metadata.labels[k]
+	parts := split(v, input.parameters.sep)
+	t := trim(v, "-._")
+	msg := sprintf("%v|%v|%v|%v|%v|%v|%v|%v|%v", [k, parts, t, lower(v), upper(k), concat("+", parts), indexof(v, "a"), trim_suffix(trim_prefix(v, "x"), "z"), count(parts)])
+}
+""")
+
+
+def test_string_builtins_trim_split_case_concat_indexof():
+    """trim / split / lower / upper / concat / indexof / trim_prefix /
+    trim_suffix (topdown/strings.go) on adversarial label values; non-ASCII
+    subjects of lower/upper and empty-separator splits go to the CPU."""
+    import random
+    rng = random.Random(11)
+    vals = ["", "-", "--a--", "a.b.c", "xAbz", "x", "z", "xz", "a..b.", ".a.", "AbC-d_e", "...", "Héllo", "é",
+            "ab.ab.ab", "-_.x._-", "aaaa"]
+    objs = []
+    for i in range(300):
+        labels = {"k%d" % j: rng.choice(vals) for j in range(rng.randint(0, 4))}
+        if rng.random() < 0.3:
+            labels["Mixed-Key"] = rng.choice(vals)
+        objs.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cm-%d" % i, "namespace": "ns",
+                                                                         "labels": labels}})
+    ns = W.namespace_obj("ns")
+    cs = [W.constraint("K8sStrBuiltins", "dot", parameters={"sep": "."}),
+          W.constraint("K8sStrBuiltins", "empty-sep", parameters={"sep": ""}),
+          W.constraint("K8sStrBuiltins", "ab", parameters={"sep": "ab"})]
+    drv = Driver()
+    rep, _ = run_objects(drv, [STR_BUILTINS], cs, objs, [ns] * len(objs))
+    _assert_backend(drv, ["K8sStrBuiltins"])
+    _assert_clean(rep, max_fallback_frac=0.6)
+    assert rep.violations > 500
