@@ -201,6 +201,7 @@ static_assert(sizeof(Viol) == 32, "Viol layout");
 
 constexpr uint32_t RULE_AUTOREJECT = 0xffffu;
 constexpr uint32_t MEMO_SLOTS = 16;  // memoized function call sites per template (per lane)
+constexpr uint32_t GMEMO_ENTRIES = 1u << 15;  // cross-lane memo table of a template launch (32 B entries)
 
 // ------------------------------------------------------------------ launch
 // Kernel arguments of one audit launch (passed by value; shared by the bytecode
@@ -238,6 +239,8 @@ struct DevArgs {
   uint32_t* rreason;          // per review fallback reason (diagnostic)
   unsigned int* pchist;       // optional (GKGPU_PROFILE=2): executions per bytecode pc
   unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]
+  uint64_t* gmemo;            // template kernels: cross-lane memo of pure function calls (4 words per entry)
+  uint32_t gmemo_mask;        // entries - 1 (power of two)
 };
 
 }  // namespace gk

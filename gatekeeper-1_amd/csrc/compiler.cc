@@ -839,7 +839,7 @@ class Comp {
           if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
           for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
           --inline_depth_;
-          if (slot >= 0) emit(OP_MEMO_PUT, (uint16_t)out, (uint16_t)regs[0], k1, 0, (uint32_t)slot);
+          if (slot >= 0) emit(OP_MEMO_PUT, (uint16_t)out, (uint16_t)regs[0], k1, pure_func(rules) ? 1u : 0u, (uint32_t)slot);
           place(Lhit);
         }
         emit_jmp(OP_JUNDEF, out, f);
@@ -904,6 +904,59 @@ class Comp {
     } else {
       k(d, f);
     }
+  }
+
+  // A function is pure when nothing under it refers to input, data, a rule of
+  // the package or an import: its value is then a function of its arguments
+  // alone, the same in every lane, so template kernels share it across lanes
+  // (devrt.h gm_get / gm_put; flagged by x = 1 on its OP_MEMO_PUT).
+  std::map<const Rule*, int> pure_;  // 1 pure, 2 impure, 3 being checked
+  bool pure_func(const std::vector<std::shared_ptr<Rule>>& rules) {
+    for (auto& r : rules) {
+      auto it = pure_.find(r.get());
+      if (it != pure_.end()) {
+        if (it->second != 1) return false;
+        continue;
+      }
+      pure_[r.get()] = 3;
+      Env env;
+      env.mod = r->mod;
+      bool ok = r->kind == Rule::FUNC && !r->is_else;
+      for (auto& a : r->args) ok = ok && pure_term(a, &env);
+      ok = ok && pure_term(r->value, &env) && pure_body(r->body, &env);
+      pure_[r.get()] = ok ? 1 : 2;
+      if (!ok) return false;
+    }
+    return true;
+  }
+  bool pure_body(const std::vector<ExprP>& body, Env* env) {
+    for (auto& e : body) {
+      if (!e->withs.empty()) return false;
+      for (auto& t : e->terms) if (!pure_term(t, env)) return false;
+    }
+    return true;
+  }
+  bool pure_term(const TermP& t, Env* env) {
+    if (!t) return true;
+    switch (t->k) {
+      case T_SCALAR: return true;
+      case T_VAR: return !is_global(env, t->s);
+      case T_CALL: {
+        if (t->op.empty()) return false;
+        auto fr = resolve_func(t->op, env);
+        if (!fr.empty()) {
+          if (!pure_func(fr)) return false;
+        } else if (t->op[0] == "input" || t->op[0] == "data" || is_global(env, t->op[0])) {
+          return false;
+        }
+        for (auto& a : t->items) if (!pure_term(a, env)) return false;
+        return true;
+      }
+      default: break;
+    }
+    if (!pure_term(t->head, env) || !pure_term(t->key, env) || !pure_term(t->value, env)) return false;
+    for (auto& a : t->items) if (!pure_term(a, env)) return false;
+    return pure_body(t->body, env);
   }
 
   // One memo slot per (function, statement-form) per template; see devrt.h

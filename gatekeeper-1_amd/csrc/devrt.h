@@ -1488,6 +1488,49 @@ __device__ __forceinline__ bool memo_stable(uint64_t v) {
   return t != V_LIST && t != V_HSTR && t != V_BFN && t != V_FMT;
 }
 
+// Cross-lane memo of pure function calls (compiler.cc pure_func: no input,
+// data or rule references anywhere under the function).  Such a call's value
+// depends only on its heap-free arguments, so every lane of the launch may
+// share it: canonify_mem("1Gi") is computed by the first lanes that meet it and
+// read by the rest.  Entries are (k0, k1, value, check) with check a hash of
+// (call site, key, value); a reader accepts an entry only if key and check
+// match, so torn or racing writes, stale cache lines and collisions all read
+// as misses (the lane then evaluates the call itself).  No atomics or fences:
+// equal keys always carry equal values.  Cleared before each launch.
+__device__ __forceinline__ uint64_t gm_mix(uint64_t x) {
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull; x ^= x >> 27; x *= 0x94d049bb133111ebull; x ^= x >> 31;
+  return x;
+}
+__device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
+  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull));
+}
+__device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
+// keys are scalars: a document node is met by one lane only and would just
+// evict shared entries
+__device__ __forceinline__ bool gm_key(uint64_t v) { return vtag(v) != V_NODE && memo_stable(v); }
+
+__device__ __forceinline__ bool gm_get(uint32_t site, uint64_t k0, uint64_t k1, uint64_t& out) {
+  if (!gk_args.gmemo || !gm_key(k0) || !gm_key(k1)) return false;
+  uint64_t h = gm_hash(site, k0, k1);
+  uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
+#pragma unroll
+  for (uint32_t p = 0; p < 2; ++p) {
+    const uint64_t* e = gk_args.gmemo + 4 * (i ^ p);
+    uint64_t a = e[0], b = e[1], v = e[2], c = e[3];
+    if (a == k0 && b == k1 && c == gm_check(h, v)) { out = v; return true; }
+  }
+  return false;
+}
+
+__device__ __forceinline__ void gm_put(const Lane& L, uint32_t site, uint64_t k0, uint64_t k1, uint64_t v) {
+  if (L.fail || !gk_args.gmemo || !gm_key(k0) || !gm_key(k1) || !memo_stable(v)) return;
+  uint64_t h = gm_hash(site, k0, k1);
+  uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
+  if (gk_args.gmemo[4 * i + 3] != 0) i ^= 1;
+  uint64_t* e = gk_args.gmemo + 4 * i;
+  e[0] = k0; e[1] = k1; e[2] = v; e[3] = gm_check(h, v);
+}
+
 // m: message register, d: details register (undefined when absent)
 __device__ __forceinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   if (vtag(m) == V_FMT) {

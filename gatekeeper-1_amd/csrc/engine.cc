@@ -158,7 +158,8 @@ struct gk_engine {
   std::vector<uint32_t> dfa_keys, dfa_meta;
   // device mirrors
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
-      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist;
+      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist,
+      d_gmemo;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
   std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
   uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
@@ -943,6 +944,13 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       const DevArgs& a = argv[i];
       int lr;
       if (plan[i].fn) {
+        // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
+        static const bool gm_on = !getenv("GKGPU_GMEMO") || atoi(getenv("GKGPU_GMEMO")) != 0;  // A/B switch
+        if (gm_on && e->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
+          argv[i].gmemo = (uint64_t*)e->d_gmemo.p;
+          argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
+          hipMemsetAsync(e->d_gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, e->stream);
+        }
         uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
         uint32_t blocks = (uint32_t)((threads + 255) / 256);
         lr = (int)hipMemcpyHtoDAsync(plan[i].args, (void*)&a, sizeof(a), e->stream);
@@ -1100,7 +1108,7 @@ void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
                   &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
-                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist})
+                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo})
     b->free_();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   for (hipEvent_t x : e->events) hipEventDestroy(x);

@@ -220,7 +220,7 @@ struct Gen {
 // on to the end yields the same lane outcome at no cost to passing lanes.
 Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   const uint32_t b0 = p.code_off, b1 = p.code_off + p.code_len;
-  std::set<uint32_t> labels, memo, memo2;
+  std::set<uint32_t> labels, memo, memo2, gslots;
   std::map<uint32_t, int> memo_sites;
   for (uint32_t pc = b0; pc < b1; ++pc) {
     const Ins& in = bank.code[pc];
@@ -232,6 +232,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
     }
     if (in.op == OP_MEMO_GET || in.op == OP_MEMO_PUT) memo.insert(in.y);
     if (in.op == OP_MEMO_GET && ++memo_sites[in.y] == 2) memo2.insert(in.y);
+    if (in.op == OP_MEMO_PUT && in.x == 1) gslots.insert(in.y);  // pure function: cross-lane memo
   }
   FmtFlow F = fmt_flow(p, bank);
   Gen g;
@@ -359,6 +360,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (memo2.count(in.y))
           o << " if (mokb_" << m << " && mkb0_" << m << " == " << b << " && mkb1_" << m << " == " << k1 << ") { " << a
             << " = mvb_" << m << "; goto " << x << "; }";
+        if (gslots.count(in.y)) o << " if (gm_get(" << m << "u, " << b << ", " << k1 << ", " << a << ")) goto " << x << ";";
         break;
       }
       case OP_MEMO_PUT: {
@@ -369,6 +371,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
             << "; mokb_" << m << " = mok_" << m << "; ";
         o << "mk0_" << m << " = " << b << "; mk1_" << m << " = " << k1 << "; mv_" << m << " = " << a << "; mok_" << m
           << " = true; }";
+        if (gslots.count(in.y)) o << " gm_put(L, " << m << "u, " << b << ", " << k1 << ", " << a << ");";
         break;
       }
       case OP_TABLE: {
