@@ -26,9 +26,15 @@ __constant__ gk::DevArgs gk_args;
 
 namespace gk {
 
-constexpr int HCAP = 128;   // heap words per lane (lists, big floats)
-constexpr int MAXLOOP = 16; // loop nesting levels with per-iteration heap reclamation
-constexpr int BCAP = 4096;  // byte buffer per lane (computed strings, staged messages)
+#ifndef GK_HCAP
+#define GK_HCAP 128
+#endif
+#ifndef GK_BCAP
+#define GK_BCAP 4096
+#endif
+constexpr int HCAP = GK_HCAP;  // heap words per lane (lists, big floats)
+constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
+constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged messages)
 constexpr int EMCAP = 32;   // staged violation tuples per lane
 
 

@@ -446,8 +446,18 @@ std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
 std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
   Gen g = generate(p, bank, st);
   std::ostringstream o;
-  o << "// generated by jit.cc from template bytecode (" << p.code_len << " instructions)\n"
-    << "#include \"devrt.h\"\n"
+  o << "// generated by jit.cc from template bytecode (" << p.code_len << " instructions)\n";
+  if (const char* pre = getenv("GKGPU_JIT_PRE")) {  // diagnostics: e.g. "GK_BCAP=1024,GK_HCAP=64"
+    std::string d = pre;
+    for (size_t i = 0, j; i < d.size(); i = j + 1) {
+      j = d.find(',', i);
+      if (j == std::string::npos) j = d.size();
+      std::string kv = d.substr(i, j - i);
+      size_t eq = kv.find('=');
+      if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
+    }
+  }
+  o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre
     << "__device__ void " << name << "_pred(Lane& L, uint64_t review, uint64_t params) {\n"

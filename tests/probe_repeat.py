@@ -27,4 +27,4 @@ for i in range(12):
     t0 = time.perf_counter()
     r = b.eval(decode=False, light=True)
     wall = (time.perf_counter() - t0) * 1e3
-    print("step %2d wall %.2f ms" % (i, wall), [(k, round(ms, 2)) for k, ms, n in r.launches], flush=True)
+    print("step %2d wall %.2f ms" % (i, wall), [(k, round(ms, 2)) for k, ms, n in r.launches], "tuples", r.device_tuples, "flagged", r.n_fallbacks + r.n_errors, flush=True)
