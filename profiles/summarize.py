@@ -51,14 +51,14 @@ def main():
     kt = bench["config"]["kernel_templates"]
     hdr = ("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0\n"
            "# (config2, %d pods, %d constraints); bench HIP-event avg of the dominant kernel %s: %.3f ms\n"
-           % (tb["config"]["pods_per_gpu"], tb["config"]["constraints"], tb["roofline"]["kernel"],
+           % (tb["config"]["resources_per_gpu"], tb["config"]["constraints"], tb["roofline"]["kernel"],
               tb["roofline"]["kernel_ms_avg"]))
     for k, kind in kt.items():
         hdr += "# %s = %s\n" % (k, kind)
     open(os.path.join(HERE, "%s_kernel_stats.txt" % rnd), "w").write(hdr + txt)
     fetch = counter(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
     write = counter(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
-    out = {"pods": bench["config"]["pods_per_gpu"], "constraints": bench["config"]["constraints"],
+    out = {"pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
            "note": "FETCH_SIZE x2 (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE, median per dispatch",
            "hbm_bytes_per_launch": {}, "fetch_bytes_x2": {}, "write_bytes": {}}
     for k, kind in kt.items():
