@@ -241,6 +241,11 @@ struct DevArgs {
   unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]
   uint64_t* gmemo;            // template kernels: cross-lane memo of pure function calls (4 words per entry)
   uint32_t gmemo_mask;        // entries - 1 (power of two)
+  uint64_t* frec;             // optional: per output tuple, a deferred-message record
+                              // (FREC_WORDS words) formatted by the format pass
 };
+// deferred-message record: w[0] = fidx | nargs << 24 | FREC_LIVE, w[1..nargs] = args
+constexpr uint32_t FREC_WORDS = 8;
+constexpr uint64_t FREC_LIVE = 1ull << 63;
 
 }  // namespace gk

@@ -411,7 +411,7 @@ __device__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
 }
 
 // ------------------------------------------------------------------ get
-__device__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
+__device__ __noinline__ uint64_t vget_slow(Lane& L, uint64_t c, uint64_t key) {
   uint32_t t = vtag(c);
   if (t == V_NODE) {
     const Node& n = gk_args.nodes[(uint32_t)vpay(c)];
@@ -455,6 +455,30 @@ __device__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
     return mkv(V_UNDEF, 0);
   }
   return mkv(V_UNDEF, 0);
+}
+// Inlined fast path of vget for the common document lookups (object member by
+// interned key, array element by small int).  Everything else, including
+// fallback-flagged nodes, goes through vget_slow: an out-of-line call costs
+// the caller a save/restore of its live registers in scratch.
+__device__ __forceinline__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
+  if (vtag(c) == V_NODE) {
+    const Node n = gk_args.nodes[(uint32_t)vpay(c)];
+    if (!(n.flags & 1)) {
+      uint32_t kt = vtag(key);
+      if (n.type == NT_OBJ && kt == V_STR) {
+        uint32_t id = (uint32_t)vpay(key);
+        for (uint32_t i = 0; i < n.n; ++i)
+          if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
+        return mkv(V_UNDEF, 0);
+      }
+      if (n.type == NT_ARR && kt == V_INT) {
+        int64_t i = intof(key);
+        if (i < 0 || i >= n.n) return mkv(V_UNDEF, 0);
+        return nodeval(n.first + (uint32_t)i);
+      }
+    }
+  }
+  return vget_slow(L, c, key);
 }
 
 // ------------------------------------------------------------------ printing
@@ -969,16 +993,30 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
   for (uint32_t i = 0; i < nt; ++i) {
     uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = dw & 0x7fffu, o = L.em_off[i];
     GOut g{(uint8_t*)gk_args.bytes, bb, bb, 0, false};
-    if (dw & 0x8000u) {
+    if ((dw & 0x8000u) && gk_args.frec) {
+      // deferred message: hand the record to the format pass (gk_format_kernel),
+      // which formats it into [bb, bb + ml) one lane per tuple; only the details
+      // bytes are written here
+      const uint64_t* rec = (const uint64_t*)(L.B + o);
+      uint32_t na = (uint32_t)rec[0] >> 24;
+      uint64_t* w = gk_args.frec + (uint64_t)(bt + i) * FREC_WORDS;
+      w[0] = rec[0] | FREC_LIVE;
+      for (uint32_t j = 0; j < na; ++j) w[1 + j] = rec[1 + j];
+      GOut gd{(uint8_t*)gk_args.bytes, bb + ml, bb + ml, 0, false};
+      puts_(gd, L.B + o + 8 * (1 + na), dl);
+      gd.finish();
+    } else if (dw & 0x8000u) {
       // deferred message (op_emit): record [fidx | nargs << 24, args...], then details
       const uint64_t* rec = (const uint64_t*)(L.B + o);
       uint32_t h = (uint32_t)rec[0], na = h >> 24;
       fmt_run(L, g, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
       puts_(g, L.B + o + 8 * (1 + na), dl);
+      g.finish();
     } else {
+      if (gk_args.frec) gk_args.frec[(uint64_t)(bt + i) * FREC_WORDS] = 0;
       puts_(g, L.B + o, ml + dl);
+      g.finish();
     }
-    g.finish();
     Viol v;
     v.review = r;
     v.constraint = c;
@@ -1417,7 +1455,20 @@ __device__ __forceinline__ bool op_iter_next(Lane& L, uint64_t coll, uint64_t& s
 
 __device__ __forceinline__ bool op_cmp(Lane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
   if (vtag(x) == V_UNDEF || vtag(y) == V_UNDEF) { out = mkv(V_UNDEF, 0); return true; }
-  int cr = vcmp(L, x, y);
+  int cr;
+  // inlined fast paths (exact ints, interned strings, booleans); the rest of
+  // ast.Compare is out of line in vcmp
+  uint32_t tx = vtag(x), ty = vtag(y);
+  if (tx == V_INT && ty == V_INT) {
+    int64_t a = intof(x), b = intof(y);
+    cr = a == b ? 0 : (a < b ? -1 : 1);
+  } else if ((tx == V_STR && ty == V_STR && x == y) || (tx == V_BOOL && ty == V_BOOL && x == y)) {
+    cr = 0;
+  } else if (tx == V_STR && ty == V_STR && (kind == CMP_EQ || kind == CMP_NE)) {
+    cr = 3;  // distinct interned ids: distinct bytes
+  } else {
+    cr = vcmp(L, x, y);
+  }
   if (cr == 2) return false;
   if (cr == 3 && kind != CMP_EQ && kind != CMP_NE) { lane_fallback(L, FB_DEEP_EQ); return false; }
   bool res = false;

@@ -25,6 +25,7 @@
 namespace gk {
 }
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
+extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream);
 extern "C" size_t gk_devargs_size();
 
 namespace gk {
@@ -159,7 +160,7 @@ struct gk_engine {
   // device mirrors
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
       d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist,
-      d_gmemo;
+      d_gmemo, d_frec;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
   std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
   uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
@@ -865,6 +866,9 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
   ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 4) &&
         e->d_counters.reserve(64 + 8 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
+  // deferred-message records for the format pass (GKGPU_FORMAT_PASS=0: format in the audit kernels)
+  const bool fpass = !getenv("GKGPU_FORMAT_PASS") || atoi(getenv("GKGPU_FORMAT_PASS")) != 0;
+  if (fpass && !e->d_frec.reserve(e->out_cap * FREC_WORDS * 8)) return fail(e, GK_EDEVICE, "device allocation failed");
   // launch plan: constraints grouped by template kernel (jit.cc); the bytecode
   // VM kernel takes every constraint whose template has no kernel / program
   ensure_jit(e, true);
@@ -930,7 +934,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     a.rflags = (uint32_t*)e->d_rflags.p;
     a.totals = (uint32_t*)e->d_totals.p;
     a.rreason = (uint32_t*)e->d_rreason.p;
-    while (e->events.size() < plan.size() + 1) {
+    a.frec = fpass ? (uint64_t*)e->d_frec.p : nullptr;
+    while (e->events.size() < plan.size() + 2) {
       hipEvent_t x;
       if (hipEventCreate(&x) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
       e->events.push_back(x);
@@ -945,7 +950,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       int lr;
       if (plan[i].fn) {
         // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
-        static const bool gm_on = !getenv("GKGPU_GMEMO") || atoi(getenv("GKGPU_GMEMO")) != 0;  // A/B switch
+        const bool gm_on = !getenv("GKGPU_GMEMO") || atoi(getenv("GKGPU_GMEMO")) != 0;  // A/B switch
         if (gm_on && e->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
           argv[i].gmemo = (uint64_t*)e->d_gmemo.p;
           argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
@@ -966,6 +971,12 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
     }
+    // format pass over the deferred messages of every launch above
+    if (fpass) {
+      int lr = gk_launch_format(&a, e->stream);
+      hipEventRecord(ev[plan.size() + 1], e->stream);
+      if (lr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)lr));
+    }
     if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
     res->launches.clear();
     std::vector<uint32_t> snap(2 * plan.size());
@@ -977,6 +988,12 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       uint32_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
       res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
+    if (fpass) {
+      float kms = 0;
+      hipEventElapsedTime(&kms, ev[plan.size()], ev[plan.size() + 1]);
+      res->ms[2] += kms;
+      res->launches.push_back({"gk_format_kernel", (double)kms, 0, 0, 0});
+    }
     auto t1 = Clock::now();
     // [0] tuples, [1] message bytes, [2] lanes that flagged their review (error/fallback)
     uint32_t counters[3];
@@ -984,7 +1001,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     if (counters[0] > e->out_cap || counters[1] > e->bytes_cap) {
       e->out_cap = std::max<size_t>(e->out_cap * 2, counters[0] + 1024);
       e->bytes_cap = std::max<size_t>(e->bytes_cap * 2, (size_t)counters[1] + 65536);
-      if (!e->d_out.reserve(e->out_cap * sizeof(Viol)) || !e->d_bytes.reserve(e->bytes_cap))
+      if (!e->d_out.reserve(e->out_cap * sizeof(Viol)) || !e->d_bytes.reserve(e->bytes_cap) ||
+          (fpass && !e->d_frec.reserve(e->out_cap * FREC_WORDS * 8)))
         return fail(e, GK_EDEVICE, "device allocation failed");
       continue;
     }
@@ -1108,7 +1126,7 @@ void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
                   &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
-                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo})
+                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo, &e->d_frec})
     b->free_();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   for (hipEvent_t x : e->events) hipEventDestroy(x);

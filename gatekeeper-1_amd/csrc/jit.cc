@@ -258,8 +258,10 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   // no initializers: the compiler writes every register before reading it (the
   // VM kernel relies on the same), and zero-initialising would make all of them
   // live from entry — register pressure, hence occupancy
+  const char* ji = getenv("GKGPU_JIT_INIT");  // diagnostics: 1 = registers start as undefined (0)
+  bool init = ji && atoi(ji) != 0;
   o << "  uint64_t ";
-  for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r);
+  for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r) << (init ? " = 0" : "");
   if (!p.nregs) o << "unused_";
   o << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)

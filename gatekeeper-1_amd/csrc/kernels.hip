@@ -88,9 +88,43 @@ __global__ void __launch_bounds__(256) audit_kernel() {
   });
 }
 
+// Format pass: one lane per output tuple whose message the audit kernels
+// deferred (devrt.h op_emit / flush_wave).  The arguments are heap-free values
+// (interned strings, slices, numbers, document nodes), so formatting reads only
+// the shared tables: the lane reference below is never dereferenced for them
+// (sview / coll_at touch a lane's buffers only for lane-heap values).  Lanes
+// write disjoint byte ranges [msg_off, msg_off + msg_len) reserved by the audit
+// kernel, consecutive tuples to consecutive ranges.
+__device__ Lane g_fmt_lane;
+
+__global__ void __launch_bounds__(256) gk_format_kernel() {
+  uint32_t n = gk_args.counters[0];
+  // an overflowed call left some reservations unwritten; the host retries it
+  if (n > gk_args.out_cap || gk_args.counters[1] > gk_args.bytes_cap) return;
+  Lane& L = g_fmt_lane;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t* w = gk_args.frec + (uint64_t)i * FREC_WORDS;
+    uint64_t h = w[0];
+    if (!(h & FREC_LIVE)) continue;
+    const Viol v = gk_args.out[i];
+    if ((uint64_t)v.msg_off + v.msg_len > gk_args.bytes_cap) continue;
+    GOut g{(uint8_t*)gk_args.bytes, v.msg_off, v.msg_off, 0, false};
+    fmt_run(L, g, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
+    g.finish();
+  }
+}
+
 }  // namespace gk
 
 // ------------------------------------------------------------------ host launch
+extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream) {
+  if (!a->frec) return 0;
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gk_args), a, sizeof(*a), 0, hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(4096), dim3(256), 0, stream);
+  return (int)hipGetLastError();
+}
+
 extern "C" int gk_launch_audit(const gk::DevArgs* a, hipStream_t stream) {
   uint64_t waves = (uint64_t)a->ntiles * a->nclist;
   uint64_t threads = waves * 64;

@@ -1,0 +1,60 @@
+"""GPU probe: decode the K8sContainerLimits violations of a staged Pod batch
+under several kernel builds (bytecode VM, template kernel at different
+waves/SIMD, cross-lane memo on/off) and diff each against the VM's."""
+import collections
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), os.path.join(ROOT, "tests")]
+import gkgpu  # noqa: E402
+from gkgpu import workloads as W  # noqa: E402
+from gkgpu.client import Client  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000
+only = sys.argv[2] if len(sys.argv) > 2 else "K8sContainerLimits"
+ts, cs = W.config2()
+cs = [c for c in cs if c["kind"] == only]
+objs, nss = W.gen_pods_json(N, seed=42, n_namespaces=1000)
+
+
+def run(jit, env):
+    for k in ("GKGPU_JIT_WPE", "GKGPU_GMEMO", "GKGPU_JIT_PRE", "GKGPU_FORMAT_PASS"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    d = gkgpu.Driver(jit=jit)
+    cl = Client(d)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    b = d.stage_objects(objs, nss)
+    out = []
+    for _ in range(2):
+        r = b.eval(decode=True)
+        out.append(collections.Counter((x.review, x.msg) for x in r.results))
+    b.free()
+    return out, r.timing_ms[2]
+
+
+base, ms = run(False, {"GKGPU_FORMAT_PASS": "0"})  # VM, messages formatted in-kernel
+print("vm: %d results, %.2f ms, repeat-equal %s" % (sum(base[0].values()), ms, base[0] == base[1]), flush=True)
+VARIANTS = [("wpe2", {}), ("wpe2_nomemo", {"GKGPU_GMEMO": "0"}), ("wpe3", {"GKGPU_JIT_WPE": "3"}),
+            ("wpe3_nomemo", {"GKGPU_JIT_WPE": "3", "GKGPU_GMEMO": "0"})]
+if len(sys.argv) > 3:  # e.g. '[["wpe3_small", {"GKGPU_JIT_WPE": "3", "GKGPU_JIT_PRE": "GK_BCAP=1024,GK_HCAP=64"}]]'
+    VARIANTS = json.loads(sys.argv[3])
+for name, env in VARIANTS:
+    got, ms = run(True, env)
+    for k, g in enumerate(got):
+        extra = g - base[0]
+        miss = base[0] - g
+        print("%s[%d]: %d results, %.2f ms, extra %d missing %d" % (name, k, sum(g.values()), ms, sum(extra.values()),
+                                                               sum(miss.values())), flush=True)
+        for (rv, msg), n in list(extra.items())[:4]:
+            pod = json.loads(objs[rv])
+            print("  EXTRA r%d x%d %r containers=%s" % (rv, n, msg, json.dumps(
+                [(c.get("name"), c.get("resources")) for c in pod["spec"].get("containers", []) +
+                 pod["spec"].get("initContainers", [])])))
+        for (rv, msg), n in list(miss.items())[:4]:
+            print("  MISSING r%d x%d %r" % (rv, n, msg))

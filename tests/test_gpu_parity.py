@@ -77,10 +77,24 @@ def test_config2_agilebank_pods():
     assert rep.violations > 5000
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
     kernels = {k for k, _, _ in res.launches}
+    assert "gk_format_kernel" in kernels, res.launches  # deferred messages formatted by the format pass
+    kernels.discard("gk_format_kernel")
     if _BACKEND["jit"]:
         assert kernels and all(k.startswith("gk_t_") for k in kernels), res.launches
     else:
         assert kernels == {"audit_kernel"}, res.launches
+
+
+def test_config2_in_kernel_formatting(monkeypatch):
+    """GKGPU_FORMAT_PASS=0: messages formatted inside the audit kernels (no format pass)."""
+    monkeypatch.setenv("GKGPU_FORMAT_PASS", "0")
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(600, seed=43, n_namespaces=50)
+    nss = [ns_objs[n] for n in ns_of]
+    rep, res = run_objects(Driver(), ts, cs, pods, nss)
+    _assert_clean(rep)
+    assert rep.violations > 1000
+    assert "gk_format_kernel" not in {k for k, _, _ in res.launches}
 
 
 def test_config2_agilebank_namespaces_regex():
@@ -409,3 +423,43 @@ def test_string_builtins_trim_split_case_concat_indexof():
     _assert_backend(drv, ["K8sStrBuiltins"])
     _assert_clean(rep, max_fallback_frac=0.6)
     assert rep.violations > 500
+
+
+def test_template_kernel_matches_vm_at_scale():
+    """Size-independent property at 200k Pods (config 2 policies): the template
+    kernels + format pass produce exactly the violation multiset of the bytecode
+    VM with in-kernel formatting, and repeat evaluations are identical."""
+    if not _BACKEND["jit"]:
+        pytest.skip("compares the two back ends; runs once")
+    import collections
+    import os
+    ts, cs = W.config2()
+    objs, nss = W.gen_pods_json(200_000, seed=42, n_namespaces=1000)
+
+    def sweep(jit, fpass):
+        old = os.environ.get("GKGPU_FORMAT_PASS")
+        os.environ["GKGPU_FORMAT_PASS"] = "1" if fpass else "0"
+        try:
+            d = gkgpu.Driver(jit=jit)
+            cl = Client(d)
+            for t in ts:
+                cl.add_template(t)
+            for c in cs:
+                cl.add_constraint(c)
+            b = d.stage_objects(objs, nss)
+            out = [collections.Counter((x.review, x.constraint_name, x.msg, x.details_json) for x in b.eval().results)
+                   for _ in range(2)]
+            b.free()
+            return out
+        finally:
+            if old is None:
+                os.environ.pop("GKGPU_FORMAT_PASS", None)
+            else:
+                os.environ["GKGPU_FORMAT_PASS"] = old
+
+    vm = sweep(False, False)
+    jit = sweep(True, True)
+    assert vm[0] == vm[1]
+    assert sum(vm[0].values()) > 500_000
+    assert jit[0] == jit[1]
+    assert jit[0] == vm[0]
