@@ -98,6 +98,17 @@ __device__ __forceinline__ void lane_error(Lane& L) {
   if (!L.fail) { L.fail = RF_ERROR; L.reason = 0; }
 }
 
+__device__ __forceinline__ uint64_t nodeval_of(const Node& n, uint32_t idx) {
+  switch (n.type) {
+    case NT_NULL: return mkv(V_NULL, 0);
+    case NT_FALSE: return mkv(V_BOOL, 0);
+    case NT_TRUE: return mkv(V_BOOL, 1);
+    case NT_NUM: return mkv(V_NUM, n.val);
+    case NT_STR: return mkv(V_STR, n.val);
+    case NT_ARR: case NT_OBJ: return mkv(V_NODE, idx);
+  }
+  return mkv(V_UNDEF, 0);
+}
 __device__ __forceinline__ uint64_t nodeval(uint32_t idx) {
   const Node& n = gk_args.nodes[idx];
   switch (n.type) {
@@ -245,7 +256,7 @@ __device__ BF bf_mul(const BF& a, const BF& b) {
 __device__ __forceinline__ uint32_t list_len(const Lane& L, uint64_t v) { return (uint32_t)L.H[list_off(v)]; }
 __device__ __forceinline__ uint64_t list_at(const Lane& L, uint64_t v, uint32_t i) { return L.H[list_off(v) + 2 + i]; }
 
-__device__ uint64_t list_new(Lane& L, uint32_t kind, uint32_t cap) {
+__device__ __forceinline__ uint64_t list_new(Lane& L, uint32_t kind, uint32_t cap) {
   if (L.hp + 2 + cap > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
   uint32_t o = L.hp;
   L.H[o] = 0;
@@ -383,7 +394,7 @@ __device__ bool list_contains(Lane& L, uint64_t l, uint64_t v) {
   return false;
 }
 // append (sets dedupe); may relocate the list to the heap top when full
-__device__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
+__device__ __noinline__ uint64_t list_add_slow(Lane& L, uint64_t l, uint64_t v) {
   if (vtag(l) != V_LIST) return l;
   if (list_kind(l) == LK_SET && list_contains(L, l, v)) return l;
   uint32_t o = list_off(l);
@@ -408,6 +419,20 @@ __device__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
   L.H[o + 2 + n] = v;
   L.H[o] = n + 1;
   return l;
+}
+// append fast path (array / object list with room), inlined: AMDGPU calls
+// save and restore the caller's live registers in scratch
+__device__ __forceinline__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
+  if (vtag(l) == V_LIST && list_kind(l) != LK_SET) {
+    uint32_t o = list_off(l);
+    uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
+    if (n < cap) {
+      L.H[o + 2 + n] = v;
+      L.H[o] = n + 1;
+      return l;
+    }
+  }
+  return list_add_slow(L, l, v);
 }
 
 // ------------------------------------------------------------------ get
@@ -1379,7 +1404,7 @@ __device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
 }
 
 // ------------------------------------------------------------------ sprintf
-__device__ uint64_t do_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+__device__ __noinline__ uint64_t do_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
   const uint32_t* f = gk_args.fmt + fidx;
   uint32_t want = f[1];
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
@@ -1408,7 +1433,7 @@ __device__ __forceinline__ uint64_t fmt_args(uint64_t f) {
 }
 __device__ __forceinline__ uint32_t fmt_fidx(uint64_t f) { return (uint32_t)(vpay(f) >> 32) & 0xffffffu; }
 
-__device__ uint64_t lazy_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+__device__ __forceinline__ uint64_t lazy_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t t = vtag(args);
   if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
@@ -1589,7 +1614,7 @@ __device__ __forceinline__ void gm_put(const Lane& L, uint32_t site, uint64_t k0
 }
 
 // m: message register, d: details register (undefined when absent)
-__device__ __forceinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+__device__ __noinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   if (vtag(m) == V_FMT) {
     // deferred message: size it now, format it into the output at flush_wave.
     // Only heap-free arguments are recorded (the record outlives this
