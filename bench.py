@@ -169,6 +169,25 @@ def main():
     achieved = algo_bytes / (k_avg_ms / 1000.0) / 1e9
     kernels = [{"kernel": ln.kernel, "avg_ms": sum(launch_ms[ln.kernel]) / len(launch_ms[ln.kernel]),
                 "constraints": ln.constraints, "tuples": ln.tuples, "bytes": ln.bytes} for ln in last.launches]
+    # the message format pass (gk_format_kernel): per tuple it reads the 32-B
+    # tuple and its record (8-B header + 8 B per argument; 8 + 8*3 at most for
+    # these templates, counted as 32 B) and writes the message bytes
+    fmt_roof = None
+    if "gk_format_kernel" in launch_ms:
+        f_ms = sum(launch_ms["gk_format_kernel"]) / len(launch_ms["gk_format_kernel"])
+        f_bytes = last.device_tuples * (32 + 32) + last.device_bytes
+        f_ach = f_bytes / (f_ms / 1000.0) / 1e9
+        f_tr = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("pods") == args.pods and tj.get("constraints") == n_cons:
+                    f_tr = tj.get("hbm_bytes_per_launch", {}).get("gk_format_kernel")
+            except Exception:
+                f_tr = None
+        fmt_roof = {"bound": "hbm", "achieved": f_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": f_ach / HBM_PEAK_GBS, "traffic": f_tr, "algo_bytes_per_launch": f_bytes,
+                    "kernel_ms_avg": f_ms, "tuples": last.device_tuples}
     fallback = last.n_fallbacks
     errors = last.n_errors
     traffic = None
@@ -230,6 +249,7 @@ def main():
                 "template": kinds_of.get(dom),
             },
             "kernels": kernels,
+            "format_pass": fmt_roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

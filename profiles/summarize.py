@@ -43,7 +43,31 @@ def bench_line(path):
     return json.loads(open(path).read().strip().splitlines()[-1])
 
 
+def traffic(d, bench):
+    """HBM bytes per launch from the two PMC passes of run dir d, per template kind."""
+    kt = dict(bench["config"]["kernel_templates"])
+    fetch = counter(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
+    write = counter(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
+    for k in fetch:
+        if k.endswith("gk_format_kernel"):
+            kt[k] = "gk_format_kernel"
+    out = {"pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
+           "note": "FETCH_SIZE x2 (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE, median per dispatch",
+           "hbm_bytes_per_launch": {}, "fetch_bytes_x2": {}, "write_bytes": {}}
+    for k, kind in kt.items():
+        if k in fetch and k in write:
+            out["fetch_bytes_x2"][kind] = 2 * fetch[k]
+            out["write_bytes"][kind] = write[k]
+            out["hbm_bytes_per_launch"][kind] = 2 * fetch[k] + write[k]
+    return out
+
+
 def main():
+    if sys.argv[1] == "--traffic-only":  # on the GPU box, before the final bench run
+        d = sys.argv[2]
+        out = traffic(d, bench_line(os.path.join(d, "bench_fetch.json")))
+        json.dump(out, open(os.path.join(d, "traffic.json"), "w"), indent=1)
+        return
     d, rnd = sys.argv[1], sys.argv[2]
     txt, avg = kernel_stats(os.path.join(d, "trace", "run_results.db"))
     bench = bench_line(os.path.join(d, "bench.json"))
@@ -56,16 +80,7 @@ def main():
     for k, kind in kt.items():
         hdr += "# %s = %s\n" % (k, kind)
     open(os.path.join(HERE, "%s_kernel_stats.txt" % rnd), "w").write(hdr + txt)
-    fetch = counter(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
-    write = counter(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
-    out = {"pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
-           "note": "FETCH_SIZE x2 (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE, median per dispatch",
-           "hbm_bytes_per_launch": {}, "fetch_bytes_x2": {}, "write_bytes": {}}
-    for k, kind in kt.items():
-        if k in fetch and k in write:
-            out["fetch_bytes_x2"][kind] = 2 * fetch[k]
-            out["write_bytes"][kind] = write[k]
-            out["hbm_bytes_per_launch"][kind] = 2 * fetch[k] + write[k]
+    out = traffic(d, bench)
     for name in ("%s_traffic.json" % rnd, "traffic_latest.json"):
         json.dump(out, open(os.path.join(HERE, name), "w"), indent=1)
     open(os.path.join(HERE, "%s_bench.json" % rnd), "w").write(json.dumps(bench) + "\n")
