@@ -97,20 +97,87 @@ __global__ void __launch_bounds__(256) audit_kernel() {
 // kernel, consecutive tuples to consecutive ranges.
 __device__ Lane g_fmt_lane;
 
+// LDS-staged writer for one wavefront's message bytes
+struct LOut {
+  uint8_t* p;
+  uint32_t pos;
+  __device__ __forceinline__ void put(char c) { p[pos++] = (uint8_t)c; }
+};
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = __shfl_xor(x, d, 64); x = o < x ? o : x; }
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = __shfl_xor(x, d, 64); x = o > x ? o : x; }
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
+
+// A wavefront takes 64 consecutive tuples.  When their output bytes (messages
+// and details) form one dense range that fits in LDS — the usual case, since a
+// wave's tuples come from one audit-kernel reservation — the range is read
+// into LDS, the live lanes format their messages into it, and it is written
+// back with coalesced dword stores (byte stores for the two edge dwords, which
+// may hold a neighbouring wave's bytes).  Otherwise each lane formats straight
+// into HBM.
 __global__ void __launch_bounds__(256) gk_format_kernel() {
+  __shared__ uint32_t stage[4][FSTAGE / 4];
   uint32_t n = gk_args.counters[0];
   // an overflowed call left some reservations unwritten; the host retries it
   if (n > gk_args.out_cap || gk_args.counters[1] > gk_args.bytes_cap) return;
   Lane& L = g_fmt_lane;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t* st = stage[wv];
+  uint8_t* stb = (uint8_t*)st;
+  uint32_t* gw = (uint32_t*)gk_args.bytes;
+  for (uint32_t base = (blockIdx.x * 4 + wv) * 64; base < n; base += gridDim.x * 256) {  // wave-uniform
+    uint32_t i = base + lane;
+    bool valid = i < n;
     const uint64_t* w = gk_args.frec + (uint64_t)i * FREC_WORDS;
-    uint64_t h = w[0];
-    if (!(h & FREC_LIVE)) continue;
-    const Viol v = gk_args.out[i];
-    if ((uint64_t)v.msg_off + v.msg_len > gk_args.bytes_cap) continue;
-    GOut g{(uint8_t*)gk_args.bytes, v.msg_off, v.msg_off, 0, false};
-    fmt_run(L, g, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
-    g.finish();
+    uint64_t h = valid ? w[0] : 0;
+    Viol v{};
+    if (valid) v = gk_args.out[i];
+    uint32_t end = v.msg_off + v.msg_len + v.det_len;
+    bool live = valid && (h & FREC_LIVE) && (uint64_t)v.msg_off + v.msg_len <= gk_args.bytes_cap;
+    if (!__any(live)) continue;
+    uint32_t lo = wave_min(valid ? v.msg_off : 0xffffffffu);
+    uint32_t hi = wave_max(valid ? end : 0u);
+    uint32_t tot = wave_sum(valid ? v.msg_len + v.det_len : 0u);
+    uint32_t lo4 = lo & ~3u, hi4 = (hi + 3) & ~3u;
+    if (tot == hi - lo && hi4 - lo4 <= FSTAGE && hi4 <= gk_args.bytes_cap) {
+      uint32_t nw = (hi4 - lo4) >> 2;
+      for (uint32_t k = lane; k < nw; k += 64) st[k] = gw[(lo4 >> 2) + k];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (live) {
+        LOut o{stb + (v.msg_off - lo4), 0};
+        fmt_run(L, o, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t k = lane; k < nw; k += 64) {
+        uint32_t a = lo4 + 4 * k;
+        if (a >= lo && a + 4 <= hi) {
+          gw[(lo4 >> 2) + k] = st[k];
+        } else {
+          for (uint32_t b = 0; b < 4; ++b)
+            if (a + b >= lo && a + b < hi) gk_args.bytes[a + b] = (char)stb[4 * k + b];
+        }
+      }
+    } else if (live) {
+      GOut g{(uint8_t*)gk_args.bytes, v.msg_off, v.msg_off, 0, false};
+      fmt_run(L, g, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
+      g.finish();
+    }
   }
 }
 
@@ -121,7 +188,7 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream) {
   if (!a->frec) return 0;
   hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gk_args), a, sizeof(*a), 0, hipMemcpyHostToDevice, stream);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(4096), dim3(256), 0, stream);
+  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(2048), dim3(256), 0, stream);
   return (int)hipGetLastError();
 }
 
