@@ -184,7 +184,9 @@ struct ReviewCol {
   uint32_t old_labels;
   uint32_t ns_labels; // labels node of the namespace object used by namespaceSelector
   uint32_t flags;
-  uint32_t pad[3];
+  uint32_t orig;      // index of the review in the caller's batch (NO_ID: its position);
+                      // staged batches are evaluated in document-size order
+  uint32_t pad[2];
 };
 static_assert(sizeof(ReviewCol) == 48, "ReviewCol layout");
 

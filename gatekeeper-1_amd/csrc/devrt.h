@@ -1669,13 +1669,15 @@ __device__ __forceinline__ void audit_body(Run run) {
   uint32_t c = gk_args.clist[wave % gk_args.nclist];
   uint32_t tile = wave / gk_args.nclist;
   if (tile >= gk_args.ntiles) return;  // wave-uniform
-  uint32_t r = tile * 64 + lane;
+  uint32_t rp = tile * 64 + lane;  // position in the (size-ordered) review columns
+  uint32_t r = rp;                   // the review's index in the caller's batch
   Lane L;
   L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
-  bool live = r < gk_args.nrev;
+  bool live = rp < gk_args.nrev;
   if (live) {
-    const ReviewCol rc = gk_args.revs[r];
+    const ReviewCol rc = gk_args.revs[rp];
+    if (rc.orig != NO_ID) r = rc.orig;
     const MatchSpec m = gk_args.cons[c];
     if (rc.flags & RC_FALLBACK) {
       L.fail = RF_FALLBACK;

@@ -571,6 +571,7 @@ static ReviewCol review_columns(gk_engine* e, uint32_t root) {
   Store& st = e->st;
   ReviewCol rc{};
   rc.root = root;
+  rc.orig = NO_ID;
   rc.group = rc.kind = rc.ns = rc.nsname = NO_ID;
   rc.labels = rc.old_labels = rc.ns_labels = NO_ID;
   if (root == NO_ID) return rc;  // input.review undefined: nothing matches
@@ -853,7 +854,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
   if (ncons == 0) {
     res->status.assign(nrev, 0);
     res->reason.assign(nrev, 0);
-    for (uint32_t r = 0; r < nrev; ++r) if (cols[r].flags & RC_FALLBACK) res->status[r] = GK_REVIEW_FALLBACK;
+    for (uint32_t r = 0; r < nrev; ++r)
+      if (cols[r].flags & RC_FALLBACK) res->status[cols[r].orig == NO_ID ? r : cols[r].orig] = GK_REVIEW_FALLBACK;
     return GK_OK;
   }
   if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
@@ -1357,8 +1359,10 @@ int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, 
 }
 
 static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
-                           const size_t* ns_lens, size_t n, std::vector<ReviewCol>& cols) {
+                           const size_t* ns_lens, size_t n, std::vector<ReviewCol>& cols, bool order_by_size) {
   JDoc od, nd;
+  std::vector<uint32_t> weight;
+  weight.reserve(n);
   std::string empty_ns = EMPTY_NS_JSON;
   // a namespace document is shared by all objects of the namespace: flatten each
   // distinct namespace text once and point every review's _unstable.namespace at it
@@ -1387,8 +1391,31 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
       nsroot = e->st.add_doc(nd, nj);
       ns_nodes[key] = {nsroot, nsname};
     }
+    size_t n0 = e->st.nodes().size();
     uint32_t root = build_object_review(e, od, oj, nd, nj, nsroot, nsname);
     cols.push_back(review_columns(e, root));
+    // size key: array elements (what templates iterate: containers, ports,
+    // volumes ...) first, then document nodes
+    uint32_t elems = 0;
+    const auto& nv = e->st.nodes();
+    for (size_t k = n0; k < nv.size(); ++k)
+      if (nv[k].type == NT_ARR) elems += nv[k].n;
+    uint32_t nn = (uint32_t)(nv.size() - n0);
+    weight.push_back((std::min<uint32_t>(elems, 0xfff) << 20) | std::min<uint32_t>(nn, 0xfffff));
+  }
+  if (order_by_size) {
+    // Divergence-aware order: a wavefront evaluates 64 consecutive reviews, and
+    // its lanes run as long as the largest document (e.g. the Pod with the most
+    // containers).  Evaluating reviews in order of document size (node count)
+    // puts similar documents in one wave; each column records the review's
+    // index in the caller's batch, which every output carries (devrt.h
+    // audit_body), so results are unchanged.
+    std::vector<uint32_t> perm(cols.size());
+    for (uint32_t i = 0; i < perm.size(); ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return weight[a] < weight[b]; });
+    std::vector<ReviewCol> sorted(cols.size());
+    for (uint32_t i = 0; i < perm.size(); ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
+    cols.swap(sorted);
   }
   return GK_OK;
 }
@@ -1409,7 +1436,7 @@ int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_l
   reset_transient(e);
   std::vector<ReviewCol> cols;
   cols.reserve(n);
-  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, cols);
+  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, cols, false);
   if (rc != GK_OK) { delete res; return rc; }
   res->ms[0] = ms_since(t0);
   rc = launch_and_collect(e, cols, &e->d_revs, true, res);
@@ -1431,7 +1458,8 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
   auto* b = new gk_batch();
   reset_transient(e);
   b->node_begin = (uint32_t)e->st.nodes().size();
-  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols);
+  const char* so = getenv("GKGPU_SIZE_ORDER");  // A/B switch (default on)
+  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols, !so || atoi(so) != 0);
   if (rc != GK_OK) { delete b; return rc; }
   b->node_end = (uint32_t)e->st.nodes().size();
   b->nrev = (uint32_t)n;

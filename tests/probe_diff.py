@@ -20,7 +20,7 @@ objs, nss = W.gen_pods_json(N, seed=42, n_namespaces=1000)
 
 
 def run(jit, env):
-    for k in ("GKGPU_JIT_WPE", "GKGPU_GMEMO", "GKGPU_JIT_PRE", "GKGPU_FORMAT_PASS"):
+    for k in ("GKGPU_JIT_WPE", "GKGPU_GMEMO", "GKGPU_JIT_PRE", "GKGPU_FORMAT_PASS", "GKGPU_SIZE_ORDER"):
         os.environ.pop(k, None)
     os.environ.update(env)
     d = gkgpu.Driver(jit=jit)
@@ -38,7 +38,7 @@ def run(jit, env):
     return out, r.timing_ms[2]
 
 
-base, ms = run(False, {"GKGPU_FORMAT_PASS": "0"})  # VM, messages formatted in-kernel
+base, ms = run(False, {"GKGPU_FORMAT_PASS": "0", "GKGPU_SIZE_ORDER": "0"})  # VM, in-kernel messages, batch order
 print("vm: %d results, %.2f ms, repeat-equal %s" % (sum(base[0].values()), ms, base[0] == base[1]), flush=True)
 VARIANTS = [("wpe2", {}), ("wpe2_nomemo", {"GKGPU_GMEMO": "0"}), ("wpe3", {"GKGPU_JIT_WPE": "3"}),
             ("wpe3_nomemo", {"GKGPU_JIT_WPE": "3", "GKGPU_GMEMO": "0"})]

@@ -427,8 +427,9 @@ def test_string_builtins_trim_split_case_concat_indexof():
 
 def test_template_kernel_matches_vm_at_scale():
     """Size-independent property at 200k Pods (config 2 policies): the template
-    kernels + format pass produce exactly the violation multiset of the bytecode
-    VM with in-kernel formatting, and repeat evaluations are identical."""
+    kernels + format pass over size-ordered reviews produce exactly the
+    violation multiset of the bytecode VM with in-kernel formatting in batch
+    order, and repeat evaluations are identical."""
     if not _BACKEND["jit"]:
         pytest.skip("compares the two back ends; runs once")
     import collections
@@ -438,7 +439,9 @@ def test_template_kernel_matches_vm_at_scale():
 
     def sweep(jit, fpass):
         old = os.environ.get("GKGPU_FORMAT_PASS")
+        old_so = os.environ.get("GKGPU_SIZE_ORDER")
         os.environ["GKGPU_FORMAT_PASS"] = "1" if fpass else "0"
+        os.environ["GKGPU_SIZE_ORDER"] = "1" if fpass else "0"
         try:
             d = gkgpu.Driver(jit=jit)
             cl = Client(d)
@@ -452,10 +455,11 @@ def test_template_kernel_matches_vm_at_scale():
             b.free()
             return out
         finally:
-            if old is None:
-                os.environ.pop("GKGPU_FORMAT_PASS", None)
-            else:
-                os.environ["GKGPU_FORMAT_PASS"] = old
+            for k, v in (("GKGPU_FORMAT_PASS", old), ("GKGPU_SIZE_ORDER", old_so)):
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
 
     vm = sweep(False, False)
     jit = sweep(True, True)
