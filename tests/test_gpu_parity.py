@@ -467,3 +467,57 @@ def test_template_kernel_matches_vm_at_scale():
     assert sum(vm[0].values()) > 500_000
     assert jit[0] == jit[1]
     assert jit[0] == vm[0]
+
+
+def _audit_rows_oracle(od):
+    from oracle.driver import details_json
+    rows = []
+    for r in od.query('hooks["%s"].audit' % gkgpu.client.TARGET):
+        rv, c = r["review"], r["constraint"]
+        ns = rv.get("namespace") if hasattr(rv, "get") else None
+        rows.append((rv.get("kind").get("kind"), ns if isinstance(ns, str) else "", rv.get("name"), c.get("kind"),
+                     c.get("metadata").get("name"), r["msg"], details_json(r["details"]), r["enforcementAction"]))
+    return rows
+
+
+def test_audit_from_cache_inventory():
+    """Client.Audit (client.go:805-833) -> hooks.audit over the synced inventory
+    (target_template_source.go:46-89 make_review / add_field): reviews carry no
+    _unstable.namespace, so namespace matching reads the synced Namespace cache.
+    The engine enumerates the inventory in path order; rows are compared as a
+    multiset (the reference iterates Go maps)."""
+    from gkgpu.client import data_path
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(300, seed=5, n_namespaces=12)
+    objs = list(ns_objs.values()) + pods
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, cs)
+    paths = []
+    for o in objs:
+        cl.add_data(o)
+        od.put_data(data_path(o), json.dumps(o))
+        paths.append(data_path(o))
+    res = cl.audit()
+    assert not any(res.status), "audit reviews flagged for fallback/error"
+    order = sorted(set(paths))
+    eng = []
+    for r in res.results:
+        seg = order[r.review].split("/")
+        ns = seg[4] if seg[3] == "namespace" else ""
+        eng.append((seg[-2], ns, seg[-1], r.constraint_kind, r.constraint_name, r.msg, r.details_json,
+                    r.enforcement_action))
+    ref = _audit_rows_oracle(od)
+    assert len(ref) > 0
+    assert sorted(eng) == sorted(ref)
+    # removing an object drops exactly its rows (DeleteData on the inventory path)
+    gone = pods[0]
+    cl.remove_data(gone)
+    od.delete_data(data_path(gone))
+    res2 = cl.audit()
+    n_gone = sum(1 for row in ref if row[2] == gone["metadata"]["name"] and row[1] == gone["metadata"]["namespace"])
+    assert len(res2.results) == len(ref) - n_gone
