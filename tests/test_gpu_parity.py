@@ -521,3 +521,43 @@ def test_audit_from_cache_inventory():
     res2 = cl.audit()
     n_gone = sum(1 for row in ref if row[2] == gone["metadata"]["name"] and row[1] == gone["metadata"]["namespace"])
     assert len(res2.results) == len(ref) - n_gone
+
+
+def test_empty_and_degenerate_inputs():
+    """Edges the reference handles without error: empty batches, an empty
+    inventory, a null Query input, no constraints, and objects with missing or
+    mistyped metadata (local.go:302-359; target.go:129-163)."""
+    ts, cs = W.config2()
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    # no constraints yet: every path returns nothing
+    assert drv.review_objects([W.namespace_obj("a")], [None]).results == []
+    for c in cs:
+        cl.add_constraint(c)
+    assert drv.review_objects([], []).results == []
+    assert drv.query_batch([]).results == []
+    assert cl.audit().results == []
+    b = drv.stage_objects([], [])
+    assert b.eval().results == []
+    b.free()
+    # null input: hooks.violation binds no review -> no results, no error
+    assert drv.query('hooks["%s"].violation' % gkgpu.client.TARGET, None).results == []
+    odd = [
+        {"apiVersion": "v1", "kind": "Pod"},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": 7, "namespace": ["x"]}, "spec": None},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "production"},
+         "spec": {"containers": []}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "q", "namespace": "production"},
+         "spec": {"containers": [{}]}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "r", "namespace": "production"},
+         "spec": {"containers": [{"name": "c", "image": "", "resources": {"limits": {}}}]}},
+        {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "n", "labels": {}}},
+        {},
+    ]
+    nss = [None, None, W.namespace_obj("production"), W.namespace_obj("production"),
+           W.namespace_obj("production"), None, None]
+    rep, _ = run_objects(Driver(), ts, cs, odd, nss)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.compared + rep.fallback + rep.errors == len(odd)
