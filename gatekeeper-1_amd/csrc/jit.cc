@@ -433,7 +433,9 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // 512/n; the compiler spills beyond).  Default 2: measured on config 2 (1M Pods,
 // MI355X), K8sContainerLimits 65 ms at the compiler's own choice (1 wave, 248
 // VGPRs), 41 ms at 2 (256 VGPRs, 8 spills), 69 ms at 4 (128 VGPRs, heavy
-// spills).  GKGPU_JIT_WPE overrides (0 = compiler's choice).
+// spills).  Re-measured after the format pass and review ordering
+// (tests/gpu_wpe_sweep.sh): ContainerLimits 11.0 ms at 1, 8.4 ms at 2, 12.5 ms
+// at 3.  GKGPU_JIT_WPE overrides (0 = compiler's choice).
 static std::string wpe_suffix() {
   const char* w = getenv("GKGPU_JIT_WPE");
   int n = w ? atoi(w) : 2;
