@@ -1410,9 +1410,52 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
     // puts similar documents in one wave; each column records the review's
     // index in the caller's batch, which every output carries (devrt.h
     // audit_body), so results are unchanged.
+    //
+    // Ahead of size, two match-affinity keys keep reviews that a constraint's
+    // match stage rejects together, so those wavefronts exit after the match
+    // instead of idling beside a few matching lanes: one bit per constraint
+    // with a namespaces / excludedNamespaces list (membership of the review's
+    // namespace), then the kind id.  Keys only reorder work; matching itself is
+    // unchanged.
+    std::vector<uint32_t> sig(cols.size(), 0);
+    const char* mo = getenv("GKGPU_MATCH_ORDER");  // A/B switch (default on)
+    const bool match_order = !mo || atoi(mo) != 0;
+    if (match_order && !e->constraints_dirty) {
+      const auto& W = e->mwords;
+      auto in_list = [&](uint32_t off, uint32_t id) {
+        if (off >= W.size()) return false;
+        uint32_t n = W[off];
+        for (uint32_t j = 0; j < n && off + 1 + j < W.size(); ++j) if (W[off + 1 + j] == id) return true;
+        return false;
+      };
+      uint32_t bit = 0;
+      for (auto* c : e->corder) {
+        if (bit >= 16) break;
+        const MatchSpec& m = c->spec;
+        if (!(m.flags & (MF_HAS_NAMESPACES | MF_HAS_EXCLUDED))) continue;
+        for (size_t i = 0; i < cols.size(); ++i) {
+          uint32_t id = cols[i].nsname;
+          bool in = ((m.flags & MF_HAS_NAMESPACES) && in_list(m.ns_off, id)) ||
+                    ((m.flags & MF_HAS_EXCLUDED) && in_list(m.exns_off, id));
+          if (in) sig[i] |= 1u << bit;
+        }
+        ++bit;
+      }
+    }
     std::vector<uint32_t> perm(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return weight[a] < weight[b]; });
+    const int mode = mo ? atoi(mo) : 2;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+      if (mode == 2) {  // kind, array elements, namespace-list bits, nodes
+        if (cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
+        if ((weight[a] >> 20) != (weight[b] >> 20)) return (weight[a] >> 20) < (weight[b] >> 20);
+        if (sig[a] != sig[b]) return sig[a] < sig[b];
+        return weight[a] < weight[b];
+      }
+      if (sig[a] != sig[b]) return sig[a] < sig[b];
+      if (match_order && cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
+      return weight[a] < weight[b];
+    });
     std::vector<ReviewCol> sorted(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
     cols.swap(sorted);
