@@ -95,6 +95,8 @@ def main():
         b, detail = drv.template_backend(k)
         if b == 2:
             kinds_of[detail] = k
+        elif b == 3 and "[guard kernel " in detail:
+            kinds_of[detail.split("[guard kernel ")[1].rstrip("]")] = k + " (guard)"
 
     t0 = time.time()
     objs, nss = cfg_gen(args.pods, rank * args.pods)
@@ -230,7 +232,7 @@ def main():
                 "gather_ms_avg_rank0": (sum(gather_ms[-args.steps:]) / args.steps) if gather_ms else 0.0,
                 "kernel_ms_per_step": sum(k["avg_ms"] for k in kernels),
                 "kernel_only_evals_per_s": evals_per_step / (sum(k["avg_ms"] for k in kernels) / 1000.0),
-                "backends": {k: ("template-kernel" if drv.template_backend(k)[0] == 2 else "bytecode-vm")
+                "backends": {k: {0: "cpu-fallback", 1: "bytecode-vm", 2: "template-kernel", 3: "guard-kernel+cpu-fallback"}[drv.template_backend(k)[0]]
                              for k in kinds},
                 "kernel_templates": kinds_of,
                 "stage_s": round(t_stage, 3),

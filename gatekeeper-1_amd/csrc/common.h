@@ -134,6 +134,7 @@ enum ReviewFlags : uint32_t {
 enum Reason : uint32_t {
   FB_NONE = 0, FB_HEAP, FB_MSG_LEN, FB_NUMBER, FB_UNICODE, FB_DEEP_EQ, FB_REGEX, FB_PRINT, FB_TYPE,
   FB_UNSUPPORTED, FB_MATCH, FB_STRING,
+  FB_TEMPLATE,  // a template expression outside the GPU subset was reached (guard programs)
 };
 
 // ----------------------------------------------------------------- match

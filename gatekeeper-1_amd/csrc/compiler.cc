@@ -70,24 +70,37 @@ const std::map<std::string, uint32_t> kArith = {{"plus", AR_PLUS}, {"minus", AR_
 
 class Comp {
  public:
-  Comp(Store& st, const ModuleSet& mods, CodeBank& bank) : st_(st), mods_(mods), bank_(bank) {}
+  Comp(Store& st, const ModuleSet& mods, CodeBank& bank, bool guard) : st_(st), mods_(mods), bank_(bank), guard_(guard) {}
 
   Program run(const std::vector<std::string>& pkg) {
     auto rules = mods_.rules(pkg, "violation");
     if (rules.empty()) throw Unsupported("template has no violation rule");
     int rule_idx = 0;
     for (auto& r : rules) {
-      if (r->kind != Rule::PSET) throw Unsupported("violation must be a partial set rule");
-      int Lr = label();
-      Env env;
-      env.mod = r->mod;
-      int save = reg_top_;
-      const auto& body = cbody(r, {});
       int idx = rule_idx++;
-      body_k(body, 0, &env, Lr, [&, idx](int f) { emit_violation(r, &env, idx, f); });
-      place(Lr);
-      reg_top_ = save;
       prog_.rules.push_back(r->name);
+      const size_t code0 = code_.size(), labels0 = labels_.size();
+      int save = reg_top_;
+      try {
+        if (r->kind != Rule::PSET) throw Unsupported("violation must be a partial set rule");
+        int Lr = label();
+        Env env;
+        env.mod = r->mod;
+        const auto& body = cbody(r, {});
+        body_k(body, 0, &env, Lr, [&, idx](int f) { emit_violation(r, &env, idx, f); });
+        place(Lr);
+      } catch (const Unsupported& ex) {
+        // guard mode: a rule whose body cannot be compiled at all sends every
+        // review that reaches it (every matched review) to the CPU
+        if (!guard_) throw;
+        code_.resize(code0);
+        labels_.resize(labels0);
+        loop_base_.clear();
+        if (prog_.fallback_reason.empty()) prog_.fallback_reason = ex.what();
+        ++prog_.fallback_sites;
+        emit(OP_FAIL_FALLBACK, 0, 0, 0, 0, FB_TEMPLATE);
+      }
+      reg_top_ = save;
     }
     emit(OP_END);
     return finish();
@@ -97,6 +110,7 @@ class Comp {
   Store& st_;
   const ModuleSet& mods_;
   CodeBank& bank_;
+  const bool guard_;
   std::vector<Ins> code_;
   std::vector<int> labels_;
   std::map<uint64_t, uint32_t> kidx_;
@@ -283,8 +297,42 @@ class Comp {
 
   // ---------------------------------------------------------------- bodies
   void body_k(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    if (guard_) { guarded_body_k(body, i, env, fail, succ); return; }
     if (i == body.size()) { succ(fail); return; }
     expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
+  }
+
+  // Guard mode (compile_template_guard): a body expression outside the subset
+  // compiles to OP_FAIL_FALLBACK at the point OPA would evaluate it.  Bodies
+  // are conjunctions evaluated in order (after OPA's safety reordering, which
+  // cbody applies), so the expressions before it act as a device-evaluated
+  // guard: a (review, constraint) whose evaluation never reaches the
+  // unsupported expression has exactly the results of the compiled prefix
+  // (usually none, e.g. `input.review.kind.kind == "Service"` for a Pod), and
+  // one that reaches it is routed whole to the CPU.  The innermost enclosing
+  // body catches; the code, labels, registers, loops and bindings emitted for
+  // the failed expression are rolled back first.
+  void guarded_body_k(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    const size_t code0 = code_.size(), labels0 = labels_.size(), loops0 = loop_base_.size();
+    const int reg0 = reg_top_, depth0 = inline_depth_;
+    const Term* key0 = stmt_key_;
+    const std::map<std::string, int> vars0 = env->vars;
+    try {
+      if (i == body.size()) succ(fail);
+      else expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
+    } catch (const Unsupported& ex) {
+      if (code_.size() < code0 || labels_.size() < labels0) throw;  // cannot roll back (nested guard already did)
+      code_.resize(code0);
+      labels_.resize(labels0);
+      loop_base_.resize(loops0);
+      reg_top_ = reg0;
+      inline_depth_ = depth0;
+      stmt_key_ = key0;
+      env->vars = vars0;
+      if (prog_.fallback_reason.empty()) prog_.fallback_reason = ex.what();
+      ++prog_.fallback_sites;
+      emit(OP_FAIL_FALLBACK, 0, 0, 0, 0, FB_TEMPLATE);
+    }
   }
 
   void expr(const ExprP& e, Env* env, int fail, const KE& k) {
@@ -1105,11 +1153,12 @@ class Comp {
 
 }  // namespace
 
-Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank) {
-  // compile into a scratch bank first so a failed template leaves no code behind
+static Program compile_impl(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank,
+                            bool guard) {
+  // a failed template leaves no code behind in the shared bank
   size_t code0 = bank.code.size(), k0 = bank.consts.size(), f0 = bank.fmt.size();
   try {
-    Comp c(st, mods, bank);
+    Comp c(st, mods, bank, guard);
     return c.run(pkg);
   } catch (...) {
     bank.code.resize(code0);
@@ -1117,6 +1166,14 @@ Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std
     bank.fmt.resize(f0);
     throw;
   }
+}
+
+Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank) {
+  return compile_impl(st, mods, pkg, bank, false);
+}
+
+Program compile_template_guard(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank) {
+  return compile_impl(st, mods, pkg, bank, true);
 }
 
 }  // namespace gk

@@ -33,6 +33,10 @@ struct Program {
   bool uses_regex = false;
   std::vector<uint32_t> regex_literals;  // string ids of literal patterns
   std::vector<std::string> rules;
+  // guard programs (compile_template_guard): expressions outside the subset
+  // compiled to OP_FAIL_FALLBACK, and the first one's reason
+  uint32_t fallback_sites = 0;
+  std::string fallback_reason;
 };
 
 // All modules known to the driver, indexed by package path.
@@ -55,6 +59,13 @@ struct CodeBank {
 
 // Compile the template entry package `pkg` (must define `violation`).
 Program compile_template(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank);
+
+// The same template with every body expression outside the subset compiled to
+// OP_FAIL_FALLBACK (reason FB_TEMPLATE) where OPA would evaluate it: the
+// expressions before it run on the device as a guard, so only the (review,
+// constraint) pairs that reach an unsupported expression go to the CPU.
+// Throws Unsupported only for constructs outside any rule body.
+Program compile_template_guard(Store& st, const ModuleSet& mods, const std::vector<std::string>& pkg, CodeBank& bank);
 
 // Tagged-value helpers shared with the engine.
 inline uint64_t tag_val(uint32_t tag, uint64_t payload) { return ((uint64_t)tag << 60) | (payload & 0x0fffffffffffffffull); }

@@ -883,7 +883,6 @@ __device__ int any_sel(const uint32_t* w, const ReviewCol& rc) {
 
 // 1 = match, 0 = no match, -1 = error (query fails), -2 = fallback
 __device__ int match_constraint(const MatchSpec& m, const ReviewCol& rc) {
-  if (m.flags & MF_FALLBACK) return -2;
   if (!(rc.flags & RC_REVIEW_DEF)) return 0;
   const uint32_t* W = gk_args.mwords;
   // kinds
@@ -1683,7 +1682,7 @@ __device__ __forceinline__ void audit_body(Run run) {
       L.fail = RF_FALLBACK;
     } else {
       // autoreject_review (target_template_source.go:12-25)
-      if ((m.flags & MF_HAS_NSSEL) && !(m.flags & MF_FALLBACK) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID &&
+      if ((m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID &&
           !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS)) {
         const char* msg = "Namespace is not cached in OPA.";
         stage_tuple(L, RULE_AUTOREJECT, msg, 31, "{}", 2, 0);
@@ -1691,6 +1690,7 @@ __device__ __forceinline__ void audit_body(Run run) {
       int mr = match_constraint(m, rc);
       if (mr == -1) L.fail = RF_ERROR;
       else if (mr == -2) L.fail = RF_FALLBACK;
+      else if (mr == 1 && (m.flags & MF_FALLBACK)) lane_fallback(L, FB_TEMPLATE);  // template served by CPU OPA
       else if (mr == 1 && m.prog != NO_ID) {
         uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
         run(L, mkv(V_NODE, rc.root), params, m.prog, r, c);

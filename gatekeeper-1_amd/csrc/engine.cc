@@ -37,6 +37,21 @@ static const char* EMPTY_NS_JSON = "{\"metadata\":{\"creationTimestamp\":null},\
 using Clock = std::chrono::steady_clock;
 static double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
 
+// Integer A/B switch from the environment: unset -> def; a decimal in
+// [0, max] -> that value; anything else is rejected loudly (stderr) and
+// read as def, so a typo cannot silently select another mode.
+static int env_mode(const char* name, int def, int max) {
+  const char* v = getenv(name);
+  if (!v || !*v) return def;
+  char* end = nullptr;
+  long x = strtol(v, &end, 10);
+  if (*end || x < 0 || x > max) {
+    fprintf(stderr, "gkgpu: ignoring %s=%s (expected an integer in [0, %d])\n", name, v, max);
+    return def;
+  }
+  return (int)x;
+}
+
 
 // ------------------------------------------------------------------ device buffers
 struct DBuf {
@@ -69,8 +84,10 @@ struct DBuf {
 // ------------------------------------------------------------------ engine state
 struct TemplateEnt {
   std::string kind;
-  bool supported = false;
+  bool supported = false;  // the whole template runs on the GPU
+  bool guard = false;      // outside the subset; prog is its guard program
   std::string reason;
+  std::string detail;      // gk_template_backend text
   int prog = -1;
 };
 
@@ -285,14 +302,31 @@ static void rebuild_modules(gk_engine* e) {
     TemplateEnt te;
     te.kind = kind;
     try {
-      Program p = compile_template(e->st, e->mods, m->pkg, e->bank);
-      if (p.nregs > 192) throw Unsupported("register file too large");
+      Program p;
+      try {
+        p = compile_template(e->st, e->mods, m->pkg, e->bank);
+        if (p.nregs > 192) throw Unsupported("register file too large");
+      } catch (const Unsupported& ex) {
+        // outside the subset: the guard program evaluates the match and every
+        // body prefix before the first unsupported expression on the device;
+        // only reviews that reach it go to the CPU (compile_template_guard)
+        te.reason = ex.what();
+        size_t code0 = e->bank.code.size();
+        p = compile_template_guard(e->st, e->mods, m->pkg, e->bank);
+        if (p.nregs > 192) {
+          e->bank.code.resize(code0);
+          throw;
+        }
+        te.guard = true;
+      }
       // structural validation of the bytecode before it can reach the device
       for (uint32_t k = 0; k < p.code_len; ++k) {
         const Ins& in = e->bank.code[p.code_off + k];
         auto reg_ok = [&](uint16_t r) { return r < p.nregs || r == 0xffff; };
         if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
-        if (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))) throw std::runtime_error("internal: register out of range");
+        const bool no_regs = in.op == OP_END || in.op == OP_JMP || in.op == OP_FAIL_FALLBACK;
+        if (!no_regs && (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))))
+          throw std::runtime_error("internal: register out of range");
         if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
         if (in.op == OP_CALL && in.b + (uint32_t)in.c > p.nregs) throw std::runtime_error("internal: call args");
         bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE ||
@@ -305,7 +339,7 @@ static void rebuild_modules(gk_engine* e) {
           throw std::runtime_error("internal: table bounds");
       }
       te.prog = (int)e->progs.size();
-      te.supported = true;
+      te.supported = !te.guard;
       e->progs.push_back(p);
       gk_engine::Jit j;
       j.name = jit_name(p, e->bank, e->st);
@@ -313,7 +347,9 @@ static void rebuild_modules(gk_engine* e) {
       e->jits.push_back(std::move(j));
     } catch (const std::exception& ex) {
       te.supported = false;
-      te.reason = ex.what();
+      te.guard = false;
+      te.prog = -1;
+      if (te.reason.empty()) te.reason = ex.what();
     }
     e->templates[kind] = te;
   }
@@ -500,8 +536,10 @@ static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
   else { c.ea = ""; c.ea_error = true; }
   auto it = e->templates.find(c.kind);
   if (it != e->templates.end()) {
-    if (it->second.supported) m.prog = (uint32_t)it->second.prog;
-    else m.flags |= MF_FALLBACK;  // template served by CPU OPA
+    // whole-template or guard program; without either, every matched review
+    // goes to CPU OPA (devrt.h audit_body)
+    if (it->second.prog >= 0) m.prog = (uint32_t)it->second.prog;
+    else m.flags |= MF_FALLBACK;
   }
   c.spec = m;
 }
@@ -869,7 +907,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
         e->d_counters.reserve(64 + 8 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
   // deferred-message records for the format pass (GKGPU_FORMAT_PASS=0: format in the audit kernels)
-  const bool fpass = !getenv("GKGPU_FORMAT_PASS") || atoi(getenv("GKGPU_FORMAT_PASS")) != 0;
+  const bool fpass = env_mode("GKGPU_FORMAT_PASS", 1, 1) != 0;
   if (fpass && !e->d_frec.reserve(e->out_cap * FREC_WORDS * 8)) return fail(e, GK_EDEVICE, "device allocation failed");
   // launch plan: constraints grouped by template kernel (jit.cc); the bytecode
   // VM kernel takes every constraint whose template has no kernel / program
@@ -952,7 +990,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       int lr;
       if (plan[i].fn) {
         // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
-        const bool gm_on = !getenv("GKGPU_GMEMO") || atoi(getenv("GKGPU_GMEMO")) != 0;  // A/B switch
+        const bool gm_on = env_mode("GKGPU_GMEMO", 1, 1) != 0;  // A/B switch
         if (gm_on && e->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
           argv[i].gmemo = (uint64_t*)e->d_gmemo.p;
           argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
@@ -1417,9 +1455,11 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
     // with a namespaces / excludedNamespaces list (membership of the review's
     // namespace), then the kind id.  Keys only reorder work; matching itself is
     // unchanged.
+    // GKGPU_MATCH_ORDER (A/B switch): 0 = size keys only, 1 = signature first,
+    // 2 (default) = kind, array elements, signature, nodes
+    const int mode = env_mode("GKGPU_MATCH_ORDER", 2, 2);
+    const bool match_order = mode != 0;
     std::vector<uint32_t> sig(cols.size(), 0);
-    const char* mo = getenv("GKGPU_MATCH_ORDER");  // A/B switch (default on)
-    const bool match_order = !mo || atoi(mo) != 0;
     if (match_order && !e->constraints_dirty) {
       const auto& W = e->mwords;
       auto in_list = [&](uint32_t off, uint32_t id) {
@@ -1428,23 +1468,30 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
         for (uint32_t j = 0; j < n && off + 1 + j < W.size(); ++j) if (W[off + 1 + j] == id) return true;
         return false;
       };
-      uint32_t bit = 0;
-      for (auto* c : e->corder) {
-        if (bit >= 16) break;
-        const MatchSpec& m = c->spec;
-        if (!(m.flags & (MF_HAS_NAMESPACES | MF_HAS_EXCLUDED))) continue;
-        for (size_t i = 0; i < cols.size(); ++i) {
-          uint32_t id = cols[i].nsname;
-          bool in = ((m.flags & MF_HAS_NAMESPACES) && in_list(m.ns_off, id)) ||
-                    ((m.flags & MF_HAS_EXCLUDED) && in_list(m.exns_off, id));
-          if (in) sig[i] |= 1u << bit;
+      // one signature per distinct namespace-name id (reviews share a few
+      // thousand namespaces), then a lookup per review
+      std::unordered_map<uint32_t, uint32_t> by_ns;
+      for (size_t i = 0; i < cols.size(); ++i) {
+        uint32_t id = cols[i].nsname;
+        auto it = by_ns.find(id);
+        if (it == by_ns.end()) {
+          uint32_t s = 0, bit = 0;
+          for (auto* c : e->corder) {
+            if (bit >= 16) break;
+            const MatchSpec& m = c->spec;
+            if (!(m.flags & (MF_HAS_NAMESPACES | MF_HAS_EXCLUDED))) continue;
+            bool in = ((m.flags & MF_HAS_NAMESPACES) && in_list(m.ns_off, id)) ||
+                      ((m.flags & MF_HAS_EXCLUDED) && in_list(m.exns_off, id));
+            if (in) s |= 1u << bit;
+            ++bit;
+          }
+          it = by_ns.emplace(id, s).first;
         }
-        ++bit;
+        sig[i] = it->second;
       }
     }
     std::vector<uint32_t> perm(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    const int mode = mo ? atoi(mo) : 2;
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
       if (mode == 2) {  // kind, array elements, namespace-list bits, nodes
         if (cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
@@ -1501,8 +1548,8 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
   auto* b = new gk_batch();
   reset_transient(e);
   b->node_begin = (uint32_t)e->st.nodes().size();
-  const char* so = getenv("GKGPU_SIZE_ORDER");  // A/B switch (default on)
-  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols, !so || atoi(so) != 0);
+  const bool size_order = env_mode("GKGPU_SIZE_ORDER", 1, 1) != 0;  // A/B switch (default on)
+  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols, size_order);
   if (rc != GK_OK) { delete b; return rc; }
   b->node_end = (uint32_t)e->st.nodes().size();
   b->nrev = (uint32_t)n;
@@ -1615,6 +1662,12 @@ int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char
     auto& j = e->jits[it->second.prog];
     b = j.state == 1 ? 2 : 1;
     d = j.state == 1 ? j.name.c_str() : (e->jit_enabled ? j.log.c_str() : "jit disabled");
+  } else if (it->second.guard) {
+    b = 3;  // guard program on the GPU, CPU OPA for the reviews that reach an unsupported expression
+    ensure_jit(e, false);
+    auto& j = e->jits[it->second.prog];
+    it->second.detail = it->second.reason + (j.state == 1 ? " [guard kernel " + j.name + "]" : " [guard: bytecode VM]");
+    d = it->second.detail.c_str();
   }
   if (backend) *backend = b;
   if (detail) *detail = d;
@@ -1736,7 +1789,7 @@ extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   std::lock_guard<std::mutex> g(e->mu);
   rebuild_modules(e);
   auto it = e->templates.find(kind);
-  if (it == e->templates.end() || !it->second.supported) return GK_ENOTFOUND;
+  if (it == e->templates.end() || it->second.prog < 0) return GK_ENOTFOUND;
   const Program& p = e->progs[it->second.prog];
   static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
                                 "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",

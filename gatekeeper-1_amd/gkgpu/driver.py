@@ -418,7 +418,9 @@ class Driver:
         return s
 
     def template_backend(self, kind: str):
-        """(backend, detail): 2 template kernel (hipRTC), 1 bytecode VM, 0 CPU fallback"""
+        """(backend, detail): 2 template kernel (hipRTC), 1 bytecode VM, 3 guard program on
+        the GPU + CPU fallback for the reviews that reach an unsupported expression,
+        0 CPU fallback for every matched review"""
         b, d = C.c_int(), C.c_char_p()
         self._check(self._lib.gk_template_backend(self._e, _b(kind), C.byref(b), C.byref(d)))
         return b.value, (d.value or b"").decode("utf-8", "replace")

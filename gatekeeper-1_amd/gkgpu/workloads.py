@@ -279,6 +279,49 @@ get_violation_message(container, review, probe) = msg {
 }
 """)
 
+# demo/agilebank/templates/k8suniqueserviceselector_template.yaml: a
+# data.inventory join (outside the GPU subset).  The engine compiles it as a
+# guard program: the three `input.review.kind` tests run on the device, so only
+# v1 Services reach the inventory join and go to the CPU.
+UNIQUE_SERVICE_SELECTOR = _tmpl("K8sUniqueServiceSelector", """package k8suniqueserviceselector
+
+make_apiversion(kind) = apiVersion {
+	g := kind.group
+	v := kind.version
+	g != ""
+	apiVersion = sprintf("%v/%v", [g, v])
+}
+
+make_apiversion(kind) = apiVersion {
+	kind.group == ""
+	apiVersion = kind.version
+}
+
+identical(obj, review) {
+	obj.metadata.namespace == review.namespace
+	obj.metadata.name == review.name
+	obj.kind == review.kind.kind
+	obj.apiVersion == make_apiversion(review.kind)
+}
+
+flatten_selector(obj) = flattened {
+	selectors := [s | s = concat(":", [key, val]); val = obj.spec.selector[key]]
+	flattened := concat(",", sort(selectors))
+}
+
+violation[{"msg": msg}] {
+	input.review.kind.kind == "Service"
+	input.review.kind.version == "v1"
+	input.review.kind.group == ""
+	input_selector := flatten_selector(input.review.object)
+	other := data.inventory.namespace[namespace][_][_][name]
+	not identical(other, input.review)
+	other_selector := flatten_selector(other)
+	input_selector == other_selector
+	msg := sprintf("same selector as service <%v> in namespace <%v>", [name, namespace])
+}
+""")
+
 ALLOWED_LABEL_REGEX = _tmpl("K8sAllowedLabelRegex", """package k8sallowedlabelregex
 
 violation[{"msg": msg, "details": {"label": key}}] {
@@ -325,8 +368,21 @@ def config1():
     return templates, constraints
 
 
-# -- config 2: demo/agilebank constraints over Pods
+# -- config 2: demo/agilebank constraints (demo/agilebank/constraints/*.yaml) over Pods
 def config2():
+    """The five demo/agilebank constraints.  unique-service-selector has no
+    match block (demo/agilebank/constraints/unique_service_selector.yaml), so it
+    matches every review; its template is served by a guard program (see
+    UNIQUE_SERVICE_SELECTOR) and no Pod falls back."""
+    templates, constraints = config2_gpu_subset()
+    templates.append(UNIQUE_SERVICE_SELECTOR)
+    constraints.append({"apiVersion": "constraints.gatekeeper.sh/v1beta1", "kind": "K8sUniqueServiceSelector",
+                        "metadata": {"name": "unique-service-selector", "labels": {"owner": "admin.agilebank.demo"}}})
+    return templates, constraints
+
+
+def config2_gpu_subset():
+    """config 2 without unique-service-selector: the four templates inside the GPU subset."""
     templates = [REQUIRED_LABELS, ALLOWED_REPOS, CONTAINER_LIMITS, REQUIRED_PROBES]
     constraints = [
         constraint("K8sRequiredLabels", "all-must-have-owner",

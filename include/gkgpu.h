@@ -154,7 +154,11 @@ void gk_results_free(gk_results* r);
 int gk_template_status(gk_engine* e, const char* kind, const char** reason);
 /* evaluation back end of a template: 2 = template kernel (hipRTC-compiled for
  * gfx950; detail = kernel name), 1 = bytecode VM kernel (detail = why not
- * compiled), 0 = CPU fallback (detail = reason).  Compiles on demand. */
+ * compiled), 3 = outside the subset, guard program on the GPU: the match and
+ * every rule-body prefix before the first unsupported expression run on the
+ * device, and only (review, constraint) pairs that reach that expression are
+ * flagged GK_REVIEW_FALLBACK (detail = reason), 0 = CPU fallback for every
+ * matched review (detail = reason).  Compiles on demand. */
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail);
 size_t gk_constraint_count(gk_engine* e);
 int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name);

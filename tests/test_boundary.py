@@ -52,6 +52,28 @@ violation[{"msg": msg}] {
     kind = cl.add_template(t)
     st, why = d.template_status(kind)
     assert st == 0 and "inventory" in why
+    # the guard program: no expression before the join, so every matched review falls back
+    b, why2 = d.template_backend(kind)
+    assert b == 3 and "inventory" in why2
+
+
+def test_guard_program_for_agilebank_unique_service_selector():
+    """demo/agilebank's unique-service-selector is outside the subset (sort,
+    data.inventory), but its `input.review.kind` tests compile into a device
+    guard ahead of the first unsupported expression."""
+    d = gkgpu.Driver(jit=False)
+    cl = Client(d)
+    kind = cl.add_template(W.UNIQUE_SERVICE_SELECTOR)
+    st, why = d.template_status(kind)
+    assert st == 0 and "sort" in why
+    b, _ = d.template_backend(kind)
+    assert b == 3
+    asm = d.debug_disasm(kind)
+    assert asm.count("FAIL_FALLBACK") >= 1
+    # the guard compares kind, version and group before the first fallback point
+    head = asm[:asm.index("FAIL_FALLBACK")]
+    for lit in ('"Service"', '"v1"', '""'):
+        assert lit in head
 
 
 def test_put_modules_replaces_and_delete_modules_counts():
@@ -77,9 +99,9 @@ def test_constraints_and_delete_data():
         cl.add_template(t)
     for c in cs:
         cl.add_constraint(c)
-    assert len(d.constraints()) == 4
+    assert len(d.constraints()) == 5
     assert cl.remove_constraint(cs[0]) is True
-    assert len(d.constraints()) == 3
+    assert len(d.constraints()) == 4
     cl.reset()
     assert d.constraints() == []
 

@@ -42,11 +42,11 @@ def Driver():
     return d
 
 
-def _assert_backend(drv, kinds):
+def _assert_backend(drv, kinds, guard=("K8sUniqueServiceSelector",)):
     want = 2 if _BACKEND["jit"] else 1
     for k in kinds:
         b, detail = drv.template_backend(k)
-        assert b == want, (k, b, detail)
+        assert b == (3 if k in guard else want), (k, b, detail)
 
 
 def _assert_clean(rep, max_fallback_frac=0.0):
@@ -83,6 +83,43 @@ def test_config2_agilebank_pods():
         assert kernels and all(k.startswith("gk_t_") for k in kernels), res.launches
     else:
         assert kernels == {"audit_kernel"}, res.launches
+
+
+def test_config2_guard_program_routes_only_services_to_cpu():
+    """All five demo/agilebank constraints over Pods + Services.  The
+    unique-service-selector template (data.inventory join) runs as a guard
+    program: its kind/version/group tests run on the device after the match,
+    so only v1 Services are flagged for CPU fallback; Pods, apps/v1
+    Deployments and a v2 Service are evaluated on the GPU, bit-exact with the
+    oracle (manager.go:376-380 per object)."""
+    ts, cs = W.config2()
+    assert len(cs) == 5
+    pods, ns_of, ns_objs = W.gen_pods(1500, seed=44, n_namespaces=60)
+    objs = list(pods)
+    nss = [ns_objs[n] for n in ns_of]
+    n_svc = 0
+    import random
+    rng = random.Random(3)
+    names = sorted(ns_objs)
+    for i in range(300):
+        ns = rng.choice(names)
+        av = "v1" if i % 10 else "v2"
+        n_svc += av == "v1"
+        objs.append({"apiVersion": av, "kind": "Service", "metadata": {"name": "svc-%d" % i, "namespace": ns},
+                     "spec": {"selector": {"app": "app-%d" % rng.randint(0, 9)}}})
+        nss.append(ns_objs[ns])
+    for i in range(100):
+        ns = rng.choice(names)
+        objs.append({"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d-%d" % i, "namespace": ns}})
+        nss.append(ns_objs[ns])
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, nss)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.fallback == n_svc, rep
+    assert all(res.status[i] == 0 for i in range(len(pods)))
+    assert all(res.reason[i] == 12 for i in range(len(objs)) if res.status[i] & 2)  # FB_TEMPLATE
+    assert rep.violations > 5000
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
 
 
 def test_config2_in_kernel_formatting(monkeypatch):

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export GKGPU_JIT_CACHE=0
 run() {
   echo "== $1" >> gpurun_out/diag3.log
-  timeout -k 10 150 python -u tests/probe_repeat.py 1000000 K8sContainerLimits 2>&1 | tail -3 >> gpurun_out/diag3.log || { echo "FAIL $1"; exit 1; }
+  timeout -k 10 150 python -u tools/probe_repeat.py 1000000 K8sContainerLimits 2>&1 | tail -3 >> gpurun_out/diag3.log || { echo "FAIL $1"; exit 1; }
 }
 GKGPU_JIT_PRE= run base
 GKGPU_JIT_PRE=GK_BCAP=1024 run bcap1024

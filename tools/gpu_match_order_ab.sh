@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU diagnostic: config 2 and config 4 bench with the match-affinity review
-# order off (0) and on (1), alternated, then the staged-batch parity tests.
+# order in mode 1 (signature first) and mode 2 (default: kind, elements, signature, nodes),
+# alternated, then the staged-batch parity tests (engine.cc env_mode documents the modes).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out

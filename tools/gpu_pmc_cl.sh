@@ -17,6 +17,6 @@ P=(
 i=0
 for p in "${P[@]}"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $p -d "$OUT/p$i" -o run -- python3 "$ROOT/tests/probe_repeat.py" 1000000 K8sContainerLimits > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; }
+  timeout -s KILL 240 rocprofv3 --pmc $p -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/probe_repeat.py" 1000000 K8sContainerLimits > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; }
   echo "pass $i done"
 done
