@@ -173,6 +173,7 @@ enum ReviewColFlags : uint32_t {
   RC_NAME_OK = 256,       // object.metadata.name defined (for Namespace kinds)
   RC_FALLBACK = 512,      // review shape outside the match fast path
   RC_REVIEW_DEF = 1024,   // input.review defined
+  RC_EXCLUDED = 2048,     // namespace excluded for the audit process (excluder.go:82-86): not reviewed
 };
 
 struct ReviewCol {
@@ -192,13 +193,18 @@ struct ReviewCol {
 static_assert(sizeof(ReviewCol) == 48, "ReviewCol layout");
 
 // ----------------------------------------------------------------- output
+// One violation tuple.  Byte offsets are 64-bit: a 10M-resource sweep can
+// write more than 4 GiB of message bytes in one call.  The details JSON
+// follows the message: [msg_off, +msg_len) then [msg_off + msg_len, +det_len).
 struct Viol {
   uint32_t review;
   uint32_t constraint;
-  uint32_t seq;       // emission order within (review, constraint)
-  uint32_t rule;      // template rule index (0xffff = autoreject)
-  uint32_t msg_off, msg_len;
-  uint32_t det_off, det_len;
+  uint16_t seq;       // emission order within (review, constraint)
+  uint16_t rule;      // template rule index (0xffff = autoreject)
+  uint32_t msg_len;
+  uint64_t msg_off;
+  uint32_t det_len;
+  uint32_t pad;
 };
 static_assert(sizeof(Viol) == 32, "Viol layout");
 
@@ -233,12 +239,12 @@ struct DevArgs {
   const uint32_t* clist;      // constraints this launch evaluates (wave -> tile x clist[j])
   uint32_t nclist;
   Viol* out;
-  uint32_t out_cap;
-  uint32_t* counters;         // [0] = tuples, [1] = bytes
+  uint64_t out_cap;
+  unsigned long long* counters;  // [0] = tuples, [1] = bytes, [2] = lanes that flagged their review
   char* bytes;
-  uint32_t bytes_cap;
+  uint64_t bytes_cap;
   uint32_t* rflags;
-  uint32_t* totals;           // per constraint violation count
+  unsigned long long* totals;    // per constraint violation count
   uint32_t* rreason;          // per review fallback reason (diagnostic)
   unsigned int* pchist;       // optional (GKGPU_PROFILE=2): executions per bytecode pc
   unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]

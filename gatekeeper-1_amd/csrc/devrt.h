@@ -526,11 +526,12 @@ struct Cnt {
 };
 struct GOut {
   uint8_t* base;
-  uint32_t start, pos, acc;
+  uint64_t start, pos;
+  uint32_t acc;
   bool ovf;
-  __device__ __forceinline__ void word(uint32_t w) {
+  __device__ __forceinline__ void word(uint64_t w) {
     if (w >= start) *(uint32_t*)(base + w) = acc;
-    else for (uint32_t i = start - w; i < 4; ++i) base[w + i] = (uint8_t)(acc >> (8 * i));
+    else for (uint32_t i = (uint32_t)(start - w); i < 4; ++i) base[w + i] = (uint8_t)(acc >> (8 * i));
   }
   __device__ __forceinline__ void put(char c) {
     acc |= (uint32_t)(uint8_t)c << ((pos & 3) * 8);
@@ -538,8 +539,8 @@ struct GOut {
   }
   __device__ __forceinline__ void finish() {
     if (pos & 3) {
-      uint32_t w = pos & ~3u, lo = w > start ? w : start;
-      for (uint32_t i = lo; i < pos; ++i) base[i] = (uint8_t)(acc >> (8 * (i - w)));
+      uint64_t w = pos & ~(uint64_t)3, lo = w > start ? w : start;
+      for (uint64_t i = lo; i < pos; ++i) base[i] = (uint8_t)(acc >> (8 * (i - w)));
     }
   }
 };
@@ -1000,11 +1001,11 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
   uint32_t tt, tb;
   uint32_t pt = wave_excl_scan(nt, lane, tt);
   uint32_t pb = wave_excl_scan(nb, lane, tb);
-  uint32_t bt = 0, bb = 0;
+  uint64_t bt = 0, bb = 0;
   if (lane == 63 && tt) {
-    bt = atomicAdd(&gk_args.counters[0], tt);
-    bb = atomicAdd(&gk_args.counters[1], tb);
-    atomicAdd(&gk_args.totals[c], tt);
+    bt = atomicAdd(&gk_args.counters[0], (unsigned long long)tt);
+    bb = atomicAdd(&gk_args.counters[1], (unsigned long long)tb);
+    atomicAdd(&gk_args.totals[c], (unsigned long long)tt);
   }
   if (!tt) return;
   bt = __shfl(bt, 63, 64) + pt;
@@ -1044,12 +1045,12 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
     Viol v;
     v.review = r;
     v.constraint = c;
-    v.seq = i;
+    v.seq = (uint16_t)i;
     v.rule = L.em_rule[i];
     v.msg_off = bb;
     v.msg_len = ml;
-    v.det_off = bb + ml;
     v.det_len = dl;
+    v.pad = 0;
     gk_args.out[bt + i] = v;
     bb += ml + dl;
   }
@@ -1697,7 +1698,7 @@ __device__ __forceinline__ void audit_body(Run run) {
       }
     }
     if (L.fail) {
-      atomicAdd(&gk_args.counters[2], 1u);
+      atomicAdd(&gk_args.counters[2], 1ull);
       atomicOr(&gk_args.rflags[r], L.fail);
       if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
     }

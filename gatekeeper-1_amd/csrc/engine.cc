@@ -8,6 +8,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <thread>
@@ -16,6 +17,7 @@
 #include "../../include/gkgpu.h"
 #include "common.h"
 #include "compiler.h"
+#include "flatten.h"
 #include "jit.h"
 #include "json.h"
 #include "rego.h"
@@ -113,6 +115,8 @@ struct gk_results {
   uint32_t nrev = 0;
   std::vector<uint64_t> totals;
   std::vector<std::string> ckind, cname, cea;
+  std::vector<uint8_t> cea_error;          // per constraint: non-string enforcementAction (Query error)
+  uint64_t excluded = 0;                   // reviews skipped by the process excluder
   double ms[5] = {0, 0, 0, 0, 0};
   uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
   const void* d_tuples = nullptr;          // engine-owned device output of this call (valid
@@ -124,11 +128,16 @@ struct gk_results {
 };
 
 struct gk_batch {
+  gk_engine* eng = nullptr;
   uint64_t node_count = 0, str_bytes = 0;  // algorithmic input bytes of the staged documents
+  bool str_bytes_done = false;
   uint64_t gen = 0;
   uint32_t nrev = 0;
   uint32_t node_begin = 0, node_end = 0;
+  uint64_t excluded = 0;                    // reviews skipped by the process excluder
+  double ms_parse = 0, ms_flatten = 0, ms_upload = 0;
   std::vector<gk::ReviewCol> cols;
+  std::vector<gk::ResourceIds> resources;   // HandleViolation identity per batch index
   gk::DBuf d_revs;
   gk::DBuf d_nodes;  // the batch's own device node array: permanent region + its documents
   uint64_t dev_bytes = 0;
@@ -168,6 +177,8 @@ struct gk_engine {
   std::map<std::string, std::string> inventory;  // external path -> json
   std::map<std::string, uint32_t> ns_cache;       // namespace name -> node (permanent)
   std::map<std::string, std::string> other_data;
+  // process excluder (pkg/controller/config/process/excluder.go): process -> namespaces
+  std::map<std::string, std::set<std::string>> excluded;
   uint32_t perm_nodes = 0;                        // nodes below this are permanent
   uint64_t gen = 1;                               // bumps on any mutation
   // regex
@@ -192,34 +203,6 @@ static void reset_transient(gk_engine* e) {
 }
 
 namespace gk {
-
-// ------------------------------------------------------------------ node helpers (host)
-static uint32_t nget(const Store& st, uint32_t node, uint32_t key) {
-  if (node == NO_ID) return NO_ID;
-  const Node& n = st.nodes()[node];
-  if (n.type != NT_OBJ) return NO_ID;
-  for (uint32_t i = 0; i < n.n; ++i) if (st.nodes()[n.first + i].key == key) return n.first + i;
-  return NO_ID;
-}
-static uint32_t nget(Store& st, uint32_t node, const char* key) {
-  uint32_t k = st.find(key, strlen(key));
-  return k == NO_ID ? NO_ID : nget(st, node, k);
-}
-static inline uint8_t ntype(const Store& st, uint32_t n) { return n == NO_ID ? NT_NONE : st.nodes()[n].type; }
-static bool nstr(const Store& st, uint32_t n, uint32_t* sid) {
-  if (n == NO_ID || st.nodes()[n].type != NT_STR) return false;
-  *sid = st.nodes()[n].val;
-  return true;
-}
-static bool is_empty_obj(const Store& st, uint32_t n) { return n != NO_ID && st.nodes()[n].type == NT_OBJ && st.nodes()[n].n == 0; }
-static bool truthy(const Store& st, uint32_t n) { return n != NO_ID && st.nodes()[n].type != NT_FALSE; }
-
-// get_default (target_template_source.go:110-125): missing / null -> default (NO_ID == {})
-static uint32_t gdef(Store& st, uint32_t obj, const char* key) {
-  uint32_t v = nget(st, obj, key);
-  if (v == NO_ID || st.nodes()[v].type == NT_NULL) return NO_ID;
-  return v;
-}
 
 // ------------------------------------------------------------------ path helpers
 static std::vector<std::string> split_path(const std::string& p) {
@@ -599,197 +582,6 @@ static void rebuild_regex(gk_engine* e) {
   }
 }
 
-// ------------------------------------------------------------------ review flattening
-struct ReviewBuild {
-  ReviewCol col{};
-};
-
-// Computes match columns for a flattened review document (target_template_source.go).
-static ReviewCol review_columns(gk_engine* e, uint32_t root) {
-  Store& st = e->st;
-  ReviewCol rc{};
-  rc.root = root;
-  rc.orig = NO_ID;
-  rc.group = rc.kind = rc.ns = rc.nsname = NO_ID;
-  rc.labels = rc.old_labels = rc.ns_labels = NO_ID;
-  if (root == NO_ID) return rc;  // input.review undefined: nothing matches
-  if (ntype(st, root) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-  rc.flags |= RC_REVIEW_DEF;
-  uint32_t kind = nget(st, root, st.s_kind);
-  if (kind != NO_ID) {
-    if (ntype(st, kind) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-    rc.flags |= RC_KIND_OK;
-    uint32_t g = nget(st, kind, st.s_group), k = nget(st, kind, st.s_kind);
-    if (g != NO_ID && ntype(st, g) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
-    if (k != NO_ID && ntype(st, k) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
-    if (g != NO_ID) rc.group = st.nodes()[g].val;
-    if (k != NO_ID) rc.kind = st.nodes()[k].val;
-    if (rc.group == st.s_empty && rc.kind == st.s_Namespace) rc.flags |= RC_IS_NS;
-  }
-  uint32_t ns = nget(st, root, st.s_namespace);
-  if (ns != NO_ID) {
-    if (ntype(st, ns) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
-    rc.flags |= RC_HAS_NS;
-    rc.ns = st.nodes()[ns].val;
-    if (rc.ns == st.s_empty) rc.flags |= RC_NS_EMPTY;
-  } else {
-    rc.flags |= RC_NS_EMPTY;
-  }
-  uint32_t obj = nget(st, root, st.s_object);
-  uint32_t old = nget(st, root, st.s_oldObject);
-  if (rc.flags & RC_IS_NS) {
-    uint32_t nm = NO_ID;
-    uint32_t md = ntype(st, obj) == NT_OBJ ? nget(st, obj, st.s_metadata) : NO_ID;
-    if (ntype(st, md) == NT_OBJ) nm = nget(st, md, st.s_name);
-    if (nm != NO_ID) {
-      if (ntype(st, nm) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
-      rc.nsname = st.nodes()[nm].val;
-      rc.flags |= RC_NAME_OK;
-    }
-  } else {
-    rc.nsname = rc.ns;
-  }
-  // object / oldObject emptiness: get_default(review, "object", {}) == {}
-  auto empty = [&](uint32_t n) { return n == NO_ID || ntype(st, n) == NT_NULL || is_empty_obj(st, n); };
-  auto labels_of = [&](uint32_t o, uint32_t* out) -> bool {
-    uint32_t md = ntype(st, o) == NT_OBJ ? gdef(st, o, "metadata") : NO_ID;
-    if (md != NO_ID && ntype(st, md) != NT_OBJ) { *out = NO_ID; return ntype(st, o) == NT_OBJ ? false : true; }
-    uint32_t lb = md == NO_ID ? NO_ID : gdef(st, md, "labels");
-    if (lb == NO_ID) { *out = NO_ID; return true; }
-    if (ntype(st, lb) != NT_OBJ) return false;
-    const Node ln = st.nodes()[lb];
-    for (uint32_t i = 0; i < ln.n; ++i) if (st.nodes()[ln.first + i].type != NT_STR) return false;
-    *out = lb;
-    return true;
-  };
-  bool oe = empty(obj), le = empty(old);
-  if (!oe && ntype(st, obj) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-  if (!le && ntype(st, old) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-  if (!oe) { if (!labels_of(obj, &rc.labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OBJ; }
-  if (!le) { if (!labels_of(old, &rc.old_labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OLD; }
-  // namespace object for namespaceSelector: _unstable.namespace, else the cache
-  uint32_t un = nget(st, root, st.s_unstable);
-  uint32_t unns = ntype(st, un) == NT_OBJ ? nget(st, un, st.s_namespace) : NO_ID;
-  if (un != NO_ID && ntype(st, un) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-  auto ns_labels = [&](uint32_t nsobj) -> bool {
-    uint32_t md = gdef(st, nsobj, "metadata");
-    if (md != NO_ID && ntype(st, md) != NT_OBJ) return false;
-    uint32_t lb = md == NO_ID ? NO_ID : gdef(st, md, "labels");
-    if (lb != NO_ID) {
-      if (ntype(st, lb) != NT_OBJ) return false;
-      const Node ln = st.nodes()[lb];
-      for (uint32_t i = 0; i < ln.n; ++i) if (st.nodes()[ln.first + i].type != NT_STR) return false;
-    }
-    rc.ns_labels = lb;
-    return true;
-  };
-  if (unns != NO_ID) {
-    if (ntype(st, unns) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-    rc.flags |= RC_UNSTABLE_NS;
-    if (!ns_labels(unns)) { rc.flags |= RC_FALLBACK; return rc; }
-  } else if (rc.flags & RC_HAS_NS) {
-    auto it = e->ns_cache.find(std::string(st.str(rc.ns)));
-    if (it != e->ns_cache.end()) {
-      uint32_t nsn = it->second;
-      if (ntype(st, nsn) == NT_FALSE) {
-        // falsy cached value: not "cached" for autoreject, no get_ns solution
-      } else {
-        if (ntype(st, nsn) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
-        rc.flags |= RC_NS_CACHED;
-        if (!ns_labels(nsn)) { rc.flags |= RC_FALLBACK; return rc; }
-      }
-    }
-  }
-  return rc;
-}
-
-// Review(AugmentedUnstructured{obj, ns}) envelope (pkg/target/target.go:129-163,
-// admission/v1beta1 AdmissionRequest json field order).
-static uint32_t build_object_review(gk_engine* e, const JDoc& od, int oj, const JDoc& nd, int nj, uint32_t ns_root,
-                                    const std::string& nsname_in) {
-  Store& st = e->st;
-  std::string apiv, kind, name;
-  int av = od.get(oj, "apiVersion");
-  if (av >= 0 && od.nodes[av].type == NT_STR) apiv = od.sval(av);
-  int kd = od.get(oj, "kind");
-  if (kd >= 0 && od.nodes[kd].type == NT_STR) kind = od.sval(kd);
-  int md = od.get(oj, "metadata");
-  if (md >= 0) { int nm = od.get(md, "name"); if (nm >= 0 && od.nodes[nm].type == NT_STR) name = od.sval(nm); }
-  std::string group, version;
-  size_t slash = apiv.find('/');
-  if (slash == std::string::npos) version = apiv;
-  else if (apiv.find('/', slash + 1) == std::string::npos) { group = apiv.substr(0, slash); version = apiv.substr(slash + 1); }
-  std::string nsname = nsname_in;
-  if (ns_root == NO_ID) {
-    int nmd = nd.get(nj, "metadata");
-    if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
-  }
-  // children: uid kind resource [name] [namespace] operation userInfo object oldObject options _unstable
-  uint32_t nch = 9 + (name.empty() ? 0 : 1) + (nsname.empty() ? 0 : 1);
-  uint32_t root = st.add_node(Node{});
-  uint32_t first = st.reserve(nch);
-  {
-    Node& r = st.nodes()[root];
-    r.type = NT_OBJ;
-    r.first = first;
-    r.n = (uint16_t)nch;
-  }
-  uint32_t i = first;
-  auto str_node = [&](uint32_t idx, uint32_t key, const std::string& v) {
-    Node n{};
-    n.key = key;
-    n.type = NT_STR;
-    n.val = st.intern(v);
-    st.nodes()[idx] = n;
-  };
-  auto obj3 = [&](uint32_t idx, uint32_t key, uint32_t k1, const std::string& v1, uint32_t k2, const std::string& v2,
-                  uint32_t k3, const std::string& v3) {
-    uint32_t f = st.reserve(3);
-    str_node(f, k1, v1);
-    str_node(f + 1, k2, v2);
-    str_node(f + 2, k3, v3);
-    Node n{};
-    n.key = key;
-    n.type = NT_OBJ;
-    n.first = f;
-    n.n = 3;
-    st.nodes()[idx] = n;
-  };
-  str_node(i++, st.s_uid, "");
-  obj3(i++, st.s_kind, st.s_group, group, st.s_version, version, st.s_kind, kind);
-  obj3(i++, st.s_resource, st.s_group, "", st.s_version, "", st.s_resource, "");
-  if (!name.empty()) str_node(i++, st.s_name, name);
-  if (!nsname.empty()) str_node(i++, st.s_namespace, nsname);
-  str_node(i++, st.s_operation, "");
-  { Node n{}; n.key = st.s_userInfo; n.type = NT_OBJ; st.nodes()[i++] = n; }
-  uint32_t objslot = i++;
-  { Node n{}; n.key = st.s_oldObject; n.type = NT_NULL; st.nodes()[i++] = n; }
-  { Node n{}; n.key = st.s_options; n.type = NT_NULL; st.nodes()[i++] = n; }
-  uint32_t unslot = i++;
-  // object subtree
-  uint32_t o = st.add_doc(od, oj);
-  {
-    Node n = st.nodes()[o];
-    n.key = st.s_object;
-    st.nodes()[objslot] = n;
-  }
-  // _unstable: {"namespace": <ns>}
-  uint32_t nsroot = ns_root != NO_ID ? ns_root : st.add_doc(nd, nj);
-  uint32_t uf = st.reserve(1);
-  {
-    Node n = st.nodes()[nsroot];
-    n.key = st.s_namespace;
-    st.nodes()[uf] = n;
-    Node u{};
-    u.key = st.s_unstable;
-    u.type = NT_OBJ;
-    u.first = uf;
-    u.n = 1;
-    st.nodes()[unslot] = u;
-  }
-  return root;
-}
-
 // ------------------------------------------------------------------ device sync + launch
 static bool ensure_device(gk_engine* e) {
   if (e->dev_ok) return true;
@@ -881,19 +673,33 @@ static void ensure_jit(gk_engine* e, bool load) {
 
 // runs the kernel over `cols` (already resident in d_revs when `resident`)
 static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, DBuf* revbuf, bool decode,
-                              gk_results* res, const void* nodes = nullptr) {
+                              gk_results* res, const void* nodes = nullptr, uint64_t n_excluded = 0) {
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
   res->nrev = nrev;
+  res->excluded = n_excluded;
   res->totals.assign(ncons, 0);
-  for (auto* c : e->corder) { res->ckind.push_back(c->kind); res->cname.push_back(c->name); res->cea.push_back(c->ea); }
+  for (auto* c : e->corder) {
+    res->ckind.push_back(c->kind);
+    res->cname.push_back(c->name);
+    res->cea.push_back(c->ea);
+    res->cea_error.push_back(c->ea_error);
+  }
   if (nrev == 0) return GK_OK;
+  // reviews the process excluder skipped (manager.go:362-365) carry GK_REVIEW_EXCLUDED
+  auto mark_excluded = [&]() {
+    if (!n_excluded) return;
+    if (res->status.empty()) { res->status.assign(nrev, 0); res->reason.assign(nrev, 0); }
+    for (uint32_t r = 0; r < nrev; ++r)
+      if (cols[r].flags & RC_EXCLUDED) res->status[cols[r].orig == NO_ID ? r : cols[r].orig] |= GK_REVIEW_EXCLUDED;
+  };
   // reviews flagged for fallback on the host never reach the device when there are no constraints
   if (ncons == 0) {
     res->status.assign(nrev, 0);
     res->reason.assign(nrev, 0);
     for (uint32_t r = 0; r < nrev; ++r)
       if (cols[r].flags & RC_FALLBACK) res->status[cols[r].orig == NO_ID ? r : cols[r].orig] = GK_REVIEW_FALLBACK;
+    mark_excluded();
     return GK_OK;
   }
   if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
@@ -903,8 +709,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     if (!up(*revbuf, cols, false)) return fail(e, GK_EDEVICE, "device upload failed");
   }
   bool ok = true;
-  ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 4) &&
-        e->d_counters.reserve(64 + 8 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
+  ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 8) &&
+        e->d_counters.reserve(64 + 16 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
   // deferred-message records for the format pass (GKGPU_FORMAT_PASS=0: format in the audit kernels)
   const bool fpass = env_mode("GKGPU_FORMAT_PASS", 1, 1) != 0;
@@ -936,8 +742,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
   for (int attempt = 0; attempt < 4; ++attempt) {
     hipMemsetAsync(e->d_rflags.p, 0, nrev * 4, e->stream);
     hipMemsetAsync(e->d_rreason.p, 0, nrev * 4, e->stream);
-    hipMemsetAsync(e->d_totals.p, 0, ncons * 4, e->stream);
-    hipMemsetAsync(e->d_counters.p, 0, 64 + 8 * plan.size(), e->stream);
+    hipMemsetAsync(e->d_totals.p, 0, ncons * 8, e->stream);
+    hipMemsetAsync(e->d_counters.p, 0, 64 + 16 * plan.size(), e->stream);
     bool prof = e->profile && e->d_prof.reserve(ncons * 32);
     if (prof) hipMemsetAsync(e->d_prof.p, 0, ncons * 32, e->stream);
     DevArgs a{};
@@ -967,12 +773,12 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     a.nrev = nrev;
     a.ntiles = (nrev + 63) / 64;
     a.out = (Viol*)e->d_out.p;
-    a.out_cap = (uint32_t)e->out_cap;
-    a.counters = (uint32_t*)e->d_counters.p;
+    a.out_cap = e->out_cap;
+    a.counters = (unsigned long long*)e->d_counters.p;
     a.bytes = (char*)e->d_bytes.p;
-    a.bytes_cap = (uint32_t)e->bytes_cap;
+    a.bytes_cap = e->bytes_cap;
     a.rflags = (uint32_t*)e->d_rflags.p;
-    a.totals = (uint32_t*)e->d_totals.p;
+    a.totals = (unsigned long long*)e->d_totals.p;
     a.rreason = (uint32_t*)e->d_rreason.p;
     a.frec = fpass ? (uint64_t*)e->d_frec.p : nullptr;
     while (e->events.size() < plan.size() + 2) {
@@ -1006,7 +812,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       }
       hipEventRecord(ev[i + 1], e->stream);
       // cumulative (tuples, bytes) after this launch -> per-launch output counts
-      hipMemcpyAsync((char*)e->d_counters.p + 64 + 8 * i, e->d_counters.p, 8, hipMemcpyDeviceToDevice, e->stream);
+      hipMemcpyAsync((char*)e->d_counters.p + 64 + 16 * i, e->d_counters.p, 16, hipMemcpyDeviceToDevice, e->stream);
       if (lr != 0) {
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
@@ -1019,13 +825,13 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
     res->launches.clear();
-    std::vector<uint32_t> snap(2 * plan.size());
-    hipMemcpy(snap.data(), (char*)e->d_counters.p + 64, 8 * plan.size(), hipMemcpyDeviceToHost);
+    std::vector<uint64_t> snap(2 * plan.size());
+    hipMemcpy(snap.data(), (char*)e->d_counters.p + 64, 16 * plan.size(), hipMemcpyDeviceToHost);
     for (size_t i = 0; i < plan.size(); ++i) {
       float kms = 0;
       hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
       res->ms[2] += kms;
-      uint32_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
+      uint64_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
       res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
     if (fpass) {
@@ -1036,8 +842,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     auto t1 = Clock::now();
     // [0] tuples, [1] message bytes, [2] lanes that flagged their review (error/fallback)
-    uint32_t counters[3];
-    hipMemcpy(counters, e->d_counters.p, 12, hipMemcpyDeviceToHost);
+    uint64_t counters[3];
+    hipMemcpy(counters, e->d_counters.p, 24, hipMemcpyDeviceToHost);
     if (counters[0] > e->out_cap || counters[1] > e->bytes_cap) {
       e->out_cap = std::max<size_t>(e->out_cap * 2, counters[0] + 1024);
       e->bytes_cap = std::max<size_t>(e->bytes_cap * 2, (size_t)counters[1] + 65536);
@@ -1051,8 +857,8 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     res->d_tuples = e->d_out.p;
     res->d_bytes = e->d_bytes.p;
     res->epoch = ++e->eval_epoch;
-    std::vector<uint32_t> tot(ncons);
-    hipMemcpy(tot.data(), e->d_totals.p, ncons * 4, hipMemcpyDeviceToHost);
+    std::vector<uint64_t> tot(ncons);
+    hipMemcpy(tot.data(), e->d_totals.p, ncons * 8, hipMemcpyDeviceToHost);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
     bool ea_err = false;
     for (auto* c : e->corder) ea_err |= c->ea_error;
@@ -1060,6 +866,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       // nothing flagged: per-review status stays implicit (all zero), so the
       // audit step downloads a few counters instead of 8 bytes per review
       res->ms[3] = ms_since(t1);
+      mark_excluded();
       return GK_OK;
     }
     res->status.assign(nrev, 0);
@@ -1076,7 +883,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     bool flagged = false;
     for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
-    if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); return GK_OK; }
+    if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); mark_excluded(); return GK_OK; }
     std::vector<Viol> vs(counters[0]);
     std::string bytes;
     if (counters[0]) hipMemcpy(vs.data(), e->d_out.p, counters[0] * sizeof(Viol), hipMemcpyDeviceToHost);
@@ -1096,6 +903,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       if (!(res->status[v.review] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK))) res->totals[v.constraint]++;
     if (!decode) {
       for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+      mark_excluded();
       res->ms[4] = ms_since(t2);
       return GK_OK;
     }
@@ -1116,10 +924,11 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       row.seq = v.seq;
       row.rule = v.rule;
       row.msg.assign(bytes.data() + v.msg_off, v.msg_len);
-      row.details.assign(bytes.data() + v.det_off, v.det_len);
+      row.details.assign(bytes.data() + v.msg_off + v.msg_len, v.det_len);
       res->rows.push_back(std::move(row));
     }
     for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+    mark_excluded();
     res->ms[4] = ms_since(t2);
     return GK_OK;
   }
@@ -1335,7 +1144,8 @@ static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, si
     if (root < 0) { delete res; return fail(e, GK_EINVAL, "invalid input JSON: " + d.err); }
     int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
     uint32_t rn = rv >= 0 ? e->st.add_doc(d, rv) : NO_ID;
-    cols.push_back(review_columns(e, rn));
+    bool glob = false;
+    cols.push_back(review_columns(e->st, e->st, e->ns_cache, rn, &glob));
   }
   res->ms[0] = ms_since(t0);
   int rc = launch_and_collect(e, cols, &e->d_revs, true, res);
@@ -1396,51 +1206,23 @@ int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, 
   return eval_inputs(e, in, out);
 }
 
-static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
-                           const size_t* ns_lens, size_t n, std::vector<ReviewCol>& cols, bool order_by_size) {
-  JDoc od, nd;
-  std::vector<uint32_t> weight;
-  weight.reserve(n);
-  std::string empty_ns = EMPTY_NS_JSON;
-  // a namespace document is shared by all objects of the namespace: flatten each
-  // distinct namespace text once and point every review's _unstable.namespace at it
-  std::unordered_map<std::string, std::pair<uint32_t, std::string>> ns_nodes;
-  for (size_t i = 0; i < n; ++i) {
-    JsonReader ro(objs[i], obj_lens ? obj_lens[i] : strlen(objs[i]), &od);
-    int oj = ro.parse();
-    if (oj < 0) return fail(e, GK_EINVAL, "invalid object JSON at " + std::to_string(i) + ": " + od.err);
-    const char* ns = (ns_json && ns_json[i]) ? ns_json[i] : nullptr;
-    size_t nl = ns ? (ns_lens ? ns_lens[i] : strlen(ns)) : 0;
-    if (!ns || nl == 0) { ns = empty_ns.data(); nl = empty_ns.size(); }
-    std::string key(ns, nl);
-    auto it = ns_nodes.find(key);
-    uint32_t nsroot = NO_ID;
-    std::string nsname;
-    int nj = 0;
-    if (it != ns_nodes.end()) {
-      nsroot = it->second.first;
-      nsname = it->second.second;
-    } else {
-      JsonReader rn(ns, nl, &nd);
-      nj = rn.parse();
-      if (nj < 0) return fail(e, GK_EINVAL, "invalid namespace JSON at " + std::to_string(i) + ": " + nd.err);
-      int nmd = nd.get(nj, "metadata");
-      if (nmd >= 0) { int nn = nd.get(nmd, "name"); if (nn >= 0 && nd.nodes[nn].type == NT_STR) nsname = nd.sval(nn); }
-      nsroot = e->st.add_doc(nd, nj);
-      ns_nodes[key] = {nsroot, nsname};
-    }
-    size_t n0 = e->st.nodes().size();
-    uint32_t root = build_object_review(e, od, oj, nd, nj, nsroot, nsname);
-    cols.push_back(review_columns(e, root));
-    // size key: array elements (what templates iterate: containers, ports,
-    // volumes ...) first, then document nodes
-    uint32_t elems = 0;
-    const auto& nv = e->st.nodes();
-    for (size_t k = n0; k < nv.size(); ++k)
-      if (nv[k].type == NT_ARR) elems += nv[k].n;
-    uint32_t nn = (uint32_t)(nv.size() - n0);
-    weight.push_back((std::min<uint32_t>(elems, 0xfff) << 20) | std::min<uint32_t>(nn, 0xfffff));
-  }
+// Flattens one page of audit objects (flatten.cc, parallel host threads) and,
+// for staged batches, chooses the evaluation order.  `out` receives the
+// columns (in evaluation order; each carries its batch index in `orig` when
+// reordered), the HandleViolation resource identity per batch index and the
+// number of reviews the process excluder skipped.
+static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size, std::vector<ReviewCol>& cols,
+                             std::vector<ResourceIds>* resources, uint64_t* excluded, double* ms_parse = nullptr) {
+  FlatResult fr;
+  std::string err;
+  auto exit_ = e->excluded.find("audit");
+  const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
+  if (!flatten_page(e->st, e->ns_cache, ex, page, default_threads(), fr, err)) return fail(e, GK_EINVAL, err);
+  if (ms_parse) *ms_parse = fr.ms_parse;
+  if (resources) resources->swap(fr.resources);
+  if (excluded) *excluded = fr.excluded;
+  cols.swap(fr.cols);
+  const std::vector<uint32_t>& weight = fr.weight;
   if (order_by_size) {
     // Divergence-aware order: a wavefront evaluates 64 consecutive reviews, and
     // its lanes run as long as the largest document (e.g. the Pod with the most
@@ -1510,10 +1292,59 @@ static int flatten_objects(gk_engine* e, const char* const* objs, const size_t* 
   return GK_OK;
 }
 
-int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
-                      const size_t* ns_lens, size_t n, gk_results** out) {
-  if (!e || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+// The char** form of a page: namespaces given per object are de-duplicated by
+// text into the page's namespace table (the audit loop's nsCache).
+struct PageBuf {
+  Page page;
+  std::vector<uint64_t> obj_offs, ns_offs;
+  std::string objs, nss;
+  std::vector<uint32_t> obj_ns;
+};
+
+static void page_from_arrays(const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                             const size_t* ns_lens, size_t n, PageBuf& pb) {
+  pb.obj_offs.resize(n + 1);
+  size_t tot = 0;
+  for (size_t i = 0; i < n; ++i) tot += obj_lens ? obj_lens[i] : strlen(objs[i]);
+  pb.objs.resize(tot);
+  uint64_t off = 0;
+  std::unordered_map<std::string_view, uint32_t> ns_idx;
+  pb.obj_ns.assign(n, NO_ID);
+  std::vector<std::string_view> ns_list;
+  for (size_t i = 0; i < n; ++i) {
+    size_t l = obj_lens ? obj_lens[i] : strlen(objs[i]);
+    pb.obj_offs[i] = off;
+    if (l) memcpy(&pb.objs[off], objs[i], l);
+    off += l;
+    const char* ns = (ns_json && ns_json[i]) ? ns_json[i] : nullptr;
+    size_t nl = ns ? (ns_lens ? ns_lens[i] : strlen(ns)) : 0;
+    if (!ns || nl == 0) continue;
+    std::string_view key(ns, nl);
+    auto it = ns_idx.find(key);
+    if (it == ns_idx.end()) {
+      it = ns_idx.emplace(key, (uint32_t)ns_list.size()).first;
+      ns_list.push_back(key);
+    }
+    pb.obj_ns[i] = it->second;
+  }
+  pb.obj_offs[n] = off;
+  pb.ns_offs.resize(ns_list.size() + 1);
+  uint64_t no = 0;
+  for (size_t k = 0; k < ns_list.size(); ++k) { pb.ns_offs[k] = no; no += ns_list[k].size(); }
+  pb.ns_offs[ns_list.size()] = no;
+  pb.nss.resize(no);
+  for (size_t k = 0; k < ns_list.size(); ++k)
+    if (!ns_list[k].empty()) memcpy(&pb.nss[pb.ns_offs[k]], ns_list[k].data(), ns_list[k].size());
+  pb.page.objs = pb.objs.data();
+  pb.page.obj_offs = pb.obj_offs.data();
+  pb.page.n = n;
+  pb.page.nss = pb.nss.data();
+  pb.page.ns_offs = pb.ns_offs.data();
+  pb.page.n_ns = ns_list.size();
+  pb.page.obj_ns = pb.obj_ns.data();
+}
+
+static int review_page(gk_engine* e, const Page& page, gk_results** out) {
   auto* res = new gk_results();
   try {
     rebuild_constraints(e);
@@ -1525,35 +1356,53 @@ int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_l
   auto t0 = Clock::now();
   reset_transient(e);
   std::vector<ReviewCol> cols;
-  cols.reserve(n);
-  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, cols, false);
+  uint64_t excluded = 0;
+  int rc = flatten_page_into(e, page, false, cols, nullptr, &excluded);
   if (rc != GK_OK) { delete res; return rc; }
   res->ms[0] = ms_since(t0);
-  rc = launch_and_collect(e, cols, &e->d_revs, true, res);
+  rc = launch_and_collect(e, cols, &e->d_revs, true, res, nullptr, excluded);
   if (rc != GK_OK) { delete res; return rc; }
   *out = res;
   return GK_OK;
 }
 
-int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
-                           const size_t* ns_lens, size_t n, gk_batch** out) {
-  if (!e || !out) return GK_EINVAL;
+int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                      const size_t* ns_lens, size_t n, gk_results** out) {
+  if (!e || !out || (n && !objs)) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
+  PageBuf pb;
+  page_from_arrays(objs, obj_lens, ns_json, ns_lens, n, pb);
+  return review_page(e, pb.page, out);
+}
+
+int gk_review_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
+                   const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_results** out) {
+  if (!e || !out || (n && (!objs || !obj_offs)) || (n_ns && (!nss || !ns_offs))) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
+  return review_page(e, pg, out);
+}
+
+static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
   try {
     rebuild_constraints(e);
     rebuild_regex(e);
   } catch (const std::exception& ex) {
     return fail(e, GK_EPARSE, ex.what());
   }
+  auto t0 = Clock::now();
   auto* b = new gk_batch();
+  b->eng = e;
   reset_transient(e);
   b->node_begin = (uint32_t)e->st.nodes().size();
   const bool size_order = env_mode("GKGPU_SIZE_ORDER", 1, 1) != 0;  // A/B switch (default on)
-  int rc = flatten_objects(e, objs, obj_lens, ns_json, ns_lens, n, b->cols, size_order);
+  int rc = flatten_page_into(e, page, size_order, b->cols, &b->resources, &b->excluded, &b->ms_parse);
   if (rc != GK_OK) { delete b; return rc; }
+  b->ms_flatten = ms_since(t0);
   b->node_end = (uint32_t)e->st.nodes().size();
-  b->nrev = (uint32_t)n;
+  b->nrev = (uint32_t)page.n;
   b->gen = e->gen;
+  auto t1 = Clock::now();
   if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
   if (!sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
       !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
@@ -1562,18 +1411,57 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
     delete b;
     return fail(e, GK_EDEVICE, "upload failed");
   }
+  b->ms_upload = ms_since(t1);
   b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
-  {
-    // one pass over every staged document node and each distinct string value it references
-    std::vector<uint8_t> seen(e->st.nstrings(), 0);
-    b->node_count = b->node_end - b->node_begin;
-    for (uint32_t k = b->node_begin; k < b->node_end; ++k) {
-      const Node& nd = e->st.nodes()[k];
-      if (nd.type == NT_STR && !seen[nd.val]) { seen[nd.val] = 1; b->str_bytes += e->st.strings()[nd.val].len; }
-    }
-  }
+  b->node_count = b->node_end - b->node_begin;
   *out = b;
   return GK_OK;
+}
+
+int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
+                           const size_t* ns_lens, size_t n, gk_batch** out) {
+  if (!e || !out || (n && !objs)) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  PageBuf pb;
+  page_from_arrays(objs, obj_lens, ns_json, ns_lens, n, pb);
+  return stage_page(e, pb.page, out);
+}
+
+int gk_batch_stage_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
+                        const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_batch** out) {
+  if (!e || !out || (n && (!objs || !obj_offs)) || (n_ns && (!nss || !ns_offs))) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
+  return stage_page(e, pg, out);
+}
+
+int gk_batch_timing(const gk_batch* b, double* ms3) {
+  if (!b || !ms3) return GK_EINVAL;
+  ms3[0] = b->ms_parse;
+  ms3[1] = b->ms_flatten;
+  ms3[2] = b->ms_upload;
+  return GK_OK;
+}
+
+uint64_t gk_batch_excluded(const gk_batch* b) { return b ? b->excluded : 0; }
+
+int gk_batch_resource(gk_engine* e, const gk_batch* b, size_t review, gk_resource* out) {
+  if (!e || !b || !out || review >= b->resources.size()) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  const ResourceIds& r = b->resources[review];
+  auto put = [&](char* dst, uint32_t sid) {
+    std::string_view v = e->st.str(sid);
+    size_t n = std::min<size_t>(v.size(), GK_RESOURCE_FIELD - 1);
+    memcpy(dst, v.data(), n);
+    dst[n] = 0;
+    return v.size() < GK_RESOURCE_FIELD;
+  };
+  int cut = !put(out->api_version, r.api_version);
+  cut += !put(out->kind, r.kind);
+  cut += !put(out->name, r.name);
+  cut += !put(out->namespace_, r.ns);
+  bool ok = cut == 0;
+  return ok ? GK_OK : GK_ERANGE;
 }
 
 int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
@@ -1582,7 +1470,7 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
   auto* res = new gk_results();
   const void* nodes = b->d_nodes.p;
-  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, nodes);
+  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, nodes, b->excluded);
   if (rc != GK_OK) { delete res; return rc; }
   *out = res;
   return GK_OK;
@@ -1597,8 +1485,23 @@ void gk_batch_free(gk_batch* b) {
 
 uint64_t gk_batch_device_bytes(const gk_batch* b) { return b ? b->dev_bytes : 0; }
 
-int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes) {
-  if (!b) return GK_EINVAL;
+int gk_batch_stats(const gk_batch* cb, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes) {
+  if (!cb) return GK_EINVAL;
+  gk_batch* b = const_cast<gk_batch*>(cb);
+  if (str_bytes && !b->str_bytes_done && b->eng && b->gen == b->eng->gen) {
+    // one pass over every staged document node and each distinct string value
+    // it references (computed on first request: not part of staging)
+    std::lock_guard<std::mutex> g(b->eng->mu);
+    const Store& st = b->eng->st;
+    if (b->node_end <= st.nodes().size()) {
+      std::vector<uint8_t> seen(st.nstrings(), 0);
+      for (uint32_t k = b->node_begin; k < b->node_end; ++k) {
+        const Node& nd = st.nodes()[k];
+        if (nd.type == NT_STR && !seen[nd.val]) { seen[nd.val] = 1; b->str_bytes += st.strings()[nd.val].len; }
+      }
+      b->str_bytes_done = true;
+    }
+  }
   if (reviews) *reviews = b->nrev;
   if (nodes) *nodes = b->node_count;
   if (str_bytes) *str_bytes = b->str_bytes;
@@ -1694,6 +1597,37 @@ int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* by
   return GK_OK;
 }
 
+int gk_excluder_add(gk_engine* e, const char* const* processes, size_t np, const char* const* namespaces, size_t nn) {
+  if (!e || (np && !processes) || (nn && !namespaces)) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  static const char* all[] = {"audit", "webhook", "sync"};  // excluder.go allProcesses
+  for (size_t i = 0; i < nn; ++i)
+    for (size_t j = 0; j < np; ++j) {
+      if (!namespaces[i] || !processes[j]) return GK_EINVAL;
+      if (!strcmp(processes[j], "*")) for (const char* p : all) e->excluded[p].insert(namespaces[i]);
+      else e->excluded[processes[j]].insert(namespaces[i]);
+    }
+  e->gen++;  // staged batches applied the previous exclusions
+  return GK_OK;
+}
+
+int gk_excluder_clear(gk_engine* e) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->excluded.clear();
+  e->gen++;
+  return GK_OK;
+}
+
+int gk_excluder_is_excluded(gk_engine* e, const char* process, const char* ns) {
+  if (!e || !process || !ns) return 0;
+  std::lock_guard<std::mutex> g(e->mu);
+  auto it = e->excluded.find(process);
+  return it != e->excluded.end() && it->second.count(ns) ? 1 : 0;
+}
+
+uint64_t gk_results_excluded(const gk_results* r) { return r ? r->excluded : 0; }
+
 int gk_dump(gk_engine* e, char** out) {
   if (!e || !out) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
@@ -1784,6 +1718,59 @@ int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** n
 }  // extern "C"
 
 // ------------------------------------------------------------------ diagnostics
+// Flattens a page on `threads` host threads without a device (diagnostics and
+// CPU tests): *hash = content hash over every review's columns and document,
+// ms2 = [parse + build, total flatten].  The documents are dropped afterwards.
+extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n,
+                                     const char* nss, const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns,
+                                     int threads, uint64_t* hash, uint64_t* nodes, double* ms2) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    rebuild_constraints(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  reset_transient(e);
+  Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
+  FlatResult fr;
+  std::string err;
+  auto t0 = Clock::now();
+  auto exit_ = e->excluded.find("audit");
+  const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
+  if (!flatten_page(e->st, e->ns_cache, ex, pg, threads > 0 ? threads : default_threads(), fr, err))
+    return fail(e, GK_EINVAL, err);
+  double tot = ms_since(t0);
+  uint64_t h = 0;
+  for (size_t i = 0; i < fr.cols.size(); ++i) {
+    const ReviewCol& c = fr.cols[i];
+    auto sh = [&](uint32_t sid) -> uint64_t {
+      if (sid == NO_ID) return 7;
+      std::string_view v = e->st.str(sid);
+      return fnv1a(v.data(), v.size());
+    };
+    uint64_t x = doc_hash(e->st, c.root) * 31 + sh(c.group);
+    x = x * 31 + sh(c.kind);
+    x = x * 31 + sh(c.ns);
+    x = x * 31 + sh(c.nsname);
+    x = x * 31 + doc_hash(e->st, c.labels);
+    x = x * 31 + doc_hash(e->st, c.old_labels);
+    x = x * 31 + doc_hash(e->st, c.ns_labels);
+    x = x * 31 + c.flags;
+    const ResourceIds& r = fr.resources[i];
+    x = x * 31 + sh(r.api_version);
+    x = x * 31 + sh(r.kind);
+    x = x * 31 + sh(r.name);
+    x = x * 31 + sh(r.ns);
+    h = (h ^ x) * 1099511628211ull + i;
+  }
+  if (hash) *hash = h;
+  if (nodes) *nodes = fr.node_count;
+  if (ms2) { ms2[0] = fr.ms_parse; ms2[1] = tot; }
+  reset_transient(e);
+  return GK_OK;
+}
+
 extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   if (!e || !kind || !out) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);

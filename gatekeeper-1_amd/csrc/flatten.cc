@@ -1,0 +1,467 @@
+// Parallel host flattener (see flatten.h).
+//
+// Phase 1 (parallel): each thread parses a contiguous range of the page's
+// objects and builds their review documents in a thread-local Store (its own
+// string / number interning, its own node arena; the well-known strings have
+// the same ids in every Store because every Store interns them first).
+// Phase 2 (serial, small): every thread's distinct strings and numbers are
+// interned into the engine's Store, giving per-thread id maps.
+// Phase 3 (parallel): each thread copies its nodes into the engine arena at its
+// offset, rewriting string / number ids and child indices, and relocates its
+// review columns.
+#include "flatten.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+
+namespace gk {
+
+static const char* EMPTY_NS_JSON = "{\"metadata\":{\"creationTimestamp\":null},\"spec\":{},\"status\":{}}";
+static constexpr uint32_t kFixedNodes = 4;  // every Store starts with nodes {} null false true
+
+int default_threads() {
+  const char* v = getenv("GKGPU_THREADS");
+  if (v && *v) {
+    int n = atoi(v);
+    if (n >= 1 && n <= 256) return n;
+  }
+  unsigned hc = std::thread::hardware_concurrency();
+  // the GPU box grants a 16-CPU share whatever the machine's CPU count
+  return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+}
+
+ReviewCol review_columns(const Store& st, const Store& gst, const NsCache& ns_cache, uint32_t root,
+                         bool* ns_labels_global) {
+  ReviewCol rc{};
+  *ns_labels_global = false;
+  rc.root = root;
+  rc.orig = NO_ID;
+  rc.group = rc.kind = rc.ns = rc.nsname = NO_ID;
+  rc.labels = rc.old_labels = rc.ns_labels = NO_ID;
+  if (root == NO_ID) return rc;  // input.review undefined: nothing matches
+  if (ntype(st, root) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  rc.flags |= RC_REVIEW_DEF;
+  uint32_t kind = nget(st, root, st.s_kind);
+  if (kind != NO_ID) {
+    if (ntype(st, kind) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_KIND_OK;
+    uint32_t g = nget(st, kind, st.s_group), k = nget(st, kind, st.s_kind);
+    if (g != NO_ID && ntype(st, g) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    if (k != NO_ID && ntype(st, k) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    if (g != NO_ID) rc.group = st.nodes()[g].val;
+    if (k != NO_ID) rc.kind = st.nodes()[k].val;
+    if (rc.group == st.s_empty && rc.kind == st.s_Namespace) rc.flags |= RC_IS_NS;
+  }
+  uint32_t ns = nget(st, root, st.s_namespace);
+  if (ns != NO_ID) {
+    if (ntype(st, ns) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_HAS_NS;
+    rc.ns = st.nodes()[ns].val;
+    if (rc.ns == st.s_empty) rc.flags |= RC_NS_EMPTY;
+  } else {
+    rc.flags |= RC_NS_EMPTY;
+  }
+  uint32_t obj = nget(st, root, st.s_object);
+  uint32_t old = nget(st, root, st.s_oldObject);
+  if (rc.flags & RC_IS_NS) {
+    uint32_t nm = NO_ID;
+    uint32_t md = ntype(st, obj) == NT_OBJ ? nget(st, obj, st.s_metadata) : NO_ID;
+    if (ntype(st, md) == NT_OBJ) nm = nget(st, md, st.s_name);
+    if (nm != NO_ID) {
+      if (ntype(st, nm) != NT_STR) { rc.flags |= RC_FALLBACK; return rc; }
+      rc.nsname = st.nodes()[nm].val;
+      rc.flags |= RC_NAME_OK;
+    }
+  } else {
+    rc.nsname = rc.ns;
+  }
+  // object / oldObject emptiness: get_default(review, "object", {}) == {}
+  auto empty = [&](uint32_t n) { return n == NO_ID || ntype(st, n) == NT_NULL || is_empty_obj(st, n); };
+  auto labels_of = [&](uint32_t o, uint32_t* out) -> bool {
+    uint32_t md = ntype(st, o) == NT_OBJ ? gdef(st, o, "metadata") : NO_ID;
+    if (md != NO_ID && ntype(st, md) != NT_OBJ) { *out = NO_ID; return ntype(st, o) == NT_OBJ ? false : true; }
+    uint32_t lb = md == NO_ID ? NO_ID : gdef(st, md, "labels");
+    if (lb == NO_ID) { *out = NO_ID; return true; }
+    if (ntype(st, lb) != NT_OBJ) return false;
+    const Node ln = st.nodes()[lb];
+    for (uint32_t i = 0; i < ln.n; ++i) if (st.nodes()[ln.first + i].type != NT_STR) return false;
+    *out = lb;
+    return true;
+  };
+  bool oe = empty(obj), le = empty(old);
+  if (!oe && ntype(st, obj) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  if (!le && ntype(st, old) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  if (!oe) { if (!labels_of(obj, &rc.labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OBJ; }
+  if (!le) { if (!labels_of(old, &rc.old_labels)) { rc.flags |= RC_FALLBACK; return rc; } rc.flags |= RC_LABELS_OLD; }
+  // namespace object for namespaceSelector: _unstable.namespace, else the cache
+  uint32_t un = nget(st, root, st.s_unstable);
+  uint32_t unns = ntype(st, un) == NT_OBJ ? nget(st, un, st.s_namespace) : NO_ID;
+  if (un != NO_ID && ntype(st, un) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+  auto ns_labels = [&](const Store& s, uint32_t nsobj) -> bool {
+    uint32_t md = gdef(s, nsobj, "metadata");
+    if (md != NO_ID && ntype(s, md) != NT_OBJ) return false;
+    uint32_t lb = md == NO_ID ? NO_ID : gdef(s, md, "labels");
+    if (lb != NO_ID) {
+      if (ntype(s, lb) != NT_OBJ) return false;
+      const Node ln = s.nodes()[lb];
+      for (uint32_t i = 0; i < ln.n; ++i) if (s.nodes()[ln.first + i].type != NT_STR) return false;
+    }
+    rc.ns_labels = lb;
+    return true;
+  };
+  if (unns != NO_ID) {
+    if (ntype(st, unns) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+    rc.flags |= RC_UNSTABLE_NS;
+    if (!ns_labels(st, unns)) { rc.flags |= RC_FALLBACK; return rc; }
+  } else if (rc.flags & RC_HAS_NS) {
+    auto it = ns_cache.find(std::string(st.str(rc.ns)));
+    if (it != ns_cache.end()) {
+      uint32_t nsn = it->second;
+      if (ntype(gst, nsn) == NT_FALSE) {
+        // falsy cached value: not "cached" for autoreject, no get_ns solution
+      } else {
+        if (ntype(gst, nsn) != NT_OBJ) { rc.flags |= RC_FALLBACK; return rc; }
+        rc.flags |= RC_NS_CACHED;
+        if (!ns_labels(gst, nsn)) { rc.flags |= RC_FALLBACK; return rc; }
+        *ns_labels_global = rc.ns_labels != NO_ID;
+      }
+    }
+  }
+  return rc;
+}
+
+namespace {
+
+struct NsDoc {
+  uint32_t root = NO_ID;   // placed root node of the Namespace document
+  std::string name;        // metadata.name ("" when absent)
+  uint32_t sid = NO_ID;    // its string id
+};
+
+// string id of member `key` of the object record `o`, if it is a string
+inline uint32_t member_str(const Store& st, const Node& o, uint32_t key) {
+  if (o.type != NT_OBJ) return NO_ID;
+  const Node* c = st.nodes().data() + o.first;
+  for (uint32_t i = 0; i < o.n; ++i)
+    if (c[i].key == key) return c[i].type == NT_STR ? c[i].val : NO_ID;
+  return NO_ID;
+}
+inline const Node* member(const Store& st, const Node& o, uint32_t key) {
+  if (o.type != NT_OBJ) return nullptr;
+  const Node* c = st.nodes().data() + o.first;
+  for (uint32_t i = 0; i < o.n; ++i)
+    if (c[i].key == key) return &c[i];
+  return nullptr;
+}
+
+struct Keys {
+  uint32_t apiVersion;
+  explicit Keys(Store& st) : apiVersion(st.intern("apiVersion")) {}
+};
+
+// Review(AugmentedUnstructured{obj, ns}) envelope (pkg/target/target.go:129-163,
+// admission/v1beta1 AdmissionRequest json field order):
+//   uid kind resource [name] [namespace] operation userInfo object oldObject options _unstable
+// `obj` is the object's parsed root record (Store::parse_doc).
+uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const NsDoc& ns, ResourceIds* res) {
+  uint32_t s_apiv = member_str(st, obj, K.apiVersion);
+  uint32_t s_kind = member_str(st, obj, st.s_kind);
+  uint32_t s_name = NO_ID, s_objns = NO_ID;
+  if (const Node* md = member(st, obj, st.s_metadata)) {
+    s_name = member_str(st, *md, st.s_name);
+    s_objns = member_str(st, *md, st.s_namespace);
+  }
+  if (s_apiv == NO_ID) s_apiv = st.s_empty;
+  if (s_kind == NO_ID) s_kind = st.s_empty;
+  if (s_name == NO_ID) s_name = st.s_empty;
+  if (s_objns == NO_ID) s_objns = st.s_empty;
+  // schema.ParseGroupVersion: "v" -> ("", v), "g/v" -> (g, v), more slashes -> ("", "")
+  uint32_t s_group = st.s_empty, s_version = st.s_empty;
+  {
+    std::string apiv(st.str(s_apiv));
+    size_t slash = apiv.find('/');
+    if (slash == std::string::npos) s_version = s_apiv;
+    else if (apiv.find('/', slash + 1) == std::string::npos) {
+      s_group = st.intern(apiv.data(), slash);
+      s_version = st.intern(apiv.data() + slash + 1, apiv.size() - slash - 1);
+    }
+  }
+  const bool has_name = s_name != st.s_empty, has_ns = !ns.name.empty();
+  uint32_t nch = 9 + (has_name ? 1 : 0) + (has_ns ? 1 : 0);
+  // the envelope: root, its children, kind{3}, resource{3}, _unstable{1}
+  uint32_t root = (uint32_t)st.nodes().size();
+  st.nodes().resize(root + 1 + nch + 3 + 3 + 1);
+  Node* N = st.nodes().data();
+  uint32_t first = root + 1, kf = first + nch, rf = kf + 3, uf = rf + 3;
+  auto obj_node = [&](uint32_t key, uint32_t f, uint32_t n) { Node x{}; x.key = key; x.type = NT_OBJ; x.first = f; x.n = (uint16_t)n; return x; };
+  auto str_node = [&](uint32_t key, uint32_t sid) { Node x{}; x.key = key; x.type = NT_STR; x.val = sid; return x; };
+  auto lit_node = [&](uint32_t key, uint8_t t) { Node x{}; x.key = key; x.type = t; return x; };
+  N[root] = obj_node(0, first, nch);
+  uint32_t i = first;
+  N[i++] = str_node(st.s_uid, st.s_empty);
+  N[i++] = obj_node(st.s_kind, kf, 3);
+  N[i++] = obj_node(st.s_resource, rf, 3);
+  if (has_name) N[i++] = str_node(st.s_name, s_name);
+  if (has_ns) N[i++] = str_node(st.s_namespace, ns.sid);
+  N[i++] = str_node(st.s_operation, st.s_empty);
+  N[i++] = obj_node(st.s_userInfo, 0, 0);
+  Node o = obj;
+  o.key = st.s_object;
+  N[i++] = o;
+  N[i++] = lit_node(st.s_oldObject, NT_NULL);
+  N[i++] = lit_node(st.s_options, NT_NULL);
+  N[i++] = obj_node(st.s_unstable, uf, 1);
+  N[kf] = str_node(st.s_group, s_group);
+  N[kf + 1] = str_node(st.s_version, s_version);
+  N[kf + 2] = str_node(st.s_kind, s_kind);
+  N[rf] = str_node(st.s_group, st.s_empty);
+  N[rf + 1] = str_node(st.s_version, st.s_empty);
+  N[rf + 2] = str_node(st.s_resource, st.s_empty);
+  // _unstable: {"namespace": <ns>} (the page's shared Namespace document)
+  Node nsn = N[ns.root];
+  nsn.key = st.s_namespace;
+  N[uf] = nsn;
+  // HandleViolation: apiVersion = group/version (version alone when group is "")
+  res->api_version = s_group == st.s_empty ? s_version : s_apiv;
+  res->kind = s_kind;
+  res->name = s_name;
+  res->ns = s_objns;
+  return root;
+}
+
+struct Part {
+  Store st;
+  size_t lo = 0, hi = 0;
+  std::vector<ReviewCol> cols;
+  std::vector<uint8_t> nsglob;       // per review: rc.ns_labels is a global node
+  std::vector<uint32_t> weight;
+  std::vector<ResourceIds> res;
+  uint64_t excluded = 0;
+  std::string err;
+  // phase 2 maps (local id -> global id)
+  std::vector<uint32_t> smap, nmap;
+  uint64_t node_off = 0;             // global index of this part's node kFixedNodes
+};
+
+void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set<std::string>* ex, const Page& pg) {
+  Store& st = p.st;
+  const Keys K(st);
+  std::vector<NsDoc> ns_docs(pg.n_ns);
+  NsDoc empty_ns;
+  const size_t n = p.hi - p.lo;
+  p.cols.reserve(n);
+  p.nsglob.reserve(n);
+  p.weight.reserve(n);
+  p.res.reserve(n);
+  // about one node per 9 bytes of JSON for these documents, plus the envelopes
+  st.nodes().reserve((pg.obj_offs[p.hi] - pg.obj_offs[p.lo]) / 8 + n * 20 + 1024);
+  std::string err;
+  auto ns_doc = [&](uint32_t k) -> NsDoc* {
+    NsDoc* d = k == NO_ID || k >= pg.n_ns ? &empty_ns : &ns_docs[k];
+    if (d->root != NO_ID) return d;
+    const char* s = EMPTY_NS_JSON;
+    size_t len = strlen(EMPTY_NS_JSON);
+    if (d != &empty_ns) { s = pg.nss + pg.ns_offs[k]; len = pg.ns_offs[k + 1] - pg.ns_offs[k]; }
+    Node r;
+    if (!st.parse_doc(s, len, &r, &err)) { p.err = "invalid namespace JSON at " + std::to_string(k) + ": " + err; return nullptr; }
+    if (const Node* md = member(st, r, st.s_metadata)) {
+      uint32_t nm = member_str(st, *md, st.s_name);
+      if (nm != NO_ID) { d->name = std::string(st.str(nm)); d->sid = nm; }
+    }
+    d->root = st.add_node(r);
+    return d;
+  };
+  for (size_t i = p.lo; i < p.hi; ++i) {
+    size_t n0 = st.nodes().size();
+    Node obj;
+    if (!st.parse_doc(pg.objs + pg.obj_offs[i], pg.obj_offs[i + 1] - pg.obj_offs[i], &obj, &err)) {
+      p.err = "invalid object JSON at " + std::to_string(i) + ": " + err;
+      return;
+    }
+    if (ex && !ex->empty()) {
+      uint32_t ons = NO_ID;
+      if (const Node* md = member(st, obj, st.s_metadata)) ons = member_str(st, *md, st.s_namespace);
+      if (ex->count(ons == NO_ID ? std::string() : std::string(st.str(ons)))) {
+        st.nodes().resize(n0);  // drop the object's nodes
+        ReviewCol rc{};
+        rc.root = NO_ID;
+        rc.group = rc.kind = rc.ns = rc.nsname = rc.labels = rc.old_labels = rc.ns_labels = NO_ID;
+        rc.orig = NO_ID;
+        rc.flags = RC_EXCLUDED;  // no RC_REVIEW_DEF: the match stage skips it
+        p.cols.push_back(rc);
+        p.nsglob.push_back(0);
+        p.weight.push_back(0);
+        p.res.push_back(ResourceIds{st.s_empty, st.s_empty, st.s_empty, st.s_empty});
+        ++p.excluded;
+        continue;
+      }
+    }
+    NsDoc* ns = ns_doc(pg.obj_ns ? pg.obj_ns[i] : NO_ID);
+    if (!ns) return;
+    ResourceIds rid{};
+    uint32_t root = build_object_review(st, K, obj, *ns, &rid);
+    bool glob = false;
+    p.cols.push_back(review_columns(st, gst, ns_cache, root, &glob));
+    p.nsglob.push_back(glob);
+    p.res.push_back(rid);
+    // size key: array elements (what templates iterate: containers, ports,
+    // volumes ...) first, then document nodes
+    uint32_t elems = 0;
+    const Node* nv = st.nodes().data();
+    const size_t n1 = st.nodes().size();
+    for (size_t k = n0; k < n1; ++k)
+      if (nv[k].type == NT_ARR) elems += nv[k].n;
+    uint32_t nn = (uint32_t)(n1 - n0);
+    p.weight.push_back((std::min<uint32_t>(elems, 0xfff) << 20) | std::min<uint32_t>(nn, 0xfffff));
+  }
+}
+
+}  // namespace
+
+bool flatten_page(Store& gst, const NsCache& ns_cache, const std::set<std::string>* excluded, const Page& pg,
+                  int threads, FlatResult& out, std::string& err) {
+  using Clock = std::chrono::steady_clock;
+  auto t0 = Clock::now();
+  const size_t n = pg.n;
+  int T = std::max(1, threads);
+  // at least ~2k objects per thread: below that the merge costs more than it saves
+  T = (int)std::min<size_t>((size_t)T, std::max<size_t>(1, n / 2048));
+  std::vector<Part> parts(T);
+  for (int t = 0; t < T; ++t) {
+    parts[t].lo = n * t / T;
+    parts[t].hi = n * (t + 1) / T;
+  }
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { run_part(parts[t], gst, ns_cache, excluded, pg); });
+    run_part(parts[0], gst, ns_cache, excluded, pg);
+    for (auto& x : th) x.join();
+  }
+  for (auto& p : parts)
+    if (!p.err.empty()) { err = p.err; return false; }
+  auto t1 = Clock::now();
+  // phase 2: intern every part's strings and numbers into the engine store
+  const uint32_t nwell = Store().nstrings();  // well-known ids shared by every Store
+  size_t extra = 0;
+  for (auto& p : parts) extra += p.st.nstrings() - nwell;
+  gst.reserve_strings(extra);
+  for (auto& p : parts) {
+    const Store& ls = p.st;
+    p.smap.resize(ls.nstrings());
+    for (uint32_t s = 0; s < nwell; ++s) p.smap[s] = s;
+    for (uint32_t s = nwell; s < ls.nstrings(); ++s) {
+      std::string_view v = ls.str(s);
+      p.smap[s] = gst.intern(v.data(), v.size());
+    }
+    const auto& nums = ls.numbers();
+    p.nmap.resize(nums.size());
+    for (uint32_t k = 0; k < nums.size(); ++k) {
+      std::string_view v = ls.str(nums[k].text);
+      p.nmap[k] = gst.number(v.data(), v.size());
+    }
+  }
+  auto t15 = Clock::now();
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "flatten: parse %.1f ms, intern %.1f ms (%zu strings)\n",
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t15 - t1).count(), extra);
+  // phase 3: relocate nodes and columns into the engine arena
+  uint64_t base = gst.nodes().size(), total = 0;
+  for (auto& p : parts) {
+    p.node_off = base + total;
+    total += p.st.nodes().size() - kFixedNodes;
+  }
+  if (base + total >= NO_ID) { err = "node arena exceeds 2^32 nodes"; return false; }
+  auto tr0 = Clock::now();
+  gst.nodes().resize(base + total);
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "flatten: arena resize %.1f ms\n", std::chrono::duration<double, std::milli>(Clock::now() - tr0).count());
+  out.cols.resize(n);
+  out.weight.resize(n);
+  out.resources.resize(n);
+  {
+    Node* dst = gst.nodes().data();
+    auto relocate = [&](Part& p) {
+      const auto& ln = p.st.nodes();
+      const uint32_t off = (uint32_t)p.node_off - kFixedNodes;
+      auto node = [&](uint32_t x) { return x == NO_ID ? NO_ID : x + off; };
+      auto str = [&](uint32_t s) { return s == NO_ID ? NO_ID : p.smap[s]; };
+      for (size_t k = kFixedNodes; k < ln.size(); ++k) {
+        Node x = ln[k];
+        if (x.type == NT_STR) x.val = p.smap[x.val];
+        else if (x.type == NT_NUM) x.val = p.nmap[x.val];
+        else if ((x.type == NT_ARR || x.type == NT_OBJ) && x.n) x.first += off;
+        dst[k + off] = x;
+      }
+      // object member keys: rewrite in the copied arena (a child is copied
+      // before or after its parent; keys are only meaningful under objects)
+      for (size_t k = kFixedNodes; k < ln.size(); ++k) {
+        const Node& x = ln[k];
+        if (x.type != NT_OBJ) continue;
+        for (uint32_t c = 0; c < x.n; ++c) dst[x.first + off + c].key = p.smap[ln[x.first + c].key];
+      }
+      for (size_t i = 0; i < p.cols.size(); ++i) {
+        ReviewCol rc = p.cols[i];
+        rc.root = node(rc.root);
+        rc.group = str(rc.group);
+        rc.kind = str(rc.kind);
+        rc.ns = str(rc.ns);
+        rc.nsname = str(rc.nsname);
+        rc.labels = node(rc.labels);
+        rc.old_labels = node(rc.old_labels);
+        if (!p.nsglob[i]) rc.ns_labels = node(rc.ns_labels);
+        out.cols[p.lo + i] = rc;
+        out.weight[p.lo + i] = p.weight[i];
+        const ResourceIds& r = p.res[i];
+        out.resources[p.lo + i] = ResourceIds{str(r.api_version), str(r.kind), str(r.name), str(r.ns)};
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { relocate(parts[t]); });
+    relocate(parts[0]);
+    for (auto& x : th) x.join();
+  }
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "flatten: relocate %.1f ms\n", std::chrono::duration<double, std::milli>(Clock::now() - t15).count());
+  out.excluded = 0;
+  for (auto& p : parts) out.excluded += p.excluded;
+  out.node_count = total;
+  auto t2 = Clock::now();
+  out.ms_parse = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  out.ms_merge = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  return true;
+}
+
+}  // namespace gk
+
+namespace gk {
+
+// Content hash of a document (type, keys, string / number text, structure),
+// independent of node and string ids: compares flattenings across thread counts.
+uint64_t doc_hash(const Store& st, uint32_t node) {
+  if (node == NO_ID) return 0x9e3779b97f4a7c15ull;
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) { h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2); };
+  auto mixs = [&](uint32_t sid) { std::string_view v = st.str(sid); mix(fnv1a(v.data(), v.size())); };
+  std::vector<std::pair<uint32_t, bool>> stack{{node, false}};
+  while (!stack.empty()) {
+    auto [k, obj_child] = stack.back();
+    stack.pop_back();
+    const Node& x = st.nodes()[k];
+    mix(x.type);
+    if (obj_child) mixs(x.key);
+    if (x.type == NT_STR) mixs(x.val);
+    else if (x.type == NT_NUM) mixs(st.numbers()[x.val].text);
+    else if (x.type == NT_ARR || x.type == NT_OBJ) {
+      mix(x.n);
+      for (uint32_t c = x.n; c-- > 0;) stack.push_back({x.first + c, x.type == NT_OBJ});
+    }
+  }
+  return h;
+}
+
+}  // namespace gk

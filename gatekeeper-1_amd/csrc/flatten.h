@@ -1,0 +1,101 @@
+// Host flattener: Kubernetes objects (JSON text) -> review documents in the
+// interned node arena + per-review match columns, on many host threads.
+//
+// Replaces the per-object JSON round trips of the reference audit loop
+// (pkg/target/target.go:129-163 json.Marshal into AdmissionRequest.Object,
+// drivers/local/local.go:331 MarshalIndent, rego.go:1478-1496 RoundTrip +
+// InterfaceToValue) with one parse per object into a layout the kernels read.
+#pragma once
+#include <stdint.h>
+
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "json.h"
+#include "store.h"
+
+namespace gk {
+
+// ------------------------------------------------------------------ node helpers (host)
+inline uint32_t nget(const Store& st, uint32_t node, uint32_t key) {
+  if (node == NO_ID) return NO_ID;
+  const Node& n = st.nodes()[node];
+  if (n.type != NT_OBJ) return NO_ID;
+  for (uint32_t i = 0; i < n.n; ++i) if (st.nodes()[n.first + i].key == key) return n.first + i;
+  return NO_ID;
+}
+inline uint32_t nget(const Store& st, uint32_t node, const char* key) {
+  uint32_t k = st.find(key, strlen(key));
+  return k == NO_ID ? NO_ID : nget(st, node, k);
+}
+inline uint8_t ntype(const Store& st, uint32_t n) { return n == NO_ID ? NT_NONE : st.nodes()[n].type; }
+inline bool nstr(const Store& st, uint32_t n, uint32_t* sid) {
+  if (n == NO_ID || st.nodes()[n].type != NT_STR) return false;
+  *sid = st.nodes()[n].val;
+  return true;
+}
+inline bool is_empty_obj(const Store& st, uint32_t n) { return n != NO_ID && st.nodes()[n].type == NT_OBJ && st.nodes()[n].n == 0; }
+// get_default (target_template_source.go:110-125): missing / null -> default (NO_ID == {})
+inline uint32_t gdef(const Store& st, uint32_t obj, const char* key) {
+  uint32_t v = nget(st, obj, key);
+  if (v == NO_ID || st.nodes()[v].type == NT_NULL) return NO_ID;
+  return v;
+}
+
+// The synced Namespace cache data.external[target].cluster.v1.Namespace
+// (node ids in the engine's global store).
+using NsCache = std::map<std::string, uint32_t>;
+
+// Match columns of a review document rooted at `root` in `st`
+// (target_template_source.go:131-386 inputs).  Cached namespaces are nodes of
+// `gst` (the engine's store); *ns_labels_global reports that rc.ns_labels
+// refers to one of them rather than to a node of `st`.
+ReviewCol review_columns(const Store& st, const Store& gst, const NsCache& ns_cache, uint32_t root,
+                         bool* ns_labels_global);
+
+// One page of audit objects: concatenated JSON texts and, per object, the
+// index of its Namespace object (nsCache.Get, pkg/audit/manager.go:96-115;
+// NO_ID = cluster-scoped, reviewed with an empty corev1.Namespace{}).
+struct Page {
+  const char* objs = nullptr;
+  const uint64_t* obj_offs = nullptr;  // n + 1 offsets
+  size_t n = 0;
+  const char* nss = nullptr;
+  const uint64_t* ns_offs = nullptr;   // n_ns + 1 offsets
+  size_t n_ns = 0;
+  const uint32_t* obj_ns = nullptr;    // per object: namespace index or NO_ID
+};
+
+// HandleViolation's Resource identity of a review (pkg/target/target.go:193-244):
+// apiVersion from review.kind {group, version}, kind = review.kind.kind, and
+// the object's metadata name / namespace (unstructured GetName/GetNamespace).
+struct ResourceIds {
+  uint32_t api_version, kind, name, ns;  // global string ids
+};
+
+struct FlatResult {
+  std::vector<ReviewCol> cols;        // batch order (orig = NO_ID)
+  std::vector<uint32_t> weight;       // size key per review: array elements << 20 | nodes
+  std::vector<ResourceIds> resources; // per review (batch order)
+  uint64_t excluded = 0;              // reviews skipped by the process excluder
+  uint64_t node_count = 0;
+  double ms_parse = 0, ms_merge = 0;
+};
+
+// Flattens a page into `st` (appending documents to its node arena) on
+// `threads` host threads.  Objects whose metadata.namespace is in
+// `excluded_ns` (Excluder.IsNamespaceExcluded(Audit, ns), manager.go:362-365)
+// get a column flagged RC_EXCLUDED and no document.  Returns false with `err`
+// on malformed JSON.
+bool flatten_page(Store& st, const NsCache& ns_cache, const std::set<std::string>* excluded_ns, const Page& page,
+                  int threads, FlatResult& out, std::string& err);
+
+int default_threads();
+
+// id-independent content hash of the document rooted at `node`
+uint64_t doc_hash(const Store& st, uint32_t node);
+
+}  // namespace gk

@@ -249,31 +249,32 @@ class JsonReader {
   void dedupe(int o) {
     // encoding/json into map[string]interface{}: a later duplicate key replaces
     // the earlier value (and Go maps have no order anyway)
-    std::vector<int> kids;
-    for (int c = d_->nodes[o].first; c >= 0; c = d_->nodes[c].next) kids.push_back(c);
-    if (kids.size() < 2) return;
+    JNode* N = d_->nodes.data();
+    const char* B = d_->buf.data();
+    if (N[o].n < 2) return;
+    auto same = [&](int a, int b) { return N[a].k_len == N[b].k_len && memcmp(B + N[a].k_off, B + N[b].k_off, N[a].k_len) == 0; };
     bool dup = false;
-    for (size_t i = 0; i < kids.size() && !dup; ++i)
-      for (size_t j = i + 1; j < kids.size(); ++j) {
-        const JNode& a = d_->nodes[kids[i]];
-        const JNode& b = d_->nodes[kids[j]];
-        if (a.k_len == b.k_len && memcmp(d_->buf.data() + a.k_off, d_->buf.data() + b.k_off, a.k_len) == 0) { dup = true; break; }
-      }
+    for (int a = N[o].first; a >= 0 && !dup; a = N[a].next)
+      for (int b = N[a].next; b >= 0; b = N[b].next)
+        if (same(a, b)) { dup = true; break; }
     if (!dup) return;
-    std::vector<int> keep;
-    for (size_t i = 0; i < kids.size(); ++i) {
+    // keep each key's last occurrence, in source order
+    int head = -1, tail = -1;
+    uint32_t cnt = 0;
+    for (int a = N[o].first; a >= 0;) {
+      int next = N[a].next;
       bool later = false;
-      for (size_t j = i + 1; j < kids.size(); ++j) {
-        const JNode& a = d_->nodes[kids[i]];
-        const JNode& b = d_->nodes[kids[j]];
-        if (a.k_len == b.k_len && memcmp(d_->buf.data() + a.k_off, d_->buf.data() + b.k_off, a.k_len) == 0) { later = true; break; }
+      for (int b = next; b >= 0 && !later; b = N[b].next) later = same(a, b);
+      if (!later) {
+        if (tail < 0) head = a; else N[tail].next = a;
+        tail = a;
+        ++cnt;
       }
-      if (!later) keep.push_back(kids[i]);
+      a = next;
     }
-    d_->nodes[o].first = keep[0];
-    for (size_t i = 0; i + 1 < keep.size(); ++i) d_->nodes[keep[i]].next = keep[i + 1];
-    d_->nodes[keep.back()].next = -1;
-    d_->nodes[o].n = (uint32_t)keep.size();
+    N[tail].next = -1;
+    N[o].first = head;
+    N[o].n = cnt;
   }
 };
 

@@ -114,6 +114,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   for (int d = 32; d >= 1; d >>= 1) { uint32_t o = __shfl_xor(x, d, 64); x = o > x ? o : x; }
   return x;
 }
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint64_t o = __shfl_xor(x, d, 64); x = o < x ? o : x; }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint64_t o = __shfl_xor(x, d, 64); x = o > x ? o : x; }
+  return x;
+}
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
@@ -131,7 +141,7 @@ constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
 // into HBM.
 __global__ void __launch_bounds__(256) gk_format_kernel() {
   __shared__ uint32_t stage[4][FSTAGE / 4];
-  uint32_t n = gk_args.counters[0];
+  const uint64_t n = gk_args.counters[0];
   // an overflowed call left some reservations unwritten; the host retries it
   if (n > gk_args.out_cap || gk_args.counters[1] > gk_args.bytes_cap) return;
   Lane& L = g_fmt_lane;
@@ -139,22 +149,22 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
   uint32_t* st = stage[wv];
   uint8_t* stb = (uint8_t*)st;
   uint32_t* gw = (uint32_t*)gk_args.bytes;
-  for (uint32_t base = (blockIdx.x * 4 + wv) * 64; base < n; base += gridDim.x * 256) {  // wave-uniform
-    uint32_t i = base + lane;
+  for (uint64_t base = ((uint64_t)blockIdx.x * 4 + wv) * 64; base < n; base += (uint64_t)gridDim.x * 256) {  // wave-uniform
+    uint64_t i = base + lane;
     bool valid = i < n;
-    const uint64_t* w = gk_args.frec + (uint64_t)i * FREC_WORDS;
+    const uint64_t* w = gk_args.frec + i * FREC_WORDS;
     uint64_t h = valid ? w[0] : 0;
     Viol v{};
     if (valid) v = gk_args.out[i];
-    uint32_t end = v.msg_off + v.msg_len + v.det_len;
-    bool live = valid && (h & FREC_LIVE) && (uint64_t)v.msg_off + v.msg_len <= gk_args.bytes_cap;
+    uint64_t end = v.msg_off + v.msg_len + v.det_len;
+    bool live = valid && (h & FREC_LIVE) && v.msg_off + v.msg_len <= gk_args.bytes_cap;
     if (!__any(live)) continue;
-    uint32_t lo = wave_min(valid ? v.msg_off : 0xffffffffu);
-    uint32_t hi = wave_max(valid ? end : 0u);
+    uint64_t lo = wave_min64(valid ? v.msg_off : ~0ull);
+    uint64_t hi = wave_max64(valid ? end : 0ull);
     uint32_t tot = wave_sum(valid ? v.msg_len + v.det_len : 0u);
-    uint32_t lo4 = lo & ~3u, hi4 = (hi + 3) & ~3u;
+    uint64_t lo4 = lo & ~(uint64_t)3, hi4 = (hi + 3) & ~(uint64_t)3;
     if (tot == hi - lo && hi4 - lo4 <= FSTAGE && hi4 <= gk_args.bytes_cap) {
-      uint32_t nw = (hi4 - lo4) >> 2;
+      uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
       for (uint32_t k = lane; k < nw; k += 64) st[k] = gw[(lo4 >> 2) + k];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -165,7 +175,7 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       for (uint32_t k = lane; k < nw; k += 64) {
-        uint32_t a = lo4 + 4 * k;
+        uint64_t a = lo4 + 4 * (uint64_t)k;
         if (a >= lo && a + 4 <= hi) {
           gw[(lo4 >> 2) + k] = st[k];
         } else {

@@ -258,23 +258,47 @@ Store::Store() {
   e.type = NT_TRUE; nodes_.push_back(e);
 }
 
-void Store::grow() {
-  std::vector<uint32_t> t(table_.size() * 2, 0);
-  size_t mask = t.size() - 1;
+// Intern table: open addressing, one 64-bit slot per entry = hash tag (high 32
+// bits of the string hash) << 32 | (string id + 1); 0 = empty.  A probe only
+// touches the string table and pool when the tags agree.
+static inline uint64_t slot_of(uint64_t h, uint32_t id) { return (h & 0xffffffff00000000ull) | (uint64_t)(id + 1); }
+
+void Store::rehash(size_t sz) {
+  std::vector<uint64_t> t(sz, 0);
+  size_t mask = sz - 1;
   for (uint32_t id = 0; id < strs_.size(); ++id) {
-    size_t h = fnv1a(pool_.data() + strs_[id].off, strs_[id].len) & mask;
+    uint64_t hv = str_hash(pool_.data() + strs_[id].off, strs_[id].len);
+    size_t h = hv & mask;
     while (t[h]) h = (h + 1) & mask;
-    t[h] = id + 1;
+    t[h] = slot_of(hv, id);
   }
   table_.swap(t);
 }
 
+void Store::grow() { rehash(table_.size() * 2); }
+
+void Store::reserve_strings(size_t n) {
+  size_t want = (strs_.size() + n) * 2 + 1;
+  if (want > table_.size()) {
+    size_t sz = table_.size();
+    while (sz < want) sz *= 2;
+    rehash(sz);
+  }
+  strs_.reserve(strs_.size() + n);
+  sflags_.reserve(sflags_.size() + n);
+}
+
 uint32_t Store::find(const char* p, size_t n) const {
   size_t mask = table_.size() - 1;
-  size_t h = fnv1a(p, n) & mask;
-  while (uint32_t e = table_[h]) {
-    const StrEnt& s = strs_[e - 1];
-    if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return e - 1;
+  uint64_t hv = str_hash(p, n);
+  uint64_t tag = hv & 0xffffffff00000000ull;
+  size_t h = hv & mask;
+  while (uint64_t e = table_[h]) {
+    if ((e & 0xffffffff00000000ull) == tag) {
+      uint32_t id = (uint32_t)e - 1;
+      const StrEnt& s = strs_[id];
+      if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return id;
+    }
     h = (h + 1) & mask;
   }
   return NO_ID;
@@ -282,10 +306,15 @@ uint32_t Store::find(const char* p, size_t n) const {
 
 uint32_t Store::intern(const char* p, size_t n) {
   size_t mask = table_.size() - 1;
-  size_t h = fnv1a(p, n) & mask;
-  while (uint32_t e = table_[h]) {
-    const StrEnt& s = strs_[e - 1];
-    if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return e - 1;
+  uint64_t hv = str_hash(p, n);
+  uint64_t tag = hv & 0xffffffff00000000ull;
+  size_t h = hv & mask;
+  while (uint64_t e = table_[h]) {
+    if ((e & 0xffffffff00000000ull) == tag) {
+      uint32_t id = (uint32_t)e - 1;
+      const StrEnt& s = strs_[id];
+      if (s.len == n && memcmp(pool_.data() + s.off, p, n) == 0) return id;
+    }
     h = (h + 1) & mask;
   }
   uint32_t id = (uint32_t)strs_.size();
@@ -300,7 +329,7 @@ uint32_t Store::intern(const char* p, size_t n) {
     else if (c == '"' || c == '\\') fl |= SF_NEEDS_ESC;
   }
   sflags_.push_back(fl);
-  table_[h] = id + 1;
+  table_[h] = slot_of(hv, id);
   if (strs_.size() * 2 > table_.size()) grow();
   return id;
 }
@@ -354,13 +383,16 @@ uint32_t Store::reserve(uint32_t n) {
 uint32_t Store::add_doc(const JDoc& d, int j) {
   uint32_t root = (uint32_t)nodes_.size();
   nodes_.push_back(Node{});
-  std::deque<std::pair<int, uint32_t>> q;
-  q.emplace_back(j, root);
-  while (!q.empty()) {
-    auto [jn, an] = q.front();
-    q.pop_front();
-    const JNode& x = d.nodes[jn];
+  std::vector<BfsEnt>& q = bfs_;
+  q.clear();
+  q.push_back(BfsEnt{j, root, 0});
+  for (size_t qi = 0; qi < q.size(); ++qi) {
+    const BfsEnt be = q[qi];
+    const uint32_t an = be.an;
+    const JNode& x = d.nodes[be.jn];
     Node& out = nodes_[an];
+    out = Node{};
+    out.key = be.key;
     out.type = x.type;
     switch (x.type) {
       case NT_STR: out.val = intern(d.buf.data() + x.s_off, x.s_len); break;
@@ -375,16 +407,248 @@ uint32_t Store::add_doc(const JDoc& d, int j) {
         o2.first = first;
         o2.n = (uint16_t)cnt;
         uint32_t i = 0;
-        for (int c = x.first; c >= 0 && i < cnt; c = d.nodes[c].next, ++i) {
-          nodes_[first + i].key = x.type == NT_OBJ ? intern(d.buf.data() + d.nodes[c].k_off, d.nodes[c].k_len) : i;
-          q.emplace_back(c, first + i);
-        }
+        for (int c = x.first; c >= 0 && i < cnt; c = d.nodes[c].next, ++i)
+          q.push_back(BfsEnt{c, first + i, x.type == NT_OBJ ? intern(d.buf.data() + d.nodes[c].k_off, d.nodes[c].k_len) : i});
         break;
       }
       default: break;
     }
   }
   return root;
+}
+
+}  // namespace gk
+
+namespace gk {
+
+// Single-pass JSON -> node arena (Store::parse_doc).  Grammar and string
+// decoding follow JsonReader (json.h) exactly; only the output differs.
+class DocParser {
+ public:
+  DocParser(Store& st, const char* p, size_t n, std::string* err) : st_(st), p_(p), e_(p + n), err_(err) {}
+
+  bool run(Node* root) {
+    st_.pend_.clear();
+    ws();
+    if (!value(root, 0)) return false;
+    ws();
+    if (p_ != e_) return fail("trailing data");
+    return true;
+  }
+
+ private:
+  Store& st_;
+  const char* p_;
+  const char* e_;
+  std::string* err_;
+
+  bool fail(const char* m) {
+    if (err_ && err_->empty()) *err_ = m;
+    return false;
+  }
+  void ws() {
+    while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\t' || *p_ == '\r')) ++p_;
+  }
+  static int hexv(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  static void put_utf8(std::string& b, uint32_t cp) {
+    if (cp < 0x80) b.push_back((char)cp);
+    else if (cp < 0x800) { b.push_back((char)(0xC0 | (cp >> 6))); b.push_back((char)(0x80 | (cp & 0x3F))); }
+    else if (cp < 0x10000) {
+      b.push_back((char)(0xE0 | (cp >> 12))); b.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      b.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      b.push_back((char)(0xF0 | (cp >> 18))); b.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      b.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); b.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  // a JSON string, interned; false on error
+  bool string(uint32_t* sid) {
+    if (p_ >= e_ || *p_ != '"') return false;
+    ++p_;
+    const char* s = p_;
+    while (p_ < e_ && *p_ != '"' && *p_ != '\\' && (unsigned char)*p_ >= 0x20) ++p_;
+    if (p_ < e_ && *p_ == '"') {  // no escapes: intern straight from the input
+      *sid = st_.intern(s, (size_t)(p_ - s));
+      ++p_;
+      return true;
+    }
+    std::string& b = st_.scratch_;
+    b.assign(s, (size_t)(p_ - s));
+    while (p_ < e_ && *p_ != '"') {
+      unsigned char c = (unsigned char)*p_;
+      if (c < 0x20) return false;
+      if (c == '\\') {
+        ++p_;
+        if (p_ >= e_) return false;
+        char esc = *p_++;
+        switch (esc) {
+          case '"': b.push_back('"'); break;
+          case '\\': b.push_back('\\'); break;
+          case '/': b.push_back('/'); break;
+          case 'b': b.push_back('\b'); break;
+          case 'f': b.push_back('\f'); break;
+          case 'n': b.push_back('\n'); break;
+          case 'r': b.push_back('\r'); break;
+          case 't': b.push_back('\t'); break;
+          case 'u': {
+            if (e_ - p_ < 4) return false;
+            uint32_t cp = 0;
+            for (int i = 0; i < 4; ++i) { int h = hexv(p_[i]); if (h < 0) return false; cp = cp * 16 + h; }
+            p_ += 4;
+            if (cp >= 0xD800 && cp < 0xDC00) {
+              if (e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+                uint32_t lo = 0;
+                bool ok = true;
+                for (int i = 0; i < 4; ++i) { int h = hexv(p_[2 + i]); if (h < 0) { ok = false; break; } lo = lo * 16 + h; }
+                if (ok && lo >= 0xDC00 && lo < 0xE000) { p_ += 6; cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); }
+                else cp = 0xFFFD;
+              } else cp = 0xFFFD;
+            } else if (cp >= 0xDC00 && cp < 0xE000) cp = 0xFFFD;
+            put_utf8(b, cp);
+            break;
+          }
+          default: return false;
+        }
+      } else {
+        b.push_back((char)c);
+        ++p_;
+      }
+    }
+    if (p_ >= e_) return false;
+    ++p_;
+    *sid = st_.intern(b.data(), b.size());
+    return true;
+  }
+  // moves pend_[base..] into a fresh contiguous arena block
+  uint32_t close_block(size_t base, uint32_t* n, uint8_t* flags) {
+    std::vector<Node>& pd = st_.pend_;
+    size_t cnt = pd.size() - base;
+    if (cnt > 0xffff) { *flags |= 1; cnt = 0xffff; }
+    uint32_t first = (uint32_t)st_.nodes_.size();
+    st_.nodes_.resize(st_.nodes_.size() + cnt);
+    if (cnt) memcpy(st_.nodes_.data() + first, pd.data() + base, cnt * sizeof(Node));
+    pd.resize(base);
+    *n = (uint32_t)cnt;
+    return first;
+  }
+  // encoding/json into map[string]interface{}: the last value of a key wins
+  // (the kept members stay in source order, as JsonReader::dedupe keeps them)
+  void dedupe(size_t base) {
+    std::vector<Node>& pd = st_.pend_;
+    size_t n = pd.size() - base;
+    if (n < 2) return;
+    bool dup = false;
+    for (size_t a = base; a < pd.size() && !dup; ++a)
+      for (size_t b = a + 1; b < pd.size(); ++b)
+        if (pd[a].key == pd[b].key) { dup = true; break; }
+    if (!dup) return;
+    size_t w = base;
+    for (size_t a = base; a < pd.size(); ++a) {
+      bool later = false;
+      for (size_t b = a + 1; b < pd.size() && !later; ++b) later = pd[a].key == pd[b].key;
+      if (!later) pd[w++] = pd[a];
+    }
+    pd.resize(w);
+  }
+  bool value(Node* out, int depth) {
+    if (depth > 512) return fail("nesting too deep");
+    if (p_ >= e_) return fail("unexpected end");
+    *out = Node{};
+    char c = *p_;
+    if (c == '{') {
+      ++p_;
+      out->type = NT_OBJ;
+      ws();
+      size_t base = st_.pend_.size();
+      if (p_ < e_ && *p_ == '}') { ++p_; return true; }
+      while (true) {
+        ws();
+        uint32_t key;
+        if (!string(&key)) return fail("bad object key");
+        ws();
+        if (p_ >= e_ || *p_ != ':') return fail("expected ':'");
+        ++p_;
+        ws();
+        Node v;
+        if (!value(&v, depth + 1)) return false;
+        v.key = key;
+        st_.pend_.push_back(v);
+        ws();
+        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (p_ < e_ && *p_ == '}') { ++p_; break; }
+        return fail("expected ',' or '}'");
+      }
+      dedupe(base);
+      uint32_t n;
+      out->first = close_block(base, &n, &out->flags);
+      out->n = (uint16_t)n;
+      return true;
+    }
+    if (c == '[') {
+      ++p_;
+      out->type = NT_ARR;
+      ws();
+      size_t base = st_.pend_.size();
+      if (p_ < e_ && *p_ == ']') { ++p_; return true; }
+      uint32_t i = 0;
+      while (true) {
+        ws();
+        Node v;
+        if (!value(&v, depth + 1)) return false;
+        v.key = i++;
+        st_.pend_.push_back(v);
+        ws();
+        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (p_ < e_ && *p_ == ']') { ++p_; break; }
+        return fail("expected ',' or ']'");
+      }
+      uint32_t n;
+      out->first = close_block(base, &n, &out->flags);
+      out->n = (uint16_t)n;
+      return true;
+    }
+    if (c == '"') {
+      out->type = NT_STR;
+      if (!string(&out->val)) return fail("bad string");
+      return true;
+    }
+    if (c == 't') { if (e_ - p_ >= 4 && memcmp(p_, "true", 4) == 0) { p_ += 4; out->type = NT_TRUE; return true; } return fail("bad literal"); }
+    if (c == 'f') { if (e_ - p_ >= 5 && memcmp(p_, "false", 5) == 0) { p_ += 5; out->type = NT_FALSE; return true; } return fail("bad literal"); }
+    if (c == 'n') { if (e_ - p_ >= 4 && memcmp(p_, "null", 4) == 0) { p_ += 4; out->type = NT_NULL; return true; } return fail("bad literal"); }
+    if (c == '-' || (c >= '0' && c <= '9')) {
+      const char* s = p_;
+      if (*p_ == '-') ++p_;
+      if (p_ >= e_) return fail("bad number");
+      if (*p_ == '0') ++p_;
+      else if (*p_ >= '1' && *p_ <= '9') { while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_; }
+      else return fail("bad number");
+      if (p_ < e_ && *p_ == '.') {
+        ++p_;
+        if (p_ >= e_ || !(*p_ >= '0' && *p_ <= '9')) return fail("bad number");
+        while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
+      }
+      if (p_ < e_ && (*p_ == 'e' || *p_ == 'E')) {
+        ++p_;
+        if (p_ < e_ && (*p_ == '+' || *p_ == '-')) ++p_;
+        if (p_ >= e_ || !(*p_ >= '0' && *p_ <= '9')) return fail("bad number");
+        while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
+      }
+      out->type = NT_NUM;
+      out->val = st_.number(s, (size_t)(p_ - s));
+      return true;
+    }
+    return fail("unexpected character");
+  }
+};
+
+bool Store::parse_doc(const char* p, size_t n, Node* root, std::string* err) {
+  DocParser d(*this, p, n, err);
+  return d.run(root);
 }
 
 }  // namespace gk

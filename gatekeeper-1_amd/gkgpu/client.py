@@ -115,7 +115,15 @@ class Client:
         return self.driver.delete_data(data_path(obj))
 
     def review(self, review: dict):
-        return self.driver.query('hooks["%s"].violation' % TARGET, {"review": review})
+        """Client.Review (client.go:763-800): Driver.Query, then HandleViolation
+        (target.go:193-244) on every result; its error fails the Review."""
+        from .target import handle_violation
+        res = self.driver.query('hooks["%s"].violation' % TARGET, {"review": review})
+        if res.results:
+            resource = handle_violation(review)
+            for r in res.results:
+                r.resource = resource
+        return res
 
     def review_objects(self, objs, namespaces):
         return self.driver.review_objects(objs, namespaces)

@@ -28,7 +28,17 @@ EXPORTS = [
     "gk_results_timing", "gk_results_free", "gk_template_status", "gk_constraint_count", "gk_constraint_info",
     "gk_batch_stats", "gk_results_device_counts", "gk_results_copy_status", "gk_results_flag_counts",
     "gk_results_launches", "gk_results_launch", "gk_template_backend", "gk_results_copy_device_output",
+    "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
+    "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
 ]
+
+GK_REVIEW_EXCLUDED = 4
+RESOURCE_FIELD = 512
+
+
+class _Resource(C.Structure):
+    _fields_ = [("api_version", C.c_char * RESOURCE_FIELD), ("kind", C.c_char * RESOURCE_FIELD),
+                ("name", C.c_char * RESOURCE_FIELD), ("namespace", C.c_char * RESOURCE_FIELD)]
 
 
 class EngineUnavailable(RuntimeError):
@@ -118,6 +128,19 @@ def load_library():
     lib.gk_constraint_count.argtypes = [vp]
     lib.gk_constraint_count.restype = sz
     lib.gk_constraint_info.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(cp)]
+    page_args = [vp, C.c_char_p, vp, sz, C.c_char_p, vp, sz, vp]
+    lib.gk_review_page.argtypes = page_args + [C.POINTER(vp)]
+    lib.gk_batch_stage_page.argtypes = page_args + [C.POINTER(vp)]
+    lib.gk_debug_flatten_page.argtypes = page_args + [C.c_int, pu64, pu64, C.POINTER(C.c_double)]
+    lib.gk_batch_timing.argtypes = [vp, C.POINTER(C.c_double)]
+    lib.gk_batch_excluded.argtypes = [vp]
+    lib.gk_batch_excluded.restype = C.c_uint64
+    lib.gk_batch_resource.argtypes = [vp, vp, sz, C.POINTER(_Resource)]
+    lib.gk_excluder_add.argtypes = [vp, ppc, sz, ppc, sz]
+    lib.gk_excluder_clear.argtypes = [vp]
+    lib.gk_excluder_is_excluded.argtypes = [vp, cp, cp]
+    lib.gk_results_excluded.argtypes = [vp]
+    lib.gk_results_excluded.restype = C.c_uint64
     _LIB = lib
     return lib
 
@@ -136,6 +159,7 @@ class Result:
     msg: str
     details_json: str
     enforcement_action: str
+    resource: Optional[dict] = None  # HandleViolation's Result.Resource (Client.review sets it)
 
 
 @dataclass
@@ -274,6 +298,25 @@ class Batch:
     def device_bytes(self) -> int:
         return self._drv._lib.gk_batch_device_bytes(self._h)
 
+    def timing_ms(self):
+        """host staging milliseconds: (parse + build documents, flatten total, upload)"""
+        t = (C.c_double * 3)()
+        self._drv._lib.gk_batch_timing(self._h, t)
+        return tuple(t)
+
+    def excluded(self) -> int:
+        return self._drv._lib.gk_batch_excluded(self._h)
+
+    def resource(self, review: int):
+        """HandleViolation's Resource identity (target.go:193-244):
+        (apiVersion, kind, name, namespace) of the review's object"""
+        r = _Resource()
+        rc = self._drv._lib.gk_batch_resource(self._drv._e, self._h, review, C.byref(r))
+        if rc not in (0, 6):
+            self._drv._check(rc)
+        dec = lambda b: b.decode("utf-8", "surrogateescape")  # noqa: E731
+        return dec(r.api_version), dec(r.kind), dec(r.name), dec(r.namespace)
+
     def stats(self):
         """(reviews, document nodes, distinct string-value bytes, match-column bytes)."""
         v = [C.c_uint64() for _ in range(4)]
@@ -396,6 +439,51 @@ class Driver:
         out = C.c_void_p()
         self._check(self._lib.gk_review_objects(self._e, oa, ol, na, nl, len(o), C.byref(out)))
         return _collect(self._lib, out)
+
+    @staticmethod
+    def _page_args(page):
+        import numpy as np
+        oo = np.ascontiguousarray(page.obj_offs, dtype=np.uint64)
+        no = np.ascontiguousarray(page.ns_offs, dtype=np.uint64)
+        on = np.ascontiguousarray(page.obj_ns, dtype=np.uint32)
+        keep = (oo, no, on)
+        return [page.objs, oo.ctypes.data, page.n, page.nss, no.ctypes.data, page.n_ns, on.ctypes.data], keep
+
+    def review_page(self, page) -> Results:
+        """audit discovery mode over one List page (gkgpu.page.Page)"""
+        args, _keep = self._page_args(page)
+        out = C.c_void_p()
+        self._check(self._lib.gk_review_page(self._e, *args, C.byref(out)))
+        return _collect(self._lib, out)
+
+    def stage_page(self, page) -> Batch:
+        """stage one List page (gkgpu.page.Page) on the device"""
+        args, _keep = self._page_args(page)
+        out = C.c_void_p()
+        self._check(self._lib.gk_batch_stage_page(self._e, *args, C.byref(out)))
+        return Batch(self, out, page.n)
+
+    def debug_flatten(self, page, threads: int = 0):
+        """flatten a page on the host only: (content hash, nodes, parse ms, total ms)"""
+        args, _keep = self._page_args(page)
+        h, n = C.c_uint64(), C.c_uint64()
+        ms = (C.c_double * 2)()
+        self._check(self._lib.gk_debug_flatten_page(self._e, *args, threads, C.byref(h), C.byref(n), ms))
+        return h.value, n.value, ms[0], ms[1]
+
+    # -- process excluder (excluder.go)
+    def excluder_add(self, processes: Sequence[str], namespaces: Sequence[str]):
+        """Excluder.Add(MatchEntry{ExcludedNamespaces, Processes}) (excluder.go:44-68)"""
+        pa, _, _k1 = _arr(list(processes))
+        na, _, _k2 = _arr(list(namespaces))
+        self._check(self._lib.gk_excluder_add(self._e, pa, len(processes), na, len(namespaces)))
+
+    def excluder_clear(self):
+        self._check(self._lib.gk_excluder_clear(self._e))
+
+    def is_namespace_excluded(self, process: str, namespace: str) -> bool:
+        """Excluder.IsNamespaceExcluded (excluder.go:82-86)"""
+        return bool(self._lib.gk_excluder_is_excluded(self._e, _b(process), _b(namespace)))
 
     def stage_objects(self, objs: Sequence, namespaces: Sequence) -> Batch:
         o = [x if isinstance(x, str) else json.dumps(x) for x in objs]

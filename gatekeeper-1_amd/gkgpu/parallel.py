@@ -8,11 +8,13 @@ pkg/audit/manager.go:462-508) and the compacted violation lists, gathered to
 rank 0 with exact-size point-to-point transfers over RCCL (xGMI) -- or gloo
 for the CPU tests.
 
-The violation records are the engine's gk_viol (include/gkgpu.h): 8 x u32
-(review, constraint, seq, rule, msg_off, msg_len, det_off, det_len).  A rank's
-review indices are rebased to global indices before sending; message offsets
-stay relative to that rank's byte buffer (a global buffer could pass 4 GiB),
-so rank 0 holds one (tuples, bytes) pair per source rank.
+The violation records are the engine's gk_viol (include/gkgpu.h), 32 bytes:
+u32 review, u32 constraint, u16 seq, u16 rule, u32 msg_len, u64 msg_off,
+u32 det_len, u32 pad (details JSON follows the message).  Viewed as 8 int32
+words: [review, constraint, seq | rule << 16, msg_len, off_lo, off_hi,
+det_len, pad].  A rank's review indices are rebased to global indices before
+sending; message offsets stay relative to that rank's byte buffer, so rank 0
+holds one (tuples, bytes) pair per source rank.
 """
 from __future__ import annotations
 
@@ -20,6 +22,21 @@ from typing import List, Optional, Tuple
 
 VIOL_WORDS = 8
 VIOL_BYTES = 32
+
+
+def pack_viol(review, constraint, seq, rule, msg_len, msg_off, det_len):
+    """one gk_viol record as 8 int32 words (two's complement)"""
+    def i32(x):
+        x &= 0xffffffff
+        return x - (1 << 32) if x >= 1 << 31 else x
+    return [i32(review), i32(constraint), i32(seq | (rule << 16)), i32(msg_len), i32(msg_off), i32(msg_off >> 32),
+            i32(det_len), 0]
+
+
+def unpack_viol(words):
+    """(review, constraint, seq, rule, msg_len, msg_off, det_len) of 8 int32 words"""
+    w = [int(x) & 0xffffffff for x in words]
+    return w[0], w[1], w[2] & 0xffff, w[2] >> 16, w[3], w[4] | (w[5] << 32), w[6]
 
 
 def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -129,7 +146,8 @@ def decode(parts, limit: Optional[int] = None):
         tt = t.cpu().numpy()
         bb = b.cpu().numpy().tobytes()
         for rec in tt:
-            rv, c, seq, rule, mo, ml, do, dl = (int(x) & 0xffffffff for x in rec)
+            rv, c, seq, rule, ml, mo, dl = unpack_viol(rec)
+            do = mo + ml
             rows.append((rv, 0 if rule == 0xffff else 1, c, seq, rule, bb[mo:mo + ml].decode("utf-8", "surrogateescape"),
                          bb[do:do + dl].decode("utf-8", "surrogateescape")))
     rows.sort(key=lambda r: (r[0], r[1], r[2], r[3]))

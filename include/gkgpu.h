@@ -34,10 +34,13 @@ extern "C" {
 #define GK_EQUERY 3      /* unsupported query path                          */
 #define GK_EDEVICE 4     /* HIP runtime failure / no MI355X visible         */
 #define GK_ENOTFOUND 5
+#define GK_ERANGE 6      /* a value did not fit the caller's fixed-size field   */
 
 /* per-review status in gk_results (bit set) */
 #define GK_REVIEW_ERROR 1u     /* reference Query would return an error    */
 #define GK_REVIEW_FALLBACK 2u  /* route this review to the CPU OPA driver  */
+#define GK_REVIEW_EXCLUDED 4u  /* namespace excluded for the audit process:
+                                  not reviewed (manager.go:362-365)          */
 
 typedef struct gk_engine gk_engine;
 typedef struct gk_results gk_results;
@@ -93,6 +96,35 @@ int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_l
  * evaluate many times.  stage_objects has gk_review_objects' semantics. */
 int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
                            const size_t* ns_lens, size_t n, gk_batch** out);
+/* The same two entry points over one List page in bulk form (the audit loop's
+ * objList.Items, manager.go:361-389): objects as concatenated JSON texts with
+ * n + 1 byte offsets, the page's distinct Namespace objects (the nsCache,
+ * manager.go:96-115) with n_ns + 1 offsets, and per object the index of its
+ * Namespace (UINT32_MAX = cluster-scoped: reviewed with an empty
+ * corev1.Namespace{}, target.go:137-139).  Objects are parsed and flattened on
+ * GKGPU_THREADS host threads (default: hardware threads, at most 16). */
+int gk_review_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
+                   const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_results** out);
+int gk_batch_stage_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
+                        const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_batch** out);
+/* host milliseconds of staging: [parse + build documents, flatten total, upload] */
+int gk_batch_timing(const gk_batch* b, double* ms3);
+/* reviews of the batch the process excluder skipped */
+uint64_t gk_batch_excluded(const gk_batch* b);
+
+/* HandleViolation's Result.Resource identity for a review of the batch
+ * (pkg/target/target.go:193-244): apiVersion = "<group>/<version>" or
+ * "<version>" when the group is "", kind = review.kind.kind, and the object's
+ * metadata name / namespace.  NUL-terminated; GK_ERANGE if a field was cut. */
+#define GK_RESOURCE_FIELD 512
+typedef struct {
+  char api_version[GK_RESOURCE_FIELD];
+  char kind[GK_RESOURCE_FIELD];
+  char name[GK_RESOURCE_FIELD];
+  char namespace_[GK_RESOURCE_FIELD];
+} gk_resource;
+int gk_batch_resource(gk_engine* e, const gk_batch* b, size_t review, gk_resource* out);
+
 /* evaluate a staged batch; decode=0 keeps results on the device (counts only) */
 int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out);
 void gk_batch_free(gk_batch* b);
@@ -101,6 +133,19 @@ uint64_t gk_batch_device_bytes(const gk_batch* b);
 /* algorithmic input of one sweep over the batch: reviews, document nodes (16 B
  * each), bytes of the distinct string values they reference, match-column bytes */
 int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes);
+
+/* ---- process excluder (pkg/controller/config/process/excluder.go) --------- */
+/* Excluder.Add(MatchEntry{ExcludedNamespaces: namespaces, Processes: processes})
+ * — excluder.go:44-68; process "*" adds the namespaces to audit, webhook and
+ * sync.  The audit entry points (gk_review_objects, gk_review_page, staged
+ * batches) skip objects whose metadata.namespace is excluded for "audit"
+ * (manager.go:362-365): no results, status GK_REVIEW_EXCLUDED.  Changing the
+ * exclusions invalidates staged batches. */
+int gk_excluder_add(gk_engine* e, const char* const* processes, size_t np, const char* const* namespaces, size_t nn);
+/* Excluder.Replace(New()) */
+int gk_excluder_clear(gk_engine* e);
+/* Excluder.IsNamespaceExcluded(process, ns) — excluder.go:82-86 */
+int gk_excluder_is_excluded(gk_engine* e, const char* process, const char* ns);
 
 /* ---- results ------------------------------------------------------------- */
 typedef struct {
@@ -124,6 +169,8 @@ uint32_t gk_results_review_reason(const gk_results* r, size_t review);
 int gk_results_copy_status(const gk_results* r, uint32_t* status, uint32_t* reason);
 /* number of reviews flagged GK_REVIEW_ERROR / GK_REVIEW_FALLBACK */
 int gk_results_flag_counts(const gk_results* r, uint64_t* errors, uint64_t* fallbacks);
+/* reviews the process excluder skipped */
+uint64_t gk_results_excluded(const gk_results* r);
 /* per-constraint violation totals (device-side counters), length = constraints */
 size_t gk_results_constraints(const gk_results* r);
 uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
@@ -137,8 +184,11 @@ int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* by
  * tensors handed to an RCCL gather).  Valid until the engine's next
  * evaluation; GK_EINVAL after that. */
 typedef struct {
-  uint32_t review, constraint, seq, rule; /* rule 0xffff = autoreject */
-  uint32_t msg_off, msg_len, det_off, det_len;
+  uint32_t review, constraint;
+  uint16_t seq, rule;    /* emission order within (review, constraint); rule 0xffff = autoreject */
+  uint32_t msg_len;
+  uint64_t msg_off;      /* message at [msg_off, +msg_len), details JSON right after it */
+  uint32_t det_len, pad;
 } gk_viol;
 int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst);
 /* kernels of the call in launch order: kernel name ("audit_kernel" = bytecode

@@ -1,0 +1,81 @@
+"""Host flattener (csrc/flatten.cc) and process excluder, on the CPU: the
+parallel flattening is content-identical at every thread count, the bulk page
+and char** forms agree, and the excluder mirrors excluder.go."""
+import json
+
+import pytest
+
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client
+from gkgpu.page import NO_NS, Page
+
+
+@pytest.fixture(scope="module")
+def drv():
+    d = gkgpu.Driver(jit=False)
+    cl = Client(d)
+    ts, cs = W.config2()
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    return d
+
+
+def test_flatten_same_content_at_every_thread_count(drv):
+    objs, nss = W.gen_pods_json(9000, seed=42, n_namespaces=50)
+    pg = Page.from_lists(objs, nss)
+    hashes = {drv.debug_flatten(pg, t)[0] for t in (1, 2, 3, 8)}
+    assert len(hashes) == 1
+
+
+def test_flatten_mixed_kinds_cluster_scoped_and_escapes(drv):
+    objs, nss = W.gen_config4_json(6000, seed=1234)
+    objs.append('{"apiVersion":"v1","kind":"ConfigMap","metadata":{"name":"esc\\u00e9\\n\\"q\\"","namespace":"c4-ns-0001"},'
+                '"data":{"k":"v","k":"dup-last-wins"}}')
+    nss.append(nss[0])
+    pg = Page.from_lists(objs, nss)
+    h1, n1, _, _ = drv.debug_flatten(pg, 1)
+    h8, n8, _, _ = drv.debug_flatten(pg, 8)
+    assert h1 == h8 and n1 > 0
+
+
+def test_flatten_rejects_bad_json(drv):
+    pg = Page.from_lists(['{"a": 1}', '{"a": }'], [None, None])
+    with pytest.raises(RuntimeError, match="invalid object JSON at 1"):
+        drv.debug_flatten(pg, 2)
+
+
+def test_page_from_lists_shares_namespaces():
+    ns = W.namespace_obj("a")
+    pg = Page.from_lists([{"k": 1}, {"k": 2}, {"k": 3}], [ns, None, ns])
+    assert pg.n == 3 and pg.n_ns == 1
+    assert list(pg.obj_ns) == [0, NO_NS, 0]
+    assert json.loads(pg.nss) == ns
+    assert pg.objs[int(pg.obj_offs[1]):int(pg.obj_offs[2])] == b'{"k":2}'
+
+
+def test_excluder_mirrors_excluder_go():
+    d = gkgpu.Driver(jit=False)
+    d.excluder_add(["audit"], ["kube-system"])
+    d.excluder_add(["*"], ["gatekeeper-system"])
+    assert d.is_namespace_excluded("audit", "kube-system")
+    assert not d.is_namespace_excluded("webhook", "kube-system")
+    for p in ("audit", "webhook", "sync"):
+        assert d.is_namespace_excluded(p, "gatekeeper-system")
+    assert not d.is_namespace_excluded("*", "gatekeeper-system")
+    d.excluder_clear()
+    assert not d.is_namespace_excluded("audit", "kube-system")
+
+
+def test_excluded_objects_carry_no_document(drv):
+    objs, nss = W.gen_pods_json(3000, seed=1, n_namespaces=20)
+    pg = Page.from_lists(objs, nss)
+    _, n_all, _, _ = drv.debug_flatten(pg, 4)
+    drv.excluder_add(["audit"], ["production"])
+    try:
+        _, n_ex, _, _ = drv.debug_flatten(pg, 4)
+    finally:
+        drv.excluder_clear()
+    assert n_ex < n_all

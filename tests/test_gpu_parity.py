@@ -598,3 +598,96 @@ def test_empty_and_degenerate_inputs():
     rep, _ = run_objects(Driver(), ts, cs, odd, nss)
     assert not rep.mismatches, rep.mismatches[:3]
     assert rep.compared + rep.fallback + rep.errors == len(odd)
+
+
+def test_review_page_and_staged_page_match_objects_path():
+    """The bulk List-page entry points (gk_review_page / gk_batch_stage_page,
+    parallel host flattening) give the char** path's results, bit for bit."""
+    from gkgpu.page import Page
+    ts, cs = W.config2()
+    objs, nss = W.gen_pods_json(5000, seed=9, n_namespaces=40)
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    key = lambda res: sorted((x.review, x.constraint, x.msg, x.details_json) for x in res.results)  # noqa: E731
+    want = key(drv.review_objects(objs, nss))
+    pg = Page.from_lists(objs, nss)
+    assert key(drv.review_page(pg)) == want
+    b = drv.stage_page(pg)
+    assert key(b.eval(decode=True)) == want
+    assert b.timing_ms()[1] > 0
+    b.free()
+
+
+def test_excluder_skips_audit_namespaces():
+    """Excluder.IsNamespaceExcluded(Audit, ns) (excluder.go:82-86) in the
+    audit loop (manager.go:362-365): objects of an excluded namespace are not
+    reviewed (status GK_REVIEW_EXCLUDED, no results); the rest are unchanged."""
+    from gkgpu.driver import GK_REVIEW_EXCLUDED
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(800, seed=17, n_namespaces=30)
+    nss = [ns_objs[n] for n in ns_of]
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    full = drv.review_objects(pods, nss)
+    drv.excluder_add(["audit"], ["production"])
+    part = drv.review_objects(pods, nss)
+    b = drv.stage_objects(pods, nss)
+    staged = b.eval(decode=True)
+    drv.excluder_add(["webhook"], ["team-0003"])  # invalidates the staged batch
+    with pytest.raises(RuntimeError, match="state changed"):
+        b.eval(decode=True)
+    ex = {i for i, n in enumerate(ns_of) if n == "production"}
+    assert ex and len(ex) < len(pods)
+    for res in (part, staged):
+        assert {i for i, s in enumerate(res.status) if s & GK_REVIEW_EXCLUDED} == ex
+        got = sorted((x.review, x.constraint, x.msg) for x in res.results)
+        assert got == sorted((x.review, x.constraint, x.msg) for x in full.results if x.review not in ex)
+    assert b.excluded() == len(ex)
+
+
+def test_batch_resource_is_handle_violation_identity():
+    """gk_batch_resource == HandleViolation's Resource (target.go:193-244) for
+    the staged reviews: apiVersion from review.kind, object metadata name/ns."""
+    from gkgpu.target import handle_violation, resource_identity
+    objs, nss = W.gen_config4_json(600, seed=77)
+    objs = [json.loads(o) for o in objs]
+    nss = [None if n is None else json.loads(n) for n in nss]
+    objs.append({"apiVersion": "a/b/c", "kind": "Weird", "metadata": {"name": 5}})
+    nss.append(None)
+    ts, cs = W.config4()
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    b = drv.stage_objects(objs, nss)
+    for i in list(range(0, len(objs), 37)) + [len(objs) - 1]:
+        want = resource_identity(handle_violation(augmented_review(objs[i], nss[i])))
+        assert b.resource(i) == want, i
+    b.free()
+
+
+def test_client_review_sets_handle_violation_resource():
+    ts, cs = W.config2()
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    pods, ns_of, ns_objs = W.gen_pods(20, seed=3, n_namespaces=3)
+    rv = augmented_review(pods[0], ns_objs[ns_of[0]])
+    res = cl.review(rv)
+    assert res.results
+    for r in res.results:
+        assert r.resource["apiVersion"] == "v1" and r.resource["kind"] == "Pod"
+        assert r.resource["metadata"]["name"] == pods[0]["metadata"]["name"]

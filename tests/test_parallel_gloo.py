@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gkgpu.parallel import Gatherer, decode, shard_range, VIOL_WORDS
+from gkgpu.parallel import Gatherer, decode, pack_viol, shard_range, unpack_viol, VIOL_WORDS
 
 
 def _free_port():
@@ -26,7 +26,7 @@ def _rank_output(rank, n_reviews):
         for seq in range((rv + rank) % 3):
             m = ("r%d-review%d-v%d" % (rank, rv, seq)).encode()
             d = b"{}"
-            rows.append([rv, (rv + seq) % 2, seq, 0, len(msgs), len(m), len(msgs) + len(m), len(d)])
+            rows.append(pack_viol(rv, (rv + seq) % 2, seq, 0, len(m), len(msgs), len(d)))
             msgs += m + d
     t = torch.tensor(rows, dtype=torch.int32).view(-1, VIOL_WORDS) if rows else torch.zeros((0, VIOL_WORDS), dtype=torch.int32)
     # shuffle: the device output order is one reservation per wavefront
@@ -78,7 +78,8 @@ def test_gather_two_ranks_gloo(n_total):
         t, b = _rank_output(r, hi - lo)
         bb = bytes(b.tolist())
         for rec in t.tolist():
-            rv, c, seq, rule, mo, ml, do, dl = rec
+            rv, c, seq, rule, ml, mo, dl = unpack_viol(rec)
+            do = mo + ml
             want.append((rv + lo, c, seq, rule, bb[mo:mo + ml].decode(), bb[do:do + dl].decode()))
     want.sort(key=lambda x: (x[0], x[1], x[2]))
     assert rows == want
