@@ -58,8 +58,27 @@ def _configs():
 CONFIGS = ("2", "3", "4", "5")
 
 
+def spawn(args):
+    """`--gpus N` without a launcher: start N rank processes under
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) before this
+    process touches a GPU, and exit with their status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args))
     if args.config == "5":
         return webhook_main(args)
     if args.steps is None:
@@ -98,12 +117,16 @@ def main():
         elif b == 3 and "[guard kernel " in detail:
             kinds_of[detail.split("[guard kernel ")[1].rstrip("]")] = k + " (guard)"
 
+    from gkgpu.page import Page
     t0 = time.time()
     objs, nss = cfg_gen(args.pods, rank * args.pods)
+    page = Page.from_lists(objs, nss)
+    del objs, nss
     t_gen = time.time() - t0
     t0 = time.time()
-    batch = drv.stage_objects(objs, nss)
+    batch = drv.stage_page(page)
     t_stage = time.time() - t0
+    stage_ms = batch.timing_ms()
     nrev, nodes, str_bytes, col_bytes = batch.stats()
 
     def sync():
@@ -111,28 +134,38 @@ def main():
             import torch
             torch.cuda.synchronize()
 
-    gather = None
+    # stage time of the slowest rank (each rank flattens and uploads its shard)
+    t_stage_max = t_stage
     if dist is not None:
         import torch
-        from gkgpu.parallel import DeviceOutput, Gatherer
-        dev_out = DeviceOutput(torch.device("cuda", local))
-        gatherer = Gatherer(dst=0)
-    gather_ms = []
+        t = torch.tensor([t_stage], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_stage_max = float(t.item())
+
+    cons_ids = drv.constraints()
+    base = rank * args.pods
+    exch_ms = []
+    writer = [None]
+
+    def resource(i):
+        _av, kind, name, ns = batch.resource(i)
+        return kind, name, ns
 
     def step():
+        # one audit sweep of the rank's shard: match + template predicates +
+        # GPU message formatting + compaction + device-side status sampling
+        # (exact totals, first 20 per constraint); then the exchange the audit
+        # status needs: totals all-reduce + samples gathered to rank 0 over RCCL
+        sweep = batch.eval_audit(limit=20)
         if dist is None:
-            return batch.eval(decode=False, light=True)
-        # sweep the rank's shard, then the exchange the audit needs: totals
-        # all-reduce + every rank's compacted violations (tuples + message
-        # bytes) gathered to rank 0 over RCCL
-        res = batch.eval(decode=False, light=True, device_out=dev_out)
+            return sweep
+        import torch
+        from gkgpu.parallel import exchange_audit
         t0 = time.perf_counter()
-        tot = torch.tensor(res.totals, dtype=torch.int64, device="cuda")
-        dist.all_reduce(tot)
-        gatherer.gather(dev_out.tuples(), dev_out.bytes(), review_base=rank * args.pods)
-        torch.cuda.synchronize()
-        gather_ms.append((time.perf_counter() - t0) * 1000.0)
-        return res
+        writer[0] = exchange_audit(sweep, base, resource, cons_ids, limit=20, dst=0,
+                                   device=torch.device("cuda", local))
+        exch_ms.append((time.perf_counter() - t0) * 1000.0)
+        return sweep
 
     for _ in range(args.warmup):
         step()
@@ -158,6 +191,13 @@ def main():
     ms_per_step = elapsed / args.steps * 1000.0
     evals_per_step = nrev * n_cons * world
     value = evals_per_step / (ms_per_step / 1000.0)
+    # end to end: a cold sweep = flatten + H2D of the shard + one sweep (the
+    # synthetic-input generation is excluded)
+    e2e_s = t_stage_max + ms_per_step / 1000.0
+    if writer[0] is None and rank == 0:
+        from gkgpu.audit import AuditWriter
+        writer[0] = AuditWriter.from_sweep(cons_ids, last, resource, 20)
+    status_totals = sum(writer[0].totals.values()) if writer[0] is not None else None
 
     # roofline of the dominant kernel (the template kernel with the largest
     # average HIP-event duration): algorithmic bytes of one launch = one pass
@@ -203,7 +243,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(templates, constraints, objs[: args.cpu_sample], nss[: args.cpu_sample])
+        sample = page.slice(0, min(args.cpu_sample, page.n))
+        so = [sample.objs[int(sample.obj_offs[i]):int(sample.obj_offs[i + 1])].decode() for i in range(sample.n)]
+        sn = [None if k == 0xFFFFFFFF else page.nss[int(page.ns_offs[k]):int(page.ns_offs[k + 1])].decode()
+              for k in sample.obj_ns]
+        cpu = cpu_baseline(templates, constraints, so, sn)
 
     if rank == 0:
         out = {
@@ -226,16 +270,24 @@ def main():
                 "templates": [t["spec"]["crd"]["spec"]["names"]["kind"] for t in templates],
                 "evals_per_step": evals_per_step,
                 "violations_per_step_rank0": last.device_tuples,
+                "excluded_reviews": last.excluded,
                 "fallback_reviews": fallback,
                 "error_reviews": errors,
-                "parallelism": "dp%d (resource shards; totals all-reduce + violation gather to rank 0 over RCCL)" % world,
-                "gather_ms_avg_rank0": (sum(gather_ms[-args.steps:]) / args.steps) if gather_ms else 0.0,
+                "parallelism": "dp%d (contiguous resource shards; per step: totals all-reduce (int64) + "
+                               "first-20-per-constraint samples gathered to rank 0 over RCCL)" % world,
+                "exchange_ms_avg_rank0": (sum(exch_ms[-args.steps:]) / args.steps) if exch_ms else 0.0,
+                "status_total_violations": status_totals,
+                "end_to_end_evals_per_s": evals_per_step / e2e_s,
+                "end_to_end_s": e2e_s,
                 "kernel_ms_per_step": sum(k["avg_ms"] for k in kernels),
                 "kernel_only_evals_per_s": evals_per_step / (sum(k["avg_ms"] for k in kernels) / 1000.0),
                 "backends": {k: {0: "cpu-fallback", 1: "bytecode-vm", 2: "template-kernel", 3: "guard-kernel+cpu-fallback"}[drv.template_backend(k)[0]]
                              for k in kinds},
                 "kernel_templates": kinds_of,
                 "stage_s": round(t_stage, 3),
+                "stage_s_max_over_ranks": round(t_stage_max, 3),
+                "stage_ms": {"parse": round(stage_ms[0], 1), "flatten": round(stage_ms[1], 1),
+                             "upload": round(stage_ms[2], 1)},
                 "gen_s": round(t_gen, 3),
             },
             "roofline": {

@@ -209,6 +209,17 @@ struct Viol {
 static_assert(sizeof(Viol) == 32, "Viol layout");
 
 constexpr uint32_t RULE_AUTOREJECT = 0xffffu;
+
+// audit status sample record (kernels.hip gk_sample_select): a tuple plus the
+// first SAMPLE_MSG bytes of its message
+constexpr uint32_t SAMPLE_MSG = 256;
+struct SampleRec {
+  uint32_t review, constraint;
+  uint16_t seq, rule;
+  uint32_t msg_len, pad;
+  uint8_t msg[SAMPLE_MSG];
+};
+static_assert(sizeof(SampleRec) == 276, "SampleRec layout");
 constexpr uint32_t MEMO_SLOTS = 16;  // memoized function call sites per template (per lane)
 constexpr uint32_t GMEMO_ENTRIES = 1u << 15;  // cross-lane memo table of a template launch (32 B entries)
 

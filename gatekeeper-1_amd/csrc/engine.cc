@@ -29,6 +29,10 @@ namespace gk {
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
 extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream);
 extern "C" size_t gk_devargs_size();
+extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
+                                uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
+                                unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
+                                unsigned int* ncand, int select_only, hipStream_t stream);
 
 namespace gk {
 
@@ -123,6 +127,9 @@ struct gk_results {
   const void* d_bytes = nullptr;           // until the engine's next evaluation)
   uint64_t epoch = 0;
   std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
+  struct Sample { uint32_t review, constraint; uint16_t seq, rule; uint32_t msg_len; std::string msg; };
+  std::vector<Sample> samples;             // gk_batch_eval_audit: first `limit` per constraint, in order
+  bool audited = false;
   struct Launch { std::string kernel; double ms; uint32_t nconstraints; uint64_t tuples, bytes; };
   std::vector<Launch> launches;            // kernels of the last attempt, in launch order
 };
@@ -167,6 +174,7 @@ struct gk_engine {
   };
   std::vector<Jit> jits;
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
+  bool host_only = false;    // opts {"host_only": true}: stage on the host only (CPU baseline / tests); no evaluation
   std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
   bool modules_dirty = true;
   // data
@@ -188,7 +196,12 @@ struct gk_engine {
   // device mirrors
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
       d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist,
-      d_gmemo, d_frec;
+      d_gmemo, d_frec, d_hist, d_cut, d_ftot, d_cand, d_ncand, d_cerr;
+  size_t cand_cap = 1 << 14;
+  // gk_debug_host_args: host copies of the per-call tables (diagnostics / CPU baseline)
+  std::vector<gk::MatchSpec> dbg_cons;
+  std::vector<uint32_t> dbg_progoff, dbg_mwords, dbg_dfa_keys, dbg_dfa_meta, dbg_dfa_words, dbg_fmt;
+  std::string dbg_pool;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
   std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
   uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
@@ -585,6 +598,7 @@ static void rebuild_regex(gk_engine* e) {
 // ------------------------------------------------------------------ device sync + launch
 static bool ensure_device(gk_engine* e) {
   if (e->dev_ok) return true;
+  if (e->host_only) return false;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= e->device) return false;
   if (hipSetDevice(e->device) != hipSuccess) return false;
@@ -956,6 +970,8 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
       if (dv >= 0 && d.nodes[dv].type == NT_NUM) e->device = atoi(d.str(d.nodes[dv]));
       int jv = d.get(r, "jit");
       if (jv >= 0 && d.nodes[jv].type == NT_FALSE) e->jit_enabled = false;
+      int hv = d.get(r, "host_only");
+      if (hv >= 0 && d.nodes[hv].type == NT_TRUE) e->host_only = true;
       int mv = d.get(r, "max_violations");
       if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap = (size_t)atoll(d.str(d.nodes[mv]));
     }
@@ -975,7 +991,7 @@ void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
                   &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
-                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo, &e->d_frec})
+                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo, &e->d_frec, &e->d_hist, &e->d_cut, &e->d_ftot, &e->d_cand, &e->d_ncand, &e->d_cerr})
     b->free_();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   for (hipEvent_t x : e->events) hipEventDestroy(x);
@@ -1403,6 +1419,11 @@ static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
   b->nrev = (uint32_t)page.n;
   b->gen = e->gen;
   auto t1 = Clock::now();
+  if (e->host_only) {  // documents stay in the host arena only (gk_debug_host_args)
+    b->node_count = b->node_end - b->node_begin;
+    *out = b;
+    return GK_OK;
+  }
   if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
   if (!sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
       !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
@@ -1474,6 +1495,109 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   if (rc != GK_OK) { delete res; return rc; }
   *out = res;
   return GK_OK;
+}
+
+// The audit status of one sweep over a staged batch (pkg/audit/manager.go:462-508):
+// exact per-constraint totals over the reviews the engine answered, and the
+// first `limit` results per constraint in evaluation order (batch index,
+// autoreject first, emission order), selected on the device (kernels.hip
+// gk_sample_*) so only O(constraints x limit) records reach the host.
+int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out) {
+  if (!e || !b || !out) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
+  auto* res = new gk_results();
+  int rc = launch_and_collect(e, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded);
+  if (rc != GK_OK) { delete res; return rc; }
+  res->audited = true;
+  const uint32_t ncons = (uint32_t)e->corder.size(), nrev = b->nrev;
+  if (ncons == 0 || nrev == 0) { *out = res; return GK_OK; }
+  if (res->dev_tuples == 0) {
+    std::fill(res->totals.begin(), res->totals.end(), 0);
+    *out = res;
+    return GK_OK;
+  }
+  const uint32_t nb = std::min<uint32_t>(8192, nrev);
+  bool any_err = false;
+  std::vector<uint8_t> cerr(ncons, 0);
+  for (uint32_t c = 0; c < ncons; ++c) { cerr[c] = e->corder[c]->ea_error; any_err |= cerr[c] != 0; }
+  bool ok = e->d_hist.reserve((size_t)ncons * nb * 4) && e->d_cut.reserve(ncons * 4) && e->d_ftot.reserve(ncons * 8) &&
+            e->d_ncand.reserve(16) && e->d_cand.reserve(e->cand_cap * sizeof(SampleRec)) &&
+            (!any_err || up(e->d_cerr, cerr, false));
+  if (!ok) { delete res; return fail(e, GK_EDEVICE, "device allocation failed"); }
+  auto t0 = Clock::now();
+  hipEvent_t ev0 = e->events[0], ev1 = e->events[1];
+  hipEventRecord(ev0, e->stream);
+  unsigned int ncand = 0;
+  for (int pass = 0; pass < 3; ++pass) {
+    int lr = gk_launch_sample((const Viol*)e->d_out.p, res->dev_tuples, (uint32_t*)e->d_rflags.p, nrev,
+                              any_err ? (const uint8_t*)e->d_cerr.p : nullptr, ncons, nb, std::max<uint32_t>(limit, 1),
+                              (uint32_t*)e->d_hist.p, (uint32_t*)e->d_cut.p, (unsigned long long*)e->d_ftot.p,
+                              (const char*)e->d_bytes.p, (SampleRec*)e->d_cand.p, (uint32_t)e->cand_cap,
+                              (unsigned int*)e->d_ncand.p, pass > 0, e->stream);
+    if (lr != 0) { delete res; return fail(e, GK_EDEVICE, std::string("sample launch failed: ") + hipGetErrorString((hipError_t)lr)); }
+    if (pass == 0) hipEventRecord(ev1, e->stream);
+    if (hipMemcpyAsync(&ncand, e->d_ncand.p, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) {
+      delete res;
+      return fail(e, GK_EDEVICE, "sample pass failed");
+    }
+    if (ncand <= e->cand_cap) break;
+    e->cand_cap = std::max<size_t>(e->cand_cap * 2, (size_t)ncand + 1024);
+    if (!e->d_cand.reserve(e->cand_cap * sizeof(SampleRec))) { delete res; return fail(e, GK_EDEVICE, "device allocation failed"); }
+  }
+  float kms = 0;
+  hipEventElapsedTime(&kms, ev0, ev1);
+  res->launches.push_back({"gk_sample", (double)kms, ncons, 0, 0});
+  std::vector<uint64_t> ftot(ncons);
+  std::vector<SampleRec> cand(ncand);
+  hipMemcpy(ftot.data(), e->d_ftot.p, ncons * 8, hipMemcpyDeviceToHost);
+  if (ncand) hipMemcpy(cand.data(), e->d_cand.p, (size_t)ncand * sizeof(SampleRec), hipMemcpyDeviceToHost);
+  for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = ftot[c];
+  std::sort(cand.begin(), cand.end(), [](const SampleRec& x, const SampleRec& y) {
+    if (x.constraint != y.constraint) return x.constraint < y.constraint;
+    if (x.review != y.review) return x.review < y.review;
+    bool ax = x.rule == RULE_AUTOREJECT, ay = y.rule == RULE_AUTOREJECT;
+    if (ax != ay) return ax;
+    return x.seq < y.seq;
+  });
+  uint32_t cur = NO_ID, taken = 0;
+  for (const SampleRec& r : cand) {
+    if (r.constraint != cur) { cur = r.constraint; taken = 0; }
+    if (taken >= limit) continue;
+    ++taken;
+    gk_results::Sample sm;
+    sm.review = r.review;
+    sm.constraint = r.constraint;
+    sm.seq = r.seq;
+    sm.rule = r.rule;
+    sm.msg_len = r.msg_len;
+    sm.msg.assign((const char*)r.msg, std::min<uint32_t>(r.msg_len, SAMPLE_MSG));
+    res->samples.push_back(std::move(sm));
+  }
+  res->ms[4] += ms_since(t0);
+  *out = res;
+  return GK_OK;
+}
+
+size_t gk_results_sample_count(const gk_results* r) { return r ? r->samples.size() : 0; }
+
+int gk_results_sample_get(const gk_results* r, size_t i, gk_sample_view* out) {
+  if (!r || !out || i >= r->samples.size()) return GK_EINVAL;
+  const auto& s = r->samples[i];
+  out->review = s.review;
+  out->constraint = s.constraint;
+  out->seq = s.seq;
+  out->rule = s.rule;
+  out->msg_len = s.msg_len;
+  out->msg = s.msg.data();
+  out->msg_stored = s.msg.size();
+  out->enforcement_action = r->cea[s.constraint].c_str();
+  return GK_OK;
+}
+
+const char* gk_results_constraint_action(const gk_results* r, size_t c) {
+  return r && c < r->cea.size() ? r->cea[c].c_str() : nullptr;
 }
 
 void gk_batch_free(gk_batch* b) {
@@ -1718,6 +1842,58 @@ int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** n
 }  // extern "C"
 
 // ------------------------------------------------------------------ diagnostics
+// The launch arguments of a staged batch with HOST pointers: the host arena
+// holds the same documents as the batch's device nodes while the batch is the
+// last one staged and the engine is unchanged.  Used only by the CPU baseline
+// (oracle/cpuvm.cc), which runs the same bytecode on host threads; `out` must
+// be a gk::DevArgs (checked by size).
+extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, size_t out_size) {
+  if (!e || !b || !out || out_size != sizeof(DevArgs)) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (b->gen != e->gen || b->node_end > e->st.nodes().size() || b->node_end < e->perm_nodes)
+    return fail(e, GK_EINVAL, "batch is not the engine's latest staged batch");
+  e->dbg_cons.clear();
+  for (auto* c : e->corder) e->dbg_cons.push_back(c->spec);
+  if (e->dbg_cons.empty()) e->dbg_cons.push_back(MatchSpec{});
+  e->dbg_progoff.clear();
+  for (auto& p : e->progs) e->dbg_progoff.push_back(p.code_off);
+  if (e->dbg_progoff.empty()) e->dbg_progoff.push_back(0);
+  e->dbg_mwords = e->mwords;
+  if (e->dbg_mwords.empty()) e->dbg_mwords.push_back(0);
+  e->dbg_fmt = e->bank.fmt;
+  if (e->dbg_fmt.empty()) e->dbg_fmt.push_back(0);
+  e->dbg_dfa_keys = e->dfa_keys;
+  e->dbg_dfa_meta = e->dfa_meta;
+  e->dbg_dfa_words = e->dfa_words;
+  if (e->dbg_dfa_keys.empty()) { e->dbg_dfa_keys.push_back(NO_ID); e->dbg_dfa_meta.push_back(2u << 30); }
+  if (e->dbg_dfa_words.empty()) e->dbg_dfa_words.push_back(0);
+  e->dbg_pool = e->st.pool();
+  e->dbg_pool.append(16, '\0');  // dword reads past the last string (devrt.h puts_)
+  DevArgs a{};
+  a.nodes = e->st.nodes().data();
+  a.strs = e->st.strings().data();
+  a.pool = (const uint8_t*)e->dbg_pool.data();
+  a.sflags = e->st.str_flags().data();
+  a.nums = e->st.numbers().data();
+  a.code = e->bank.code.data();
+  a.K = e->bank.consts.data();
+  a.fmt = e->dbg_fmt.data();
+  a.cons = e->dbg_cons.data();
+  a.mwords = e->dbg_mwords.data();
+  a.prog_off = e->dbg_progoff.data();
+  a.revs = b->cols.data();
+  a.dfa_keys = e->dbg_dfa_keys.data();
+  a.dfa_meta = e->dbg_dfa_meta.data();
+  a.dfa_words = e->dbg_dfa_words.data();
+  a.ndfa = (uint32_t)e->dbg_dfa_keys.size();
+  a.ncode = (uint32_t)e->bank.code.size();
+  a.ncons = (uint32_t)e->corder.size();
+  a.nrev = (uint32_t)b->cols.size();
+  a.ntiles = (a.nrev + 63) / 64;
+  memcpy(out, &a, sizeof a);
+  return GK_OK;
+}
+
 // Flattens a page on `threads` host threads without a device (diagnostics and
 // CPU tests): *hash = content hash over every review's columns and document,
 // ms2 = [parse + build, total flatten].  The documents are dropped afterwards.

@@ -11,6 +11,8 @@
 //   stage 3  compact  — violations staged per lane, one output reservation per
 //                       wavefront (wave prefix sum); messages are formatted on
 //                       the GPU (Go fmt / ast.Term.String rules).
+#include <algorithm>
+
 #include "devrt.h"
 
 namespace gk {
@@ -214,3 +216,109 @@ extern "C" int gk_launch_audit(const gk::DevArgs* a, hipStream_t stream) {
 }
 
 extern "C" size_t gk_devargs_size() { return sizeof(gk::DevArgs); }
+
+// ------------------------------------------------------------------ audit samples
+// The audit status keeps, per constraint, the first `limit` results in
+// evaluation order (pkg/audit/manager.go:485, --constraint-violations-limit)
+// and the exact total of results (:470).  The tuples are unordered (one
+// reservation per wavefront), so the first `limit` by (batch review index,
+// autoreject first, emission order) are found in three passes over them:
+//   hist   — per constraint, a histogram of review indices in `nb` buckets
+//            (reviews flagged error / fallback excluded: CPU OPA answers them);
+//   cut    — one wavefront per constraint: the first bucket where the running
+//            count reaches `limit`, and the filtered exact total;
+//   select — tuples in buckets up to the cut are copied out with the first
+//            GK_SAMPLE_MSG bytes of their message (enough for the status's
+//            256-byte truncateString, manager.go:622-631).
+namespace gk {
+
+__global__ void __launch_bounds__(256) gk_mark_ea_error(const Viol* out, uint64_t n, const uint8_t* cerr,
+                                                        uint32_t* rflags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Viol v = out[i];
+    if (cerr[v.constraint]) atomicOr(&rflags[v.review], (uint32_t)RF_ERROR);
+  }
+}
+
+__device__ __forceinline__ uint32_t sample_bucket(uint32_t review, uint32_t nrev, uint32_t nb) {
+  return (uint32_t)(((uint64_t)review * nb) / nrev);
+}
+
+__global__ void __launch_bounds__(256) gk_sample_hist(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
+                                                      uint32_t nb, uint32_t* hist) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Viol v = out[i];
+    if (rflags[v.review] & (RF_ERROR | RF_FALLBACK)) continue;
+    atomicAdd(&hist[(uint64_t)v.constraint * nb + sample_bucket(v.review, nrev, nb)], 1u);
+  }
+}
+
+__global__ void __launch_bounds__(64) gk_sample_cut(const uint32_t* hist, uint32_t nb, uint32_t limit, uint32_t* cut,
+                                                    unsigned long long* ftot) {
+  const uint32_t c = blockIdx.x, lane = threadIdx.x;
+  const uint32_t* h = hist + (uint64_t)c * nb;
+  uint64_t run = 0;
+  uint32_t cb = 0xffffffffu;
+  for (uint32_t base = 0; base < nb; base += 64) {
+    uint32_t x = base + lane < nb ? h[base + lane] : 0u;
+    uint32_t incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    uint32_t tot = __shfl(incl, 63, 64);
+    if (cb == 0xffffffffu && run + tot >= limit) {
+      // first lane whose inclusive count reaches the limit
+      unsigned long long m = __ballot(run + incl >= limit);
+      cb = base + (uint32_t)__ffsll((long long)m) - 1;
+    }
+    run += tot;
+  }
+  if (lane == 0) {
+    cut[c] = cb == 0xffffffffu ? nb - 1 : cb;
+    ftot[c] = run;
+  }
+}
+
+__global__ void __launch_bounds__(256) gk_sample_select(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
+                                                        uint32_t nb, const uint32_t* cut, const char* bytes,
+                                                        SampleRec* cand, uint32_t cap, unsigned int* ncand) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Viol v = out[i];
+    if (rflags[v.review] & (RF_ERROR | RF_FALLBACK)) continue;
+    if (sample_bucket(v.review, nrev, nb) > cut[v.constraint]) continue;
+    uint32_t slot = atomicAdd(ncand, 1u);
+    if (slot >= cap) continue;  // the host grows the buffer and runs this pass again
+    SampleRec& r = cand[slot];
+    r.review = v.review;
+    r.constraint = v.constraint;
+    r.seq = v.seq;
+    r.rule = v.rule;
+    r.msg_len = v.msg_len;
+    r.pad = 0;
+    uint32_t m = v.msg_len < SAMPLE_MSG ? v.msg_len : SAMPLE_MSG;
+    const char* src = bytes + v.msg_off;
+    for (uint32_t k = 0; k < m; ++k) r.msg[k] = (uint8_t)src[k];
+  }
+}
+
+}  // namespace gk
+
+extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
+                                uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
+                                unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
+                                unsigned int* ncand, int select_only, hipStream_t stream) {
+  uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  if (blocks == 0) blocks = 1;
+  if (!select_only) {
+    if (cerr) hipLaunchKernelGGL(gk::gk_mark_ea_error, dim3(blocks), dim3(256), 0, stream, out, n, cerr, rflags);
+    (void)hipMemsetAsync(hist, 0, (size_t)ncons * nb * 4, stream);
+    hipLaunchKernelGGL(gk::gk_sample_hist, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev, nb, hist);
+    hipLaunchKernelGGL(gk::gk_sample_cut, dim3(ncons), dim3(64), 0, stream, (const uint32_t*)hist, nb, limit, cut, ftot);
+  }
+  (void)hipMemsetAsync(ncand, 0, 4, stream);
+  hipLaunchKernelGGL(gk::gk_sample_select, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev, nb,
+                     (const uint32_t*)cut, bytes, cand, cap, ncand);
+  return (int)hipGetLastError();
+}

@@ -21,14 +21,22 @@ DEFAULT_LIMIT = 20                  # manager.go:43 (--constraint-violations-lim
 KNOWN_ACTIONS = ("deny", "dryrun", "unrecognized")  # pkg/util/enforcement_action.go:11-17
 
 
+def truncate_bytes(head: bytes, total_len: int, size: int = MSG_SIZE) -> str:
+    """truncateString (manager.go:623-631) of a message known by its first
+    bytes `head` (at least min(total_len, size) of them) and its byte length;
+    the status is JSON, so a cut inside a UTF-8 sequence marshals as U+FFFD."""
+    if total_len <= size:
+        return head[:total_len].decode("utf-8", "surrogateescape")
+    cut = size - 3 if size > 3 else size
+    return (head[:cut] + b"...").decode("utf-8", "replace")
+
+
 def truncate_string(msg: str, size: int = MSG_SIZE) -> str:
-    """truncateString (manager.go:623-631) on the message's bytes; the status
-    is JSON, so a cut inside a UTF-8 sequence marshals as U+FFFD."""
+    """truncateString (manager.go:623-631) on the message's bytes"""
     b = msg.encode("utf-8", "surrogateescape")
     if len(b) <= size:
         return msg
-    cut = size - 3 if size > 3 else size
-    return (b[:cut] + b"...").decode("utf-8", "replace")
+    return truncate_bytes(b, len(b), size)
 
 
 class AuditWriter:
@@ -51,6 +59,35 @@ class AuditWriter:
                         "enforcementAction": enforcement_action})
         self.per_action[enforcement_action] = self.per_action.get(enforcement_action, 0) + 1
 
+    def add_sample(self, constraint: int, resource: Tuple[str, str, str], head: bytes, msg_len: int,
+                   enforcement_action: str):
+        """one sampled result whose message is known by its first bytes (the
+        engine's device sample, gk_results_sample_get); totals come separately"""
+        lst = self.samples.setdefault(constraint, [])
+        if len(lst) < self.limit:
+            kind, name, ns = resource
+            lst.append({"kind": kind, "name": name, "namespace": ns, "final": truncate_bytes(head, msg_len),
+                        "enforcementAction": enforcement_action})
+
+    def set_totals(self, totals: Sequence[int], actions: Sequence[str]):
+        """per-constraint totals of a sweep and the per-action totals they imply
+        (every result of a constraint carries its enforcementAction)"""
+        self.totals = {c: int(n) for c, n in enumerate(totals) if n}
+        self.per_action = {a: 0 for a in KNOWN_ACTIONS}
+        for c, n in enumerate(totals):
+            if n:
+                self.per_action[actions[c]] = self.per_action.get(actions[c], 0) + int(n)
+
+    @staticmethod
+    def from_sweep(constraints, sweep, resource_of_review, limit: int = DEFAULT_LIMIT) -> "AuditWriter":
+        """status writer of one engine sweep (Batch.eval_audit);
+        resource_of_review(i) -> (kind, name, namespace)"""
+        w = AuditWriter(constraints, limit)
+        w.set_totals(sweep.totals, sweep.actions)
+        for s in sweep.samples:
+            w.add_sample(s.constraint, resource_of_review(s.review), s.msg, s.msg_len, s.enforcement_action)
+        return w
+
     def add_results(self, results, resources: Sequence[Tuple[str, str, str]]):
         """engine or oracle results, already in evaluation order (review, then
         the per-review result order), each with .review/.constraint/.msg/
@@ -66,7 +103,7 @@ class AuditWriter:
             v = {"kind": ar["kind"], "name": ar["name"]}
             if ar["namespace"]:
                 v["namespace"] = ar["namespace"]
-            v["message"] = truncate_string(ar["message"])
+            v["message"] = ar["final"] if "final" in ar else truncate_string(ar["message"])
             v["enforcementAction"] = ar["enforcementAction"]
             vs.append(v)
         if vs:

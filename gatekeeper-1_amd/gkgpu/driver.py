@@ -30,7 +30,14 @@ EXPORTS = [
     "gk_results_launches", "gk_results_launch", "gk_template_backend", "gk_results_copy_device_output",
     "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
+    "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
 ]
+
+
+class _SampleView(C.Structure):
+    _fields_ = [("review", C.c_uint32), ("constraint", C.c_uint32), ("seq", C.c_uint16), ("rule", C.c_uint16),
+                ("msg_len", C.c_uint32), ("msg", C.c_void_p), ("msg_stored", C.c_size_t),
+                ("enforcement_action", C.c_char_p)]
 
 GK_REVIEW_EXCLUDED = 4
 RESOURCE_FIELD = 512
@@ -141,6 +148,12 @@ def load_library():
     lib.gk_excluder_is_excluded.argtypes = [vp, cp, cp]
     lib.gk_results_excluded.argtypes = [vp]
     lib.gk_results_excluded.restype = C.c_uint64
+    lib.gk_batch_eval_audit.argtypes = [vp, vp, C.c_uint32, C.POINTER(vp)]
+    lib.gk_results_sample_count.argtypes = [vp]
+    lib.gk_results_sample_count.restype = sz
+    lib.gk_results_sample_get.argtypes = [vp, sz, C.POINTER(_SampleView)]
+    lib.gk_results_constraint_action.argtypes = [vp, sz]
+    lib.gk_results_constraint_action.restype = cp
     _LIB = lib
     return lib
 
@@ -213,6 +226,57 @@ def _launches(lib, h):
         lib.gk_results_launch(h, i, C.byref(k), C.byref(ms), C.byref(n), C.byref(t), C.byref(b))
         out.append(Launch(k.value.decode(), ms.value, n.value, t.value, b.value))
     return out
+
+
+@dataclass
+class Sample:
+    """one of the first `limit` results of a constraint (gk_sample_view)"""
+    review: int
+    constraint: int
+    seq: int
+    rule: int               # 0xffff = autoreject
+    msg_len: int            # full message length in bytes
+    msg: bytes              # its first min(msg_len, 256) bytes
+    enforcement_action: str
+
+
+@dataclass
+class AuditSweep:
+    """gk_batch_eval_audit: what one audit sweep hands the status writer"""
+    totals: List[int]       # per constraint, over the reviews the engine answered
+    samples: List[Sample]   # first `limit` per constraint, evaluation order
+    actions: List[str]      # per constraint enforcementAction
+    n_errors: int
+    n_fallbacks: int
+    excluded: int
+    timing_ms: List[float]
+    device_tuples: int
+    device_bytes: int
+    launches: List["Launch"]
+
+
+def _collect_audit(lib, h) -> AuditSweep:
+    try:
+        nc = lib.gk_results_constraints(h)
+        totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
+        actions = [(lib.gk_results_constraint_action(h, i) or b"").decode("utf-8", "surrogateescape") for i in range(nc)]
+        v = _SampleView()
+        samples = []
+        for i in range(lib.gk_results_sample_count(h)):
+            lib.gk_results_sample_get(h, i, C.byref(v))
+            samples.append(Sample(v.review, v.constraint, v.seq, v.rule, v.msg_len,
+                                  C.string_at(v.msg, v.msg_stored) if v.msg_stored else b"",
+                                  v.enforcement_action.decode("utf-8", "surrogateescape")))
+        t = (C.c_double * 5)()
+        lib.gk_results_timing(h, t)
+        dt, db = C.c_uint64(), C.c_uint64()
+        lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
+        ne, nf = C.c_uint64(), C.c_uint64()
+        lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
+        return AuditSweep(totals, samples, actions, ne.value, nf.value, lib.gk_results_excluded(h), list(t), dt.value,
+                          db.value, _launches(lib, h))
+    finally:
+        lib.gk_results_free(h)
 
 
 def _collect_light(lib, h) -> Results:
@@ -295,6 +359,14 @@ class Batch:
                 self._drv._check(rc)
         return _collect_light(lib, out) if light else _collect(lib, out)
 
+    def eval_audit(self, limit: int = 20) -> AuditSweep:
+        """one audit sweep: exact totals + first `limit` results per constraint
+        (gk_batch_eval_audit; pkg/audit/manager.go:462-508)"""
+        lib = self._drv._lib
+        out = C.c_void_p()
+        self._drv._check(lib.gk_batch_eval_audit(self._drv._e, self._h, limit, C.byref(out)))
+        return _collect_audit(lib, out)
+
     def device_bytes(self) -> int:
         return self._drv._lib.gk_batch_device_bytes(self._h)
 
@@ -338,11 +410,15 @@ class Batch:
 class Driver:
     """drivers.Driver over libgkgpu (interface.go:21-39)."""
 
-    def __init__(self, device: int = 0, jit: bool = True):
-        """jit=False pins every template to the bytecode VM kernel (A/B parity)."""
+    def __init__(self, device: int = 0, jit: bool = True, host_only: bool = False):
+        """jit=False pins every template to the bytecode VM kernel (A/B parity);
+        host_only=True stages batches on the host only (CPU baseline, tests)."""
         self._lib = load_library()
         e = C.c_void_p()
-        rc = self._lib.gk_engine_create(_b(json.dumps({"device": device, "jit": jit})), C.byref(e))
+        opts = {"device": device, "jit": jit}
+        if host_only:
+            opts["host_only"] = True
+        rc = self._lib.gk_engine_create(_b(json.dumps(opts)), C.byref(e))
         if rc != 0:
             raise EngineUnavailable("gk_engine_create failed (%d)" % rc)
         self._e = e

@@ -153,3 +153,100 @@ def decode(parts, limit: Optional[int] = None):
     rows.sort(key=lambda r: (r[0], r[1], r[2], r[3]))
     out = [(r[0], r[2], r[3], r[4], r[5], r[6]) for r in rows]
     return out[:limit] if limit is not None else out
+
+
+# ------------------------------------------------------------------ audit exchange
+# SURVEY 8(e): after each rank's sweep, the only exchange the audit status
+# needs is (i) the per-constraint totals, all-reduced as int64, and (ii) per
+# constraint the first `limit` results by global resource index, which each
+# rank has already selected on its device (Batch.eval_audit); rank 0 merges the
+# ranks' candidates (at most constraints x limit each) and writes the statuses.
+# The reference audits one object at a time in discovery order
+# (manager.go:333-389), which Go map iteration makes nondeterministic; the
+# engine fixes that order as the global resource index.
+
+def _sample_rows(sweep, review_base: int, resource_of_review):
+    """[global review, constraint, autoreject first (0/1), seq, msg_len, head
+    (latin-1 str), enforcementAction, kind, name, namespace] per sample"""
+    rows = []
+    for s in sweep.samples:
+        kind, name, ns = resource_of_review(s.review)
+        rows.append([int(review_base) + s.review, s.constraint, 0 if s.rule == 0xffff else 1, s.seq, s.msg_len,
+                     s.msg.decode("latin-1"), s.enforcement_action, kind, name, ns])
+    return rows
+
+
+def gather_bytes(payload: bytes, dst: int = 0, device=None, group=None):
+    """every rank's payload to `dst` (list in rank order there, None elsewhere):
+    an all-gather of sizes, then exact-size point-to-point transfers
+    (device tensors under RCCL, CPU tensors under gloo)"""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = device if device is not None else torch.device("cpu")
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev) if payload else \
+        torch.zeros(0, dtype=torch.uint8, device=dev)
+    ops, recv = [], {}
+    if rank == dst:
+        for r in range(world):
+            if r != rank and sizes[r]:
+                recv[r] = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+                ops.append(dist.P2POp(dist.irecv, recv[r], r, group))
+    elif sizes[rank]:
+        ops.append(dist.P2POp(dist.isend, buf, dst, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if rank != dst:
+        return None
+    out = []
+    for r in range(world):
+        if r == rank:
+            out.append(payload)
+        else:
+            out.append(bytes(recv[r].cpu().numpy().tobytes()) if r in recv else b"")
+    return out
+
+
+def merge_samples(rows, limit: int):
+    """first `limit` rows per constraint by (global review, autoreject first, seq)"""
+    rows = sorted(rows, key=lambda r: (r[1], r[0], r[2], r[3]))
+    out, cur, taken = [], None, 0
+    for r in rows:
+        if r[1] != cur:
+            cur, taken = r[1], 0
+        if taken < limit:
+            out.append(r)
+            taken += 1
+    return out
+
+
+def exchange_audit(sweep, review_base: int, resource_of_review, constraints, limit: int = 20, dst: int = 0,
+                   device=None, group=None):
+    """The multi-rank audit exchange: totals all-reduce (int64) + samples
+    gathered to `dst`, merged into an AuditWriter there (None elsewhere)."""
+    import json
+    import torch
+    import torch.distributed as dist
+    from .audit import AuditWriter
+    dev = device if device is not None else torch.device("cpu")
+    tot = torch.tensor([int(x) for x in sweep.totals], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot, group=group)
+    payload = json.dumps(_sample_rows(sweep, review_base, resource_of_review)).encode()
+    parts = gather_bytes(payload, dst, dev, group)
+    if parts is None:
+        return None
+    rows = []
+    for p in parts:
+        if p:
+            rows.extend(json.loads(p.decode()))
+    w = AuditWriter(constraints, limit)
+    w.set_totals(tot.cpu().tolist(), sweep.actions)
+    for r in merge_samples(rows, limit):
+        w.add_sample(r[1], (r[7], r[8], r[9]), r[5].encode("latin-1"), r[4], r[6])
+    return w

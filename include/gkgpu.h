@@ -134,6 +134,29 @@ uint64_t gk_batch_device_bytes(const gk_batch* b);
  * each), bytes of the distinct string values they reference, match-column bytes */
 int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes);
 
+/* One audit sweep of a staged batch as the audit status needs it
+ * (pkg/audit/manager.go:462-508): gk_results_constraint_total = exact
+ * per-constraint totals over the reviews the engine answered (flagged reviews
+ * excluded: CPU OPA answers them), and gk_results_sample_* = the first `limit`
+ * results per constraint in evaluation order (batch review index, autoreject
+ * first, emission order), selected on the device so that only
+ * constraints x limit records leave it.  Messages carry their first
+ * GK_SAMPLE_MSG bytes (the status truncates at 256, manager.go:622-631). */
+#define GK_SAMPLE_MSG 256
+int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out);
+typedef struct {
+  uint32_t review, constraint;
+  uint16_t seq, rule;          /* rule 0xffff = autoreject */
+  uint32_t msg_len;            /* full message length */
+  const char* msg;             /* first msg_stored bytes (not NUL-terminated) */
+  size_t msg_stored;
+  const char* enforcement_action;
+} gk_sample_view;
+size_t gk_results_sample_count(const gk_results* r);
+int gk_results_sample_get(const gk_results* r, size_t i, gk_sample_view* out);
+/* the constraint's enforcementAction as results report it */
+const char* gk_results_constraint_action(const gk_results* r, size_t constraint);
+
 /* ---- process excluder (pkg/controller/config/process/excluder.go) --------- */
 /* Excluder.Add(MatchEntry{ExcludedNamespaces: namespaces, Processes: processes})
  * — excluder.go:44-68; process "*" adds the namespaces to audit, webhook and

@@ -1,0 +1,45 @@
+"""ctypes front of oracle/libgkcpu.so (cpuvm.cc) -- the CPU baseline of the
+audit sweep.  TEST / MEASUREMENT INFRASTRUCTURE: only tests/ and bench.py's
+cpu_baseline leg use it; it never evaluates anything for the product path.
+
+It runs the engine's compiled template bytecode with the engine's own device
+runtime (devrt.h) compiled for the host, on host threads, over a staged batch
+whose documents are still in the engine's host arena (gk_debug_host_args).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "libgkcpu.so")
+
+
+def load():
+    global _LIB
+    if _LIB is None:
+        lib = C.CDLL(lib_path())
+        lib.gkcpu_devargs_size.restype = C.c_size_t
+        lib.gkcpu_sweep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]
+        lib.gkcpu_sweep.restype = C.c_double
+        _LIB = lib
+    return _LIB
+
+
+def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1):
+    """(seconds, evals, violations, message bytes, flagged pairs) of reviews
+    [lo, hi) of `batch` x every constraint, on `threads` host threads"""
+    lib = load()
+    glib = driver._lib
+    n = lib.gkcpu_devargs_size()
+    buf = (C.c_uint8 * n)()
+    glib.gk_debug_host_args.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
+    out = (C.c_uint64 * 4)()
+    hi = batch.n if hi is None else hi
+    s = lib.gkcpu_sweep(buf, lo, hi, threads, out)
+    return s, out[0], out[1], out[2], out[3]

@@ -1,0 +1,212 @@
+// CPU baseline of the audit sweep -- TEST / MEASUREMENT INFRASTRUCTURE, NOT
+// THE PRODUCT AND NOT OPA.
+//
+// The reference's own CPU path (Go OPA v0.21 topdown, drivers/local/local.go)
+// cannot be built here (no Go toolchain), so bench.py's
+// cpu_baseline times this native multi-threaded evaluator instead, labelled
+// kind "port" with its thread count.  It runs the SAME compiled template
+// bytecode and the same match / builtin / printing semantics as the device
+// (the engine's devrt.h compiled for the host), one (review, constraint) pair
+// per call, over std::thread workers -- i.e. an interpreter of the engine's
+// own program, with none of OPA's per-Review JSON round trips
+// (local.go:331, rego.go:1478-1496), so it is a much stronger baseline than
+// the reference as deployed.  Messages are formatted, as the GPU format pass
+// does.  Only bench.py's cpu_baseline leg and tests load it; the product
+// (gatekeeper-1_amd/) never does.
+//
+// Per pair it follows devrt.h audit_body (autoreject, matching_constraints,
+// template program) and kernels.hip run_program (the bytecode VM loop).
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+// ---- host spellings of the device-language words devrt.h uses
+namespace __hip_internal {
+using ::int16_t;
+using ::int32_t;
+using ::int64_t;
+using ::int8_t;
+using ::uint16_t;
+using ::uint32_t;
+using ::uint64_t;
+using ::uint8_t;
+}  // namespace __hip_internal
+#define __HIPCC_RTC__ 1
+#define __device__
+#define __global__
+#define __host__
+#define __constant__
+#define __forceinline__ inline __attribute__((always_inline))
+#define __noinline__ __attribute__((noinline))
+// single-lane stand-ins: the wave-level paths (flush_wave, audit_body) are
+// compiled but never called here
+template <class T> static inline T __shfl_up(T v, int, int) { return v; }
+template <class T> static inline T __shfl(T v, int, int) { return v; }
+template <class T> static inline T __shfl_xor(T v, int, int) { return v; }
+template <class T, class U> static inline T atomicAdd(T* p, U v) { T o = *p; *p = (T)(o + v); return o; }
+template <class T, class U> static inline T atomicOr(T* p, U v) { T o = *p; *p = (T)(o | v); return o; }
+template <class T, class U> static inline T atomicMax(T* p, U v) { T o = *p; if ((T)v > o) *p = (T)v; return o; }
+static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+struct CpuDim3 { uint32_t x = 0, y = 0, z = 0; };
+static CpuDim3 blockIdx, threadIdx, blockDim{64, 1, 1}, gridDim{1, 1, 1};
+
+#include "../gatekeeper-1_amd/csrc/devrt.h"
+
+namespace gk {
+namespace cpu {
+
+constexpr int NREG = 192;
+
+// kernels.hip run_program on the host
+static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  uint64_t R[NREG];
+  for (int guard = 0; guard < (1 << 22); ++guard) {
+    if (pc >= gk_args.ncode) { lane_fallback(L, FB_UNSUPPORTED); return; }
+    const Ins in = gk_args.code[pc];
+    ++pc;
+    switch (in.op) {
+      case OP_END: return;
+      case OP_JMP: pc = in.x; break;
+      case OP_JUNDEF: if (vtag(R[in.a]) == V_UNDEF) pc = in.x; break;
+      case OP_JFALSE: if (vtag(R[in.a]) == V_BOOL && vpay(R[in.a]) == 0) pc = in.x; break;
+      case OP_JTRUE: if (vtag(R[in.a]) == V_BOOL && vpay(R[in.a]) == 1) pc = in.x; break;
+      case OP_LOADK: R[in.a] = gk_args.K[in.x]; break;
+      case OP_LOADREV: R[in.a] = review; break;
+      case OP_LOADPARAM: R[in.a] = params; break;
+      case OP_MOV: R[in.a] = R[in.b]; break;
+      case OP_GET: R[in.a] = vget(L, R[in.b], R[in.c]); break;
+      case OP_GETK: R[in.a] = vget(L, R[in.b], gk_args.K[in.x]); break;
+      case OP_ITER_INIT: op_iter_init(L, R[in.a], R[in.a + 1], R[in.b], in.y); break;
+      case OP_ITER_NEXT: {
+        uint64_t k = UND, v = UND;
+        if (!op_iter_next(L, R[in.a], R[in.a + 1], in.y, k, v)) { pc = in.x; break; }
+        if (in.b != 0xffff) R[in.b] = k;
+        if (in.c != 0xffff) R[in.c] = v;
+        break;
+      }
+      case OP_CMP: if (!op_cmp(L, in.y, R[in.b], R[in.c], R[in.a])) return; break;
+      case OP_ARITH: R[in.a] = arith(L, in.y, R[in.b], R[in.c]); if (L.fail) return; break;
+      case OP_LIST_NEW: R[in.a] = list_new(L, in.y, 4); if (L.fail) return; break;
+      case OP_LIST_ADD: if (!op_list_add(L, R[in.a], R[in.b], in.y)) return; break;
+      case OP_OBJ_PUT: if (!op_obj_put(L, R[in.a], R[in.b], R[in.c], in.y)) return; break;
+      case OP_YIELD: if (!op_yield(L, R[in.a], R[in.b], in.y)) return; break;
+      case OP_CALL: R[in.a] = call_builtin(L, in.y, &R[in.b]); if (L.fail) return; break;
+      case OP_SPRINTF: R[in.a] = do_sprintf(L, in.x, R[in.b]); if (L.fail) return; break;
+      case OP_LEN_EQ: R[in.a] = op_len_eq(L, R[in.b], in.y); break;
+      case OP_EMIT: if (!op_emit(L, R[in.a], in.b == 0xffff ? UND : R[in.b], in.c, in.y)) return; break;
+      case OP_TABLE: R[in.a] = op_table(L, gk_args.K + in.x, R[in.b]); break;
+      case OP_MEMO_GET: {
+        uint64_t k1 = in.c == 0xffff ? 0 : R[in.c];
+        if (((L.memo_ok >> in.y) & 1) && L.memo_k0[in.y] == R[in.b] && L.memo_k1[in.y] == k1) {
+          R[in.a] = L.memo_v[in.y];
+          pc = in.x;
+        }
+        break;
+      }
+      case OP_MEMO_PUT: {
+        uint64_t k1 = in.c == 0xffff ? 0 : R[in.c];
+        if (memo_stable(R[in.b]) && memo_stable(k1) && memo_stable(R[in.a])) {
+          L.memo_k0[in.y] = R[in.b];
+          L.memo_k1[in.y] = k1;
+          L.memo_v[in.y] = R[in.a];
+          L.memo_ok |= 1u << in.y;
+        }
+        break;
+      }
+      case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
+      default: lane_fallback(L, FB_UNSUPPORTED); return;
+    }
+  }
+  lane_fallback(L, FB_UNSUPPORTED);
+}
+
+struct Counts {
+  uint64_t evals = 0, violations = 0, msg_bytes = 0, flagged = 0;
+};
+
+// devrt.h audit_body for one (review position, constraint), then the message
+// bytes of every staged violation (the format pass's work)
+static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t fcap) {
+  Lane L;
+  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+  const ReviewCol rc = gk_args.revs[rp];
+  const MatchSpec m = gk_args.cons[c];
+  ++k.evals;
+  if (rc.flags & RC_FALLBACK) {
+    L.fail = RF_FALLBACK;
+  } else {
+    if ((m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) &&
+        !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS))
+      stage_tuple(L, RULE_AUTOREJECT, "Namespace is not cached in OPA.", 31, "{}", 2, 0);
+    int mr = match_constraint(m, rc);
+    if (mr == -1) L.fail = RF_ERROR;
+    else if (mr == -2) L.fail = RF_FALLBACK;
+    else if (mr == 1 && (m.flags & MF_FALLBACK)) lane_fallback(L, FB_TEMPLATE);
+    else if (mr == 1 && m.prog != NO_ID) {
+      uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
+      run_program(L, gk_args.prog_off[m.prog], mkv(V_NODE, rc.root), params);
+    }
+  }
+  if (L.fail) { ++k.flagged; return; }
+  for (uint32_t i = 0; i < L.en; ++i) {
+    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], o = L.em_off[i];
+    if (dw & 0x8000u) {
+      const uint64_t* rec = (const uint64_t*)(L.B + o);
+      uint32_t h = (uint32_t)rec[0];
+      Out out{fbuf, 0, fcap, false};
+      fmt_run(L, out, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
+      k.msg_bytes += out.n;
+    } else {
+      k.msg_bytes += ml;
+    }
+    ++k.violations;
+  }
+}
+
+}  // namespace cpu
+}  // namespace gk
+
+extern "C" {
+
+size_t gkcpu_devargs_size() { return sizeof(gk::DevArgs); }
+
+// Evaluates reviews [lo, hi) of the staged batch described by `args` (host
+// pointers, gk_debug_host_args) against every constraint on `threads` threads.
+// out4 = [evals, violations, message bytes, flagged pairs]; returns seconds.
+double gkcpu_sweep(const void* args, uint32_t lo, uint32_t hi, int threads, uint64_t* out4) {
+  memcpy(&gk_args, args, sizeof(gk::DevArgs));
+  if (hi > gk_args.nrev) hi = gk_args.nrev;
+  if (lo > hi) lo = hi;
+  const uint32_t ncons = gk_args.ncons;
+  if (threads < 1) threads = 1;
+  std::vector<gk::cpu::Counts> per(threads);
+  std::atomic<uint32_t> next{lo};
+  auto t0 = std::chrono::steady_clock::now();
+  auto work = [&](int t) {
+    std::vector<char> fbuf(1 << 16);
+    gk::cpu::Counts& k = per[t];
+    for (;;) {
+      uint32_t a = next.fetch_add(256);
+      if (a >= hi) break;
+      uint32_t b = a + 256 < hi ? a + 256 : hi;
+      for (uint32_t rp = a; rp < b; ++rp)
+        for (uint32_t c = 0; c < ncons; ++c) gk::cpu::eval_pair(rp, c, k, fbuf.data(), (uint32_t)fbuf.size());
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t tot[4] = {0, 0, 0, 0};
+  for (auto& k : per) { tot[0] += k.evals; tot[1] += k.violations; tot[2] += k.msg_bytes; tot[3] += k.flagged; }
+  if (out4) memcpy(out4, tot, sizeof tot);
+  return s;
+}
+
+}  // extern "C"

@@ -93,3 +93,97 @@ def test_shard_range_covers_exactly():
             got = [shard_range(n, r, world) for r in range(world)]
             flat = [i for lo, hi in got for i in range(lo, hi)]
             assert flat == list(range(n))
+
+
+# -- the audit exchange (totals all-reduce + first-limit samples, gkgpu/parallel.py exchange_audit)
+
+def _oracle_rows(n_pods=240):
+    """per review: [(constraint index, autoreject?, seq, msg, enforcementAction)] from the CPU oracle"""
+    import json as _json
+    from gkgpu import workloads as W
+    from gkgpu.client import augmented_review
+    from parity import oracle_for, oracle_review
+    ts, cs = W.config2()
+    cs = [dict(c) for c in cs]
+    cs[3] = W.constraint("K8sRequiredProbes", "must-have-probes", match=cs[3]["spec"]["match"],
+                         parameters=cs[3]["spec"]["parameters"], enforcement_action="dryrun")
+    od = oracle_for(ts, cs)
+    pods, ns_of, ns_objs = W.gen_pods(n_pods, seed=23, n_namespaces=12)
+    cidx = {(c["kind"], c["metadata"]["name"]): i for i, c in enumerate(cs)}
+    per = []
+    for p, n in zip(pods, ns_of):
+        rows, seq = [], {}
+        for kind, name, msg, _det, ea in oracle_review(od, augmented_review(p, ns_objs[n])):
+            c = cidx[(kind, name)]
+            rows.append((c, 1, seq.get(c, 0), msg, ea))
+            seq[c] = seq.get(c, 0) + 1
+        per.append(rows)
+    cons = [(c["kind"], c["metadata"]["name"]) for c in cs]
+    actions = [c.get("spec", {}).get("enforcementAction", "deny") for c in cs]
+    res = [("Pod", p["metadata"]["name"], p["metadata"]["namespace"]) for p in pods]
+    return per, cons, actions, res
+
+
+def _sweep_of(per, lo, hi, ncons, actions, limit):
+    """an engine-shaped AuditSweep for reviews [lo, hi) (local review indices)"""
+    from gkgpu.driver import AuditSweep, Sample
+    totals = [0] * ncons
+    cand = []
+    for r in range(lo, hi):
+        for c, ar, seq, msg, ea in per[r]:
+            totals[c] += 1
+            cand.append((c, r - lo, ar, seq, msg, ea))
+    cand.sort(key=lambda x: (x[0], x[1], x[2], x[3]))
+    samples, taken = [], {}
+    for c, rv, ar, seq, msg, ea in cand:
+        if taken.get(c, 0) < limit:
+            taken[c] = taken.get(c, 0) + 1
+            b = msg.encode()
+            samples.append(Sample(rv, c, seq, 0 if ar else 0xffff, len(b), b[:256], ea))
+    return AuditSweep(totals, samples, actions, 0, 0, 0, [], 0, 0, [])
+
+
+def _audit_worker(rank, world, port, limit, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "gatekeeper-1_amd")]
+        from gkgpu.audit import AuditWriter
+        from gkgpu.parallel import exchange_audit
+        per, cons, actions, res = _oracle_rows()
+        lo, hi = shard_range(len(per), rank, world)
+        sweep = _sweep_of(per, lo, hi, len(cons), actions, limit)
+        merged = exchange_audit(sweep, lo, lambda i: res[lo + i], cons, limit=limit)
+        if rank == 0:
+            single = AuditWriter(cons, limit)
+            for r, rows in enumerate(per):
+                for c, _ar, _seq, msg, ea in rows:
+                    single.add(c, res[r], msg, ea)
+            q.put(("ok", merged.statuses() == single.statuses(), merged.per_action == single.per_action,
+                   sum(merged.totals.values())))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put(("err", traceback.format_exc(), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,limit", [(2, 3), (2, 20), (3, 5)])
+def test_audit_exchange_equals_single_process_sweep(world, limit):
+    """shards' engine-shaped sweeps, exchanged over gloo, give exactly the
+    statuses of one sweep over all resources (manager.go:462-508)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_audit_worker, args=(r, world, port, limit, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    status, same, same_act, total = q.get(timeout=240)
+    for p in ps:
+        p.join(60)
+    assert status == "ok", same
+    assert same and same_act and total > 100
