@@ -36,7 +36,12 @@ def parse():
     ap.add_argument("--load", type=int, default=50, help="config 5: constraints loaded (policy_benchmark_test.go:268)")
     ap.add_argument("--batch", type=int, default=256, help="config 5: AdmissionReviews per launch")
     ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
-    ap.add_argument("--cpu-sample", type=int, default=1500, help="Pods timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="resources of the staged batch timed on the native CPU baseline (oracle/cpuvm.cc; "
+                         "-1 = all of them, 0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cpu count))")
+    ap.add_argument("--oracle-sample", type=int, default=0,
+                    help="resources also timed on the Python oracle (1 core; 0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch for this workload (rocprofv3 --pmc), if measured")
     return ap.parse_args()
@@ -242,12 +247,15 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        sample = page.slice(0, min(args.cpu_sample, page.n))
-        so = [sample.objs[int(sample.obj_offs[i]):int(sample.obj_offs[i + 1])].decode() for i in range(sample.n)]
-        sn = [None if k == 0xFFFFFFFF else page.nss[int(page.ns_offs[k]):int(page.ns_offs[k + 1])].decode()
-              for k in sample.obj_ns]
-        cpu = cpu_baseline(templates, constraints, so, sn)
+    if rank == 0 and world == 1 and args.cpu_sample != 0:
+        n_cpu = nrev if args.cpu_sample < 0 else min(args.cpu_sample, nrev)
+        cpu = native_cpu_baseline(drv, batch, n_cpu, args.cpu_threads, last)
+        if args.oracle_sample > 0:
+            sample = page.slice(0, min(args.oracle_sample, page.n))
+            so = [sample.objs[int(sample.obj_offs[i]):int(sample.obj_offs[i + 1])].decode() for i in range(sample.n)]
+            sn = [None if k == 0xFFFFFFFF else page.nss[int(page.ns_offs[k]):int(page.ns_offs[k + 1])].decode()
+                  for k in sample.obj_ns]
+            cpu["python_oracle"] = cpu_baseline(templates, constraints, so, sn)
 
     if rank == 0:
         out = {
@@ -309,6 +317,39 @@ def main():
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def native_cpu_baseline(drv, batch, n_cpu, threads, gpu_sweep):
+    """The native CPU baseline (oracle/cpuvm.cc): the engine's compiled
+    template bytecode and device runtime, built for the host, over the first
+    `n_cpu` reviews of the same staged batch x every constraint on `threads`
+    host threads (messages formatted).  NOT OPA: Go/OPA v0.21 cannot be built
+    offline; this is a far leaner CPU evaluator than the
+    reference's per-Review topdown + JSON round trips."""
+    sys.path.insert(0, ROOT)
+    from oracle import cpu_baseline as CB
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    secs, evals, viol, mbytes, flagged = CB.sweep(drv, batch, 0, n_cpu, threads)
+    out = {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port",
+           "sample": "%d resources x %d constraints of the same staged batch (%s); oracle/cpuvm.cc: the engine's "
+                     "compiled bytecode + device runtime on host threads, NOT OPA (Go/OPA not buildable offline)"
+                     % (n_cpu, len(gpu_sweep.totals), "all" if n_cpu == batch.n else "prefix"),
+           "seconds": secs, "cpu_model": cpu_model(), "violations": viol, "message_bytes": mbytes,
+           "flagged_pairs": flagged}
+    if n_cpu == batch.n:
+        out["violations_equal_gpu"] = viol == gpu_sweep.device_tuples
+    return out
 
 
 def cpu_baseline(templates, constraints, objs_json, nss_json):

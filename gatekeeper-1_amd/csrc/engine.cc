@@ -1140,6 +1140,23 @@ int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
   return GK_OK;
 }
 
+// Query inputs ({"review": ...} documents) into the transient region
+static int flatten_inputs(gk_engine* e, const std::vector<std::pair<const char*, size_t>>& inputs,
+                          std::vector<ReviewCol>& cols) {
+  cols.reserve(inputs.size());
+  JDoc d;
+  for (auto& in : inputs) {
+    JsonReader rd(in.first, in.second, &d);
+    int root = rd.parse();
+    if (root < 0) return fail(e, GK_EINVAL, "invalid input JSON: " + d.err);
+    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
+    uint32_t rn = rv >= 0 ? e->st.add_doc(d, rv) : NO_ID;
+    bool glob = false;
+    cols.push_back(review_columns(e->st, e->st, e->ns_cache, rn, &glob));
+  }
+  return GK_OK;
+}
+
 static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, size_t>>& inputs, gk_results** out) {
   auto* res = new gk_results();
   try {
@@ -1152,17 +1169,8 @@ static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, si
   auto t0 = Clock::now();
   reset_transient(e);
   std::vector<ReviewCol> cols;
-  cols.reserve(inputs.size());
-  JDoc d;
-  for (auto& in : inputs) {
-    JsonReader rd(in.first, in.second, &d);
-    int root = rd.parse();
-    if (root < 0) { delete res; return fail(e, GK_EINVAL, "invalid input JSON: " + d.err); }
-    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
-    uint32_t rn = rv >= 0 ? e->st.add_doc(d, rv) : NO_ID;
-    bool glob = false;
-    cols.push_back(review_columns(e->st, e->st, e->ns_cache, rn, &glob));
-  }
+  int frc = flatten_inputs(e, inputs, cols);
+  if (frc != GK_OK) { delete res; return frc; }
   res->ms[0] = ms_since(t0);
   int rc = launch_and_collect(e, cols, &e->d_revs, true, res);
   if (rc != GK_OK) { delete res; return rc; }
@@ -1842,6 +1850,44 @@ int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** n
 }  // extern "C"
 
 // ------------------------------------------------------------------ diagnostics
+// A staged batch of Query inputs ({"review": ...} documents, as gk_query_batch
+// takes them): lets tests evaluate arbitrary review documents through
+// gk_batch_eval, and through the CPU baseline on a host-only engine.
+extern "C" int gk_debug_stage_inputs(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n,
+                                     gk_batch** out) {
+  if (!e || !out || (n && !inputs)) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    rebuild_constraints(e);
+    rebuild_regex(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  std::vector<std::pair<const char*, size_t>> in;
+  for (size_t i = 0; i < n; ++i) in.push_back({inputs[i], lens ? lens[i] : strlen(inputs[i])});
+  auto* b = new gk_batch();
+  b->eng = e;
+  reset_transient(e);
+  b->node_begin = (uint32_t)e->st.nodes().size();
+  int rc = flatten_inputs(e, in, b->cols);
+  if (rc != GK_OK) { delete b; return rc; }
+  b->node_end = (uint32_t)e->st.nodes().size();
+  b->nrev = (uint32_t)n;
+  b->gen = e->gen;
+  b->resources.assign(n, ResourceIds{e->st.s_empty, e->st.s_empty, e->st.s_empty, e->st.s_empty});
+  b->node_count = b->node_end - b->node_begin;
+  if (e->host_only) { *out = b; return GK_OK; }
+  if (!ensure_device(e) || !sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
+      !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
+    b->d_revs.free_();
+    b->d_nodes.free_();
+    delete b;
+    return fail(e, GK_EDEVICE, "upload failed");
+  }
+  *out = b;
+  return GK_OK;
+}
+
 // The launch arguments of a staged batch with HOST pointers: the host arena
 // holds the same documents as the batch's device nodes while the batch is the
 // last one staged and the engine is unchanged.  Used only by the CPU baseline

@@ -561,6 +561,16 @@ class Driver:
         """Excluder.IsNamespaceExcluded (excluder.go:82-86)"""
         return bool(self._lib.gk_excluder_is_excluded(self._e, _b(process), _b(namespace)))
 
+    def debug_stage_inputs(self, inputs: Sequence) -> Batch:
+        """a staged batch of Query inputs ({"review": ...}; diagnostics / tests)"""
+        strs = [x if isinstance(x, str) else json.dumps(x) for x in inputs]
+        arr, lens, _keep = _arr(strs)
+        out = C.c_void_p()
+        self._lib.gk_debug_stage_inputs.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                                    C.c_size_t, C.POINTER(C.c_void_p)]
+        self._check(self._lib.gk_debug_stage_inputs(self._e, arr, lens, len(strs), C.byref(out)))
+        return Batch(self, out, len(strs))
+
     def stage_objects(self, objs: Sequence, namespaces: Sequence) -> Batch:
         o = [x if isinstance(x, str) else json.dumps(x) for x in objs]
         n = [None if x is None else (x if isinstance(x, str) else json.dumps(x)) for x in namespaces]

@@ -691,3 +691,37 @@ def test_client_review_sets_handle_violation_resource():
     for r in res.results:
         assert r.resource["apiVersion"] == "v1" and r.resource["kind"] == "Pod"
         assert r.resource["metadata"]["name"] == pods[0]["metadata"]["name"]
+
+
+def test_match_kats_replayed_through_the_device():
+    """Every function-level vector of the reference's match-library KATs
+    (pkg/target/regolib/*_test.rego via tests/golden/match_kats.jsonl) as a
+    (constraint, review, namespace cache) triple under a deny-all template,
+    evaluated on the MI355X (gk_batch_eval of a staged batch of Query inputs
+    and gk_query_batch): the rows equal the oracle's, including the
+    autoreject branch (devrt.h audit_body, target_template_source.go:12-25)
+    and match errors; for `direct` vectors the deny-all row appears iff the
+    KAT's own result is true."""
+    from kat_replay import UNDEF, cases, engine_for, expected, query_input
+    cs = cases()
+    n_auto = n_direct = 0
+    for case in cs:
+        want = expected(case)
+        drv = Driver()
+        engine_for(drv, case)
+        for res in (drv.query_batch([query_input(case)]), drv.debug_stage_inputs([query_input(case)]).eval()):
+            if want == "ERROR":
+                assert res.status[0] & 1, case["id"]
+                continue
+            assert res.status[0] == 0, case["id"]
+            got = sorted((r.msg, r.details_json, r.enforcement_action) for r in res.results)
+            assert got == want, (case["id"], got, want)
+        if want != "ERROR" and case["fn"] == "autoreject_review":
+            n_auto += sum(1 for w in want if w[0] == "Namespace is not cached in OPA.")
+        if want != "ERROR" and case["fn"] != "autoreject_review" and isinstance(case["kat"], bool):
+            denied = any(w[0] == "denied" for w in want)
+            if case["fn"] == "matches_label_selector" or denied == case["kat"]:
+                n_direct += 1
+                assert denied == case["kat"], case["id"]
+    assert n_auto >= 2
+    assert n_direct >= 80
