@@ -206,12 +206,36 @@ class Comp {
   }
 
   // ---------------------------------------------------------------- values
+  // A literal whose text is a canonical integer below 2^46 in magnitude ("0",
+  // "1000", "-3"; not "1.0", "01", "-0", "1e3") loads as an exact V_INT: it
+  // prints, compares and serialises exactly like its V_NUM form, and the
+  // device's inline int/int compare and arithmetic paths apply to it.
+  static bool canonical_small_int(const std::string& s, int64_t* v) {
+    size_t i = 0;
+    bool neg = false;
+    if (i < s.size() && s[i] == '-') { neg = true; ++i; }
+    if (i >= s.size() || s.size() - i > 14) return false;
+    if (s[i] == '0' && (s.size() - i > 1 || neg)) return false;
+    int64_t x = 0;
+    for (; i < s.size(); ++i) {
+      if (s[i] < '0' || s[i] > '9') return false;
+      x = x * 10 + (s[i] - '0');
+    }
+    if (x >= (1ll << 46)) return false;
+    *v = neg ? -x : x;
+    return true;
+  }
+
   uint64_t scalar_val(const TermP& t) {
     switch (t->stype) {
       case S_NULL: return tag_val(V_NULL, 0);
       case S_FALSE: return tag_val(V_BOOL, 0);
       case S_TRUE: return tag_val(V_BOOL, 1);
-      case S_NUM: return tag_val(V_NUM, st_.number(t->s.data(), t->s.size()));
+      case S_NUM: {
+        int64_t iv;
+        if (canonical_small_int(t->s, &iv)) return tag_val(V_INT, (uint64_t)iv & 0x0000ffffffffffffull);
+        return tag_val(V_NUM, st_.number(t->s.data(), t->s.size()));
+      }
       case S_STR: return tag_val(V_STR, st_.intern(t->s));
     }
     throw Unsupported("bad scalar");

@@ -24,8 +24,35 @@ extern "C" {
 __constant__ gk::DevArgs gk_args;
 }
 
+// Reference accounting hooks (empty on the device): the CPU build of this
+// runtime (oracle/cpuvm.cc) defines them to record which document nodes and
+// which strings' bytes an evaluation references -- SURVEY 8(d)'s algorithmic
+// bytes for the roofline are counted from that record.
+#ifndef GK_TOUCH_NODE
+#define GK_TOUCH_NODE(i) ((void)0)
+#endif
+#ifndef GK_TOUCH_STR
+#define GK_TOUCH_STR(s) ((void)0)
+#endif
+
 namespace gk {
 
+// GK_INLINE_HOT: the builtins template bodies call per container (startswith /
+// endswith / contains, to_number, substring, literal-regex DFAs, integer
+// arithmetic) are inlined at their call sites.  An out-of-line call makes the
+// caller save and restore its live VGPRs in scratch, which dominates these
+// kernels' memory traffic; the JIT enables it per template (jit.cc).
+#ifndef GK_INLINE_HOT
+#define GK_INLINE_HOT 0
+#endif
+#if GK_INLINE_HOT
+#define GK_HOT __forceinline__
+#else
+#define GK_HOT
+#endif
+#ifndef GK_VGET_UNROLL
+#define GK_VGET_UNROLL 0
+#endif
 #ifndef GK_HCAP
 #define GK_HCAP 128
 #endif
@@ -35,7 +62,10 @@ namespace gk {
 constexpr int HCAP = GK_HCAP;  // heap words per lane (lists, big floats)
 constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
 constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged messages)
-constexpr int EMCAP = 32;   // staged violation tuples per lane
+#ifndef GK_EMCAP
+#define GK_EMCAP 32
+#endif
+constexpr int EMCAP = GK_EMCAP;  // staged violation tuples per lane
 
 
 
@@ -99,6 +129,7 @@ __device__ __forceinline__ void lane_error(Lane& L) {
 }
 
 __device__ __forceinline__ uint64_t nodeval_of(const Node& n, uint32_t idx) {
+  GK_TOUCH_NODE(idx);
   switch (n.type) {
     case NT_NULL: return mkv(V_NULL, 0);
     case NT_FALSE: return mkv(V_BOOL, 0);
@@ -110,6 +141,7 @@ __device__ __forceinline__ uint64_t nodeval_of(const Node& n, uint32_t idx) {
   return mkv(V_UNDEF, 0);
 }
 __device__ __forceinline__ uint64_t nodeval(uint32_t idx) {
+  GK_TOUCH_NODE(idx);
   const Node& n = gk_args.nodes[idx];
   switch (n.type) {
     case NT_NULL: return mkv(V_NULL, 0);
@@ -126,10 +158,11 @@ __device__ __forceinline__ uint64_t nodeval(uint32_t idx) {
 struct SView { const char* p; uint32_t n; };
 __device__ __forceinline__ SView sview(const Lane& L, uint64_t v) {
   uint32_t t = vtag(v);
-  if (t == V_STR) { const StrEnt& s = gk_args.strs[(uint32_t)vpay(v)]; return SView{(const char*)gk_args.pool + s.off, s.len}; }
+  if (t == V_STR) { GK_TOUCH_STR((uint32_t)vpay(v)); const StrEnt& s = gk_args.strs[(uint32_t)vpay(v)]; return SView{(const char*)gk_args.pool + s.off, s.len}; }
   if (t == V_HSTR) { uint64_t p = vpay(v); return SView{L.B + (uint32_t)(p >> 16), (uint32_t)(p & 0xffff)}; }
   if (t == V_SLICE) {
     uint64_t p = vpay(v);
+    GK_TOUCH_STR((uint32_t)(p >> 28));
     const StrEnt& s = gk_args.strs[(uint32_t)(p >> 28)];
     return SView{(const char*)gk_args.pool + s.off + (uint32_t)((p >> 14) & 0x3fff), (uint32_t)(p & 0x3fff)};
   }
@@ -272,7 +305,7 @@ __device__ __forceinline__ int tclass(uint64_t v) {
     case V_BOOL: return 2;
     case V_NUM: case V_INT: case V_BFN: return 3;
     case V_STR: case V_HSTR: case V_SLICE: return 4;
-    case V_NODE: return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
+    case V_NODE: GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
     case V_LIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
   }
   return 0;
@@ -280,7 +313,7 @@ __device__ __forceinline__ int tclass(uint64_t v) {
 
 // collection view helpers (NODE arrays/objects and heap lists)
 __device__ uint32_t coll_len(const Lane& L, uint64_t v) {
-  if (vtag(v) == V_NODE) return gk_args.nodes[(uint32_t)vpay(v)].n;
+  if (vtag(v) == V_NODE) { GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].n; }
   if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
   return 0;
 }
@@ -439,6 +472,7 @@ __device__ __forceinline__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
 __device__ __noinline__ uint64_t vget_slow(Lane& L, uint64_t c, uint64_t key) {
   uint32_t t = vtag(c);
   if (t == V_NODE) {
+    GK_TOUCH_NODE((uint32_t)vpay(c));
     const Node& n = gk_args.nodes[(uint32_t)vpay(c)];
     if (n.flags & 1) { lane_fallback(L, FB_UNSUPPORTED); return mkv(V_UNDEF, 0); }
     if (n.type == NT_OBJ) {
@@ -482,18 +516,37 @@ __device__ __noinline__ uint64_t vget_slow(Lane& L, uint64_t c, uint64_t key) {
   return mkv(V_UNDEF, 0);
 }
 // Inlined fast path of vget for the common document lookups (object member by
-// interned key, array element by small int).  Everything else, including
-// fallback-flagged nodes, goes through vget_slow: an out-of-line call costs
-// the caller a save/restore of its live registers in scratch.
+// interned key, array element by small int), and for containers that cannot
+// be indexed at all (scalars, undefined: undefined).  Everything else,
+// including fallback-flagged nodes, goes through vget_slow: an out-of-line
+// call costs the caller a save/restore of its live registers in scratch.
 __device__ __forceinline__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
+  if (vtag(c) != V_NODE && vtag(c) != V_LIST) return mkv(V_UNDEF, 0);
   if (vtag(c) == V_NODE) {
+    GK_TOUCH_NODE((uint32_t)vpay(c));
     const Node n = gk_args.nodes[(uint32_t)vpay(c)];
     if (!(n.flags & 1)) {
       uint32_t kt = vtag(key);
       if (n.type == NT_OBJ && kt == V_STR) {
         uint32_t id = (uint32_t)vpay(key);
+#if GK_VGET_UNROLL
+        // four member keys per round trip: the loads are independent, so the
+        // lane waits once per four members instead of once per member
+        const Node* ch = gk_args.nodes + n.first;
+        uint32_t i = 0;
+        for (; i + 4 <= n.n; i += 4) {
+          uint32_t k0 = ch[i].key, k1 = ch[i + 1].key, k2 = ch[i + 2].key, k3 = ch[i + 3].key;
+          if (k0 == id) return nodeval(n.first + i);
+          if (k1 == id) return nodeval(n.first + i + 1);
+          if (k2 == id) return nodeval(n.first + i + 2);
+          if (k3 == id) return nodeval(n.first + i + 3);
+        }
+        for (; i < n.n; ++i)
+          if (ch[i].key == id) return nodeval(n.first + i);
+#else
         for (uint32_t i = 0; i < n.n; ++i)
           if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
+#endif
         return mkv(V_UNDEF, 0);
       }
       if (n.type == NT_ARR && kt == V_INT) {
@@ -601,6 +654,7 @@ template <class O> __device__ void put_intv(O& o, uint64_t v) {
   put(o, (char)('0' + e % 10));
 }
 template <class O> __device__ void put_sid(O& o, uint32_t sid) {
+  GK_TOUCH_STR(sid);
   const StrEnt& s = gk_args.strs[sid];
   puts_(o, (const char*)gk_args.pool + s.off, s.len);
 }
@@ -821,10 +875,11 @@ __device__ int re_run(const Lane& L, uint64_t pat, uint64_t val) {
 // ------------------------------------------------------------------ match
 __device__ __forceinline__ bool label_lookup(uint32_t labels, uint32_t key, uint32_t& val) {
   if (labels == NO_ID) return false;
+  GK_TOUCH_NODE(labels);
   const Node& n = gk_args.nodes[labels];
   for (uint32_t i = 0; i < n.n; ++i) {
     const Node& c = gk_args.nodes[n.first + i];
-    if (c.key == key) { val = c.val; return true; }
+    if (c.key == key) { GK_TOUCH_NODE(n.first + i); val = c.val; return true; }
   }
   return false;
 }
@@ -1083,7 +1138,7 @@ __device__ uint64_t bi_anyall(Lane& L, uint32_t id, uint64_t a) {
 }
 
 // startswith / endswith / contains (topdown/strings.go:135-175, byte-wise)
-__device__ uint64_t bi_strpred(Lane& L, uint32_t id, uint64_t a, uint64_t b) {
+__device__ GK_HOT uint64_t bi_strpred(Lane& L, uint32_t id, uint64_t a, uint64_t b) {
   if (!is_strv(a) || !is_strv(b)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a), p = sview(L, b);
   if (p.n > s.n) return mkv(V_BOOL, 0);
@@ -1112,7 +1167,7 @@ __device__ __forceinline__ uint64_t bi_re_match(Lane& L, uint64_t a, uint64_t b)
 // to_number (topdown/casts.go:14-33).  The number keeps the string's text, so
 // only canonical integer texts become V_INT (no '+', no leading zero, no "-0":
 // those print differently); other valid forms go to the CPU fallback.
-__device__ uint64_t bi_to_number(Lane& L, uint64_t a) {
+__device__ GK_HOT uint64_t bi_to_number(Lane& L, uint64_t a) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   uint32_t t = vtag(a);
   if (t == V_NULL) return mkint(0);
@@ -1172,7 +1227,7 @@ __device__ uint64_t bi_replace(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
 }
 
 // substring(s, start, length), byte-indexed (topdown/strings.go:100-133)
-__device__ uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
+__device__ GK_HOT uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (!is_strv(a0)) { lane_error(L); return UND; }
   int64_t st, ln;
@@ -1346,7 +1401,23 @@ __device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
   return mkv(V_UNDEF, 0);
 }
 
-__device__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+__device__ __noinline__ uint64_t arith_slow(Lane& L, uint32_t kind, uint64_t x, uint64_t y);
+// exact small-integer +, -, * inline (the common case: canonical quantities
+// times a constant); everything else out of line
+__device__ __forceinline__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+  if (vtag(x) == V_INT && vtag(y) == V_INT && kind <= AR_MUL) {
+    const int64_t LIM = (1ll << 46);
+    int64_t a = intof(x), b = intof(y);
+    if (a < LIM && a > -LIM && b < LIM && b > -LIM) {
+      if (kind == AR_PLUS) return mkint_g(a + b);
+      if (kind == AR_MINUS) return mkint_g(a - b);
+      uint64_t ua = a < 0 ? (uint64_t)(-a) : (uint64_t)a, ub = b < 0 ? (uint64_t)(-b) : (uint64_t)b;
+      if (__umul64hi(ua, ub) == 0 && ua * ub < (uint64_t)LIM) return mkint_g(a * b);
+    }
+  }
+  return arith_slow(L, kind, x, y);
+}
+__device__ __noinline__ uint64_t arith_slow(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (kind == AR_MINUS && tclass(x) == 9 && tclass(y) == 9) {
     uint64_t out = list_new(L, LK_SET, coll_len(L, x));

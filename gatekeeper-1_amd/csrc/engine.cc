@@ -1850,6 +1850,14 @@ int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** n
 }  // extern "C"
 
 // ------------------------------------------------------------------ diagnostics
+extern "C" int gk_debug_store_sizes(gk_engine* e, uint64_t* nodes, uint64_t* strings) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (nodes) *nodes = e->st.nodes().size();
+  if (strings) *strings = e->st.nstrings();
+  return GK_OK;
+}
+
 // A staged batch of Query inputs ({"review": ...} documents, as gk_query_batch
 // takes them): lets tests evaluate arbitrary review documents through
 // gk_batch_eval, and through the CPU baseline on a host-only engine.

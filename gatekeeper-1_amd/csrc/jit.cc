@@ -143,7 +143,7 @@ std::string regex_fn(const std::string& fn, const std::vector<uint32_t>& d) {
   if (nst > 64) return "";
   std::ostringstream o;
   size_t ranges = 0;
-  o << "__device__ int " << fn << "(SView v) {\n  uint32_t s = " << start << "u;\n"
+  o << "__device__ GK_HOT int " << fn << "(SView v) {\n  uint32_t s = " << start << "u;\n"
     << "  for (uint32_t i = 0; i < v.n; ++i) {\n    uint32_t c = (uint8_t)v.p[i];\n";
   if (sens) o << "    if (c >= 0x80u) return -2;\n";
   o << "    switch (s) {\n";
@@ -442,9 +442,14 @@ static std::string wpe_suffix() {
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 
+static std::string inline_hot_tag() {
+  const char* v = getenv("GKGPU_INLINE_HOT");
+  return (!v || atoi(v) != 0) ? "h1" : "h0";
+}
+
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
   Gen g = generate(p, bank, st);
-  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix()));
+  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix() + inline_hot_tag()));
 }
 
 std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
@@ -461,6 +466,8 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
       if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
     }
   }
+  // GKGPU_INLINE_HOT (A/B switch, default on): inline the per-container builtins
+  if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre

@@ -43,3 +43,24 @@ def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1):
     hi = batch.n if hi is None else hi
     s = lib.gkcpu_sweep(buf, lo, hi, threads, out)
     return s, out[0], out[1], out[2], out[3]
+
+
+def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1):
+    """SURVEY 8(d) reference accounting of reviews [lo, hi) x constraint `only`
+    (all when < 0): dict(nodes, strings, string_bytes, violations, flagged)"""
+    lib = load()
+    glib = driver._lib
+    lib.gkcpu_referenced.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                     C.POINTER(C.c_uint64)]
+    lib.gkcpu_referenced.restype = C.c_int
+    n = lib.gkcpu_devargs_size()
+    buf = (C.c_uint8 * n)()
+    glib.gk_debug_host_args.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
+    glib.gk_debug_store_sizes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    nn, ns = C.c_uint64(), C.c_uint64()
+    glib.gk_debug_store_sizes(driver._e, C.byref(nn), C.byref(ns))
+    out = (C.c_uint64 * 5)()
+    hi = batch.n if hi is None else hi
+    lib.gkcpu_referenced(buf, nn.value, ns.value, lo, hi, only, threads, out)
+    return {"nodes": out[0], "strings": out[1], "string_bytes": out[2], "violations": out[3], "flagged": out[4]}

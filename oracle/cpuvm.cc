@@ -53,6 +53,17 @@ static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((
 struct CpuDim3 { uint32_t x = 0, y = 0, z = 0; };
 static CpuDim3 blockIdx, threadIdx, blockDim{64, 1, 1}, gridDim{1, 1, 1};
 
+#ifdef GKCPU_TOUCH
+// Reference accounting build (cpuvm_touch.cc): the same runtime in its own
+// namespace, recording every document node and string the evaluation reads.
+namespace gkcpu_touch {
+thread_local uint64_t* node_bits = nullptr;
+thread_local uint64_t* str_bits = nullptr;
+}  // namespace gkcpu_touch
+#define GK_TOUCH_NODE(i) (gkcpu_touch::node_bits[(uint32_t)(i) >> 6] |= 1ull << ((uint32_t)(i) & 63))
+#define GK_TOUCH_STR(s) (gkcpu_touch::str_bits[(uint32_t)(s) >> 6] |= 1ull << ((uint32_t)(s) & 63))
+#endif
+
 #include "../gatekeeper-1_amd/csrc/devrt.h"
 
 namespace gk {
@@ -171,6 +182,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
 }  // namespace cpu
 }  // namespace gk
 
+#ifndef GKCPU_TOUCH
 extern "C" {
 
 size_t gkcpu_devargs_size() { return sizeof(gk::DevArgs); }
@@ -210,3 +222,68 @@ double gkcpu_sweep(const void* args, uint32_t lo, uint32_t hi, int threads, uint
 }
 
 }  // extern "C"
+#else
+extern "C" {
+
+// SURVEY 8(d) reference accounting for the roofline: evaluates reviews
+// [lo, hi) against constraint `only` (or all when only < 0) and reports
+// out5 = [document nodes referenced, distinct strings whose bytes were read,
+// their bytes, violations, flagged pairs].  n_nodes / n_strings: the host
+// store's sizes (gk_debug_store_sizes).
+int gkcpu_referenced(const void* args, uint64_t n_nodes, uint64_t n_strings, uint32_t lo, uint32_t hi, int only,
+                     int threads, uint64_t* out5) {
+  memcpy(&gk_args_touch, args, sizeof(gk_touch::DevArgs));
+  auto& A = gk_args_touch;
+  if (hi > A.nrev) hi = A.nrev;
+  if (lo > hi) lo = hi;
+  if (threads < 1) threads = 1;
+  const size_t nwords = (size_t)(n_nodes + 63) / 64, swords = (size_t)(n_strings + 63) / 64;
+  std::vector<std::vector<uint64_t>> nb(threads), sb(threads);
+  std::vector<gk_touch::cpu::Counts> per(threads);
+  std::atomic<uint32_t> next{lo};
+  auto work = [&](int t) {
+    nb[t].assign(nwords, 0);
+    sb[t].assign(swords, 0);
+    gkcpu_touch::node_bits = nb[t].data();
+    gkcpu_touch::str_bits = sb[t].data();
+    std::vector<char> fbuf(1 << 16);
+    auto& k = per[t];
+    for (;;) {
+      uint32_t a = next.fetch_add(256);
+      if (a >= hi) break;
+      uint32_t b = a + 256 < hi ? a + 256 : hi;
+      for (uint32_t rp = a; rp < b; ++rp)
+        for (uint32_t c = 0; c < A.ncons; ++c)
+          if (only < 0 || (uint32_t)only == c) gk_touch::cpu::eval_pair(rp, c, k, fbuf.data(), (uint32_t)fbuf.size());
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  uint64_t nodes = 0, strs = 0, sbytes = 0;
+  for (size_t w = 0; w < nwords; ++w) {
+    uint64_t x = 0;
+    for (int t = 0; t < threads; ++t) x |= nb[t][w];
+    nodes += (uint64_t)__builtin_popcountll(x);
+  }
+  for (size_t w = 0; w < swords; ++w) {
+    uint64_t x = 0;
+    for (int t = 0; t < threads; ++t) x |= sb[t][w];
+    while (x) {
+      int bit = __builtin_ctzll(x);
+      x &= x - 1;
+      uint64_t sid = w * 64 + (uint64_t)bit;
+      ++strs;
+      sbytes += A.strs[sid].len;
+    }
+  }
+  uint64_t viol = 0, flagged = 0;
+  for (auto& k : per) { viol += k.violations; flagged += k.flagged; }
+  uint64_t o[5] = {nodes, strs, sbytes, viol, flagged};
+  memcpy(out5, o, sizeof o);
+  return 0;
+}
+
+}  // extern "C"
+#endif
