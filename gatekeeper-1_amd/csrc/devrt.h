@@ -107,13 +107,24 @@ struct Lane {
   uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP];
 };
 
+// A lane's state lives in private (scratch) memory.  Helpers take it through
+// PLane&.  A template kernel may be compiled with GK_PRIV set to
+// __attribute__((address_space(5))) (GKGPU_PRIV=1), so the compiler emits
+// scratch_load/store with a 32-bit offset instead of flat accesses through a
+// 64-bit generic pointer; the default is the generic address space (the VM
+// kernel does not compile in address space 5 with this toolchain).
+#ifndef GK_PRIV
+#define GK_PRIV
+#endif
+typedef GK_PRIV Lane PLane;
+
 // a heap-resident value (must survive a loop's per-iteration heap reset when it
 // escapes to a register that outlives the iteration)
 __device__ __forceinline__ bool heap_val(uint64_t v) {
   uint32_t t = v >> 60;
   return t == V_LIST || t == V_BFN || t == V_HSTR || t == V_FMT;
 }
-__device__ __forceinline__ void pin_escape(Lane& L, uint32_t range) {
+__device__ __forceinline__ void pin_escape(PLane& L, uint32_t range) {
   uint32_t lo = range & 0xff, hi = (range >> 8) & 0xff;
   for (uint32_t d = lo; d <= hi && d < MAXLOOP; ++d) {
     if (L.keepH[d] < L.hp) L.keepH[d] = (uint16_t)L.hp;
@@ -121,10 +132,10 @@ __device__ __forceinline__ void pin_escape(Lane& L, uint32_t range) {
   }
 }
 
-__device__ __forceinline__ void lane_fallback(Lane& L, uint32_t reason) {
+__device__ __forceinline__ void lane_fallback(PLane& L, uint32_t reason) {
   if (!L.fail) { L.fail = RF_FALLBACK; L.reason = reason; }
 }
-__device__ __forceinline__ void lane_error(Lane& L) {
+__device__ __forceinline__ void lane_error(PLane& L) {
   if (!L.fail) { L.fail = RF_ERROR; L.reason = 0; }
 }
 
@@ -156,7 +167,7 @@ __device__ __forceinline__ uint64_t nodeval(uint32_t idx) {
 
 // string bytes of a string value
 struct SView { const char* p; uint32_t n; };
-__device__ __forceinline__ SView sview(const Lane& L, uint64_t v) {
+__device__ __forceinline__ SView sview(const PLane& L, uint64_t v) {
   uint32_t t = vtag(v);
   if (t == V_STR) { GK_TOUCH_STR((uint32_t)vpay(v)); const StrEnt& s = gk_args.strs[(uint32_t)vpay(v)]; return SView{(const char*)gk_args.pool + s.off, s.len}; }
   if (t == V_HSTR) { uint64_t p = vpay(v); return SView{L.B + (uint32_t)(p >> 16), (uint32_t)(p & 0xffff)}; }
@@ -180,7 +191,7 @@ __device__ __forceinline__ int bytes_cmp(SView a, SView b) {
 // ------------------------------------------------------------------ numbers
 // exact 64-bit-mantissa big-float view of a numeric value; returns false if unavailable
 struct BF { uint64_t m; int32_t e; bool neg; bool zero; };
-__device__ bool num_bf(const Lane& L, uint64_t v, BF& out) {
+__device__ bool num_bf(const PLane& L, uint64_t v, BF& out) {
   uint32_t t = vtag(v);
   if (t == V_NUM) {
     const NumEnt& n = gk_args.nums[(uint32_t)vpay(v)];
@@ -221,7 +232,7 @@ __device__ int bf_cmp(const BF& a, const BF& b) {
   return a.neg ? -mag : mag;
 }
 // integer view: true if the value is an exact integer representable in int64
-__device__ bool num_int(const Lane& L, uint64_t v, int64_t& out) {
+__device__ bool num_int(const PLane& L, uint64_t v, int64_t& out) {
   uint32_t t = vtag(v);
   if (t == V_INT) { out = intof(v); return true; }
   if (t == V_NUM) {
@@ -252,7 +263,7 @@ __device__ bool num_int(const Lane& L, uint64_t v, int64_t& out) {
   }
   return false;
 }
-__device__ uint64_t heap_bf(Lane& L, const BF& b) {
+__device__ uint64_t heap_bf(PLane& L, const BF& b) {
   if (L.hp + 2 > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
   uint32_t o = L.hp;
   L.hp += 2;
@@ -286,10 +297,10 @@ __device__ BF bf_mul(const BF& a, const BF& b) {
 }
 
 // ------------------------------------------------------------------ lists
-__device__ __forceinline__ uint32_t list_len(const Lane& L, uint64_t v) { return (uint32_t)L.H[list_off(v)]; }
-__device__ __forceinline__ uint64_t list_at(const Lane& L, uint64_t v, uint32_t i) { return L.H[list_off(v) + 2 + i]; }
+__device__ __forceinline__ uint32_t list_len(const PLane& L, uint64_t v) { return (uint32_t)L.H[list_off(v)]; }
+__device__ __forceinline__ uint64_t list_at(const PLane& L, uint64_t v, uint32_t i) { return L.H[list_off(v) + 2 + i]; }
 
-__device__ __forceinline__ uint64_t list_new(Lane& L, uint32_t kind, uint32_t cap) {
+__device__ __forceinline__ uint64_t list_new(PLane& L, uint32_t kind, uint32_t cap) {
   if (L.hp + 2 + cap > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
   uint32_t o = L.hp;
   L.H[o] = 0;
@@ -312,13 +323,13 @@ __device__ __forceinline__ int tclass(uint64_t v) {
 }
 
 // collection view helpers (NODE arrays/objects and heap lists)
-__device__ uint32_t coll_len(const Lane& L, uint64_t v) {
+__device__ uint32_t coll_len(const PLane& L, uint64_t v) {
   if (vtag(v) == V_NODE) { GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].n; }
   if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
   return 0;
 }
 // i-th (key, value) of a collection
-__device__ void coll_at(const Lane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
+__device__ void coll_at(const PLane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
   if (vtag(v) == V_NODE) {
     const Node& n = gk_args.nodes[(uint32_t)vpay(v)];
     uint32_t c = n.first + i;
@@ -333,7 +344,7 @@ __device__ void coll_at(const Lane& L, uint64_t v, uint32_t i, uint64_t& k, uint
 }
 
 // scalar compare within one type class (1..4); 2 = undecidable (fallback set)
-__device__ int scmp(Lane& L, uint64_t a, uint64_t b, int cls) {
+__device__ int scmp(PLane& L, uint64_t a, uint64_t b, int cls) {
   switch (cls) {
     case 1: return 0;
     case 2: { uint64_t x = vpay(a), y = vpay(b); return x == y ? 0 : (x < y ? -1 : 1); }
@@ -353,7 +364,7 @@ __device__ int scmp(Lane& L, uint64_t a, uint64_t b, int cls) {
 
 // element comparison inside a composite: scalars, or identical document nodes;
 // anything deeper is served by the CPU fallback
-__device__ int ecmp(Lane& L, uint64_t a, uint64_t b) {
+__device__ int ecmp(PLane& L, uint64_t a, uint64_t b) {
   int ca = tclass(a), cb = tclass(b);
   if (ca != cb) return ca < cb ? -1 : 1;
   if (ca <= 4) return scmp(L, a, b, ca);
@@ -364,7 +375,7 @@ __device__ int ecmp(Lane& L, uint64_t a, uint64_t b) {
 }
 
 // ast.Compare: -1/0/1; 3 = "not equal, order undefined here"; 2 = undecidable
-__device__ int vcmp(Lane& L, uint64_t a, uint64_t b) {
+__device__ int vcmp(PLane& L, uint64_t a, uint64_t b) {
   int ca = tclass(a), cb = tclass(b);
   if (ca != cb) return ca < cb ? -1 : 1;
   if (ca <= 4) return scmp(L, a, b, ca);
@@ -404,7 +415,7 @@ __device__ int vcmp(Lane& L, uint64_t a, uint64_t b) {
   return 0;
 }
 
-__device__ bool veq(Lane& L, uint64_t a, uint64_t b) {
+__device__ bool veq(PLane& L, uint64_t a, uint64_t b) {
   if (a == b) {
     uint32_t t = vtag(a);
     if (t != V_HSTR && t != V_BFN) return true;
@@ -421,13 +432,13 @@ __device__ bool veq(Lane& L, uint64_t a, uint64_t b) {
   return c == 0;
 }
 
-__device__ bool list_contains(Lane& L, uint64_t l, uint64_t v) {
+__device__ bool list_contains(PLane& L, uint64_t l, uint64_t v) {
   uint32_t n = list_len(L, l);
   for (uint32_t i = 0; i < n; ++i) if (veq(L, list_at(L, l, i), v)) return true;
   return false;
 }
 // append (sets dedupe); may relocate the list to the heap top when full
-__device__ __noinline__ uint64_t list_add_slow(Lane& L, uint64_t l, uint64_t v) {
+__device__ __noinline__ uint64_t list_add_slow(PLane& L, uint64_t l, uint64_t v) {
   if (vtag(l) != V_LIST) return l;
   if (list_kind(l) == LK_SET && list_contains(L, l, v)) return l;
   uint32_t o = list_off(l);
@@ -455,7 +466,7 @@ __device__ __noinline__ uint64_t list_add_slow(Lane& L, uint64_t l, uint64_t v) 
 }
 // append fast path (array / object list with room), inlined: AMDGPU calls
 // save and restore the caller's live registers in scratch
-__device__ __forceinline__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
+__device__ __forceinline__ uint64_t list_add(PLane& L, uint64_t l, uint64_t v) {
   if (vtag(l) == V_LIST && list_kind(l) != LK_SET) {
     uint32_t o = list_off(l);
     uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
@@ -469,7 +480,7 @@ __device__ __forceinline__ uint64_t list_add(Lane& L, uint64_t l, uint64_t v) {
 }
 
 // ------------------------------------------------------------------ get
-__device__ __noinline__ uint64_t vget_slow(Lane& L, uint64_t c, uint64_t key) {
+__device__ __noinline__ uint64_t vget_slow(PLane& L, uint64_t c, uint64_t key) {
   uint32_t t = vtag(c);
   if (t == V_NODE) {
     GK_TOUCH_NODE((uint32_t)vpay(c));
@@ -520,7 +531,7 @@ __device__ __noinline__ uint64_t vget_slow(Lane& L, uint64_t c, uint64_t key) {
 // be indexed at all (scalars, undefined: undefined).  Everything else,
 // including fallback-flagged nodes, goes through vget_slow: an out-of-line
 // call costs the caller a save/restore of its live registers in scratch.
-__device__ __forceinline__ uint64_t vget(Lane& L, uint64_t c, uint64_t key) {
+__device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
   if (vtag(c) != V_NODE && vtag(c) != V_LIST) return mkv(V_UNDEF, 0);
   if (vtag(c) == V_NODE) {
     GK_TOUCH_NODE((uint32_t)vpay(c));
@@ -705,7 +716,7 @@ template <class O> __device__ bool put_json_str(O& o, SView s) {
 }
 
 // scalar Term.String()/JSON; returns 0 not-scalar, 1 ok, -1 fallback
-template <class O> __device__ int put_scalar(Lane& L, O& o, uint64_t v, bool json) {
+template <class O> __device__ int put_scalar(PLane& L, O& o, uint64_t v, bool json) {
   switch (vtag(v)) {
     case V_UNDEF: if (json) { put_cstr(o, "{}"); return 1; } return -1;
     case V_NULL: put_cstr(o, "null"); return 1;
@@ -724,7 +735,7 @@ struct PFrame { uint64_t v; uint32_t i, n; uint64_t last; int cls; };
 
 // ast.Term.String() (json=false) or encoding/json of ast.JSON (json=true, map
 // keys in byte order), iterative with an explicit stack; false => fallback
-template <class O> __device__ bool put_value(Lane& L, O& o, uint64_t v, bool json) {
+template <class O> __device__ bool put_value(PLane& L, O& o, uint64_t v, bool json) {
   int r = put_scalar(L, o, v, json);
   if (r != 0) return r > 0;
   PFrame st[8];
@@ -778,11 +789,11 @@ template <class O> __device__ bool put_value(Lane& L, O& o, uint64_t v, bool jso
   return true;
 }
 
-template <class O> __device__ __forceinline__ bool put_term(Lane& L, O& o, uint64_t v) { return put_value(L, o, v, false); }
-template <class O> __device__ __forceinline__ bool put_json(Lane& L, O& o, uint64_t v) { return put_value(L, o, v, true); }
+template <class O> __device__ __forceinline__ bool put_term(PLane& L, O& o, uint64_t v) { return put_value(L, o, v, false); }
+template <class O> __device__ __forceinline__ bool put_json(PLane& L, O& o, uint64_t v) { return put_value(L, o, v, true); }
 
 // Go fmt conversion of one sprintf argument (topdown/strings.go:355-367)
-template <class O> __device__ bool put_fmt_arg(Lane& L, O& o, uint64_t v, uint32_t verb) {
+template <class O> __device__ bool put_fmt_arg(PLane& L, O& o, uint64_t v, uint32_t verb) {
   uint32_t t = vtag(v);
   if (t == V_STR || t == V_HSTR || t == V_SLICE) {
     SView s = sview(L, v);
@@ -818,7 +829,7 @@ template <class O> __device__ bool put_fmt_arg(Lane& L, O& o, uint64_t v, uint32
 }
 
 // the segments of format fidx (compiler.cc parse_format) with argument i = arg(i)
-template <class O, class A> __device__ bool fmt_run(Lane& L, O& o, uint32_t fidx, A arg) {
+template <class O, class A> __device__ bool fmt_run(PLane& L, O& o, uint32_t fidx, A arg) {
   const uint32_t* f = gk_args.fmt + fidx;
   uint32_t nseg = f[0];
   for (uint32_t s = 0; s < nseg; ++s) {
@@ -844,7 +855,7 @@ __device__ int re_lookup(uint32_t sid) {
   return -1;
 }
 // returns 1 match, 0 no match, -1 error (invalid pattern), -2 fallback
-__device__ int re_run(const Lane& L, uint64_t pat, uint64_t val) {
+__device__ int re_run(const PLane& L, uint64_t pat, uint64_t val) {
   if (vtag(pat) != V_STR) return -2;
   int e = re_lookup((uint32_t)vpay(pat));
   if (e < 0) return -2;
@@ -1014,7 +1025,7 @@ __device__ int match_constraint(const MatchSpec& m, const ReviewCol& rc) {
 // enclosing loop's per-iteration reset); output space is reserved once per
 // wavefront at the end of the kernel (flush_wave), so the global tuple/byte
 // cursors see one atomic per wave instead of one per violation.
-__device__ void stage_tuple(Lane& L, uint32_t rule, const char* msg, uint32_t mlen, const char* det, uint32_t dlen,
+__device__ void stage_tuple(PLane& L, uint32_t rule, const char* msg, uint32_t mlen, const char* det, uint32_t dlen,
                             uint32_t depth) {
   if (L.en >= EMCAP || L.bp + mlen + dlen > BCAP) { lane_fallback(L, FB_MSG_LEN); return; }
   uint32_t off = L.bp;
@@ -1049,7 +1060,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-__device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
+__device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
   uint32_t nt = keep ? L.en : 0, nb = 0;
   if (keep)
     for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + (L.em_dlen[i] & 0x7fffu);
@@ -1114,7 +1125,7 @@ __device__ void flush_wave(Lane& L, uint32_t lane, uint32_t r, uint32_t c, bool 
 // ------------------------------------------------------------------ builtins
 // One device function per builtin: template kernels call them directly with
 // register operands (jit.cc); the VM dispatches through call_builtin.
-__device__ __forceinline__ uint64_t bi_count(Lane& L, uint64_t a) {
+__device__ __forceinline__ uint64_t bi_count(PLane& L, uint64_t a) {
   uint32_t t = vtag(a);
   if (t == V_NODE || t == V_LIST) return mkint(coll_len(L, a));
   if (is_strv(a)) return mkint(sview(L, a).n);
@@ -1122,7 +1133,7 @@ __device__ __forceinline__ uint64_t bi_count(Lane& L, uint64_t a) {
   return mkv(V_UNDEF, 0);
 }
 
-__device__ uint64_t bi_anyall(Lane& L, uint32_t id, uint64_t a) {
+__device__ uint64_t bi_anyall(PLane& L, uint32_t id, uint64_t a) {
   int cls = tclass(a);
   if (cls != 7 && cls != 9) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t n = coll_len(L, a);
@@ -1138,7 +1149,7 @@ __device__ uint64_t bi_anyall(Lane& L, uint32_t id, uint64_t a) {
 }
 
 // startswith / endswith / contains (topdown/strings.go:135-175, byte-wise)
-__device__ GK_HOT uint64_t bi_strpred(Lane& L, uint32_t id, uint64_t a, uint64_t b) {
+__device__ GK_HOT uint64_t bi_strpred(PLane& L, uint32_t id, uint64_t a, uint64_t b) {
   if (!is_strv(a) || !is_strv(b)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a), p = sview(L, b);
   if (p.n > s.n) return mkv(V_BOOL, 0);
@@ -1154,12 +1165,12 @@ __device__ GK_HOT uint64_t bi_strpred(Lane& L, uint32_t id, uint64_t a, uint64_t
 
 // re_run / a literal pattern's compiled DFA (jit.cc) -> value: 1/0 match,
 // -1 invalid pattern (builtin error), -2 CPU fallback
-__device__ __forceinline__ uint64_t re_result(Lane& L, int r) {
+__device__ __forceinline__ uint64_t re_result(PLane& L, int r) {
   if (r == -1) { lane_error(L); return mkv(V_UNDEF, 0); }
   if (r == -2) { lane_fallback(L, FB_REGEX); return mkv(V_UNDEF, 0); }
   return mkv(V_BOOL, r);
 }
-__device__ __forceinline__ uint64_t bi_re_match(Lane& L, uint64_t a, uint64_t b) {
+__device__ __forceinline__ uint64_t bi_re_match(PLane& L, uint64_t a, uint64_t b) {
   if (!is_strv(a) || !is_strv(b)) { lane_error(L); return mkv(V_UNDEF, 0); }
   return re_result(L, re_run(L, a, b));
 }
@@ -1167,7 +1178,7 @@ __device__ __forceinline__ uint64_t bi_re_match(Lane& L, uint64_t a, uint64_t b)
 // to_number (topdown/casts.go:14-33).  The number keeps the string's text, so
 // only canonical integer texts become V_INT (no '+', no leading zero, no "-0":
 // those print differently); other valid forms go to the CPU fallback.
-__device__ GK_HOT uint64_t bi_to_number(Lane& L, uint64_t a) {
+__device__ GK_HOT uint64_t bi_to_number(PLane& L, uint64_t a) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   uint32_t t = vtag(a);
   if (t == V_NULL) return mkint(0);
@@ -1198,7 +1209,7 @@ __device__ GK_HOT uint64_t bi_to_number(Lane& L, uint64_t a) {
 }
 
 // replace = strings.Replace(s, old, new, -1) (topdown/strings.go:212-229)
-__device__ uint64_t bi_replace(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
+__device__ uint64_t bi_replace(PLane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (!is_strv(a0) || !is_strv(a1) || !is_strv(a2)) { lane_error(L); return UND; }
   SView s = sview(L, a0), old = sview(L, a1), nw = sview(L, a2);
@@ -1227,7 +1238,7 @@ __device__ uint64_t bi_replace(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
 }
 
 // substring(s, start, length), byte-indexed (topdown/strings.go:100-133)
-__device__ GK_HOT uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
+__device__ GK_HOT uint64_t bi_substring(PLane& L, uint64_t a0, uint64_t a1, uint64_t a2) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (!is_strv(a0)) { lane_error(L); return UND; }
   int64_t st, ln;
@@ -1250,7 +1261,7 @@ __device__ GK_HOT uint64_t bi_substring(Lane& L, uint64_t a0, uint64_t a1, uint6
 
 // the byte range [st, st+len) of string value a0 (s = its view) as a value
 // that shares the bytes: a slice of an interned string or of the lane buffer
-__device__ uint64_t str_sub(Lane& L, uint64_t a0, SView s, uint32_t st, uint32_t len) {
+__device__ uint64_t str_sub(PLane& L, uint64_t a0, SView s, uint32_t st, uint32_t len) {
   if (st == 0 && len == s.n) return a0;
   if (len == 0) return mkv(V_STR, 0);
   if (vtag(a0) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a0), st, len);
@@ -1272,7 +1283,7 @@ __device__ __forceinline__ bool bytes_at(SView s, uint32_t o, SView p) {
 // trim(s, cutset) = strings.Trim (topdown/strings.go:261-273).  The cutset is a
 // set of runes; for an ASCII cutset byte-wise trimming is exact (UTF-8 lead and
 // continuation bytes are >= 0x80), otherwise the review goes to the CPU.
-__device__ uint64_t bi_trim(Lane& L, uint64_t a0, uint64_t a1) {
+__device__ uint64_t bi_trim(PLane& L, uint64_t a0, uint64_t a1) {
   if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a0), c = sview(L, a1);
   for (uint32_t i = 0; i < c.n; ++i) if ((unsigned char)c.p[i] >= 0x80) { lane_fallback(L, FB_UNICODE); return mkv(V_UNDEF, 0); }
@@ -1284,7 +1295,7 @@ __device__ uint64_t bi_trim(Lane& L, uint64_t a0, uint64_t a1) {
 }
 
 // trim_prefix / trim_suffix = strings.TrimPrefix / TrimSuffix (byte-wise)
-__device__ uint64_t bi_trim_fix(Lane& L, uint32_t id, uint64_t a0, uint64_t a1) {
+__device__ uint64_t bi_trim_fix(PLane& L, uint32_t id, uint64_t a0, uint64_t a1) {
   if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a0), p = sview(L, a1);
   if (p.n > s.n) return a0;
@@ -1295,7 +1306,7 @@ __device__ uint64_t bi_trim_fix(Lane& L, uint32_t id, uint64_t a0, uint64_t a1) 
 // split(s, sep) = strings.Split (topdown/strings.go:195-210): an array of the
 // pieces, each sharing the subject's bytes.  An empty separator splits into
 // runes (ASCII subjects only; others go to the CPU).
-__device__ uint64_t bi_split(Lane& L, uint64_t a0, uint64_t a1) {
+__device__ uint64_t bi_split(PLane& L, uint64_t a0, uint64_t a1) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return UND; }
   SView s = sview(L, a0), d = sview(L, a1);
@@ -1323,7 +1334,7 @@ __device__ uint64_t bi_split(Lane& L, uint64_t a0, uint64_t a1) {
 }
 
 // lower / upper = strings.ToLower / ToUpper: ASCII subjects on the GPU
-__device__ uint64_t bi_case(Lane& L, uint32_t id, uint64_t a0) {
+__device__ uint64_t bi_case(PLane& L, uint32_t id, uint64_t a0) {
   if (!is_strv(a0)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a0);
   bool change = false;
@@ -1346,7 +1357,7 @@ __device__ uint64_t bi_case(Lane& L, uint32_t id, uint64_t a0) {
 
 // concat(delim, array|set) = strings.Join (topdown/strings.go:48-83); non-string
 // elements and other collections are operand errors
-__device__ uint64_t bi_concat(Lane& L, uint64_t a0, uint64_t a1) {
+__device__ uint64_t bi_concat(PLane& L, uint64_t a0, uint64_t a1) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   int cls = tclass(a1);
   if (!is_strv(a0) || (cls != 7 && cls != 9)) { lane_error(L); return UND; }
@@ -1366,14 +1377,14 @@ __device__ uint64_t bi_concat(Lane& L, uint64_t a0, uint64_t a1) {
 }
 
 // indexof(s, sub) = strings.Index: byte offset or -1 (topdown/strings.go:85-98)
-__device__ uint64_t bi_indexof(Lane& L, uint64_t a0, uint64_t a1) {
+__device__ uint64_t bi_indexof(PLane& L, uint64_t a0, uint64_t a1) {
   if (!is_strv(a0) || !is_strv(a1)) { lane_error(L); return mkv(V_UNDEF, 0); }
   SView s = sview(L, a0), p = sview(L, a1);
   for (uint32_t o = 0; o + p.n <= s.n; ++o) if (bytes_at(s, o, p)) return mkint(o);
   return mkint(-1);
 }
 
-__device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
+__device__ uint64_t call_builtin(PLane& L, uint32_t id, const uint64_t* a) {
   switch (id) {
     case BI_COUNT: return bi_count(L, a[0]);
     case BI_ANY: case BI_ALL: return bi_anyall(L, id, a[0]);
@@ -1401,10 +1412,10 @@ __device__ uint64_t call_builtin(Lane& L, uint32_t id, const uint64_t* a) {
   return mkv(V_UNDEF, 0);
 }
 
-__device__ __noinline__ uint64_t arith_slow(Lane& L, uint32_t kind, uint64_t x, uint64_t y);
+__device__ __noinline__ uint64_t arith_slow(PLane& L, uint32_t kind, uint64_t x, uint64_t y);
 // exact small-integer +, -, * inline (the common case: canonical quantities
 // times a constant); everything else out of line
-__device__ __forceinline__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+__device__ __forceinline__ uint64_t arith(PLane& L, uint32_t kind, uint64_t x, uint64_t y) {
   if (vtag(x) == V_INT && vtag(y) == V_INT && kind <= AR_MUL) {
     const int64_t LIM = (1ll << 46);
     int64_t a = intof(x), b = intof(y);
@@ -1417,7 +1428,7 @@ __device__ __forceinline__ uint64_t arith(Lane& L, uint32_t kind, uint64_t x, ui
   }
   return arith_slow(L, kind, x, y);
 }
-__device__ __noinline__ uint64_t arith_slow(Lane& L, uint32_t kind, uint64_t x, uint64_t y) {
+__device__ __noinline__ uint64_t arith_slow(PLane& L, uint32_t kind, uint64_t x, uint64_t y) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   if (kind == AR_MINUS && tclass(x) == 9 && tclass(y) == 9) {
     uint64_t out = list_new(L, LK_SET, coll_len(L, x));
@@ -1475,7 +1486,7 @@ __device__ __noinline__ uint64_t arith_slow(Lane& L, uint32_t kind, uint64_t x, 
 }
 
 // ------------------------------------------------------------------ sprintf
-__device__ __noinline__ uint64_t do_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+__device__ __noinline__ uint64_t do_sprintf(PLane& L, uint32_t fidx, uint64_t args) {
   const uint32_t* f = gk_args.fmt + fidx;
   uint32_t want = f[1];
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
@@ -1504,7 +1515,7 @@ __device__ __forceinline__ uint64_t fmt_args(uint64_t f) {
 }
 __device__ __forceinline__ uint32_t fmt_fidx(uint64_t f) { return (uint32_t)(vpay(f) >> 32) & 0xffffffu; }
 
-__device__ __forceinline__ uint64_t lazy_sprintf(Lane& L, uint32_t fidx, uint64_t args) {
+__device__ __forceinline__ uint64_t lazy_sprintf(PLane& L, uint32_t fidx, uint64_t args) {
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t t = vtag(args);
   if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
@@ -1515,7 +1526,7 @@ __device__ __forceinline__ uint64_t lazy_sprintf(Lane& L, uint32_t fidx, uint64_
 }
 
 // the string a deferred sprintf denotes, built in the lane buffer
-__device__ uint64_t force_fmt(Lane& L, uint64_t v) {
+__device__ uint64_t force_fmt(PLane& L, uint64_t v) {
   if (vtag(v) != V_FMT) return v;
   return do_sprintf(L, fmt_fidx(v), fmt_args(v));
 }
@@ -1524,7 +1535,7 @@ __device__ uint64_t force_fmt(Lane& L, uint64_t v) {
 // Per-instruction semantics (OP_* in common.h).  The VM dispatches to these
 // from its switch; the JIT emits one call per instruction with register
 // operands bound to locals.  A `false` return means "leave the program".
-__device__ __forceinline__ void op_iter_init(Lane& L, uint64_t& it, uint64_t& st, uint64_t coll, uint32_t y) {
+__device__ __forceinline__ void op_iter_init(PLane& L, uint64_t& it, uint64_t& st, uint64_t coll, uint32_t y) {
   it = coll;
   st = ((uint64_t)L.hp << 32) | ((uint64_t)L.bp << 48);
   uint32_t d = y < MAXLOOP ? y : 0;
@@ -1533,7 +1544,7 @@ __device__ __forceinline__ void op_iter_init(Lane& L, uint64_t& it, uint64_t& st
 }
 
 // advances the iterator; false when exhausted (jump to the loop exit)
-__device__ __forceinline__ bool op_iter_next(Lane& L, uint64_t coll, uint64_t& st, uint32_t y,
+__device__ __forceinline__ bool op_iter_next(PLane& L, uint64_t coll, uint64_t& st, uint32_t y,
                                              uint64_t& k, uint64_t& v) {
   uint32_t pos = (uint32_t)st;
   // per-iteration reclamation: everything allocated by the previous
@@ -1549,7 +1560,7 @@ __device__ __forceinline__ bool op_iter_next(Lane& L, uint64_t coll, uint64_t& s
   return true;
 }
 
-__device__ __forceinline__ bool op_cmp(Lane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
+__device__ __forceinline__ bool op_cmp(PLane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
   if (vtag(x) == V_UNDEF || vtag(y) == V_UNDEF) { out = mkv(V_UNDEF, 0); return true; }
   int cr;
   // inlined fast paths (exact ints, interned strings, booleans); the rest of
@@ -1580,14 +1591,14 @@ __device__ __forceinline__ bool op_cmp(Lane& L, uint32_t kind, uint64_t x, uint6
   return true;
 }
 
-__device__ __forceinline__ bool op_list_add(Lane& L, uint64_t& l, uint64_t v, uint32_t y) {
+__device__ __forceinline__ bool op_list_add(PLane& L, uint64_t& l, uint64_t v, uint32_t y) {
   l = list_add(L, l, v);
   if (L.fail) return false;
   if (y) pin_escape(L, y);
   return true;
 }
 
-__device__ __forceinline__ bool op_obj_put(Lane& L, uint64_t& o, uint64_t k, uint64_t v, uint32_t y) {
+__device__ __forceinline__ bool op_obj_put(PLane& L, uint64_t& o, uint64_t k, uint64_t v, uint32_t y) {
   uint32_t n = list_len(L, o);
   bool found = false;
   for (uint32_t i = 0; i + 1 < n; i += 2) {
@@ -1602,7 +1613,7 @@ __device__ __forceinline__ bool op_obj_put(Lane& L, uint64_t& o, uint64_t k, uin
   return true;
 }
 
-__device__ __forceinline__ bool op_yield(Lane& L, uint64_t& out, uint64_t v, uint32_t y) {
+__device__ __forceinline__ bool op_yield(PLane& L, uint64_t& out, uint64_t v, uint32_t y) {
   if (vtag(out) != V_UNDEF) {
     if (vtag(out) == V_FMT || vtag(v) == V_FMT) { out = force_fmt(L, out); v = force_fmt(L, v); if (L.fail) return false; }
     if (!veq(L, out, v)) { lane_error(L); return false; }  // conflicting function/rule outputs
@@ -1614,7 +1625,7 @@ __device__ __forceinline__ bool op_yield(Lane& L, uint64_t& out, uint64_t v, uin
   return true;
 }
 
-__device__ __forceinline__ uint64_t op_len_eq(Lane& L, uint64_t v, uint32_t y) {
+__device__ __forceinline__ uint64_t op_len_eq(PLane& L, uint64_t v, uint32_t y) {
   uint32_t want = y & 0xffffff, kind = y >> 24;
   int cls = tclass(v);
   bool ok = (kind == LK_ARR ? cls == 7 : cls == 8) && coll_len(L, v) == want;
@@ -1623,7 +1634,7 @@ __device__ __forceinline__ uint64_t op_len_eq(Lane& L, uint64_t v, uint32_t y) {
 
 // f("k1") = v1 {true} ... compiled to a table (compiler.cc table_func): the
 // value of the (at most one) entry whose key equals the argument, else undefined
-__device__ __forceinline__ uint64_t op_table(Lane& L, const uint64_t* T, uint64_t arg) {
+__device__ __forceinline__ uint64_t op_table(PLane& L, const uint64_t* T, uint64_t arg) {
   if (vtag(arg) == V_UNDEF) return mkv(V_UNDEF, 0);
   uint32_t n = (uint32_t)T[0];
   for (uint32_t i = 0; i < n; ++i)
@@ -1675,7 +1686,7 @@ __device__ __forceinline__ bool gm_get(uint32_t site, uint64_t k0, uint64_t k1, 
   return false;
 }
 
-__device__ __forceinline__ void gm_put(const Lane& L, uint32_t site, uint64_t k0, uint64_t k1, uint64_t v) {
+__device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k0, uint64_t k1, uint64_t v) {
   if (L.fail || !gk_args.gmemo || !gm_key(k0) || !gm_key(k1) || !memo_stable(v)) return;
   uint64_t h = gm_hash(site, k0, k1);
   uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
@@ -1685,7 +1696,7 @@ __device__ __forceinline__ void gm_put(const Lane& L, uint32_t site, uint64_t k0
 }
 
 // m: message register, d: details register (undefined when absent)
-__device__ __noinline__ bool op_emit(Lane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+__device__ __noinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   if (vtag(m) == V_FMT) {
     // deferred message: size it now, format it into the output at flush_wave.
     // Only heap-free arguments are recorded (the record outlives this
@@ -1742,7 +1753,8 @@ __device__ __forceinline__ void audit_body(Run run) {
   if (tile >= gk_args.ntiles) return;  // wave-uniform
   uint32_t rp = tile * 64 + lane;  // position in the (size-ordered) review columns
   uint32_t r = rp;                   // the review's index in the caller's batch
-  Lane L;
+  Lane L0;
+  PLane& L = *(PLane*)&L0;
   L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   bool live = rp < gk_args.nrev;

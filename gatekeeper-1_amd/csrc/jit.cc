@@ -471,11 +471,11 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre
-    << "__device__ void " << name << "_pred(Lane& L, uint64_t review, uint64_t params) {\n"
+    << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params) {\n"
     << g.body << "}\n"
     << "}  // namespace gk\n"
     << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix() << ") " << name << "() {\n"
-    << "  gk::audit_body([&](gk::Lane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"
+    << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"
     << "    gk::" << name << "_pred(L, review, params);\n"
     << "  });\n"
     << "}\n";

@@ -19,7 +19,7 @@ namespace gk {
 
 constexpr int NREG = 192;
 
-__device__ void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) {
+__device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t params) {
   const uint64_t UND = mkv(V_UNDEF, 0);
   uint64_t R[NREG];
   for (int guard = 0; guard < (1 << 22); ++guard) {
@@ -85,7 +85,7 @@ __device__ void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t para
 }
 
 __global__ void __launch_bounds__(256) audit_kernel() {
-  audit_body([&](Lane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
+  audit_body([&](PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
     run_program(L, gk_args.prog_off[prog], review, params);
   });
 }
@@ -97,7 +97,6 @@ __global__ void __launch_bounds__(256) audit_kernel() {
 // (sview / coll_at touch a lane's buffers only for lane-heap values).  Lanes
 // write disjoint byte ranges [msg_off, msg_off + msg_len) reserved by the audit
 // kernel, consecutive tuples to consecutive ranges.
-__device__ Lane g_fmt_lane;
 
 // LDS-staged writer for one wavefront's message bytes
 struct LOut {
@@ -146,7 +145,8 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
   const uint64_t n = gk_args.counters[0];
   // an overflowed call left some reservations unwritten; the host retries it
   if (n > gk_args.out_cap || gk_args.counters[1] > gk_args.bytes_cap) return;
-  Lane& L = g_fmt_lane;
+  Lane L0;  // never dereferenced: the arguments are heap-free values
+  PLane& L = *(PLane*)&L0;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* st = stage[wv];
   uint8_t* stb = (uint8_t*)st;

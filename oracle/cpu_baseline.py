@@ -45,13 +45,15 @@ def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1):
     return s, out[0], out[1], out[2], out[3]
 
 
-def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1):
+def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1, pc_hist=None):
     """SURVEY 8(d) reference accounting of reviews [lo, hi) x constraint `only`
-    (all when < 0): dict(nodes, strings, string_bytes, violations, flagged)"""
+    (all when < 0): dict(nodes, strings, string_bytes, violations, flagged);
+    pc_hist: a ctypes uint64 array of the code size receiving per-instruction
+    execution counts (one thread)"""
     lib = load()
     glib = driver._lib
     lib.gkcpu_referenced.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
-                                     C.POINTER(C.c_uint64)]
+                                     C.POINTER(C.c_uint64), C.c_void_p]
     lib.gkcpu_referenced.restype = C.c_int
     n = lib.gkcpu_devargs_size()
     buf = (C.c_uint8 * n)()
@@ -62,5 +64,6 @@ def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int
     glib.gk_debug_store_sizes(driver._e, C.byref(nn), C.byref(ns))
     out = (C.c_uint64 * 5)()
     hi = batch.n if hi is None else hi
-    lib.gkcpu_referenced(buf, nn.value, ns.value, lo, hi, only, threads, out)
+    lib.gkcpu_referenced(buf, nn.value, ns.value, lo, hi, only, threads, out,
+                         C.cast(pc_hist, C.c_void_p) if pc_hist is not None else None)
     return {"nodes": out[0], "strings": out[1], "string_bytes": out[2], "violations": out[3], "flagged": out[4]}

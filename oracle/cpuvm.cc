@@ -35,6 +35,7 @@ using ::uint64_t;
 using ::uint8_t;
 }  // namespace __hip_internal
 #define __HIPCC_RTC__ 1
+#define GK_PRIV
 #define __device__
 #define __global__
 #define __host__
@@ -59,6 +60,7 @@ static CpuDim3 blockIdx, threadIdx, blockDim{64, 1, 1}, gridDim{1, 1, 1};
 namespace gkcpu_touch {
 thread_local uint64_t* node_bits = nullptr;
 thread_local uint64_t* str_bits = nullptr;
+thread_local uint64_t* pc_hist = nullptr;  // executions per bytecode instruction
 }  // namespace gkcpu_touch
 #define GK_TOUCH_NODE(i) (gkcpu_touch::node_bits[(uint32_t)(i) >> 6] |= 1ull << ((uint32_t)(i) & 63))
 #define GK_TOUCH_STR(s) (gkcpu_touch::str_bits[(uint32_t)(s) >> 6] |= 1ull << ((uint32_t)(s) & 63))
@@ -78,6 +80,9 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
   for (int guard = 0; guard < (1 << 22); ++guard) {
     if (pc >= gk_args.ncode) { lane_fallback(L, FB_UNSUPPORTED); return; }
     const Ins in = gk_args.code[pc];
+#ifdef GKCPU_TOUCH
+    if (gkcpu_touch::pc_hist) ++gkcpu_touch::pc_hist[pc];
+#endif
     ++pc;
     switch (in.op) {
       case OP_END: return;
@@ -231,7 +236,8 @@ extern "C" {
 // their bytes, violations, flagged pairs].  n_nodes / n_strings: the host
 // store's sizes (gk_debug_store_sizes).
 int gkcpu_referenced(const void* args, uint64_t n_nodes, uint64_t n_strings, uint32_t lo, uint32_t hi, int only,
-                     int threads, uint64_t* out5) {
+                     int threads, uint64_t* out5, uint64_t* pc_hist) {
+  if (pc_hist) threads = 1;  // pc_hist: executions per bytecode instruction (diagnostics)
   memcpy(&gk_args_touch, args, sizeof(gk_touch::DevArgs));
   auto& A = gk_args_touch;
   if (hi > A.nrev) hi = A.nrev;
@@ -246,6 +252,7 @@ int gkcpu_referenced(const void* args, uint64_t n_nodes, uint64_t n_strings, uin
     sb[t].assign(swords, 0);
     gkcpu_touch::node_bits = nb[t].data();
     gkcpu_touch::str_bits = sb[t].data();
+    gkcpu_touch::pc_hist = pc_hist;
     std::vector<char> fbuf(1 << 16);
     auto& k = per[t];
     for (;;) {

