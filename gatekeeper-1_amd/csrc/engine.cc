@@ -33,6 +33,8 @@ extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflag
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
                                 unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
                                 unsigned int* ncand, int select_only, hipStream_t stream);
+extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflags, const uint8_t* cerr,
+                                gk::Viol* dst, unsigned long long* count, hipStream_t stream);
 
 namespace gk {
 
@@ -1709,16 +1711,33 @@ int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char
   return GK_OK;
 }
 
-int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst) {
+int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst,
+                                  uint64_t* n_tuples) {
   if (!e || !r) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   if (r->epoch == 0 || r->epoch != e->eval_epoch)
     return fail(e, GK_EINVAL, "device output was overwritten by a later evaluation on this engine");
-  if (tuples_dst && r->dev_tuples &&
-      hipMemcpy(tuples_dst, r->d_tuples, r->dev_tuples * sizeof(Viol), hipMemcpyDeviceToDevice) != hipSuccess)
-    return fail(e, GK_EDEVICE, "device copy failed");
+  uint64_t kept = 0;
+  if (tuples_dst && r->dev_tuples) {
+    // only the tuples of reviews the engine answered (rows of
+    // reviews flagged error / fallback, or of a constraint whose
+    // enforcementAction is invalid, belong to the CPU re-run, not to this output)
+    const uint32_t ncons = (uint32_t)e->corder.size();
+    bool any_err = false;
+    std::vector<uint8_t> cerr(ncons, 0);
+    for (uint32_t c = 0; c < ncons; ++c) { cerr[c] = e->corder[c]->ea_error; any_err |= cerr[c] != 0; }
+    if (!e->d_ncand.reserve(16) || (any_err && !up(e->d_cerr, cerr, false)))
+      return fail(e, GK_EDEVICE, "device allocation failed");
+    int lr = gk_launch_filter((const Viol*)r->d_tuples, r->dev_tuples, (uint32_t*)e->d_rflags.p,
+                              any_err ? (const uint8_t*)e->d_cerr.p : nullptr, (Viol*)tuples_dst,
+                              (unsigned long long*)e->d_ncand.p, e->stream);
+    if (lr != 0 || hipMemcpyAsync(&kept, e->d_ncand.p, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+      return fail(e, GK_EDEVICE, "device copy failed");
+  }
   if (bytes_dst && r->dev_bytes && hipMemcpy(bytes_dst, r->d_bytes, r->dev_bytes, hipMemcpyDeviceToDevice) != hipSuccess)
     return fail(e, GK_EDEVICE, "device copy failed");
+  if (n_tuples) *n_tuples = kept;
   return GK_OK;
 }
 

@@ -303,7 +303,43 @@ __global__ void __launch_bounds__(256) gk_sample_select(const Viol* out, uint64_
   }
 }
 
+// The raw-output copy (gk_results_copy_device_output): the tuples of reviews
+// the engine answered, i.e. without those of reviews flagged error or
+// fallback (the caller re-runs those on CPU OPA) -- the same set the totals
+// count.  Order is not kept (a wave-aggregated atomic cursor); consumers sort
+// by (review, autoreject first, constraint, seq).
+__global__ void __launch_bounds__(256) gk_filter_viol(const Viol* out, uint64_t n, const uint32_t* rflags, Viol* dst,
+                                                      unsigned long long* count) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    Viol v;
+    bool keep = false;
+    if (i < n) {
+      v = out[i];
+      keep = !(rflags[v.review] & (RF_ERROR | RF_FALLBACK));
+    }
+    const unsigned long long m = __ballot(keep);
+    if (!m) continue;
+    unsigned long long slot0 = 0;
+    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+    if (lane == leader) slot0 = atomicAdd(count, (unsigned long long)__popcll(m));
+    slot0 = __shfl(slot0, (int)leader, 64);
+    if (keep) dst[slot0 + __popcll(m & ((1ull << lane) - 1))] = v;
+  }
+}
+
 }  // namespace gk
+
+extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflags, const uint8_t* cerr,
+                                gk::Viol* dst, unsigned long long* count, hipStream_t stream) {
+  uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  if (blocks == 0) blocks = 1;
+  if (cerr) hipLaunchKernelGGL(gk::gk_mark_ea_error, dim3(blocks), dim3(256), 0, stream, out, n, cerr, rflags);
+  (void)hipMemsetAsync(count, 0, 8, stream);
+  hipLaunchKernelGGL(gk::gk_filter_viol, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, dst, count);
+  return (int)hipGetLastError();
+}
 
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,

@@ -26,14 +26,110 @@ def template_kind(template: dict) -> str:
     return template["spec"]["crd"]["spec"]["names"]["kind"]
 
 
+class TemplateError(ValueError):
+    """AddTemplate's rejection of a template's Rego (client.go:280-347)."""
+
+
+# fields under `data` a template may read besides its libs (rego_helpers.go:12-14)
+ALLOWED_DATA_FIELDS = ("inventory",)
+
+
+def _code_spans(src: str):
+    """[start, end) spans of src outside string literals and comments"""
+    spans, i, start, n = [], 0, 0, len(src)
+    while i < n:
+        c = src[i]
+        if c == '"' or c == "`" or c == "#":
+            if i > start:
+                spans.append((start, i))
+            if c == "#":
+                j = src.find("\n", i)
+                i = n if j < 0 else j
+            elif c == "`":
+                j = src.find("`", i + 1)
+                i = n if j < 0 else j + 1
+            else:
+                j = i + 1
+                while j < n and src[j] != '"':
+                    j += 2 if src[j] == "\\" else 1
+                i = min(n, j + 1)
+            start = i
+            continue
+        i += 1
+    if start < n:
+        spans.append((start, n))
+    return spans
+
+
+_DATA_REF = re.compile(r"(?<![\w.])data((?:\s*\.\s*[A-Za-z_][A-Za-z0-9_]*|\s*\[\s*\"[^\"\\\\]*\"\s*\])*)")
+_SEG = re.compile(r"\.\s*([A-Za-z_][A-Za-z0-9_]*)|\[\s*\"([^\"\\\\]*)\"\s*\]")
+
+
+def _ref_path(tail: str):
+    return [a or b for a, b in _SEG.findall(tail)]
+
+
+def _rewrite_module(src: str, lib_prefix, is_lib: bool):
+    """regorewriter.Rewrite (regorewriter.go:366-419) over one module's text:
+    checks every `data` ref (a lib or an allowed extern, :250-271) and every
+    import (:274-291), prefixes `data.lib...` refs and imports with lib_prefix
+    (PackagePrefixer.Transform, packagetransformer.go:32-40), and for a lib
+    moves its `package lib.<x>` under the prefix (:371-373; the package must
+    be strictly below `lib`, :224-247)."""
+    out, pos = [], 0
+    pkg_done = False
+    for a, b in _code_spans(src):
+        out.append(src[pos:a])
+        seg = src[a:b]
+        res, p = [], 0
+        if not pkg_done:
+            m = re.search(r"(?m)^\s*package\s+([A-Za-z_][\w.]*)", seg)
+            if m:
+                pkg_done = True
+                if is_lib:
+                    path = m.group(1).split(".")
+                    if path[0] != "lib" or len(path) < 2:
+                        raise TemplateError("path data.%s not found in lib prefixes" % m.group(1))
+                    res.append(seg[:m.start(1)] + ".".join(lib_prefix + path))
+                    p = m.end(1)
+        for m in re.finditer(r"(?m)^\s*import\s+([A-Za-z_][\w.\[\]\"]*)", seg[p:]):
+            imp = m.group(1)
+            if not (imp == "data.lib" or imp.startswith("data.lib.") or imp.startswith('data["lib"]')):
+                raise TemplateError("bad import")
+        for m in _DATA_REF.finditer(seg, p):
+            path = _ref_path(m.group(1))
+            if not path:
+                continue  # bare `data`: checkRef finds no rule to reject (a local use of the whole tree)
+            if path[0] in ALLOWED_DATA_FIELDS:
+                continue
+            if path[0] != "lib":
+                raise TemplateError("disallowed ref data.%s" % ".".join(path))
+            res.append(seg[p:m.start()] + "data." + ".".join(lib_prefix + path))
+            p = m.end()
+        res.append(seg[p:])
+        out.append("".join(res))
+        pos = b
+    out.append(src[pos:])
+    return "".join(out)
+
+
 def template_modules(template: dict):
-    """(prefix, [entry module, libs...]) as createTemplateArtifacts builds them."""
+    """(prefix, [entry module, libs...]) as createTemplateArtifacts builds them
+    (client.go:280-347): the entry module's package becomes
+    `templates["<target>"]["<Kind>"]`, and the libs and every `data.lib` ref
+    move under `libs.<target>.<Kind>` (templateLibPrefix, client.go:147-150),
+    so two templates' libs never collide.  Raises TemplateError where
+    regorewriter rejects the sources."""
     kind = template_kind(template)
     tgt = template["spec"]["targets"][0]
     src = tgt["rego"]
     prefix = 'templates["%s"]["%s"]' % (TARGET, kind)
+    lib_prefix = ("libs.%s.%s" % (TARGET, kind)).split(".")
     src = re.sub(r"^\s*package\s+\S+", "package " + prefix, src, count=1, flags=re.M)
-    return prefix, [src] + list(tgt.get("libs", []))
+    mods = [_rewrite_module(src, lib_prefix, False)]
+    for lib in tgt.get("libs", []) or []:
+        mods.append(_rewrite_module(lib, lib_prefix, True))
+    return prefix, mods
 
 
 def constraint_path(constraint: dict) -> str:

@@ -127,7 +127,7 @@ def load_library():
     lib.gk_results_launches.restype = sz
     lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32), pu64, pu64]
     lib.gk_template_backend.argtypes = [vp, cp, C.POINTER(C.c_int), C.POINTER(cp)]
-    lib.gk_results_copy_device_output.argtypes = [vp, vp, vp, vp]
+    lib.gk_results_copy_device_output.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_uint64)]
     lib.gk_results_vm_profile.argtypes = [vp, C.c_void_p, sz]
     lib.gk_results_vm_profile.restype = sz
     lib.gk_template_status.argtypes = [vp, cp, C.POINTER(cp)]
@@ -344,7 +344,9 @@ class Batch:
     def eval(self, decode=True, light=False, device_out=None) -> Results:
         """device_out(n_tuples, n_bytes) -> (tuples_ptr, bytes_ptr): device
         buffers (e.g. torch tensors' data_ptr()) that receive the call's raw
-        output (gk_viol records + message bytes) before the handle is freed."""
+        output (gk_viol records of the reviews the engine answered + message
+        bytes) before the handle is freed; device_out.copied(n) is then told
+        how many records were written, if it has that method."""
         lib = self._drv._lib
         out = C.c_void_p()
         rc = lib.gk_batch_eval(self._drv._e, self._h, 1 if decode else 0, C.byref(out))
@@ -353,10 +355,13 @@ class Batch:
             dt, db = C.c_uint64(), C.c_uint64()
             lib.gk_results_device_counts(out, C.byref(dt), C.byref(db))
             tp, bp = device_out(dt.value, db.value)
-            rc = lib.gk_results_copy_device_output(self._drv._e, out, tp, bp)
+            kept = C.c_uint64()
+            rc = lib.gk_results_copy_device_output(self._drv._e, out, tp, bp, C.byref(kept))
             if rc != 0:
                 lib.gk_results_free(out)
                 self._drv._check(rc)
+            if hasattr(device_out, "copied"):
+                device_out.copied(kept.value)
         return _collect_light(lib, out) if light else _collect(lib, out)
 
     def eval_audit(self, limit: int = 20) -> AuditSweep:

@@ -68,6 +68,10 @@ class DeviceOutput:
         self.n_tuples, self.n_bytes = n_tuples, n_bytes
         return self._t.data_ptr(), self._b.data_ptr()
 
+    def copied(self, n_tuples: int):
+        """records actually written (the engine drops those of flagged reviews)"""
+        self.n_tuples = n_tuples
+
     def tuples(self):
         """int32 [n, 8] view of the gk_viol records."""
         return self._t[: self.n_tuples * VIOL_BYTES].view(self.torch.int32).view(-1, VIOL_WORDS)

@@ -213,7 +213,12 @@ typedef struct {
   uint64_t msg_off;      /* message at [msg_off, +msg_len), details JSON right after it */
   uint32_t det_len, pad;
 } gk_viol;
-int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst);
+/* tuples_dst receives only the tuples of reviews the engine answered (not
+ * those of reviews flagged GK_REVIEW_ERROR / GK_REVIEW_FALLBACK, nor rows of a
+ * constraint with an invalid enforcementAction): *n_tuples of them, in no
+ * particular order; size it for dev_tuples. */
+int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst,
+                                  uint64_t* n_tuples);
 /* kernels of the call in launch order: kernel name ("audit_kernel" = bytecode
  * VM, "gk_t_<hash>" = a template kernel), duration (HIP events), how many
  * constraints it evaluated and the violation tuples / message bytes it wrote */
