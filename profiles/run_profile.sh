@@ -14,6 +14,8 @@ OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 export GKGPU_JIT_CACHE=$ROOT/.jitcache
 cd /tmp && export TMPDIR=/tmp
+# GPU clocks around the run (box-to-box variance: compare only inside one call)
+rocm-smi --showclocks > "$OUT/clocks_before.txt" 2>&1 || true
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- \
   python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/bench_trace.json"
 echo "trace done"
@@ -24,5 +26,10 @@ timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 > "$OUT/bench_write.json"
 echo "write done"
 python3 "$ROOT/profiles/summarize.py" --traffic-only "$OUT"
+# sample the clocks while the bench runs (killed by its PID afterwards)
+( while :; do date +%T; rocm-smi --showclocks 2>&1 | grep -E "sclk|mclk|fclk"; sleep 2; done ) > "$OUT/clocks_during.txt" &
+SAMPLER=$!
 timeout -k 10 500 python3 "$ROOT/bench.py" --traffic-json "$OUT/traffic.json" > "$OUT/bench.json"
+kill $SAMPLER 2>/dev/null || true
 echo "bench done"
+rocm-smi --showclocks > "$OUT/clocks_after.txt" 2>&1 || true
