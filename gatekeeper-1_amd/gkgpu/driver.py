@@ -279,9 +279,17 @@ def _collect_audit(lib, h) -> AuditSweep:
         lib.gk_results_free(h)
 
 
-def _collect_light(lib, h) -> Results:
-    """totals, counters and flag counts only (no per-review arrays)."""
+def _collect_light(lib, h, with_status: bool = False) -> Results:
+    """totals, counters and flag counts only (no result rows; the per-review
+    status words as a numpy uint32 array when with_status)."""
     try:
+        status = []
+        if with_status:
+            import numpy as np
+            nr = lib.gk_results_reviews(h)
+            status = np.zeros(max(nr, 1), dtype=np.uint32)[:nr]
+            if nr:
+                lib.gk_results_copy_status(h, status.ctypes.data, None)
         nc = lib.gk_results_constraints(h)
         totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
         t = (C.c_double * 5)()
@@ -290,7 +298,7 @@ def _collect_light(lib, h) -> Results:
         lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
         ne, nf = C.c_uint64(), C.c_uint64()
         lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
-        return Results([], [], [], totals, list(t), dt.value, db.value, ne.value, nf.value, _vm_profile(lib, h),
+        return Results([], status, [], totals, list(t), dt.value, db.value, ne.value, nf.value, _vm_profile(lib, h),
                        _launches(lib, h))
     finally:
         lib.gk_results_free(h)
@@ -341,7 +349,7 @@ class Batch:
         self._h = handle
         self.n = n
 
-    def eval(self, decode=True, light=False, device_out=None) -> Results:
+    def eval(self, decode=True, light=False, device_out=None, with_status=False) -> Results:
         """device_out(n_tuples, n_bytes) -> (tuples_ptr, bytes_ptr): device
         buffers (e.g. torch tensors' data_ptr()) that receive the call's raw
         output (gk_viol records of the reviews the engine answered + message
@@ -362,7 +370,7 @@ class Batch:
                 self._drv._check(rc)
             if hasattr(device_out, "copied"):
                 device_out.copied(kept.value)
-        return _collect_light(lib, out) if light else _collect(lib, out)
+        return _collect_light(lib, out, with_status) if light else _collect(lib, out)
 
     def eval_audit(self, limit: int = 20) -> AuditSweep:
         """one audit sweep: exact totals + first `limit` results per constraint
