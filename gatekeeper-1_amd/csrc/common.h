@@ -104,6 +104,8 @@ enum Op : uint16_t {
   OP_TABLE,        // a = lookup(K[x..]: n, (key, value) x n ; R[b]) — constant-table function call
   OP_MEMO_GET,     // memo slot y holds (R[b], R[c]) -> R[a] = cached value, jump x   (c = 0xffff: one arg)
   OP_MEMO_PUT,     // memo slot y := (R[b], R[c]) -> R[a] when arguments and value are heap-free
+  OP_ORD,          // y: emission order key of fused rule bodies (compiler.cc rule_group):
+                   //    y < 2^31: key = base + y; else base += y & 0x7fffffff, key = base
   OP_COUNT_
 };
 

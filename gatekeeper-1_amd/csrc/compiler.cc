@@ -87,9 +87,12 @@ class Comp {
         Env env;
         env.mod = r->mod;
         const auto& body = cbody(r, {});
+        fuse_ok_ = !getenv("GKGPU_FUSE") || atoi(getenv("GKGPU_FUSE")) != 0;  // A/B switch, default on
         body_k(body, 0, &env, Lr, [&, idx](int f) { emit_violation(r, &env, idx, f); });
+        fuse_ok_ = false;
         place(Lr);
       } catch (const Unsupported& ex) {
+        fuse_ok_ = false;
         // guard mode: a rule whose body cannot be compiled at all sends every
         // review that reaches it (every matched review) to the CPU
         if (!guard_) throw;
@@ -533,6 +536,7 @@ class Comp {
   }
 
   void compr(const TermP& t, Env* env, int fail, const K& k) {
+    NoFuse nf(this);  // array order is observable
     int save = reg_top_;
     uint32_t kind = t->k == T_SETCOMPR ? LK_SET : t->k == T_ARRCOMPR ? LK_ARR : LK_OBJ;
     int out = alloc();
@@ -676,14 +680,8 @@ class Comp {
     stmt_key_ = nullptr;
     if (i == path.size()) { full_set(rules, fail, k); return; }
     const TermP& key = path[i];
-    for (auto& r : rules) {
-      if (r->is_else) throw Unsupported("else");
-      int save = reg_top_;
-      int Lr = label();
-      Env renv;
-      renv.mod = r->mod;
-      // prebind rule-head variables from ground parts of the caller's key
-      std::vector<std::string> pre;
+    // rule-head variables prebound from ground parts of the caller's key
+    auto prebinds = [&](const std::shared_ptr<Rule>& r) {
       std::vector<std::pair<std::string, TermP>> pre_terms;
       if (r->key->k == T_VAR && ground(env, key)) pre_terms.push_back({r->key->s, key});
       if (r->key->k == T_OBJECT && key->k == T_OBJECT) {
@@ -697,27 +695,137 @@ class Comp {
           }
         }
       }
-      prebind(pre_terms, 0, env, &renv, Lr, [&, r](int f) {
-        std::vector<std::string> safe;
-        for (auto& pt : pre_terms) safe.push_back(pt.first);
+      return pre_terms;
+    };
+    auto safe_of = [](const std::vector<std::pair<std::string, TermP>>& pts) {
+      std::vector<std::string> safe;
+      for (auto& pt : pts) safe.push_back(pt.first);
+      return safe;
+    };
+    // the rule's key unified with the caller's key, then the caller's continuation
+    auto head_k = [&](const std::shared_ptr<Rule>& r, Env* renv, int f2) {
+      if (stmt && same_object_keys(key, r->key)) {
+        // `s[{"msg": msg, "field": "x"}]` as a statement against a rule head
+        // `s[{"msg": m, "field": f}]`: object unification is member-wise
+        // unification over equal key sets, so the head object is never built
+        unify_members(key, r->key, 0, env, renv, f2, [&](int f4) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f4); });
+        return;
+      }
+      term(r->key, renv, f2, [&](int kv, int f3) {
+        unify_value(key, kv, env, f3, [&](int f4) { walk(kv, path, i + 1, env, f4, k); });
+      });
+    };
+    for (size_t ri = 0; ri < rules.size();) {
+      const auto& r = rules[ri];
+      if (r->is_else) throw Unsupported("else");
+      auto pre_terms = prebinds(r);
+      const auto safe = safe_of(pre_terms);
+      size_t rj = ri + 1;
+      if (fuse_ok_ && !guard_)
+        while (rj < rules.size() && fusable(rules[ri], rules[rj], pre_terms, prebinds(rules[rj]), safe)) ++rj;
+      if (rj - ri >= 2) {
+        rule_group(rules, ri, rj, pre_terms, safe, env, head_k);
+        ri = rj;
+        continue;
+      }
+      int save = reg_top_;
+      int Lr = label();
+      Env renv;
+      renv.mod = r->mod;
+      prebind(pre_terms, 0, env, &renv, Lr, [&](int f) {
         const auto& body = cbody(r, safe);
-        body_k(body, 0, &renv, f, [&](int f2) {
-          if (stmt && same_object_keys(key, r->key)) {
-            // `s[{"msg": msg, "field": "x"}]` as a statement against a rule head
-            // `s[{"msg": m, "field": f}]`: object unification is member-wise
-            // unification over equal key sets, so the head object is never built
-            unify_members(key, r->key, 0, env, &renv, f2, [&](int f4) { int tr = loadk(tag_val(V_BOOL, 1)); k(tr, f4); });
-            return;
-          }
-          term(r->key, &renv, f2, [&](int kv, int f3) {
-            unify_value(key, kv, env, f3, [&](int f4) { walk(kv, path, i + 1, env, f4, k); });
-          });
-        });
+        body_k(body, 0, &renv, f, [&](int f2) { head_k(r, &renv, f2); });
       });
       place(Lr);
       reg_top_ = save;
+      ++ri;
     }
     emit_jmp(OP_JMP, 0, fail);
+  }
+
+  // ---------------------------------------------------------------- rule groups
+  // Consecutive bodies of one partial set whose first expression is the same
+  // (the ContainerLimits shape: eight bodies each starting with
+  // `container := input.review.object.spec[field][_]`) are fused: that
+  // expression is evaluated once and, for each of its solutions, the rest of
+  // every body in turn -- one pass over the containers instead of eight.
+  // Rego bodies have no side effects, so the group yields the same solutions;
+  // only their order changes (solution-major instead of body-major), and OP_ORD
+  // keys let flush_wave number the emissions in the reference's body-major
+  // order (devrt.h op_ord).  Errors and fallbacks abort the lane either way.
+  // Fusion is confined to contexts whose solutions only reach emissions (not
+  // comprehensions, function or complete-rule values, sets) and does not nest.
+  bool fuse_ok_ = false;
+  struct NoFuse {
+    Comp* c;
+    bool saved;
+    explicit NoFuse(Comp* cc) : c(cc), saved(cc->fuse_ok_) { c->fuse_ok_ = false; }
+    ~NoFuse() { c->fuse_ok_ = saved; }
+  };
+
+  static bool same_term(const TermP& a, const TermP& b) {
+    if (a == b) return true;
+    if (!a || !b) return false;
+    // wildcards (`_`, renamed $_N by the parser) are each used once: any two match
+    const bool wild = a->k == T_VAR && b->k == T_VAR && a->s.rfind("$_", 0) == 0 && b->s.rfind("$_", 0) == 0;
+    if (a->k != b->k || a->stype != b->stype || (a->s != b->s && !wild) || a->op != b->op) return false;
+    if (!same_term(a->head, b->head) || !same_term(a->key, b->key) || !same_term(a->value, b->value)) return false;
+    if (a->items.size() != b->items.size() || a->body.size() != b->body.size()) return false;
+    for (size_t x = 0; x < a->items.size(); ++x) if (!same_term(a->items[x], b->items[x])) return false;
+    for (size_t x = 0; x < a->body.size(); ++x) if (!same_expr(a->body[x], b->body[x])) return false;
+    return true;
+  }
+  static bool same_expr(const ExprP& a, const ExprP& b) {
+    if (a->kind != b->kind || a->negated != b->negated || !a->withs.empty() || !b->withs.empty()) return false;
+    if (a->terms.size() != b->terms.size()) return false;
+    for (size_t x = 0; x < a->terms.size(); ++x) if (!same_term(a->terms[x], b->terms[x])) return false;
+    return true;
+  }
+
+  bool fusable(const std::shared_ptr<Rule>& a, const std::shared_ptr<Rule>& b,
+               const std::vector<std::pair<std::string, TermP>>& pa,
+               const std::vector<std::pair<std::string, TermP>>& pb, const std::vector<std::string>& safe) {
+    if (b->is_else || a->mod != b->mod || pa.size() != pb.size()) return false;
+    for (size_t x = 0; x < pa.size(); ++x)
+      if (pa[x].first != pb[x].first || pa[x].second.get() != pb[x].second.get()) return false;
+    const auto& ba = cbody(a, safe);
+    const auto& bb = cbody(b, safe);
+    if (ba.size() < 2 || bb.size() < 2) return false;
+    return ba[0]->kind != Expr::SOME && same_expr(ba[0], bb[0]);
+  }
+
+  using HeadK = std::function<void(const std::shared_ptr<Rule>&, Env*, int)>;
+  void rule_group(const std::vector<std::shared_ptr<Rule>>& rules, size_t lo, size_t hi,
+                  const std::vector<std::pair<std::string, TermP>>& pre_terms, const std::vector<std::string>& safe,
+                  Env* env, const HeadK& head_k) {
+    NoFuse nf(this);
+    int save = reg_top_;
+    int Lg = label();
+    Env renv;
+    renv.mod = rules[lo]->mod;
+    const auto& first = cbody(rules[lo], safe);
+    prebind(pre_terms, 0, env, &renv, Lg, [&](int f) {
+      expr(first[0], &renv, f, [&](int fnext) {
+        const int save2 = reg_top_;
+        for (size_t j = lo; j < hi; ++j) {
+          const auto& r = rules[j];
+          const auto& body = cbody(r, safe);
+          int Ln = label();
+          emit(OP_ORD, 0, 0, 0, 0, (uint32_t)(j - lo));
+          Env e2;
+          e2.mod = r->mod;
+          e2.parent = renv.parent;
+          e2.vars = renv.vars;
+          body_k(body, 1, &e2, Ln, [&](int f2) { head_k(r, &e2, f2); });
+          place(Ln);
+          reg_top_ = save2;
+        }
+        emit_jmp(OP_JMP, 0, fnext);
+      });
+    });
+    place(Lg);
+    emit(OP_ORD, 0, 0, 0, 0, 0x80000000u | (uint32_t)(hi - lo));
+    reg_top_ = save;
   }
 
   // both object literals with scalar keys, the same key set, no duplicates
@@ -759,6 +867,7 @@ class Comp {
   }
 
   void full_set(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    NoFuse nf(this);
     int save = reg_top_;
     int out = alloc();
     emit(OP_LIST_NEW, (uint16_t)out, 0, 0, 0, LK_SET);
@@ -776,6 +885,7 @@ class Comp {
   }
 
   void complete_value(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    NoFuse nf(this);
     auto it = crule_.find(rules[0].get());
     if (it == crule_.end() && crule_.size() < kMaxCachedRules) {
       int n = (int)crule_.size();
@@ -830,6 +940,7 @@ class Comp {
   }
 
   void complete_eval(const std::vector<std::shared_ptr<Rule>>& rules, int fail, const K& k) {
+    NoFuse nf(this);
     int save = reg_top_;
     int out = loadk(tag_val(V_UNDEF, 0));
     TermP def;
@@ -887,6 +998,7 @@ class Comp {
   }
 
   void call(const TermP& t, Env* env, int fail, bool stmt, const K& k) {
+    NoFuse nf(this);  // function values (and builtin arguments) are not emissions
     std::string name;
     for (size_t i = 0; i < t->op.size(); ++i) name += (i ? "." : "") + t->op[i];
     auto rules = resolve_func(t->op, env);

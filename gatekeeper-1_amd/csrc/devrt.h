@@ -96,7 +96,10 @@ __device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); retu
 struct Lane {
   uint64_t H[HCAP];
   char B[BCAP];
-  uint32_t hp, bp, seq, fail;  // fail: 0 ok, RF_ERROR, RF_FALLBACK
+  uint32_t hp, bp, fail;  // fail: 0 ok, RF_ERROR, RF_FALLBACK
+  // emission order key (OP_ORD, fused rule bodies): emissions are numbered by
+  // (key, emission index) at flush, which is the reference's evaluation order
+  uint16_t ord, ord_base;
   uint32_t reason;
   // per loop depth: heap / byte watermarks that values escaping the loop pinned
   uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
@@ -104,7 +107,7 @@ struct Lane {
   uint32_t en, steps;
   uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
   uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
-  uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP];
+  uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP], em_ord[EMCAP];
 };
 
 // A lane's state lives in private (scratch) memory.  Helpers take it through
@@ -1042,6 +1045,7 @@ __device__ void stage_tuple(PLane& L, uint32_t rule, const char* msg, uint32_t m
   L.em_off[L.en] = (uint16_t)off;
   L.em_mlen[L.en] = (uint16_t)mlen;
   L.em_dlen[L.en] = (uint16_t)dlen;
+  L.em_ord[L.en] = L.ord;
   ++L.en;
   // only the staged bytes escape: the iteration's list heap stays reclaimable
   for (uint32_t d = 1; d <= depth && d < MAXLOOP; ++d)
@@ -1081,8 +1085,18 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
     atomicOr(&gk_args.rflags[r], (uint32_t)RF_OVERFLOW);
     return;
   }
+  const bool fused = L.ord_base != 0;  // an OP_ORD group ran: number by (key, index)
   for (uint32_t i = 0; i < nt; ++i) {
     uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = dw & 0x7fffu, o = L.em_off[i];
+    uint32_t seq = i;
+    if (fused) {
+      const uint32_t oi = L.em_ord[i];
+      seq = 0;
+      for (uint32_t j = 0; j < nt; ++j) {
+        const uint32_t oj = L.em_ord[j];
+        seq += (oj < oi || (oj == oi && j < i)) ? 1u : 0u;
+      }
+    }
     GOut g{(uint8_t*)gk_args.bytes, bb, bb, 0, false};
     if ((dw & 0x8000u) && gk_args.frec) {
       // deferred message: hand the record to the format pass (gk_format_kernel),
@@ -1111,7 +1125,7 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
     Viol v;
     v.review = r;
     v.constraint = c;
-    v.seq = (uint16_t)i;
+    v.seq = (uint16_t)seq;
     v.rule = L.em_rule[i];
     v.msg_off = bb;
     v.msg_len = ml;
@@ -1632,6 +1646,19 @@ __device__ __forceinline__ uint64_t op_len_eq(PLane& L, uint64_t v, uint32_t y) 
   return mkv(V_BOOL, ok);
 }
 
+// OP_ORD (compiler.cc rule_group): rule bodies that share their first
+// expression are evaluated in one pass over its solutions, body after body for
+// each solution; the reference evaluates them body by body (topdown
+// evalOneRule per rule), so each fused body's emissions carry key base + j and
+// the group's exit moves the base past them.  flush_wave numbers a lane's
+// emissions by (key, emission index), which restores the reference's order.
+__device__ __forceinline__ void op_ord(PLane& L, uint32_t y) {
+  const uint32_t k = (uint32_t)L.ord_base + (y & 0x7fffffffu);
+  if (k > 0xffffu) { lane_fallback(L, FB_MSG_LEN); return; }
+  if (y & 0x80000000u) L.ord_base = (uint16_t)k;
+  L.ord = (uint16_t)k;
+}
+
 // f("k1") = v1 {true} ... compiled to a table (compiler.cc table_func): the
 // value of the (at most one) entry whose key equals the argument, else undefined
 __device__ __forceinline__ uint64_t op_table(PLane& L, const uint64_t* T, uint64_t arg) {
@@ -1721,6 +1748,7 @@ __device__ __noinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t 
       L.em_off[L.en] = (uint16_t)off;
       L.em_mlen[L.en] = (uint16_t)cn.n;
       L.em_dlen[L.en] = (uint16_t)(o.n | 0x8000u);
+      L.em_ord[L.en] = L.ord;
       ++L.en;
       for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
         if (L.keepB[dd] < L.bp) L.keepB[dd] = (uint16_t)L.bp;
@@ -1755,7 +1783,7 @@ __device__ __forceinline__ void audit_body(Run run) {
   uint32_t r = rp;                   // the review's index in the caller's batch
   Lane L0;
   PLane& L = *(PLane*)&L0;
-  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   bool live = rp < gk_args.nrev;
   if (live) {

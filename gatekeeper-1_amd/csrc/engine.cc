@@ -322,7 +322,7 @@ static void rebuild_modules(gk_engine* e) {
         const Ins& in = e->bank.code[p.code_off + k];
         auto reg_ok = [&](uint16_t r) { return r < p.nregs || r == 0xffff; };
         if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
-        const bool no_regs = in.op == OP_END || in.op == OP_JMP || in.op == OP_FAIL_FALLBACK;
+        const bool no_regs = in.op == OP_END || in.op == OP_JMP || in.op == OP_FAIL_FALLBACK || in.op == OP_ORD;
         if (!no_regs && (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))))
           throw std::runtime_error("internal: register out of range");
         if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
@@ -2030,7 +2030,8 @@ extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
                                 "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",
                                 "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK", "TABLE",
-                                "MEMO_GET", "MEMO_PUT"};
+                                "MEMO_GET", "MEMO_PUT", "ORD"};
+  static_assert(sizeof(names) / sizeof(names[0]) == OP_COUNT_, "opcode names");
   std::string s = "nregs=" + std::to_string(p.nregs) + " len=" + std::to_string(p.code_len) + "\n";
   for (uint32_t i = 0; i < p.code_len; ++i) {
     const Ins& in = e->bank.code[p.code_off + i];

@@ -122,7 +122,7 @@ FmtFlow fmt_flow(const Program& p, const CodeBank& bank) {
       case OP_MOV: put(s, in.a, has(s, in.b)); break;
       case OP_YIELD: if (has(s, in.b)) put(s, in.a, true); break;
       case OP_ITER_INIT: put(s, in.a, false); put(s, in.a + 1u, false); break;
-      case OP_EMIT: case OP_MEMO_PUT: break;
+      case OP_EMIT: case OP_MEMO_PUT: case OP_ORD: break;
       default: put(s, in.a, lazy_fmt(in)); break;
     }
     flow(next, s);
@@ -383,6 +383,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         break;
       }
       case OP_FAIL_FALLBACK: o << "lane_fallback(L, " << y << "); return;"; break;
+      case OP_ORD: o << "op_ord(L, " << y << ");"; break;
       default: o << "lane_fallback(L, FB_UNSUPPORTED); return;"; break;
     }
     o << "\n";

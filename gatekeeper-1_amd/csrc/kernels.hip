@@ -78,6 +78,7 @@ __device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t par
         break;
       }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
+      case OP_ORD: op_ord(L, in.y); break;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }

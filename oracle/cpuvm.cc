@@ -134,6 +134,7 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
         break;
       }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
+      case OP_ORD: op_ord(L, in.y); break;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
@@ -148,7 +149,7 @@ struct Counts {
 // bytes of every staged violation (the format pass's work)
 static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t fcap) {
   Lane L;
-  L.hp = 0; L.bp = 0; L.seq = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   const ReviewCol rc = gk_args.revs[rp];
   const MatchSpec m = gk_args.cons[c];

@@ -13,7 +13,7 @@ import gkgpu
 from gkgpu import workloads as W
 from gkgpu.client import Client, augmented_review
 
-from parity import Report, compare, oracle_for, run_objects
+from parity import Report, compare, oracle_for, oracle_review, run_objects
 
 pytestmark = pytest.mark.gpu
 
@@ -845,3 +845,38 @@ def test_template_with_libs_bats_container_limits():
     denied = {r.review for r in res.results}
     for i, p in enumerate(bats["pods"]):
         assert (i in denied) == p["denied"]
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_emission_order_is_topdown_order(monkeypatch, fuse):
+    """Within a (review, constraint) the engine's rows come in the order topdown
+    emits them: body by body of the partial set, each body in iteration order.
+    K8sContainerLimits' eight general_violation bodies share their first
+    expression, so the compiler fuses them into one pass over the containers
+    (GKGPU_FUSE, compiler.cc rule_group) and the OP_ORD keys restore the order
+    (devrt.h op_ord / flush_wave)."""
+    monkeypatch.setenv("GKGPU_FUSE", fuse)
+    ts, cs = W.config2()
+    t = [x for x in ts if x["spec"]["crd"]["spec"]["names"]["kind"] == "K8sContainerLimits"]
+    c = [x for x in cs if x["kind"] == "K8sContainerLimits"]
+    pods, ns_of, ns_objs = W.gen_pods(800, seed=515, n_namespaces=10)
+    pods.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
+                 "spec": {"containers": [{"name": "a", "image": "x"},
+                                         {"name": "b", "resources": {"limits": {"cpu": "9", "memory": "9Gi"}}},
+                                         {"name": "c", "resources": {"limits": {"cpu": "zz"}}}]}})
+    nss = [ns_objs[n] for n in ns_of] + [{"metadata": {"name": "default"}}]
+    drv = Driver()
+    rep, res = run_objects(drv, t, c, pods, nss)
+    _assert_clean(rep)
+    prog = drv.debug_disasm("K8sContainerLimits")
+    assert (" ORD " in prog) == (fuse == "1")
+    od = oracle_for(t, c)
+    got = [[] for _ in pods]
+    for r in res.results:
+        got[r.review].append(r.msg)
+    multi = 0
+    for i, (p, n) in enumerate(zip(pods, nss)):
+        want = [row[2] for row in oracle_review(od, augmented_review(p, n))]
+        assert got[i] == want, (i, got[i], want)
+        multi += len(want) > 1
+    assert multi > 100
