@@ -234,6 +234,17 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
     if (in.op == OP_MEMO_GET && ++memo_sites[in.y] == 2) memo2.insert(in.y);
     if (in.op == OP_MEMO_PUT && in.x == 1) gslots.insert(in.y);  // pure function: cross-lane memo
   }
+  // Register pressure: a memo slot's register entries (key, key, value, flag;
+  // two entries for slots with several call sites) stay live across the whole
+  // predicate.  Slots of pure functions also have the cross-lane memo (gm_get),
+  // which answers them from L2 without the registers: measured on config 2 (1M
+  // Pods, tools/gpu_r02h.sh) K8sContainerLimits 6.34 -> 5.02 ms without the
+  // register entries, 5.45 ms with one entry per slot.  GKGPU_JIT_LMEMO=1 keeps
+  // them (A/B); GKGPU_JIT_MEMO2=0 keeps one register entry per other slot.
+  if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) if (atoi(m2) == 0) memo2.clear();
+  std::set<uint32_t> lslots = memo;  // slots with register entries
+  const char* lm = getenv("GKGPU_JIT_LMEMO");
+  if (!lm || atoi(lm) == 0) for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
   FmtFlow F = fmt_flow(p, bank);
   Gen g;
   // literal re_match patterns compiled to code
@@ -265,7 +276,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   if (!p.nregs) o << "unused_";
   o << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)
-  for (uint32_t m : memo) {
+  for (uint32_t m : lslots) {
     o << "  uint64_t mk0_" << m << ", mk1_" << m << ", mv_" << m << "; bool mok_" << m << " = false;\n";
     if (memo2.count(m))
       o << "  uint64_t mkb0_" << m << ", mkb1_" << m << ", mvb_" << m << "; bool mokb_" << m << " = false;\n";
@@ -357,8 +368,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         // two entries per slot (most recent first): call sites of one function
         // with alternating arguments (canonify_mem(x) vs canonify_mem(max)) hit
         std::string m = std::to_string(in.y), k1 = in.c == 0xffff ? std::string("0ull") : c;
-        o << "if (mok_" << m << " && mk0_" << m << " == " << b << " && mk1_" << m << " == " << k1 << ") { " << a
-          << " = mv_" << m << "; goto " << x << "; }";
+        if (lslots.count(in.y))
+          o << "if (mok_" << m << " && mk0_" << m << " == " << b << " && mk1_" << m << " == " << k1 << ") { " << a
+            << " = mv_" << m << "; goto " << x << "; }";
         if (memo2.count(in.y))
           o << " if (mokb_" << m << " && mkb0_" << m << " == " << b << " && mkb1_" << m << " == " << k1 << ") { " << a
             << " = mvb_" << m << "; goto " << x << "; }";
@@ -367,12 +379,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       }
       case OP_MEMO_PUT: {
         std::string m = std::to_string(in.y), k1 = in.c == 0xffff ? std::string("0ull") : c;
-        o << "if (memo_stable(" << b << ") && memo_stable(" << k1 << ") && memo_stable(" << a << ")) { ";
-        if (memo2.count(in.y))
-          o << "mkb0_" << m << " = mk0_" << m << "; mkb1_" << m << " = mk1_" << m << "; mvb_" << m << " = mv_" << m
-            << "; mokb_" << m << " = mok_" << m << "; ";
-        o << "mk0_" << m << " = " << b << "; mk1_" << m << " = " << k1 << "; mv_" << m << " = " << a << "; mok_" << m
-          << " = true; }";
+        if (lslots.count(in.y)) {
+          o << "if (memo_stable(" << b << ") && memo_stable(" << k1 << ") && memo_stable(" << a << ")) { ";
+          if (memo2.count(in.y))
+            o << "mkb0_" << m << " = mk0_" << m << "; mkb1_" << m << " = mk1_" << m << "; mvb_" << m << " = mv_" << m
+              << "; mokb_" << m << " = mok_" << m << "; ";
+          o << "mk0_" << m << " = " << b << "; mk1_" << m << " = " << k1 << "; mv_" << m << " = " << a << "; mok_" << m
+            << " = true; }";
+        }
         if (gslots.count(in.y)) o << " gm_put(L, " << m << "u, " << b << ", " << k1 << ", " << a << ");";
         break;
       }
@@ -445,7 +459,10 @@ static std::string wpe_suffix() {
 
 static std::string inline_hot_tag() {
   const char* v = getenv("GKGPU_INLINE_HOT");
-  return (!v || atoi(v) != 0) ? "h1" : "h0";
+  std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
+  if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) t += std::string("m") + m2;
+  if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
+  return t;
 }
 
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
