@@ -75,9 +75,30 @@ class Comp {
   Program run(const std::vector<std::string>& pkg) {
     auto rules = mods_.rules(pkg, "violation");
     if (rules.empty()) throw Unsupported("template has no violation rule");
-    int rule_idx = 0;
-    for (auto& r : rules) {
-      int idx = rule_idx++;
+    const bool fuse_on = !getenv("GKGPU_FUSE") || atoi(getenv("GKGPU_FUSE")) != 0;  // A/B switch, default on
+    for (size_t ri = 0; ri < rules.size();) {
+      const auto& r = rules[ri];
+      // violation bodies sharing their first expression: one fused group
+      // (the OP_ORD keys keep topdown's rule-by-rule emission order)
+      size_t rj = ri + 1;
+      if (fuse_on && !guard_ && r->kind == Rule::PSET && !r->is_else)
+        while (rj < rules.size() && rules[rj]->kind == Rule::PSET && fusable(r, rules[rj], {}, {}, {})) ++rj;
+      if (rj - ri >= 2) {
+        int save = reg_top_;
+        for (size_t j = ri; j < rj; ++j) prog_.rules.push_back(rules[j]->name);
+        int Lg = label();
+        Env env;
+        env.mod = r->mod;
+        fuse_ok_ = false;  // groups do not nest
+        fused_bodies(rules, ri, rj, {}, &env, nullptr, Lg,
+                     [&](size_t j, Env* e2, int f) { emit_violation(rules[j], e2, (int)j, f); });
+        place(Lg);
+        emit(OP_ORD, 0, 0, 0, 0, 0x80000000u | (uint32_t)(rj - ri));
+        reg_top_ = save;
+        ri = rj;
+        continue;
+      }
+      const int idx = (int)ri;
       prog_.rules.push_back(r->name);
       const size_t code0 = code_.size(), labels0 = labels_.size();
       int save = reg_top_;
@@ -87,7 +108,7 @@ class Comp {
         Env env;
         env.mod = r->mod;
         const auto& body = cbody(r, {});
-        fuse_ok_ = !getenv("GKGPU_FUSE") || atoi(getenv("GKGPU_FUSE")) != 0;  // A/B switch, default on
+        fuse_ok_ = fuse_on;
         body_k(body, 0, &env, Lr, [&, idx](int f) { emit_violation(r, &env, idx, f); });
         fuse_ok_ = false;
         place(Lr);
@@ -104,6 +125,7 @@ class Comp {
         emit(OP_FAIL_FALLBACK, 0, 0, 0, 0, FB_TEMPLATE);
       }
       reg_top_ = save;
+      ++ri;
     }
     emit(OP_END);
     return finish();
@@ -638,8 +660,15 @@ class Comp {
       return;
     }
     if (sel->k == T_SCALAR) {
+      const uint64_t key = scalar_val(sel);
+      auto pc = path_cache_.find({r, key});
+      if (pc != path_cache_.end()) {  // looked up once per solution of a fused group's generator
+        emit_jmp(OP_JUNDEF, pc->second, fail);
+        walk(pc->second, path, i + 1, env, fail, k);
+        return;
+      }
       int v = alloc();
-      emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(scalar_val(sel)));
+      emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(key));
       emit_jmp(OP_JUNDEF, v, fail);
       walk(v, path, i + 1, env, fail, k);
       return;
@@ -794,6 +823,74 @@ class Comp {
     return ba[0]->kind != Expr::SOME && same_expr(ba[0], bb[0]);
   }
 
+  // Shared lookups of a fused group: constant-key paths below the generator's
+  // variable (`container.resources.limits`, `container.name`) that two or more
+  // of the group's bodies read are looked up once per solution, in the group's
+  // prologue, and walk() reads them from registers (keyed by (base register,
+  // key), so a shadowing variable never hits).  A lookup is total and pure
+  // (vget of a missing member or of a scalar is undefined), so evaluating it
+  // ahead of the bodies changes nothing but the count of lookups.
+  std::map<std::pair<int, uint64_t>, int> path_cache_;
+
+  void collect_paths(const TermP& t, const std::string& var, std::vector<std::vector<TermP>>& out) {
+    if (!t) return;
+    if (t->k == T_REF && t->head && t->head->k == T_VAR && t->head->s == var) {
+      std::vector<TermP> keys;
+      for (auto& it : t->items) {
+        if (it->k != T_SCALAR) break;
+        keys.push_back(it);
+      }
+      if (!keys.empty()) out.push_back(keys);
+    }
+    collect_paths(t->head, var, out);
+    collect_paths(t->key, var, out);
+    collect_paths(t->value, var, out);
+    for (auto& it : t->items) collect_paths(it, var, out);
+    for (auto& e : t->body)
+      for (auto& x : e->terms) collect_paths(x, var, out);
+  }
+
+  // prologue of a fused group: the shared paths under each variable the
+  // generator bound (registers allocated here stay live for the bodies)
+  void group_prologue(const std::vector<std::shared_ptr<Rule>>& rules, size_t lo, size_t hi,
+                      const std::vector<std::string>& safe, const Env& renv, const Env* outer) {
+    if (getenv("GKGPU_FUSE_CSE") && atoi(getenv("GKGPU_FUSE_CSE")) == 0) return;  // A/B switch, default on
+    for (auto& vr : renv.vars) {
+      if (outer && outer->lookup(vr.first) == vr.second) continue;  // bound before the generator
+      std::map<std::vector<std::string>, std::set<size_t>> users;
+      std::map<std::vector<std::string>, std::vector<TermP>> terms;
+      for (size_t j = lo; j < hi; ++j) {
+        const auto& body = cbody(rules[j], safe);
+        std::vector<std::vector<TermP>> refs;
+        for (size_t x = 1; x < body.size(); ++x)
+          for (auto& t : body[x]->terms) collect_paths(t, vr.first, refs);
+        for (auto& keys : refs)
+          for (size_t n = 1; n <= keys.size(); ++n) {
+            std::vector<std::string> sig;
+            for (size_t q = 0; q < n; ++q) sig.push_back(std::to_string(keys[q]->stype) + ":" + keys[q]->s);
+            users[sig].insert(j);
+            terms[sig] = std::vector<TermP>(keys.begin(), keys.begin() + n);
+          }
+      }
+      std::map<std::vector<std::string>, int> reg_of;  // ordered: a prefix precedes its extensions
+      for (auto& u : users) {
+        if (u.second.size() < 2 || reg_of.size() >= 12) continue;
+        const auto& keys = terms[u.first];
+        int base = vr.second;
+        if (keys.size() > 1) {
+          auto pit = reg_of.find(std::vector<std::string>(u.first.begin(), u.first.end() - 1));
+          if (pit == reg_of.end()) continue;
+          base = pit->second;
+        }
+        const uint64_t key = scalar_val(keys.back());
+        int v = alloc();
+        emit(OP_GETK, (uint16_t)v, (uint16_t)base, 0, kconst(key));
+        reg_of[u.first] = v;
+        path_cache_[{base, key}] = v;
+      }
+    }
+  }
+
   using HeadK = std::function<void(const std::shared_ptr<Rule>&, Env*, int)>;
   void rule_group(const std::vector<std::shared_ptr<Rule>>& rules, size_t lo, size_t hi,
                   const std::vector<std::pair<std::string, TermP>>& pre_terms, const std::vector<std::string>& safe,
@@ -803,29 +900,40 @@ class Comp {
     int Lg = label();
     Env renv;
     renv.mod = rules[lo]->mod;
-    const auto& first = cbody(rules[lo], safe);
     prebind(pre_terms, 0, env, &renv, Lg, [&](int f) {
-      expr(first[0], &renv, f, [&](int fnext) {
-        const int save2 = reg_top_;
-        for (size_t j = lo; j < hi; ++j) {
-          const auto& r = rules[j];
-          const auto& body = cbody(r, safe);
-          int Ln = label();
-          emit(OP_ORD, 0, 0, 0, 0, (uint32_t)(j - lo));
-          Env e2;
-          e2.mod = r->mod;
-          e2.parent = renv.parent;
-          e2.vars = renv.vars;
-          body_k(body, 1, &e2, Ln, [&](int f2) { head_k(r, &e2, f2); });
-          place(Ln);
-          reg_top_ = save2;
-        }
-        emit_jmp(OP_JMP, 0, fnext);
-      });
+      fused_bodies(rules, lo, hi, safe, &renv, env, f, [&](size_t j, Env* e2, int f2) { head_k(rules[j], e2, f2); });
     });
     place(Lg);
     emit(OP_ORD, 0, 0, 0, 0, 0x80000000u | (uint32_t)(hi - lo));
     reg_top_ = save;
+  }
+
+  // the shared first expression of rules [lo, hi), then per solution the rest
+  // of each body in turn (OP_ORD key j - lo), each ending in tail(j, env, fail)
+  void fused_bodies(const std::vector<std::shared_ptr<Rule>>& rules, size_t lo, size_t hi,
+                    const std::vector<std::string>& safe, Env* renv, const Env* outer, int fail,
+                    const std::function<void(size_t, Env*, int)>& tail) {
+    const auto& first = cbody(rules[lo], safe);
+    expr(first[0], renv, fail, [&](int fnext) {
+      auto saved_cache = path_cache_;
+      group_prologue(rules, lo, hi, safe, *renv, outer);
+      const int save2 = reg_top_;
+      for (size_t j = lo; j < hi; ++j) {
+        const auto& r = rules[j];
+        const auto& body = cbody(r, safe);
+        int Ln = label();
+        emit(OP_ORD, 0, 0, 0, 0, (uint32_t)(j - lo));
+        Env e2;
+        e2.mod = r->mod;
+        e2.parent = renv->parent;
+        e2.vars = renv->vars;
+        body_k(body, 1, &e2, Ln, [&, j](int f2) { tail(j, &e2, f2); });
+        place(Ln);
+        reg_top_ = save2;
+      }
+      path_cache_ = saved_cache;
+      emit_jmp(OP_JMP, 0, fnext);
+    });
   }
 
   // both object literals with scalar keys, the same key set, no duplicates

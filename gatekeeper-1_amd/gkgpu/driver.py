@@ -68,6 +68,23 @@ def lib_path() -> str:
     return os.environ.get("GKGPU_LIB", os.path.join(_HERE, "libgkgpu.so"))
 
 
+def _one_hip_runtime():
+    """PyTorch-ROCm bundles its own HIP runtime, loaded under the file name
+    libamdhip64.so; the engine links libamdhip64.so.7 from /opt/rocm.  Loaded
+    engine-first, a process later importing torch gets a second HIP/HSA
+    runtime, and torch then sees no GPU ("No HIP GPUs are available").  Loaded
+    torch-first, the engine's NEEDED libamdhip64.so.7 matches the SONAME torch
+    already loaded and there is one runtime.  The engine hands device buffers to
+    torch tensors (DeviceOutput, the RCCL exchange), so torch goes first when it
+    is installed (GKGPU_NO_TORCH=1 skips it)."""
+    if os.environ.get("GKGPU_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def load_library():
     global _LIB
     if _LIB is not None:
@@ -75,6 +92,7 @@ def load_library():
     p = lib_path()
     if not os.path.exists(p):
         raise EngineUnavailable("libgkgpu.so not built (%s); run __graft_entry__.build()" % p)
+    _one_hip_runtime()
     lib = C.CDLL(p)
     vp = C.c_void_p
     sz = C.c_size_t

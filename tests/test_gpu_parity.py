@@ -859,6 +859,13 @@ def test_emission_order_is_topdown_order(monkeypatch, fuse):
     ts, cs = W.config2()
     t = [x for x in ts if x["spec"]["crd"]["spec"]["names"]["kind"] == "K8sContainerLimits"]
     c = [x for x in cs if x["kind"] == "K8sContainerLimits"]
+    _check_emission_order(t, c, fuse)
+    # the bats template: eight top-level violation bodies (fused in run())
+    bats = json.load(open(os.path.join(HERE, "golden", "bats_fixtures.json")))
+    _check_emission_order([bats["template"]], [bats["constraint"]], fuse)
+
+
+def _check_emission_order(t, c, fuse):
     pods, ns_of, ns_objs = W.gen_pods(800, seed=515, n_namespaces=10)
     pods.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
                  "spec": {"containers": [{"name": "a", "image": "x"},
