@@ -194,6 +194,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1000.0
+    # the core clock this box ran at, right after the timed region (box-to-box
+    # variance of kernel times tracks it: DESIGN.md section 5)
+    try:
+        sclk_mhz = round(drv.debug_clock_mhz(), 1)
+    except Exception:
+        sclk_mhz = None
     evals_per_step = nrev * n_cons * world
     value = evals_per_step / (ms_per_step / 1000.0)
     # end to end: a cold sweep = flatten + H2D of the shard + one sweep (the
@@ -303,6 +309,7 @@ def main():
                 "backends": {k: {0: "cpu-fallback", 1: "bytecode-vm", 2: "template-kernel", 3: "guard-kernel+cpu-fallback"}[drv.template_backend(k)[0]]
                              for k in kinds},
                 "kernel_templates": kinds_of,
+                "sclk_mhz_measured": sclk_mhz,
                 "stage_s": round(t_stage, 3),
                 "stage_s_max_over_ranks": round(t_stage_max, 3),
                 "stage_ms": {"parse": round(stage_ms[0], 1), "flatten": round(stage_ms[1], 1),

@@ -33,6 +33,7 @@ extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflag
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
                                 unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
                                 unsigned int* ncand, int select_only, hipStream_t stream);
+extern "C" int gk_launch_clock_probe(unsigned long long* out, uint32_t iters, hipStream_t stream);
 extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflags, const uint8_t* cerr,
                                 gk::Viol* dst, unsigned long long* count, hipStream_t stream);
 
@@ -1920,6 +1921,25 @@ extern "C" int gk_debug_stage_inputs(gk_engine* e, const char* const* inputs, co
 // last one staged and the engine is unchanged.  Used only by the CPU baseline
 // (oracle/cpuvm.cc), which runs the same bytecode on host threads; `out` must
 // be a gk::DevArgs (checked by size).
+// The shader clock (MHz) a spinning wavefront sees on the engine's device:
+// s_memtime ticks over s_memrealtime's 100 MHz reference (kernels.hip
+// gk_clock_probe).  Diagnostics for box-to-box variance of kernel times.
+extern "C" int gk_debug_clock_mhz(gk_engine* e, double* mhz) {
+  if (!e || !mhz) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
+  unsigned long long* d = nullptr;
+  unsigned long long h[3] = {0, 0, 0};
+  if (hipMalloc(&d, sizeof h) != hipSuccess) return fail(e, GK_EDEVICE, "device allocation failed");
+  int lr = gk_launch_clock_probe(d, 1u << 22, e->stream);
+  bool ok = lr == 0 && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+            hipStreamSynchronize(e->stream) == hipSuccess;
+  hipFree(d);
+  if (!ok || h[1] == 0) return fail(e, GK_EDEVICE, "clock probe failed");
+  *mhz = 100.0 * (double)h[0] / (double)h[1];
+  return GK_OK;
+}
+
 extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, size_t out_size) {
   if (!e || !b || !out || out_size != sizeof(DevArgs)) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);

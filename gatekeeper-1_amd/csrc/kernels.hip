@@ -332,6 +332,32 @@ __global__ void __launch_bounds__(256) gk_filter_viol(const Viol* out, uint64_t 
 
 }  // namespace gk
 
+namespace gk {
+
+// Clock probe: one wavefront spins on dependent integer ops while reading the
+// shader-clock counter (s_memtime) and the fixed 100 MHz reference counter
+// (s_memrealtime); their ratio is the core clock the kernels actually ran at
+// (box-to-box variance: MI355X boxes in a low-power state run the same code
+// objects at a fraction of the clock).  Results are written by a vector store.
+__global__ void __launch_bounds__(64) gk_clock_probe(unsigned long long* out, uint32_t iters) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t x = threadIdx.x;
+  for (uint32_t i = 0; i < iters; ++i) x = x * 1664525u + 1013904223u;
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[0] = t1 - t0;
+    out[1] = r1 - r0;
+    out[2] = x;
+  }
+}
+
+}  // namespace gk
+
+extern "C" int gk_launch_clock_probe(unsigned long long* out, uint32_t iters, hipStream_t stream) {
+  hipLaunchKernelGGL(gk::gk_clock_probe, dim3(1), dim3(64), 0, stream, out, iters);
+  return (int)hipGetLastError();
+}
+
 extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflags, const uint8_t* cerr,
                                 gk::Viol* dst, unsigned long long* count, hipStream_t stream) {
   uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);

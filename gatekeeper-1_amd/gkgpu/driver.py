@@ -612,6 +612,14 @@ class Driver:
         return Batch(self, out, len(o))
 
     # -- introspection
+    def debug_clock_mhz(self) -> float:
+        """the shader clock (MHz) a spinning wavefront measures on this device
+        (s_memtime over the 100 MHz s_memrealtime reference)"""
+        v = C.c_double()
+        self._lib.gk_debug_clock_mhz.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        self._check(self._lib.gk_debug_clock_mhz(self._e, C.byref(v)))
+        return v.value
+
     def debug_disasm(self, kind: str) -> str:
         """bytecode listing of a compiled template (diagnostics; with GKGPU_PROFILE=2
         the first column is the last launch's per-instruction execution count)"""
