@@ -120,6 +120,7 @@ class Comp {
         code_.resize(code0);
         labels_.resize(labels0);
         loop_base_.clear();
+        loop_var_lo_.clear();
         if (prog_.fallback_reason.empty()) prog_.fallback_reason = ex.what();
         ++prog_.fallback_sites;
         emit(OP_FAIL_FALLBACK, 0, 0, 0, 0, FB_TEMPLATE);
@@ -169,8 +170,10 @@ class Comp {
     if (loop_base_.size() >= 15) throw Unsupported("loop nesting too deep");
     emit(OP_ITER_INIT, (uint16_t)it, (uint16_t)coll, 0, 0, (uint32_t)loop_base_.size() + 1);
     loop_base_.push_back(reg_top_);
+    loop_var_lo_.push_back(it + 2);  // the key / value registers (allocated right after the iterator's)
   }
-  void close_loop() { loop_base_.pop_back(); }
+  void close_loop() { loop_base_.pop_back(); loop_var_lo_.pop_back(); }
+  std::vector<int> loop_var_lo_;  // per open loop: its lowest register written per iteration
   int depth() const { return (int)loop_base_.size(); }
   std::map<std::pair<const Rule*, std::string>, std::vector<ExprP>> cbody_cache_;
 
@@ -374,6 +377,7 @@ class Comp {
       code_.resize(code0);
       labels_.resize(labels0);
       loop_base_.resize(loops0);
+      loop_var_lo_.resize(loops0);
       reg_top_ = reg0;
       inline_depth_ = depth0;
       stmt_key_ = key0;
@@ -1124,7 +1128,17 @@ class Comp {
           emit(OP_TABLE, (uint16_t)out, (uint16_t)regs[0], 0, (uint32_t)tab);
         } else {
           out = loadk(tag_val(V_UNDEF, 0));
-          int slot = nargs >= 1 && nargs <= 2 ? memo_slot(rules, stmt && !has_out) : -1;
+          // A call whose argument is computed inside the innermost loop (the
+          // loop's element, a path below it) meets new arguments every
+          // iteration; an impure function's lane memo would only cost
+          // registers there.  Pure functions keep theirs: the cross-lane memo
+          // serves other lanes.  GKGPU_MEMO_LOOPVAR=1 memoizes them anyway (A/B).
+          bool varying = false;
+          if (!loop_var_lo_.empty())
+            for (int r : regs) varying |= r >= loop_var_lo_.back() && r < kVReg;
+          static const bool memo_loopvar = getenv("GKGPU_MEMO_LOOPVAR") && atoi(getenv("GKGPU_MEMO_LOOPVAR")) != 0;
+          bool skip = varying && !memo_loopvar && !pure_func(rules);
+          int slot = nargs >= 1 && nargs <= 2 && !skip ? memo_slot(rules, stmt && !has_out) : -1;
           int Lhit = label();
           uint16_t k1 = nargs == 2 ? (uint16_t)regs[1] : NOREG;
           if (slot >= 0) emit(OP_MEMO_GET, (uint16_t)out, (uint16_t)regs[0], k1, (uint32_t)Lhit, (uint32_t)slot);

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Clock probe + K8sRequiredProbes cost breakdown by template variants.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r02k
+export GKGPU_JIT_CACHE=$PWD/.jitcache
+timeout -k 10 240 python -u tools/probe_repeat.py 1000000 > gpurun_out/r02k/all.log 2>&1 || { tail -5 gpurun_out/r02k/all.log; exit 1; }
+tail -2 gpurun_out/r02k/all.log
+timeout -k 10 600 python -u tools/probe_variants_rp.py 1000000 > gpurun_out/r02k/rp_variants.log 2>&1 || { tail -5 gpurun_out/r02k/rp_variants.log; exit 1; }
+cat gpurun_out/r02k/rp_variants.log
