@@ -310,6 +310,7 @@ def main():
                              for k in kinds},
                 "kernel_templates": kinds_of,
                 "sclk_mhz_measured": sclk_mhz,
+                "device": device_info(local),
                 "stage_s": round(t_stage, 3),
                 "stage_s_max_over_ranks": round(t_stage_max, 3),
                 "stage_ms": {"parse": round(stage_ms[0], 1), "flatten": round(stage_ms[1], 1),
@@ -364,6 +365,17 @@ def referenced_bytes(drv, batch, kind, cons_ids, threads):
             tot[f] += r[f]
         tot["constraints"].append(name)
     return tot
+
+
+def device_info(dev):
+    """the GPU the bench ran on: CU count (partition mode), memory, L2"""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(dev)
+        return {"name": p.name, "arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+                "memory_gib": round(p.total_memory / 2**30, 1), "l2_bytes": getattr(p, "L2_cache_size", None)}
+    except Exception:
+        return None
 
 
 def cpu_model():

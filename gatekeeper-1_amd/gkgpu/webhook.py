@@ -14,14 +14,24 @@ Mirrors pkg/webhook/policy.go for the part that reaches the policy engine:
   500 on a Query error).  Requests the engine flags for fallback are returned
   as such: the caller re-runs them on the CPU driver.
 
-The service-account bypass, DELETE handling of oldObject and the Gatekeeper
-self-validation steps of Handle run before the engine and are out of scope.
+* ``handle_requests``  — Handle's steps ahead of the engine for raw
+  AdmissionRequests: the Gatekeeper service-account bypass (policy.go:147-149,
+  304-306), DELETE reviewing oldObject (:151-166), the webhook process
+  excluder (:192-196, 425-427) and the Namespace fetch of reviewRequest
+  (:372-383: the cached client first, the API reader on NotFound, any other
+  error fails the request with 500), then one ``handle_batch`` launch for the
+  requests that reach the engine.
+
+Validation of Gatekeeper's own resources (validateGatekeeperResources,
+:168-179: ConstraintTemplate / constraint admission) is the control plane's and
+out of scope.
 """
 from __future__ import annotations
 
 import json
+import os
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 from .driver import GK_REVIEW_ERROR, GK_REVIEW_FALLBACK, TARGET
 
@@ -88,3 +98,71 @@ def handle_batch(driver, inputs: Sequence) -> List[Response]:
     for r in res.results:
         per[r.review].append(r)
     return [respond(res.status[i], per[i]) for i in range(len(inputs))]
+
+
+# -- Handle's steps ahead of the engine (policy.go:142-223, 363-400) --------------
+
+class NotFound(Exception):
+    """k8serrors.IsNotFound for a Namespace Get."""
+
+
+class NamespaceFetcher:
+    """reviewRequest's Namespace lookup (policy.go:372-383): the cached client
+    (h.client.Get) first; only on NotFound the API reader (h.reader.Get, which
+    bypasses the cache); any other error, or the reader's error, fails the
+    request.  `cache_get(name)` / `reader_get(name)` return the Namespace
+    object or raise (NotFound for a missing one)."""
+
+    def __init__(self, cache_get: Callable[[str], dict], reader_get: Callable[[str], dict]):
+        self.cache_get = cache_get
+        self.reader_get = reader_get
+
+    def get(self, name: str) -> dict:
+        try:
+            return self.cache_get(name)
+        except NotFound:
+            return self.reader_get(name)
+
+
+def gk_service_account() -> str:
+    """serviceaccount (policy.go:67, 77): system:serviceaccount:<POD_NAMESPACE,
+    default gatekeeper-system (pkg/util/pod_info.go:15-21)>:gatekeeper-admin"""
+    return "system:serviceaccount:%s:gatekeeper-admin" % os.environ.get("POD_NAMESPACE", "gatekeeper-system")
+
+
+def handle_requests(driver, requests: Sequence[dict], fetcher: NamespaceFetcher) -> List[Response]:
+    """Handle (policy.go:142-223) for a micro-batch of AdmissionRequests (dicts
+    in admission/v1beta1 JSON form): the host steps per request, then one
+    engine launch for every request that reaches reviewRequest's Review."""
+    out: List[Optional[Response]] = [None] * len(requests)
+    inputs, where = [], []
+    for i, req in enumerate(requests):
+        user = (req.get("userInfo") or {}).get("username", "")
+        if user == gk_service_account():
+            out[i] = Response(True, ALLOWED, "Gatekeeper does not self-manage")
+            continue
+        if req.get("operation") == "DELETE":
+            if req.get("oldObject") is None:
+                out[i] = Response(False, ERROR, "For admission webhooks registered for DELETE operations, "
+                                                 "please use Kubernetes v1.15.0+.")
+                continue
+            req = dict(req)
+            req["object"] = req["oldObject"]
+        if driver.is_namespace_excluded("webhook", req.get("namespace", "") or ""):
+            out[i] = Response(True, ALLOWED, "Namespace is set to be ignored by Gatekeeper config")
+            continue
+        kind = req.get("kind") or {}
+        ns_name = "" if (kind.get("kind") == "Namespace" and kind.get("group", "") == "") else (req.get("namespace") or "")
+        ns = None
+        if ns_name:
+            try:
+                ns = fetcher.get(ns_name)
+            except Exception as err:  # reviewRequest's error: Handle answers 500 with its text
+                out[i] = Response(False, ERROR, str(err))
+                continue
+        inputs.append(review_input(req, ns))
+        where.append(i)
+    if inputs:
+        for i, r in zip(where, handle_batch(driver, inputs)):
+            out[i] = r
+    return out

@@ -28,4 +28,6 @@ for i in range(12):
     r = b.eval(decode=False, light=True)
     wall = (time.perf_counter() - t0) * 1e3
     print("step %2d wall %.2f ms" % (i, wall), [(k, round(ms, 2)) for k, ms, n in r.launches], "tuples", r.device_tuples, "flagged", r.n_fallbacks + r.n_errors, flush=True)
-print("sclk_mhz %.1f" % d.debug_clock_mhz(), flush=True)
+import torch  # noqa: E402
+_p = torch.cuda.get_device_properties(0)
+print("sclk_mhz %.1f cus %d" % (d.debug_clock_mhz(), _p.multi_processor_count), flush=True)

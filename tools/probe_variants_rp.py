@@ -24,17 +24,30 @@ CONST_MSG = VIOL.replace("msg := get_violation_message(container, input.review, 
 EMPTY_ALT = ('probe_field_empty(ctr, probe) = true {\n\tcount(ctr[probe]) == 0\n}\n\n' +
              REST[REST.index("get_violation_message"):])
 
+INLINE_MSG = VIOL.replace("msg := get_violation_message(container, input.review, probe)",
+                          'msg := sprintf("Container <%v> in your <%v> <%v> has no <%v>", '
+                          '[container.name, input.review.kind.kind, input.review.object.metadata.name, probe])')
+ONE_ARG = VIOL.replace("msg := get_violation_message(container, input.review, probe)",
+                       'msg := sprintf("Container <%v> has no probe", [container.name])')
+CONST_ARGS = VIOL.replace("msg := get_violation_message(container, input.review, probe)",
+                          'msg := sprintf("Container <%v> in your <%v> <%v> has no <%v>", ["a", "b", "c", "d"])')
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 variants = {
     "full": src,
     "const_msg": HEAD + CONST_MSG + MISSING1 + MISSING2 + REST,
     "missing_only": HEAD + VIOL + MISSING1 + REST,
     "missing_only_const_msg": HEAD + CONST_MSG + MISSING1 + REST,
     "empty_by_count": HEAD + VIOL + MISSING1 + MISSING2 + EMPTY_ALT,
+    "inline_msg": HEAD + INLINE_MSG + MISSING1 + MISSING2 + REST,
+    "one_arg_msg": HEAD + ONE_ARG + MISSING1 + MISSING2 + REST,
+    "const_args_msg": HEAD + CONST_ARGS + MISSING1 + MISSING2 + REST,
     "loops_only": HEAD + ('violation[{"msg": msg}] {\n\tcontainer := input.review.object.spec.containers[_]\n'
                           '\tprobe := input.parameters.probes[_]\n\tcontainer.name == "zz-never"\n\tmsg := "x"\n}\n'),
 }
 objs, nss = W.gen_pods_json(N, seed=42, n_namespaces=1000)
 for name, rego in variants.items():
+    if only and name not in only:
+        continue
     t = dict(rp_t)
     t["spec"] = dict(rp_t["spec"])
     t["spec"]["targets"] = [dict(rp_t["spec"]["targets"][0], rego=rego)]
