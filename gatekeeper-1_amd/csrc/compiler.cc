@@ -152,6 +152,22 @@ class Comp {
   std::map<const Rule*, std::pair<int, int>> crule_;
   int inline_depth_ = 0;
   std::map<std::pair<const void*, bool>, int> memo_;  // memo slot per (function, statement form)
+  // Lane constants (registers numbered from kLReg while compiling, renumbered
+  // by finish()): the input roots, loaded at entry, and constant-key paths
+  // below them, each with a "looked up" flag cleared at entry.
+  static constexpr int kLReg = 11000, kMaxLaneRegs = 40;
+  int lreg_n_ = 0, rev_reg_ = -1, par_reg_ = -1;
+  std::map<std::pair<int, uint64_t>, std::pair<int, int>> lpath_;  // (base, key) -> (value, flag)
+  bool lane_const(int r) const { return r >= kLReg && r < kLReg + lreg_n_; }
+  static bool lane_paths_on() {
+    static const bool on = !getenv("GKGPU_LANE_PATHS") || atoi(getenv("GKGPU_LANE_PATHS")) != 0;  // A/B
+    return on;
+  }
+  int input_root(bool review) {
+    int& r = review ? rev_reg_ : par_reg_;
+    if (r < 0) r = kLReg + lreg_n_++;
+    return r;
+  }
   std::vector<int> loop_base_;  // register base of each enclosing ITER loop (innermost last)
   Program prog_;
 
@@ -206,16 +222,26 @@ class Comp {
   }
 
   Program finish() {
-    if (!crule_.empty()) {
-      const int base = max_reg_;
-      auto remap = [&](uint16_t& r) { if (r != NOREG && r >= kVReg) r = (uint16_t)(base + (r - kVReg)); };
+    if (!crule_.empty() || lreg_n_) {
+      const int base = max_reg_, lbase = base + 2 * (int)crule_.size();
+      auto map = [&](int r) {
+        if (r >= kLReg) return lbase + (r - kLReg);
+        if (r >= kVReg) return base + (r - kVReg);
+        return r;
+      };
+      auto remap = [&](uint16_t& r) { if (r != NOREG) r = (uint16_t)map(r); };
       for (auto& in : code_) { remap(in.a); remap(in.b); remap(in.c); }
       std::vector<Ins> pro;
       uint32_t kf = kconst(tag_val(V_BOOL, 0));
-      for (auto& cr : crule_) pro.push_back(Ins{OP_LOADK, (uint16_t)(base + (cr.second.second - kVReg)), 0, 0, kf, 0});
+      for (auto& cr : crule_) pro.push_back(Ins{OP_LOADK, (uint16_t)map(cr.second.second), 0, 0, kf, 0});
+      // lane constants: the review and parameters roots, and the "looked up"
+      // flags of the cached paths below them
+      if (rev_reg_ >= 0) pro.push_back(Ins{OP_LOADREV, (uint16_t)map(rev_reg_), 0, 0, 0, 0});
+      if (par_reg_ >= 0) pro.push_back(Ins{OP_LOADPARAM, (uint16_t)map(par_reg_), 0, 0, 0, 0});
+      for (auto& lp : lpath_) pro.push_back(Ins{OP_LOADK, (uint16_t)map(lp.second.second), 0, 0, kf, 0});
       code_.insert(code_.begin(), pro.begin(), pro.end());
       for (auto& l : labels_) if (l >= 0) l += (int)pro.size();
-      max_reg_ = base + 2 * (int)crule_.size();
+      max_reg_ = lbase + lreg_n_;
     }
     prog_.code_off = (uint32_t)bank_.code.size();
     prog_.code_len = (uint32_t)code_.size();
@@ -607,11 +633,9 @@ class Comp {
       const TermP& p0 = path[0];
       if (p0->k != T_SCALAR || p0->stype != S_STR) throw Unsupported("dynamic input key");
       std::vector<TermP> rest(path.begin() + 1, path.end());
-      int rr = alloc();
-      if (p0->s == "review") emit(OP_LOADREV, (uint16_t)rr);
-      else if (p0->s == "parameters") emit(OP_LOADPARAM, (uint16_t)rr);
-      else { emit_jmp(OP_JMP, 0, fail); return; }  // input.<other> is undefined
-      walk(rr, rest, 0, env, fail, k);
+      if (p0->s != "review" && p0->s != "parameters") { emit_jmp(OP_JMP, 0, fail); return; }  // input.<other> is undefined
+      // the lane's input roots are loaded once, at program entry
+      walk(input_root(p0->s == "review"), rest, 0, env, fail, k);
       return;
     }
     if (head->s == "data") { data_ref(path, env, fail, k); return; }
@@ -665,6 +689,28 @@ class Comp {
     }
     if (sel->k == T_SCALAR) {
       const uint64_t key = scalar_val(sel);
+      if (lane_const(r) && lane_paths_on()) {
+        // a path below the lane's input is the same for the whole lane: looked
+        // up at its first use, then read from its register (input.review.kind,
+        // input.parameters.cpu, ... re-read per container otherwise)
+        auto lp = lpath_.find({r, key});
+        if (lp == lpath_.end() && lreg_n_ + 2 <= kMaxLaneRegs) {
+          int v = kLReg + lreg_n_++, d = kLReg + lreg_n_++;
+          lp = lpath_.emplace(std::make_pair(r, key), std::make_pair(v, d)).first;
+        }
+        if (lp != lpath_.end()) {
+          const int v = lp->second.first, d = lp->second.second;
+          int Lhave = label();
+          emit_jmp(OP_JTRUE, d, Lhave);
+          emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(key));
+          int t = loadk(tag_val(V_BOOL, 1));
+          emit(OP_MOV, (uint16_t)d, (uint16_t)t);
+          place(Lhave);
+          emit_jmp(OP_JUNDEF, v, fail);
+          walk(v, path, i + 1, env, fail, k);
+          return;
+        }
+      }
       auto pc = path_cache_.find({r, key});
       if (pc != path_cache_.end()) {  // looked up once per solution of a fused group's generator
         emit_jmp(OP_JUNDEF, pc->second, fail);

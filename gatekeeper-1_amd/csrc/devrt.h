@@ -60,6 +60,11 @@ namespace gk {
 #define GK_BCAP 4096
 #endif
 constexpr int HCAP = GK_HCAP;  // heap words per lane (lists, big floats)
+#ifndef GK_LDS_HWORDS
+#define GK_LDS_HWORDS 0
+#endif
+#define GK_LDS_HWORDS_DEF GK_LDS_HWORDS
+static_assert(GK_LDS_HWORDS < GK_HCAP, "LDS heap words must leave a private-segment tail");
 constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
 constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged messages)
 #ifndef GK_EMCAP
@@ -94,7 +99,7 @@ __device__ __forceinline__ bool is_strv(uint64_t v) { uint32_t t = vtag(v); retu
 __device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); return t == V_NUM || t == V_INT || t == V_BFN; }
 
 struct Lane {
-  uint64_t H[HCAP];
+  uint64_t H[HCAP - GK_LDS_HWORDS_DEF];  // heap words GK_LDS_HWORDS_DEF.. (the first ones are in LDS)
   char B[BCAP];
   uint32_t hp, bp, fail;  // fail: 0 ok, RF_ERROR, RF_FALLBACK
   // emission order key (OP_ORD, fused rule bodies): emissions are numbered by
@@ -120,6 +125,27 @@ struct Lane {
 #define GK_PRIV
 #endif
 typedef GK_PRIV Lane PLane;
+
+// The first GK_LDS_HWORDS words of each lane's heap live in LDS (template and
+// VM kernels; 0 = all in the private segment, as in the CPU build).  Lists and
+// big floats are allocated by bumping L.hp and reclaimed per loop iteration,
+// so the hot words are the low ones: list headers and the short argument lists
+// sprintf and the set builtins build per container.  Layout: word w of thread t
+// at gk_lds_heap[w][t], so a wavefront's access to one word touches 64
+// consecutive 8-byte slots (no bank conflicts).  256 threads per block.
+#if GK_LDS_HWORDS_DEF > 0
+__shared__ uint64_t gk_lds_heap[GK_LDS_HWORDS_DEF][256];
+__device__ __forceinline__ uint64_t hget(const PLane& L, uint32_t w) {
+  return w < GK_LDS_HWORDS_DEF ? gk_lds_heap[w][threadIdx.x] : L.H[w - GK_LDS_HWORDS_DEF];
+}
+__device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) {
+  if (w < GK_LDS_HWORDS_DEF) gk_lds_heap[w][threadIdx.x] = v;
+  else L.H[w - GK_LDS_HWORDS_DEF] = v;
+}
+#else
+__device__ __forceinline__ uint64_t hget(const PLane& L, uint32_t w) { return L.H[w]; }
+__device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) { L.H[w] = v; }
+#endif
 
 // a heap-resident value (must survive a loop's per-iteration heap reset when it
 // escapes to a register that outlives the iteration)
@@ -215,8 +241,8 @@ __device__ bool num_bf(const PLane& L, uint64_t v, BF& out) {
   }
   if (t == V_BFN) {
     uint32_t o = (uint32_t)vpay(v);
-    out.m = L.H[o];
-    uint64_t w = L.H[o + 1];
+    out.m = hget(L, o);
+    uint64_t w = hget(L, o + 1);
     out.e = (int32_t)(uint32_t)w;
     out.neg = (w >> 32) & 1;
     out.zero = out.m == 0;
@@ -270,8 +296,8 @@ __device__ uint64_t heap_bf(PLane& L, const BF& b) {
   if (L.hp + 2 > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
   uint32_t o = L.hp;
   L.hp += 2;
-  L.H[o] = b.zero ? 0 : b.m;
-  L.H[o + 1] = (uint64_t)(uint32_t)b.e | ((uint64_t)(b.neg ? 1 : 0) << 32);
+  hset(L, o, b.zero ? 0 : b.m);
+  hset(L, o + 1, (uint64_t)(uint32_t)b.e | ((uint64_t)(b.neg ? 1 : 0) << 32));
   return mkv(V_BFN, o);
 }
 // big.Float Mul at prec 64, ToNearestEven
@@ -300,14 +326,14 @@ __device__ BF bf_mul(const BF& a, const BF& b) {
 }
 
 // ------------------------------------------------------------------ lists
-__device__ __forceinline__ uint32_t list_len(const PLane& L, uint64_t v) { return (uint32_t)L.H[list_off(v)]; }
-__device__ __forceinline__ uint64_t list_at(const PLane& L, uint64_t v, uint32_t i) { return L.H[list_off(v) + 2 + i]; }
+__device__ __forceinline__ uint32_t list_len(const PLane& L, uint64_t v) { return (uint32_t)hget(L, list_off(v)); }
+__device__ __forceinline__ uint64_t list_at(const PLane& L, uint64_t v, uint32_t i) { return hget(L, list_off(v) + 2 + i); }
 
 __device__ __forceinline__ uint64_t list_new(PLane& L, uint32_t kind, uint32_t cap) {
   if (L.hp + 2 + cap > HCAP) { lane_fallback(L, FB_HEAP); return mkv(V_UNDEF, 0); }
   uint32_t o = L.hp;
-  L.H[o] = 0;
-  L.H[o + 1] = cap;
+  hset(L, o, 0);
+  hset(L, o + 1, cap);
   L.hp += 2 + cap;
   return mklist(kind, o);
 }
@@ -445,26 +471,26 @@ __device__ __noinline__ uint64_t list_add_slow(PLane& L, uint64_t l, uint64_t v)
   if (vtag(l) != V_LIST) return l;
   if (list_kind(l) == LK_SET && list_contains(L, l, v)) return l;
   uint32_t o = list_off(l);
-  uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
+  uint32_t n = (uint32_t)hget(L, o), cap = (uint32_t)hget(L, o + 1);
   if (n == cap) {
     // grow: move to top of heap if this list is the last allocation, else copy
     uint32_t ncap = cap < 4 ? 8 : cap * 2;
     if (o + 2 + cap == L.hp) {
       if (o + 2 + ncap > HCAP) { lane_fallback(L, FB_HEAP); return l; }
       L.hp = o + 2 + ncap;
-      L.H[o + 1] = ncap;
+      hset(L, o + 1, ncap);
     } else {
       if (L.hp + 2 + ncap > HCAP) { lane_fallback(L, FB_HEAP); return l; }
       uint32_t no = L.hp;
       L.hp += 2 + ncap;
-      for (uint32_t i = 0; i < n + 2; ++i) L.H[no + i] = L.H[o + i];
-      L.H[no + 1] = ncap;
+      for (uint32_t i = 0; i < n + 2; ++i) hset(L, no + i, hget(L, o + i));
+      hset(L, no + 1, ncap);
       o = no;
       l = mklist(list_kind(l), o);
     }
   }
-  L.H[o + 2 + n] = v;
-  L.H[o] = n + 1;
+  hset(L, o + 2 + n, v);
+  hset(L, o, n + 1);
   return l;
 }
 // append fast path (array / object list with room), inlined: AMDGPU calls
@@ -472,10 +498,10 @@ __device__ __noinline__ uint64_t list_add_slow(PLane& L, uint64_t l, uint64_t v)
 __device__ __forceinline__ uint64_t list_add(PLane& L, uint64_t l, uint64_t v) {
   if (vtag(l) == V_LIST && list_kind(l) != LK_SET) {
     uint32_t o = list_off(l);
-    uint32_t n = (uint32_t)L.H[o], cap = (uint32_t)L.H[o + 1];
+    uint32_t n = (uint32_t)hget(L, o), cap = (uint32_t)hget(L, o + 1);
     if (n < cap) {
-      L.H[o + 2 + n] = v;
-      L.H[o] = n + 1;
+      hset(L, o + 2 + n, v);
+      hset(L, o, n + 1);
       return l;
     }
   }
@@ -1335,15 +1361,15 @@ __device__ uint64_t bi_split(PLane& L, uint64_t a0, uint64_t a1) {
   if (vtag(l) != V_LIST) return UND;
   uint32_t o = list_off(l);
   if (d.n == 0) {
-    for (uint32_t i = 0; i < n; ++i) L.H[o + 2 + i] = str_sub(L, a0, s, i, 1);
+    for (uint32_t i = 0; i < n; ++i) hset(L, o + 2 + i, str_sub(L, a0, s, i, 1));
   } else {
     uint32_t k = 0, st = 0;
     for (uint32_t i = 0; i + d.n <= s.n;) {
-      if (bytes_at(s, i, d)) { L.H[o + 2 + k++] = str_sub(L, a0, s, st, i - st); i += d.n; st = i; } else ++i;
+      if (bytes_at(s, i, d)) { hset(L, o + 2 + k++, str_sub(L, a0, s, st, i - st)); i += d.n; st = i; } else ++i;
     }
-    L.H[o + 2 + k++] = str_sub(L, a0, s, st, s.n - st);
+    hset(L, o + 2 + k++, str_sub(L, a0, s, st, s.n - st));
   }
-  L.H[o] = n;
+  hset(L, o, n);
   return l;
 }
 

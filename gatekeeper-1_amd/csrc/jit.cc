@@ -457,11 +457,20 @@ static std::string wpe_suffix() {
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 
+// Lane heap words kept in LDS by template kernels (devrt.h GK_LDS_HWORDS;
+// GKGPU_LDS_HEAP overrides, 0 = all in the private segment)
+static int lds_heap_words() {
+  const char* v = getenv("GKGPU_LDS_HEAP");
+  int n = v ? atoi(v) : 0;
+  return n < 0 ? 0 : (n > 64 ? 64 : n);
+}
+
 static std::string inline_hot_tag() {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
   if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) t += std::string("m") + m2;
   if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
+  t += "d" + std::to_string(lds_heap_words());
   return t;
 }
 
@@ -486,6 +495,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   }
   // GKGPU_INLINE_HOT (A/B switch, default on): inline the per-container builtins
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
+  if (lds_heap_words() > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words() << "\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre
