@@ -154,10 +154,11 @@ class Comp {
   std::map<std::pair<const void*, bool>, int> memo_;  // memo slot per (function, statement form)
   // Lane constants (registers numbered from kLReg while compiling, renumbered
   // by finish()): the input roots, loaded at entry, and constant-key paths
-  // below them, each with a "looked up" flag cleared at entry.
-  static constexpr int kLReg = 11000, kMaxLaneRegs = 40;
+  // below them read inside loops, set to false at entry and looked up at
+  // their first use.
+  static constexpr int kLReg = 11000, kMaxLaneRegs = 16;
   int lreg_n_ = 0, rev_reg_ = -1, par_reg_ = -1;
-  std::map<std::pair<int, uint64_t>, std::pair<int, int>> lpath_;  // (base, key) -> (value, flag)
+  std::map<std::pair<int, std::vector<uint64_t>>, int> lpath_;  // (root, keys) -> value register
   bool lane_const(int r) const { return r >= kLReg && r < kLReg + lreg_n_; }
   static bool lane_paths_on() {
     static const bool on = !getenv("GKGPU_LANE_PATHS") || atoi(getenv("GKGPU_LANE_PATHS")) != 0;  // A/B
@@ -238,7 +239,7 @@ class Comp {
       // flags of the cached paths below them
       if (rev_reg_ >= 0) pro.push_back(Ins{OP_LOADREV, (uint16_t)map(rev_reg_), 0, 0, 0, 0});
       if (par_reg_ >= 0) pro.push_back(Ins{OP_LOADPARAM, (uint16_t)map(par_reg_), 0, 0, 0, 0});
-      for (auto& lp : lpath_) pro.push_back(Ins{OP_LOADK, (uint16_t)map(lp.second.second), 0, 0, kf, 0});
+      for (auto& lp : lpath_) pro.push_back(Ins{OP_LOADK, (uint16_t)map(lp.second), 0, 0, kf, 0});
       code_.insert(code_.begin(), pro.begin(), pro.end());
       for (auto& l : labels_) if (l >= 0) l += (int)pro.size();
       max_reg_ = lbase + lreg_n_;
@@ -689,25 +690,32 @@ class Comp {
     }
     if (sel->k == T_SCALAR) {
       const uint64_t key = scalar_val(sel);
-      if (lane_const(r) && lane_paths_on()) {
-        // a path below the lane's input is the same for the whole lane: looked
-        // up at its first use, then read from its register (input.review.kind,
-        // input.parameters.cpu, ... re-read per container otherwise)
-        auto lp = lpath_.find({r, key});
-        if (lp == lpath_.end() && lreg_n_ + 2 <= kMaxLaneRegs) {
-          int v = kLReg + lreg_n_++, d = kLReg + lreg_n_++;
-          lp = lpath_.emplace(std::make_pair(r, key), std::make_pair(v, d)).first;
-        }
+      if (lane_const(r) && lane_paths_on() && depth() > 0) {
+        // inside a loop, a constant-key path below the lane's input (input.
+        // review.kind.kind, input.parameters.cpu) is the same every iteration:
+        // looked up at its first use, then read from one register (initially
+        // false: a genuinely false value is just looked up again)
+        size_t j = i;
+        std::vector<uint64_t> keys;
+        while (j < path.size() && path[j]->k == T_SCALAR) keys.push_back(scalar_val(path[j++]));
+        auto lp = lpath_.find({r, keys});
+        if (lp == lpath_.end() && lreg_n_ < kMaxLaneRegs) lp = lpath_.emplace(std::make_pair(r, keys), kLReg + lreg_n_++).first;
         if (lp != lpath_.end()) {
-          const int v = lp->second.first, d = lp->second.second;
-          int Lhave = label();
-          emit_jmp(OP_JTRUE, d, Lhave);
-          emit(OP_GETK, (uint16_t)v, (uint16_t)r, 0, kconst(key));
-          int t = loadk(tag_val(V_BOOL, 1));
-          emit(OP_MOV, (uint16_t)d, (uint16_t)t);
+          const int v = lp->second;
+          int Lhave = label(), Lcomp = label();
+          emit_jmp(OP_JFALSE, v, Lcomp);
+          emit_jmp(OP_JMP, 0, Lhave);
+          place(Lcomp);
+          int cur = r;
+          for (uint64_t kk : keys) {
+            int t = alloc();
+            emit(OP_GETK, (uint16_t)t, (uint16_t)cur, 0, kconst(kk));  // vget of undefined is undefined
+            cur = t;
+          }
+          emit(OP_MOV, (uint16_t)v, (uint16_t)cur);
           place(Lhave);
           emit_jmp(OP_JUNDEF, v, fail);
-          walk(v, path, i + 1, env, fail, k);
+          walk(v, path, j, env, fail, k);
           return;
         }
       }

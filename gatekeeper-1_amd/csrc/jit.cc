@@ -457,11 +457,17 @@ static std::string wpe_suffix() {
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 
-// Lane heap words kept in LDS by template kernels (devrt.h GK_LDS_HWORDS;
-// GKGPU_LDS_HEAP overrides, 0 = all in the private segment)
+// Lane heap words kept in LDS by template kernels (devrt.h GK_LDS_HWORDS):
+// 32 words = 64 KB per 256-thread block, two blocks per CU, which is the
+// occupancy the 256-VGPR template kernels have anyway.  Measured on config 2
+// (1M Pods, tools/gpu_r02m.sh): K8sContainerLimits 5.30 -> 4.84 ms,
+// K8sRequiredProbes 6.07 -> 5.14 ms (16 words: 4.83 / 5.74).  The VM kernel
+// keeps its heap in the private segment (its module also holds the format
+// kernel, whose occupancy a module-wide LDS array would halve).
+// GKGPU_LDS_HEAP overrides (0 = all in the private segment).
 static int lds_heap_words() {
   const char* v = getenv("GKGPU_LDS_HEAP");
-  int n = v ? atoi(v) : 0;
+  int n = v ? atoi(v) : 32;
   return n < 0 ? 0 : (n > 64 ? 64 : n);
 }
 
