@@ -110,6 +110,7 @@ struct Lane {
   uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
   // staged emissions: msg bytes then details JSON at B[off..off+mlen+dlen)
   uint32_t en, steps;
+  uint32_t nsz;  // op_emit staged a record that size_deferred has not sized yet
   uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
   uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
   uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP], em_ord[EMCAP];
@@ -493,13 +494,32 @@ __device__ __noinline__ uint64_t list_add_slow(PLane& L, uint64_t l, uint64_t v)
   hset(L, o, n + 1);
   return l;
 }
-// append fast path (array / object list with room), inlined: AMDGPU calls
-// save and restore the caller's live registers in scratch
+// Identity-decidable equality: 1 equal, 0 different, -1 undecided (needs veq).
+// Interned strings are equal iff their ids are; booleans and nulls by bits;
+// plain ints by value (the INT_G print flag does not take part).
+__device__ __forceinline__ int id_eq(uint64_t a, uint64_t b) {
+  if (a == b) { uint32_t t = vtag(a); return (t == V_STR || t == V_BOOL || t == V_NULL || t == V_INT) ? 1 : -1; }
+  uint32_t ta = vtag(a), tb = vtag(b);
+  if (ta != tb) return -1;
+  if (ta == V_STR || ta == V_BOOL) return 0;
+  if (ta == V_INT) return intof(a) == intof(b) ? 1 : 0;
+  return -1;
+}
+// append fast path, inlined: AMDGPU calls save and restore the caller's live
+// registers in scratch.  Arrays / objects with room append; a set with room
+// appends after an inline duplicate scan when every member compares by
+// identity (interned strings, booleans, ints: the set-comprehension case).
 __device__ __forceinline__ uint64_t list_add(PLane& L, uint64_t l, uint64_t v) {
-  if (vtag(l) == V_LIST && list_kind(l) != LK_SET) {
+  if (vtag(l) == V_LIST) {
     uint32_t o = list_off(l);
     uint32_t n = (uint32_t)hget(L, o), cap = (uint32_t)hget(L, o + 1);
     if (n < cap) {
+      if (list_kind(l) == LK_SET) {
+        int found = 0;
+        for (uint32_t i = 0; i < n && found == 0; ++i) found = id_eq(hget(L, o + 2 + i), v);
+        if (found == 1) return l;
+        if (found < 0) return list_add_slow(L, l, v);
+      }
       hset(L, o + 2 + n, v);
       hset(L, o, n + 1);
       return l;
@@ -1466,6 +1486,25 @@ __device__ __forceinline__ uint64_t arith(PLane& L, uint32_t kind, uint64_t x, u
       if (__umul64hi(ua, ub) == 0 && ua * ub < (uint64_t)LIM) return mkint_g(a * b);
     }
   }
+  // set difference of heap sets whose members compare by identity (e.g.
+  // probe_type_set - {field | ctr[probe][field]}), inline
+  if (kind == AR_MINUS && vtag(x) == V_LIST && vtag(y) == V_LIST && list_kind(x) == LK_SET && list_kind(y) == LK_SET) {
+    const uint32_t nx = list_len(L, x), ny = list_len(L, y), hp0 = L.hp;
+    uint64_t out = list_new(L, LK_SET, nx);
+    if (vtag(out) == V_UNDEF) return out;
+    const uint32_t oo = list_off(out);
+    uint32_t n = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < nx && ok; ++i) {
+      const uint64_t v = list_at(L, x, i);
+      int found = 0;
+      for (uint32_t j = 0; j < ny && found == 0; ++j) found = id_eq(list_at(L, y, j), v);
+      if (found < 0) ok = false;
+      else if (found == 0) hset(L, oo + 2 + n++, v);
+    }
+    if (ok) { hset(L, oo, n); return out; }
+    L.hp = hp0;
+  }
   return arith_slow(L, kind, x, y);
 }
 __device__ __noinline__ uint64_t arith_slow(PLane& L, uint32_t kind, uint64_t x, uint64_t y) {
@@ -1749,7 +1788,7 @@ __device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k
 }
 
 // m: message register, d: details register (undefined when absent)
-__device__ __noinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+__device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   if (vtag(m) == V_FMT) {
     // deferred message: size it now, format it into the output at flush_wave.
     // Only heap-free arguments are recorded (the record outlives this
@@ -1792,6 +1831,116 @@ __device__ __noinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t 
   return !L.fail;
 }
 
+// Emission fast path, inlined at every emission site: a deferred sprintf
+// message without details whose arguments are plain scalars (interned
+// strings, ints) is staged as its argument record only; its
+// printed length is computed once per lane by size_deferred at the end of the
+// program, where no predicate registers are live.  An out-of-line op_emit per
+// violation made every emission save and restore the predicate's live VGPRs
+// in scratch.  Printing such arguments can only fail on an over-long message
+// (FB_MSG_LEN) or a verb/argument mismatch (FB_PRINT); size_deferred then
+// marks the lane as the reference-equivalent emission-time fallback.
+#ifndef GK_EMIT_FAST
+#define GK_EMIT_FAST 1
+#endif
+constexpr uint16_t EM_UNSIZED = 0xffffu;  // em_mlen of a record size_deferred has not sized yet
+__device__ __forceinline__ bool plain_scalar(uint64_t v) { return vtag(v) == V_STR || vtag(v) == V_INT; }
+__device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
+#if GK_EMIT_FAST
+  if (vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EMCAP) {
+    const uint64_t args = fmt_args(m);
+    if (vtag(args) == V_LIST) {
+      const uint32_t n = list_len(L, args);
+      const uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
+      if (n <= FMT_MAXARGS && off + rec <= BCAP) {
+        uint64_t* w = (uint64_t*)(L.B + off);
+        bool ok = true;
+        for (uint32_t i = 0; i < n && ok; ++i) {
+          const uint64_t v = list_at(L, args, i);
+          ok = plain_scalar(v);
+          w[1 + i] = v;
+        }
+        if (ok) {
+          w[0] = fmt_fidx(m) | (n << 24);
+          L.bp = off + rec;
+          L.em_rule[L.en] = (uint16_t)rule;
+          L.em_off[L.en] = (uint16_t)off;
+          L.em_mlen[L.en] = EM_UNSIZED;
+          L.em_dlen[L.en] = 0x8000u;
+          L.em_ord[L.en] = L.ord;
+          ++L.en;
+          L.nsz = 1;
+          for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
+            if (L.keepB[dd] < L.bp) L.keepB[dd] = (uint16_t)L.bp;
+          return true;
+        }
+      }
+    }
+  }
+#endif
+  return op_emit_slow(L, m, d, depth, rule);
+}
+
+// Printed length of a deferred message whose arguments are plain scalars:
+// put_fmt_arg restricted to interned strings and ints, on a counter.  (Sizing
+// through the generic fmt_run here made this gfx950 toolchain emit an illegal
+// V_CMP on src_shared_base: the heap-value printing paths test the LDS
+// aperture of the lane pointer.)
+__device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, uint32_t& len) {
+  const uint32_t* f = gk_args.fmt + fidx;
+  const uint32_t nseg = f[0];
+  Cnt o{0, false};
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
+    if (kind == 0) { put_sid(o, a); continue; }
+    const uint64_t v = args[a & 0xffff];
+    const uint32_t verb = a >> 16;
+    if (vtag(v) == V_STR) {
+      const uint32_t n = gk_args.strs[(uint32_t)vpay(v)].len;
+      GK_TOUCH_STR((uint32_t)vpay(v));
+      if (verb == 'd') { put_cstr(o, "%!d(string="); o.n += n; put(o, ')'); } else o.n += n;
+    } else if (intv_gform(v)) {
+      if (verb != 'v') return false;
+      put_intv(o, v);
+    } else if (verb == 's') {
+      put_cstr(o, "%!s(int="); put_int(o, intof(v)); put(o, ')');
+    } else {
+      put_int(o, intof(v));
+    }
+  }
+  len = o.n;
+  return true;
+}
+// sizes the records op_emit staged unsized (once per lane, after the program;
+// inlined into finish_lane, out of line, where no predicate registers are live)
+__device__ __forceinline__ void size_deferred(PLane& L) {
+  for (uint32_t i = 0; i < L.en; ++i) {
+    if (L.em_mlen[i] != EM_UNSIZED) continue;
+    const uint64_t* rec = (const uint64_t*)(L.B + L.em_off[i]);
+    uint32_t n = 0;
+    const bool ok = size_plain((uint32_t)rec[0] & 0xffffffu, rec + 1, n);
+    if (!ok || n > 0x7fffu) {
+      // the emission-time outcome: the program would have stopped here
+      L.fail = RF_FALLBACK;
+      L.reason = ok ? FB_MSG_LEN : FB_PRINT;
+      return;
+    }
+    L.em_mlen[i] = (uint16_t)n;
+  }
+  L.nsz = 0;
+}
+
+// end of a lane's evaluation (out of line: the predicate's registers are dead)
+__device__ __noinline__ void finish_lane(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool live) {
+  if (live && !L.fail && L.nsz) size_deferred(L);
+  if (live && L.fail) {
+    atomicAdd(&gk_args.counters[2], 1ull);
+    atomicOr(&gk_args.rflags[r], L.fail);
+    if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
+  }
+  flush_wave(L, lane, r, c, live && !L.fail);
+}
+
 // ------------------------------------------------------------------ kernel body
 // lane -> (review tile, constraint): a wave = 64 consecutive reviews x ONE
 // constraint of the launch's list, so every lane runs the same predicate and
@@ -1810,6 +1959,7 @@ __device__ __forceinline__ void audit_body(Run run) {
   Lane L0;
   PLane& L = *(PLane*)&L0;
   L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  L.nsz = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   bool live = rp < gk_args.nrev;
   if (live) {
@@ -1834,14 +1984,10 @@ __device__ __forceinline__ void audit_body(Run run) {
         run(L, mkv(V_NODE, rc.root), params, m.prog, r, c);
       }
     }
-    if (L.fail) {
-      atomicAdd(&gk_args.counters[2], 1ull);
-      atomicOr(&gk_args.rflags[r], L.fail);
-      if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
-    }
   }
-  // every lane of the wave reaches here (reconverged): reserve + write output
-  flush_wave(L, lane, r, c, live && !L.fail);
+  // every lane of the wave reaches here (reconverged): size deferred records,
+  // flag failed reviews, reserve + write output
+  finish_lane(L, lane, r, c, live);
   if (gk_args.prof) {
     uint32_t mx = L.steps;
 #pragma unroll

@@ -150,6 +150,7 @@ struct Counts {
 static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t fcap) {
   Lane L;
   L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  L.nsz = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   const ReviewCol rc = gk_args.revs[rp];
   const MatchSpec m = gk_args.cons[c];
@@ -167,6 +168,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
     else if (mr == 1 && m.prog != NO_ID) {
       uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
       run_program(L, gk_args.prog_off[m.prog], mkv(V_NODE, rc.root), params);
+      if (L.nsz) size_deferred(L);
     }
   }
   if (L.fail) { ++k.flagged; return; }

@@ -528,7 +528,7 @@ def test_string_builtins_trim_split_case_concat_indexof():
 
 
 def test_template_kernel_matches_vm_at_scale():
-    """Size-independent property at 200k Pods (config 2 policies): the template
+    """Size-independent property at 100k Pods (config 2 policies): the template
     kernels + format pass over size-ordered reviews produce exactly the
     violation multiset of the bytecode VM with in-kernel formatting in batch
     order, and repeat evaluations are identical."""
@@ -537,7 +537,7 @@ def test_template_kernel_matches_vm_at_scale():
     import collections
     import os
     ts, cs = W.config2()
-    objs, nss = W.gen_pods_json(200_000, seed=42, n_namespaces=1000)
+    objs, nss = W.gen_pods_json(100_000, seed=42, n_namespaces=1000)
 
     def sweep(jit, fpass):
         old = os.environ.get("GKGPU_FORMAT_PASS")
@@ -566,7 +566,7 @@ def test_template_kernel_matches_vm_at_scale():
     vm = sweep(False, False)
     jit = sweep(True, True)
     assert vm[0] == vm[1]
-    assert sum(vm[0].values()) > 500_000
+    assert sum(vm[0].values()) > 250_000
     assert jit[0] == jit[1]
     assert jit[0] == vm[0]
 
