@@ -11,6 +11,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <thread>
 #include <vector>
 
@@ -63,6 +64,48 @@ static int env_mode(const char* name, int def, int max) {
 
 
 // ------------------------------------------------------------------ device buffers
+// Large host-to-device copies (a staged batch's node arena, ~1 GB per 1M Pods)
+// go through two pinned 64 MB bounce buffers: host threads copy chunk k+1 into
+// one while the DMA engine reads chunk k from the other.  A pageable
+// hipMemcpy of the same bytes runs at a fraction of the link rate.
+// GKGPU_PINNED_UPLOAD=0 keeps the plain hipMemcpy (A/B).
+static bool upload_bounce(void* dst, const char* src, size_t n) {
+  constexpr size_t CH = 64ull << 20;
+  static std::mutex mu;
+  static char* pin[2] = {nullptr, nullptr};
+  static hipStream_t st = nullptr;
+  static hipEvent_t ev[2] = {nullptr, nullptr};
+  static int ok = -1;
+  std::lock_guard<std::mutex> g(mu);
+  if (ok < 0) {
+    ok = env_mode("GKGPU_PINNED_UPLOAD", 1, 1) != 0 && hipHostMalloc((void**)&pin[0], CH, hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc((void**)&pin[1], CH, hipHostMallocDefault) == hipSuccess &&
+         hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess;
+  const int T = std::max(1, std::min(16, default_threads()));
+  for (size_t off = 0, k = 0; off < n; off += CH, ++k) {
+    const size_t len = std::min(CH, n - off);
+    const int b = (int)(k & 1);
+    if (k >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) return false;
+    char* dstp = pin[b];
+    const char* srcp = src + off;
+    std::vector<std::thread> th;
+    auto part = [&](int t) {
+      const size_t lo = len * t / T, hi = len * (t + 1) / T;
+      memcpy(dstp + lo, srcp + lo, hi - lo);
+    };
+    for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    if (hipMemcpyAsync((char*)dst + off, dstp, len, hipMemcpyHostToDevice, st) != hipSuccess) return false;
+    if (hipEventRecord(ev[b], st) != hipSuccess) return false;
+  }
+  return hipStreamSynchronize(st) == hipSuccess;
+}
+
 struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -82,7 +125,9 @@ struct DBuf {
   bool upload(const void* src, size_t n, bool append_only) {
     if (!reserve(n)) return false;
     size_t from = append_only ? std::min(used, n) : 0;
-    if (n > from && hipMemcpy((char*)p + from, (const char*)src + from, n - from, hipMemcpyHostToDevice) != hipSuccess)
+    if (n > from && n - from >= (256u << 20)) {
+      if (!upload_bounce((char*)p + from, (const char*)src + from, n - from)) return false;
+    } else if (n > from && hipMemcpy((char*)p + from, (const char*)src + from, n - from, hipMemcpyHostToDevice) != hipSuccess)
       return false;
     used = n;
     return true;
@@ -1250,6 +1295,8 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
   if (excluded) *excluded = fr.excluded;
   cols.swap(fr.cols);
   const std::vector<uint32_t>& weight = fr.weight;
+  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  auto t_ord = Clock::now();
   if (order_by_size) {
     // Divergence-aware order: a wavefront evaluates 64 consecutive reviews, and
     // its lanes run as long as the largest document (e.g. the Pod with the most
@@ -1301,7 +1348,41 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
     }
     std::vector<uint32_t> perm(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+    // the keys packed into one 60-bit integer per review (kind ids ranked, so
+    // their order is kept), then a stable LSD radix sort: the same permutation
+    // as the comparison sort below, which stays for more than 4096 kinds
+    std::vector<uint32_t> kind_ids;
+    kind_ids.reserve(64);
+    {
+      std::unordered_set<uint32_t> seen;
+      for (const auto& c : cols)
+        if (seen.insert(c.kind).second) kind_ids.push_back(c.kind);
+      std::sort(kind_ids.begin(), kind_ids.end());
+    }
+    if (kind_ids.size() <= 4096) {
+      std::unordered_map<uint32_t, uint64_t> krank;
+      for (size_t k = 0; k < kind_ids.size(); ++k) krank[kind_ids[k]] = k;
+      std::vector<uint64_t> key(cols.size());
+      uint32_t last_kind = NO_ID;
+      uint64_t last_rank = 0;
+      for (size_t i = 0; i < cols.size(); ++i) {
+        if (cols[i].kind != last_kind) { last_kind = cols[i].kind; last_rank = krank[last_kind]; }
+        const uint64_t w = weight[i], sg = sig[i] & 0xffffu;
+        if (mode == 2) key[i] = (last_rank << 48) | ((w >> 20) << 36) | (sg << 20) | (w & 0xfffffu);
+        else key[i] = (sg << 44) | ((match_order ? last_rank : 0) << 32) | w;
+      }
+      std::vector<uint32_t> tmp(perm.size());
+      std::vector<uint32_t> cnt(256);
+      for (int sh = 0; sh < 64; sh += 8) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (uint32_t x : perm) ++cnt[(key[x] >> sh) & 0xff];
+        if (*std::max_element(cnt.begin(), cnt.end()) == perm.size()) continue;  // one bucket: order kept
+        uint32_t run = 0;
+        for (auto& c : cnt) { uint32_t v = c; c = run; run += v; }
+        for (uint32_t x : perm) tmp[cnt[(key[x] >> sh) & 0xff]++] = x;
+        perm.swap(tmp);
+      }
+    } else std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
       if (mode == 2) {  // kind, array elements, namespace-list bits, nodes
         if (cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
         if ((weight[a] >> 20) != (weight[b] >> 20)) return (weight[a] >> 20) < (weight[b] >> 20);
@@ -1315,6 +1396,7 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
     std::vector<ReviewCol> sorted(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
     cols.swap(sorted);
+    if (trace) fprintf(stderr, "flatten: review order %.1f ms\n", ms_since(t_ord));
   }
   return GK_OK;
 }

@@ -348,15 +348,15 @@ bool flatten_page(Store& gst, const NsCache& ns_cache, const std::set<std::strin
   const uint32_t nwell = Store().nstrings();  // well-known ids shared by every Store
   size_t extra = 0;
   for (auto& p : parts) extra += p.st.nstrings() - nwell;
-  gst.reserve_strings(extra);
+  {
+    std::vector<const Store*> src;
+    for (auto& p : parts) src.push_back(&p.st);
+    std::vector<std::vector<uint32_t>> maps;
+    gst.intern_parts(src, nwell, maps, T);
+    for (size_t k = 0; k < parts.size(); ++k) parts[k].smap.swap(maps[k]);
+  }
   for (auto& p : parts) {
     const Store& ls = p.st;
-    p.smap.resize(ls.nstrings());
-    for (uint32_t s = 0; s < nwell; ++s) p.smap[s] = s;
-    for (uint32_t s = nwell; s < ls.nstrings(); ++s) {
-      std::string_view v = ls.str(s);
-      p.smap[s] = gst.intern(v.data(), v.size());
-    }
     const auto& nums = ls.numbers();
     p.nmap.resize(nums.size());
     for (uint32_t k = 0; k < nums.size(); ++k) {

@@ -2,7 +2,13 @@
 // conversions matching Go's math/big / strconv behaviour.
 #include "store.h"
 
+#include <atomic>
 #include <charconv>
+#include <chrono>
+#include <cstdio>
+#include <functional>
+#include <stdexcept>
+#include <thread>
 #include <cmath>
 #include <cstdlib>
 #include <deque>
@@ -304,6 +310,17 @@ uint32_t Store::find(const char* p, size_t n) const {
   return NO_ID;
 }
 
+static uint8_t str_flags_of(const char* p, size_t n) {
+  uint8_t fl = SF_ASCII_PRINT;
+  for (size_t i = 0; i < n; ++i) {
+    unsigned char c = (unsigned char)p[i];
+    if (c >= 0x80) { fl |= SF_NON_ASCII; fl &= ~SF_ASCII_PRINT; }
+    else if (c < 0x20 || c == 0x7f) { fl &= ~SF_ASCII_PRINT; }
+    else if (c == '"' || c == '\\') fl |= SF_NEEDS_ESC;
+  }
+  return fl;
+}
+
 uint32_t Store::intern(const char* p, size_t n) {
   size_t mask = table_.size() - 1;
   uint64_t hv = str_hash(p, n);
@@ -321,14 +338,7 @@ uint32_t Store::intern(const char* p, size_t n) {
   StrEnt se{(uint32_t)pool_.size(), (uint32_t)n};
   pool_.append(p, n);
   strs_.push_back(se);
-  uint8_t fl = SF_ASCII_PRINT;
-  for (size_t i = 0; i < n; ++i) {
-    unsigned char c = (unsigned char)p[i];
-    if (c >= 0x80) { fl |= SF_NON_ASCII; fl &= ~SF_ASCII_PRINT; }
-    else if (c < 0x20 || c == 0x7f) { fl &= ~SF_ASCII_PRINT; }
-    else if (c == '"' || c == '\\') fl |= SF_NEEDS_ESC;
-  }
-  sflags_.push_back(fl);
+  sflags_.push_back(str_flags_of(p, n));
   table_[h] = slot_of(hv, id);
   if (strs_.size() * 2 > table_.size()) grow();
   return id;
@@ -649,6 +659,149 @@ class DocParser {
 bool Store::parse_doc(const char* p, size_t n, Node* root, std::string* err) {
   DocParser d(*this, p, n, err);
   return d.run(root);
+}
+
+}  // namespace gk
+
+namespace gk {
+
+// Parallel merge of thread-local stores' strings (flatten.cc phase 2).
+//  A (per part): strings already in this store map to their ids; the rest
+//    become candidates, bucketed into 256 shards by the hash's top byte.
+//  B (per shard): candidates are de-duplicated across parts (hash, then bytes).
+//  C: shard id / byte ranges by prefix sum; the tables are resized once.
+//  D (per shard): entries, bytes and flags are written in place, and each new
+//    string is inserted into the open-addressing table with a CAS on its slot
+//    (new strings are distinct, so a taken slot only means "probe on").
+//  E (per part): candidates' map entries point at their shard's ids.
+// Ids are assigned shard by shard, so they differ from serial interning's;
+// nothing depends on id order (the engine compares strings by id for equality
+// and by bytes for order).
+void Store::intern_parts(const std::vector<const Store*>& src, uint32_t first,
+                         std::vector<std::vector<uint32_t>>& maps, int threads) {
+  const size_t P = src.size();
+  constexpr uint32_t S = 256;
+  struct Cand { uint64_t hv; uint32_t lid, gidx; };
+  auto t0 = std::chrono::steady_clock::now();
+  maps.assign(P, {});
+  std::vector<std::vector<std::vector<Cand>>> cand(P, std::vector<std::vector<Cand>>(S));
+  auto pfor = [&](size_t n, const std::function<void(size_t)>& f) {
+    std::atomic<size_t> next{0};
+    auto work = [&] { for (size_t i; (i = next.fetch_add(1)) < n;) f(i); };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::max(1, threads); ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+  };
+  // A
+  pfor(P, [&](size_t p) {
+    const Store& ls = *src[p];
+    auto& m = maps[p];
+    m.resize(ls.nstrings());
+    for (uint32_t s = 0; s < first && s < ls.nstrings(); ++s) m[s] = s;
+    const size_t mask = table_.size() - 1;
+    for (uint32_t s = first; s < ls.nstrings(); ++s) {
+      std::string_view v = ls.str(s);
+      const uint64_t hv = str_hash(v.data(), v.size()), tag = hv & 0xffffffff00000000ull;
+      uint32_t id = NO_ID;
+      for (size_t h = hv & mask; uint64_t e = table_[h]; h = (h + 1) & mask) {
+        if ((e & 0xffffffff00000000ull) != tag) continue;
+        const StrEnt& se = strs_[(uint32_t)e - 1];
+        if (se.len == v.size() && memcmp(pool_.data() + se.off, v.data(), v.size()) == 0) { id = (uint32_t)e - 1; break; }
+      }
+      if (id != NO_ID) m[s] = id;
+      else cand[p][hv >> 56].push_back(Cand{hv, s, 0});
+    }
+  });
+  {
+    size_t ncand = 0;  // an upper bound of the new strings: room without rehashing later
+    for (auto& cp : cand)
+      for (auto& v : cp) ncand += v.size();
+    reserve_strings(ncand);
+  }
+  auto tA = std::chrono::steady_clock::now();
+  // B
+  struct Rep { uint64_t hv; uint32_t part, lid; };
+  std::vector<std::vector<Rep>> reps(S);
+  std::vector<uint64_t> shard_bytes(S, 0);
+  pfor(S, [&](size_t sh) {
+    size_t tot = 0;
+    for (size_t p = 0; p < P; ++p) tot += cand[p][sh].size();
+    if (!tot) return;
+    size_t sz = 16;
+    while (sz < tot * 2) sz *= 2;
+    std::vector<uint32_t> tab(sz, 0);  // rep index + 1
+    auto& R = reps[sh];
+    R.reserve(tot);
+    for (size_t p = 0; p < P; ++p) {
+      for (Cand& c : cand[p][sh]) {
+        std::string_view v = src[p]->str(c.lid);
+        size_t h = (size_t)(c.hv * 0x9e3779b97f4a7c15ull >> 20) & (sz - 1);
+        for (;; h = (h + 1) & (sz - 1)) {
+          const uint32_t e = tab[h];
+          if (!e) {
+            tab[h] = (uint32_t)R.size() + 1;
+            c.gidx = (uint32_t)R.size();
+            R.push_back(Rep{c.hv, (uint32_t)p, c.lid});
+            shard_bytes[sh] += v.size();
+            break;
+          }
+          const Rep& r = R[e - 1];
+          if (r.hv == c.hv && src[r.part]->str(r.lid) == v) { c.gidx = e - 1; break; }
+        }
+      }
+    }
+  });
+  auto tB = std::chrono::steady_clock::now();
+  // C
+  std::vector<uint32_t> base_id(S);
+  std::vector<uint64_t> base_off(S);
+  uint32_t nid = (uint32_t)strs_.size();
+  uint64_t off = pool_.size();
+  for (uint32_t sh = 0; sh < S; ++sh) {
+    base_id[sh] = nid;
+    base_off[sh] = off;
+    nid += (uint32_t)reps[sh].size();
+    off += shard_bytes[sh];
+  }
+  if (off > 0xffffffffull) throw std::runtime_error("string pool exceeds 4 GiB");
+  while ((size_t)nid * 2 > table_.size()) grow();  // (reserve_strings above already made room)
+  strs_.resize(nid);
+  sflags_.resize(nid);
+  pool_.resize(off);
+  auto tC = std::chrono::steady_clock::now();
+  // D
+  const size_t mask = table_.size() - 1;
+  pfor(S, [&](size_t sh) {
+    uint64_t o = base_off[sh];
+    char* pool = &pool_[0];
+    for (size_t k = 0; k < reps[sh].size(); ++k) {
+      const Rep& r = reps[sh][k];
+      std::string_view v = src[r.part]->str(r.lid);
+      const uint32_t id = base_id[sh] + (uint32_t)k;
+      if (!v.empty()) memcpy(pool + o, v.data(), v.size());
+      strs_[id] = StrEnt{(uint32_t)o, (uint32_t)v.size()};
+      sflags_[id] = str_flags_of(v.data(), v.size());
+      o += v.size();
+      const uint64_t slot = slot_of(r.hv, id);
+      for (size_t h = r.hv & mask;; h = (h + 1) & mask) {
+        uint64_t zero = 0;
+        if (__atomic_compare_exchange_n(&table_[h], &zero, slot, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) break;
+      }
+    }
+  });
+  auto tD = std::chrono::steady_clock::now();
+  // E
+  pfor(P, [&](size_t p) {
+    auto& m = maps[p];
+    for (uint32_t sh = 0; sh < S; ++sh)
+      for (const Cand& c : cand[p][sh]) m[c.lid] = base_id[sh] + c.gidx;
+  });
+  if (getenv("GKGPU_FLATTEN_TRACE")) {
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "intern_parts: A %.1f B %.1f C %.1f D %.1f E %.1f ms\n", ms(t0, tA), ms(tA, tB), ms(tB, tC), ms(tC, tD),
+            ms(tD, std::chrono::steady_clock::now()));
+  }
 }
 
 }  // namespace gk

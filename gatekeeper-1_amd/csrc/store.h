@@ -79,6 +79,10 @@ class Store {
   uint32_t find(const char* p, size_t n) const;  // NO_ID if absent
   // make room for `n` more strings without rehashing while they are interned
   void reserve_strings(size_t n);
+  // intern strings [first, nstrings) of every store in `src` on `threads`
+  // threads; maps[p][s] = this store's id of src[p]'s string s (s < first: s)
+  void intern_parts(const std::vector<const Store*>& src, uint32_t first, std::vector<std::vector<uint32_t>>& maps,
+                    int threads);
 
   // -- numbers (interned by text)
   uint32_t number(const char* p, size_t n);
