@@ -98,19 +98,52 @@ __device__ __forceinline__ uint64_t mkslice(uint32_t sid, uint32_t st, uint32_t 
 __device__ __forceinline__ bool is_strv(uint64_t v) { uint32_t t = vtag(v); return t == V_STR || t == V_HSTR || t == V_SLICE; }
 __device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); return t == V_NUM || t == V_INT || t == V_BFN; }
 
+// GK_LDS_SCALARS (template kernels, jit.cc): the lane's hot scalars (heap and
+// buffer tops, failure word, emission count and order keys) live in LDS, one
+// 32-bit slot per thread and field (gk_lds_scal[field][threadIdx.x]), instead
+// of the lane's private segment.  Every helper reads and writes them, and the
+// private segment is reached through a generic pointer that byte stores into
+// the lane buffer may alias, so in scratch they were reloaded from memory
+// after almost every helper.  Fields keep their names: LdsField converts.
+#ifndef GK_LDS_SCALARS
+#define GK_LDS_SCALARS 0
+#endif
+#if GK_LDS_SCALARS
+constexpr int LDS_NSCAL = 8;
+__shared__ uint32_t gk_lds_scal[LDS_NSCAL][256];
+template <class T, int F>
+struct LdsField {
+  __device__ __forceinline__ operator T() const { return (T)gk_lds_scal[F][threadIdx.x]; }
+  __device__ __forceinline__ LdsField& operator=(uint32_t v) { gk_lds_scal[F][threadIdx.x] = (T)v; return *this; }
+  __device__ __forceinline__ LdsField& operator=(const LdsField& o) { return *this = (uint32_t)(T)o; }
+  __device__ __forceinline__ LdsField& operator+=(uint32_t v) { return *this = (uint32_t)(T)*this + v; }
+  __device__ __forceinline__ LdsField& operator-=(uint32_t v) { return *this = (uint32_t)(T)*this - v; }
+  __device__ __forceinline__ LdsField& operator|=(uint32_t v) { return *this = (uint32_t)(T)*this | v; }
+  __device__ __forceinline__ LdsField& operator++() { return *this += 1u; }
+  __device__ __forceinline__ T operator++(int) { T o = *this; *this += 1u; return o; }
+};
+#define GK_LSCAL(T, name, F) LdsField<T, F> name
+#else
+#define GK_LSCAL(T, name, F) T name
+#endif
+
 struct Lane {
   uint64_t H[HCAP - GK_LDS_HWORDS_DEF];  // heap words GK_LDS_HWORDS_DEF.. (the first ones are in LDS)
   char B[BCAP];
-  uint32_t hp, bp, fail;  // fail: 0 ok, RF_ERROR, RF_FALLBACK
+  GK_LSCAL(uint32_t, hp, 0);
+  GK_LSCAL(uint32_t, bp, 1);
+  GK_LSCAL(uint32_t, fail, 2);  // fail: 0 ok, RF_ERROR, RF_FALLBACK
   // emission order key (OP_ORD, fused rule bodies): emissions are numbered by
   // (key, emission index) at flush, which is the reference's evaluation order
-  uint16_t ord, ord_base;
-  uint32_t reason;
+  GK_LSCAL(uint16_t, ord, 3);
+  GK_LSCAL(uint16_t, ord_base, 4);
+  GK_LSCAL(uint32_t, reason, 5);
   // per loop depth: heap / byte watermarks that values escaping the loop pinned
   uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
   // staged emissions: msg bytes then details JSON at B[off..off+mlen+dlen)
-  uint32_t en, steps;
-  uint32_t nsz;  // op_emit staged a record that size_deferred has not sized yet
+  GK_LSCAL(uint32_t, en, 6);
+  uint32_t steps;
+  GK_LSCAL(uint32_t, nsz, 7);  // op_emit staged a record that size_deferred has not sized yet
   uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
   uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
   uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP], em_ord[EMCAP];
@@ -1852,7 +1885,7 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
     if (vtag(args) == V_LIST) {
       const uint32_t n = list_len(L, args);
       const uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
-      if (n <= FMT_MAXARGS && off + rec <= BCAP) {
+      if (n <= FMT_MAXARGS && off + rec + 2 <= BCAP) {
         uint64_t* w = (uint64_t*)(L.B + off);
         bool ok = true;
         for (uint32_t i = 0; i < n && ok; ++i) {
@@ -1862,11 +1895,14 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
         }
         if (ok) {
           w[0] = fmt_fidx(m) | (n << 24);
-          L.bp = off + rec;
+          // absent details print as the hook's default "{}" (put_json of undefined)
+          L.B[off + rec] = '{';
+          L.B[off + rec + 1] = '}';
+          L.bp = off + rec + 2;
           L.em_rule[L.en] = (uint16_t)rule;
           L.em_off[L.en] = (uint16_t)off;
           L.em_mlen[L.en] = EM_UNSIZED;
-          L.em_dlen[L.en] = 0x8000u;
+          L.em_dlen[L.en] = 0x8000u | 2u;
           L.em_ord[L.en] = L.ord;
           ++L.en;
           L.nsz = 1;

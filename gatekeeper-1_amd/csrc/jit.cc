@@ -471,12 +471,20 @@ static int lds_heap_words() {
   return n < 0 ? 0 : (n > 64 ? 64 : n);
 }
 
+// Lane scalars in LDS (devrt.h GK_LDS_SCALARS): 8 KB per 256-thread block.
+// GKGPU_LDS_SCALARS=0 keeps them in the private segment (A/B).
+static bool lds_scalars() {
+  const char* v = getenv("GKGPU_LDS_SCALARS");
+  return !v || atoi(v) != 0;
+}
+
 static std::string inline_hot_tag() {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
   if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) t += std::string("m") + m2;
   if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
   t += "d" + std::to_string(lds_heap_words());
+  if (!lds_scalars()) t += "s0";
   return t;
 }
 
@@ -502,6 +510,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   // GKGPU_INLINE_HOT (A/B switch, default on): inline the per-container builtins
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words() > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words() << "\n";
+  if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre

@@ -563,8 +563,14 @@ def test_template_kernel_matches_vm_at_scale():
                 else:
                     os.environ[k] = v
 
+    import sys
+    import time
+    t0 = time.time()
     vm = sweep(False, False)
+    print("scale test: VM sweeps %.1f s" % (time.time() - t0), file=sys.stderr, flush=True)
+    t0 = time.time()
     jit = sweep(True, True)
+    print("scale test: JIT sweeps %.1f s" % (time.time() - t0), file=sys.stderr, flush=True)
     assert vm[0] == vm[1]
     assert sum(vm[0].values()) > 250_000
     assert jit[0] == jit[1]
