@@ -31,6 +31,7 @@ struct Program {
   uint32_t code_len = 0;
   uint32_t nregs = 0;
   bool uses_regex = false;
+  bool uses_inventory = false;  // reads data.inventory (the engine keeps its tree current)
   std::vector<uint32_t> regex_literals;  // string ids of literal patterns
   std::vector<std::string> rules;
   // guard programs (compile_template_guard): expressions outside the subset
@@ -54,6 +55,9 @@ struct CodeBank {
   std::vector<Ins> code;
   std::vector<uint64_t> consts;    // K table (tagged values)
   std::vector<uint32_t> fmt;       // sprintf format words
+  // the engine's data.inventory node (an object node whose members the engine
+  // points at the current inventory tree; NO_ID: joins are unsupported)
+  uint32_t inventory_node = 0xffffffffu;
   void clear() { code.clear(); consts.clear(); fmt.clear(); }
 };
 

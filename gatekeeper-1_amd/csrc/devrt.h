@@ -1477,6 +1477,36 @@ __device__ uint64_t bi_indexof(PLane& L, uint64_t a0, uint64_t a1) {
   return mkint(-1);
 }
 
+// sort (topdown/sets.go builtinSort via ast.Compare, v0.21): an array or a
+// set -> sorted array.  Insertion sort into a new heap array; elements whose
+// order this runtime cannot decide (composites) go to the CPU fallback.
+__device__ uint64_t bi_sort(PLane& L, uint64_t a) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  const int cls = tclass(a);
+  if (cls != 7 && cls != 9) { lane_error(L); return UND; }
+  const uint32_t n = coll_len(L, a);
+  uint64_t out = list_new(L, LK_ARR, n);
+  if (vtag(out) == V_UNDEF) return UND;
+  const uint32_t o = list_off(out);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t k, v;
+    coll_at(L, a, i, k, v);
+    uint32_t j = i;
+    while (j > 0) {
+      const uint64_t p = hget(L, o + 2 + j - 1);
+      const int c = vcmp(L, p, v);
+      if (c == 2) return UND;
+      if (c == 3) { lane_fallback(L, FB_DEEP_EQ); return UND; }
+      if (c <= 0) break;
+      hset(L, o + 2 + j, p);
+      --j;
+    }
+    hset(L, o + 2 + j, v);
+  }
+  hset(L, o, n);
+  return out;
+}
+
 __device__ uint64_t call_builtin(PLane& L, uint32_t id, const uint64_t* a) {
   switch (id) {
     case BI_COUNT: return bi_count(L, a[0]);
@@ -1499,6 +1529,7 @@ __device__ uint64_t call_builtin(PLane& L, uint32_t id, const uint64_t* a) {
     case BI_LOWER: case BI_UPPER: return bi_case(L, id, a[0]);
     case BI_CONCAT: return bi_concat(L, a[0], a[1]);
     case BI_INDEXOF: return bi_indexof(L, a[0], a[1]);
+    case BI_SORT: return bi_sort(L, a[0]);
     default: break;
   }
   lane_fallback(L, FB_UNSUPPORTED);

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -236,6 +237,11 @@ struct gk_engine {
   // process excluder (pkg/controller/config/process/excluder.go): process -> namespaces
   std::map<std::string, std::set<std::string>> excluded;
   uint32_t perm_nodes = 0;                        // nodes below this are permanent
+  // data.inventory (templates' cross-resource joins): one permanent object
+  // node whose members sync_inventory points at the current inventory tree
+  uint32_t inv_node = gk::NO_ID;
+  bool inv_dirty = true;        // /external/ data changed since the tree was built
+  bool uses_inventory = false;  // some compiled template reads data.inventory
   uint64_t gen = 1;                               // bumps on any mutation
   // regex
   std::map<uint32_t, std::pair<uint32_t, uint32_t>> dfa_index;  // pattern sid -> (word offset, status)
@@ -331,6 +337,14 @@ static void rebuild_modules(gk_engine* e) {
   e->templates.clear();
   // drop the transient region before appending new permanent constant nodes
   reset_transient(e);
+  if (e->inv_node == NO_ID) {
+    Node n{};
+    n.type = NT_OBJ;
+    e->inv_node = e->st.add_node(n);  // {} until sync_inventory builds the tree
+    e->perm_nodes = (uint32_t)e->st.nodes().size();
+  }
+  e->bank.inventory_node = e->inv_node;
+  e->uses_inventory = false;
   std::vector<std::shared_ptr<rego::Module>> parsed;
   for (auto& kv : e->modules) {
     auto m = rego::parse_module(kv.second);
@@ -384,6 +398,7 @@ static void rebuild_modules(gk_engine* e) {
       }
       te.prog = (int)e->progs.size();
       te.supported = !te.guard;
+      e->uses_inventory |= p.uses_inventory;
       e->progs.push_back(p);
       gk_engine::Jit j;
       j.name = jit_name(p, e->bank, e->st);
@@ -588,8 +603,70 @@ static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
   c.spec = m;
 }
 
+// data.inventory = data.external[target], or {} without one (regolib
+// src.go:66-72).  The synced objects (gk_put_data on /external/<target>/...)
+// are assembled into one JSON tree by path segment, parsed into the permanent
+// node region, and the engine's inventory node is pointed at its members, so
+// compiled templates (a constant V_NODE of that node) see the current tree.
+// Rebuilt lazily, only when a compiled template reads data.inventory; the
+// previous tree's nodes stay behind in the permanent region.
+static void sync_inventory(gk_engine* e) {
+  if (!e->uses_inventory || !e->inv_dirty || e->inv_node == NO_ID) return;
+  std::vector<std::pair<std::vector<std::string>, const std::string*>> ents;
+  for (auto& kv : e->inventory) {
+    auto p = split_path(kv.first);
+    if (p.size() < 3 || p[0] != "external" || p[1] != TARGET) continue;
+    ents.push_back({std::vector<std::string>(p.begin() + 2, p.end()), &kv.second});
+  }
+  std::sort(ents.begin(), ents.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::string js;
+  auto quote = [&](const std::string& v) {
+    js.push_back('"');
+    for (unsigned char c : v) {
+      if (c == '"' || c == '\\') { js.push_back('\\'); js.push_back((char)c); }
+      else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); js += b; }
+      else js.push_back((char)c);
+    }
+    js.push_back('"');
+  };
+  // entries [lo, hi) share their first `depth` segments; a leaf at a segment
+  // shadows deeper paths under it (one value per path)
+  std::function<void(size_t, size_t, size_t)> emit = [&](size_t lo, size_t hi, size_t depth) {
+    js.push_back('{');
+    for (size_t i = lo; i < hi;) {
+      const std::string& seg = ents[i].first[depth];
+      size_t j = i;
+      while (j < hi && ents[j].first[depth] == seg) ++j;
+      if (i != lo) js.push_back(',');
+      quote(seg);
+      js.push_back(':');
+      if (ents[i].first.size() == depth + 1) js += *ents[i].second;
+      else emit(i, j, depth + 1);
+      i = j;
+    }
+    js.push_back('}');
+  };
+  emit(0, ents.size(), 0);
+  JDoc d;
+  JsonReader rd(js.data(), js.size(), &d);
+  int root = rd.parse();
+  if (root < 0) throw std::runtime_error("inventory tree: " + d.err);
+  reset_transient(e);
+  const uint32_t r = e->st.add_doc(d, root);
+  Node& slot = e->st.nodes()[e->inv_node];
+  const Node& t = e->st.nodes()[r];
+  slot.type = t.type;
+  slot.first = t.first;
+  slot.n = t.n;
+  slot.flags = t.flags;
+  e->perm_nodes = (uint32_t)e->st.nodes().size();
+  e->dev_nodes_ok = std::min<uint32_t>(e->dev_nodes_ok, e->inv_node);
+  e->inv_dirty = false;
+}
+
 static void rebuild_constraints(gk_engine* e) {
   rebuild_modules(e);
+  sync_inventory(e);
   if (!e->constraints_dirty) return;
   e->mwords.clear();
   e->corder.clear();
@@ -1142,6 +1219,7 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
   if (p.size() >= 2 && p[0] == "external" && p[1] == TARGET) {
     std::string key(path);
     e->inventory[key] = std::string(json, len);
+    e->inv_dirty = true;
     if (p.size() == 6 && p[2] == "cluster" && p[3] == "v1" && p[4] == "Namespace") {
       rebuild_modules(e);
       reset_transient(e);
@@ -1171,7 +1249,7 @@ int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
     else ++it;
   }
   for (auto it = e->inventory.begin(); it != e->inventory.end();) {
-    if (prefix_match(split_path(it->first))) { it = e->inventory.erase(it); d = 1; }
+    if (prefix_match(split_path(it->first))) { it = e->inventory.erase(it); d = 1; e->inv_dirty = true; }
     else ++it;
   }
   for (auto it = e->ns_cache.begin(); it != e->ns_cache.end();) {
@@ -1183,7 +1261,7 @@ int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
     if (prefix_match(split_path(it->first))) { it = e->other_data.erase(it); d = 1; }
     else ++it;
   }
-  if (p.empty()) { e->constraints.clear(); e->inventory.clear(); e->ns_cache.clear(); e->other_data.clear(); d = 1; }
+  if (p.empty()) { e->constraints.clear(); e->inventory.clear(); e->ns_cache.clear(); e->other_data.clear(); d = 1; e->inv_dirty = true; }
   if (deleted) *deleted = d;
   return GK_OK;
 }

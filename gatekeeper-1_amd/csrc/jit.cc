@@ -444,30 +444,27 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 
 }  // namespace
 
-// Minimum waves per SIMD the template kernels are compiled for (caps VGPRs at
-// 512/n; the compiler spills beyond).  Default 2: measured on config 2 (1M Pods,
-// MI355X), K8sContainerLimits 65 ms at the compiler's own choice (1 wave, 248
-// VGPRs), 41 ms at 2 (256 VGPRs, 8 spills), 69 ms at 4 (128 VGPRs, heavy
-// spills).  Re-measured after the format pass and review ordering
-// (tests/gpu_wpe_sweep.sh): ContainerLimits 11.0 ms at 1, 8.4 ms at 2, 12.5 ms
-// at 3.  GKGPU_JIT_WPE overrides (0 = compiler's choice).
-static std::string wpe_suffix() {
+// Occupancy of a template kernel: minimum waves per SIMD it is compiled for
+// (caps VGPRs at 512/n; the compiler spills beyond) and the lane-heap words it
+// keeps in LDS (devrt.h GK_LDS_HWORDS; with the 8 KB of lane scalars, LDS
+// caps the 256-thread blocks per CU).  History: round 1 measured 2 waves best
+// for K8sContainerLimits (65 ms at the compiler's choice of 1, 41 ms at 2, 69
+// at 4; later 11.0 / 8.4 / 12.5 ms at 1 / 2 / 3).  Round 2 (tools/gpu_r02s.sh,
+// config 2 at 1M Pods, one call): K8sContainerLimits (64 registers) 4.70 ms
+// at 2 waves + 32 heap words, 5.87 at 3 + 16, 6.55 at 4 + 16; K8sRequiredProbes
+// (40 registers) 3.39 / 2.83 / 2.98.  So programs with at most 48 registers
+// get 3 waves and 16 LDS heap words (40 KB per block, three blocks per CU),
+// larger ones 2 waves and 32 words (72 KB, two blocks).  GKGPU_JIT_WPE and
+// GKGPU_LDS_HEAP override both choices (WPE 0 = the compiler's choice).
+static bool small_program(const Program& p) { return p.nregs <= 48; }
+static std::string wpe_suffix(const Program& p) {
   const char* w = getenv("GKGPU_JIT_WPE");
-  int n = w ? atoi(w) : 2;
+  int n = w ? atoi(w) : (small_program(p) ? 3 : 2);
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
-
-// Lane heap words kept in LDS by template kernels (devrt.h GK_LDS_HWORDS):
-// 32 words = 64 KB per 256-thread block, two blocks per CU, which is the
-// occupancy the 256-VGPR template kernels have anyway.  Measured on config 2
-// (1M Pods, tools/gpu_r02m.sh): K8sContainerLimits 5.30 -> 4.84 ms,
-// K8sRequiredProbes 6.07 -> 5.14 ms (16 words: 4.83 / 5.74).  The VM kernel
-// keeps its heap in the private segment (its module also holds the format
-// kernel, whose occupancy a module-wide LDS array would halve).
-// GKGPU_LDS_HEAP overrides (0 = all in the private segment).
-static int lds_heap_words() {
+static int lds_heap_words(const Program& p) {
   const char* v = getenv("GKGPU_LDS_HEAP");
-  int n = v ? atoi(v) : 32;
+  int n = v ? atoi(v) : (small_program(p) ? 16 : 32);
   return n < 0 ? 0 : (n > 64 ? 64 : n);
 }
 
@@ -478,19 +475,19 @@ static bool lds_scalars() {
   return !v || atoi(v) != 0;
 }
 
-static std::string inline_hot_tag() {
+static std::string inline_hot_tag(const Program& p) {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
   if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) t += std::string("m") + m2;
   if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
-  t += "d" + std::to_string(lds_heap_words());
+  t += "d" + std::to_string(lds_heap_words(p));
   if (!lds_scalars()) t += "s0";
   return t;
 }
 
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
   Gen g = generate(p, bank, st);
-  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix() + inline_hot_tag()));
+  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix(p) + inline_hot_tag(p)));
 }
 
 std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
@@ -509,7 +506,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   }
   // GKGPU_INLINE_HOT (A/B switch, default on): inline the per-container builtins
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
-  if (lds_heap_words() > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words() << "\n";
+  if (lds_heap_words(p) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(p) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
@@ -517,7 +514,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
     << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params) {\n"
     << g.body << "}\n"
     << "}  // namespace gk\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix() << ") " << name << "() {\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p) << ") " << name << "() {\n"
     << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"
     << "    gk::" << name << "_pred(L, review, params);\n"
     << "  });\n"

@@ -39,33 +39,45 @@ def test_subset_templates_compile_to_gpu_bytecode():
         assert st == 1, (kind, why)
 
 
+GUARDED = W._tmpl("K8sGuardedEncode", """package k8sguardedencode
+
+violation[{"msg": msg}] {
+	input.review.kind.kind == "Service"
+	input.review.kind.version == "v1"
+	input.review.kind.group == ""
+	x := base64.encode(input.review.object.metadata.name)
+	msg := sprintf("encoded <%v>", [x])
+}
+""")
+
+
 def test_out_of_subset_template_is_explicit_fallback():
     d = gkgpu.Driver()
     cl = Client(d)
-    t = W._tmpl("K8sUniqueServiceSelector", """package k8suniqueserviceselector
+    t = W._tmpl("K8sEncode", """package k8sencode
 
 violation[{"msg": msg}] {
-	other := data.inventory.namespace[namespace][_][_][name]
-	msg := sprintf("same selector as service <%v> in namespace <%v>", [name, namespace])
+	x := base64.encode(input.review.object.metadata.name)
+	msg := sprintf("encoded <%v>", [x])
 }
 """)
     kind = cl.add_template(t)
     st, why = d.template_status(kind)
-    assert st == 0 and "inventory" in why
-    # the guard program: no expression before the join, so every matched review falls back
+    assert st == 0 and "base64.encode" in why
+    # the guard program: no expression before the builtin, so every matched review falls back
     b, why2 = d.template_backend(kind)
-    assert b == 3 and "inventory" in why2
+    assert b == 3 and "base64.encode" in why2
 
 
-def test_guard_program_for_agilebank_unique_service_selector():
-    """demo/agilebank's unique-service-selector is outside the subset (sort,
-    data.inventory), but its `input.review.kind` tests compile into a device
-    guard ahead of the first unsupported expression."""
+def test_guard_program_evaluates_the_supported_prefix():
+    """A template outside the subset (an unsupported builtin) compiles into a
+    device guard: its `input.review.kind` tests run ahead of the first
+    unsupported expression, which is the only fallback point."""
     d = gkgpu.Driver(jit=False)
     cl = Client(d)
-    kind = cl.add_template(W.UNIQUE_SERVICE_SELECTOR)
+    kind = cl.add_template(GUARDED)
     st, why = d.template_status(kind)
-    assert st == 0 and "sort" in why
+    assert st == 0 and "base64.encode" in why
     b, _ = d.template_backend(kind)
     assert b == 3
     asm = d.debug_disasm(kind)
@@ -74,6 +86,26 @@ def test_guard_program_for_agilebank_unique_service_selector():
     head = asm[:asm.index("FAIL_FALLBACK")]
     for lit in ('"Service"', '"v1"', '""'):
         assert lit in head
+
+
+def test_unique_service_selector_join_compiles_to_the_gpu_subset():
+    """demo/agilebank's unique-service-selector (sort + the data.inventory join,
+    regolib src.go:30-31,66-72) is inside the subset: data.inventory is a
+    constant document node the engine points at the synced inventory tree."""
+    for jit in (False, True):
+        d = gkgpu.Driver(jit=jit)
+        cl = Client(d)
+        kind = cl.add_template(W.UNIQUE_SERVICE_SELECTOR)
+        st, why = d.template_status(kind)
+        assert st == 1, why
+        b, detail = d.template_backend(kind)
+        assert b == (2 if jit else 1), detail
+    asm = gkgpu.Driver(jit=False)
+    cl = Client(asm)
+    cl.add_template(W.UNIQUE_SERVICE_SELECTOR)
+    text = asm.debug_disasm("K8sUniqueServiceSelector")
+    assert "FAIL_FALLBACK" not in text
+    assert "sort" in text or "CALL" in text
 
 
 def test_put_modules_replaces_and_delete_modules_counts():

@@ -13,7 +13,7 @@ import gkgpu
 from gkgpu import workloads as W
 from gkgpu.client import Client, augmented_review
 
-from parity import Report, compare, oracle_for, oracle_review, run_objects
+from parity import Report, compare, engine_for, oracle_for, oracle_review, run_objects
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +42,7 @@ def Driver():
     return d
 
 
-def _assert_backend(drv, kinds, guard=("K8sUniqueServiceSelector",)):
+def _assert_backend(drv, kinds, guard=()):
     want = 2 if _BACKEND["jit"] else 1
     for k in kinds:
         b, detail = drv.template_backend(k)
@@ -85,33 +85,98 @@ def test_config2_agilebank_pods():
         assert kernels == {"audit_kernel"}, res.launches
 
 
-def test_config2_guard_program_routes_only_services_to_cpu():
-    """All five demo/agilebank constraints over Pods + Services.  The
-    unique-service-selector template (data.inventory join) runs as a guard
-    program: its kind/version/group tests run on the device after the match,
-    so only v1 Services are flagged for CPU fallback; Pods, apps/v1
-    Deployments and a v2 Service are evaluated on the GPU, bit-exact with the
-    oracle (manager.go:376-380 per object)."""
-    ts, cs = W.config2()
-    assert len(cs) == 5
-    pods, ns_of, ns_objs = W.gen_pods(1500, seed=44, n_namespaces=60)
+def _pods_services_deployments(seed=44, n_pods=1500, n_svc=300, n_dep=100):
+    import random
+    pods, ns_of, ns_objs = W.gen_pods(n_pods, seed=seed, n_namespaces=60)
     objs = list(pods)
     nss = [ns_objs[n] for n in ns_of]
-    n_svc = 0
-    import random
     rng = random.Random(3)
     names = sorted(ns_objs)
-    for i in range(300):
+    svcs = []
+    for i in range(n_svc):
         ns = rng.choice(names)
         av = "v1" if i % 10 else "v2"
-        n_svc += av == "v1"
-        objs.append({"apiVersion": av, "kind": "Service", "metadata": {"name": "svc-%d" % i, "namespace": ns},
-                     "spec": {"selector": {"app": "app-%d" % rng.randint(0, 9)}}})
+        sel = {"app": "app-%d" % rng.randint(0, 9)}
+        if i % 7 == 0:
+            sel["tier"] = rng.choice(["web", "db"])
+        svcs.append({"apiVersion": av, "kind": "Service", "metadata": {"name": "svc-%d" % i, "namespace": ns},
+                     "spec": {"selector": sel}})
         nss.append(ns_objs[ns])
-    for i in range(100):
+    objs += svcs
+    for i in range(n_dep):
         ns = rng.choice(names)
         objs.append({"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d-%d" % i, "namespace": ns}})
         nss.append(ns_objs[ns])
+    return pods, svcs, objs, nss
+
+
+def test_config2_unique_service_selector_join_on_gpu():
+    """All five demo/agilebank constraints over Pods + Services + Deployments,
+    with the Services synced into the inventory (target.go ProcessData paths).
+    unique-service-selector's data.inventory join (regolib src.go:30-31,66-72)
+    and sort run on the device: no review falls back, and every review's
+    results equal the oracle's (manager.go:376-380 per object)."""
+    from gkgpu.client import data_path
+    ts, cs = W.config2()
+    assert len(cs) == 5
+    pods, svcs, objs, nss = _pods_services_deployments()
+    extra = [(data_path(o), o) for o in svcs]
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, nss, extra_data=extra)
+    _assert_clean(rep)
+    per = {}
+    for v in res.results:
+        per[v.constraint_name] = per.get(v.constraint_name, 0) + 1
+    assert per.get("unique-service-selector", 0) > 500, per
+    assert rep.violations > 5000
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
+
+
+def test_unique_service_selector_inventory_changes():
+    """The inventory tree follows put/delete of synced objects between sweeps."""
+    from gkgpu.client import data_path
+    ts, cs = W.config2()
+    _, svcs, objs, nss = _pods_services_deployments(seed=45, n_pods=50, n_svc=80, n_dep=5)
+    drv = Driver()
+    engine_for(drv, ts, cs)
+    od = oracle_for(ts, cs)
+    reviews = [augmented_review(o, n) for o, n in zip(objs, nss)]
+    for step in range(3):
+        if step == 1:
+            for o in svcs[:40]:
+                drv.put_data(data_path(o), o)
+                od.put_data(data_path(o), json.dumps(o))
+        if step == 2:
+            for o in svcs[:20]:
+                drv.delete_data(data_path(o))
+                od.delete_data(data_path(o))
+        rep = compare(od, reviews, drv.review_objects(objs, nss))
+        _assert_clean(rep)
+
+
+GUARDED = W._tmpl("K8sGuardedEncode", """package k8sguardedencode
+
+violation[{"msg": msg}] {
+	input.review.kind.kind == "Service"
+	input.review.kind.version == "v1"
+	input.review.kind.group == ""
+	x := base64.encode(input.review.object.metadata.name)
+	msg := sprintf("encoded <%v>", [x])
+}
+""")
+
+
+def test_guard_program_routes_only_matching_reviews_to_cpu():
+    """A template outside the subset (base64.encode) runs as a guard program:
+    its kind/version/group tests run on the device after the match, so only
+    v1 Services are flagged for CPU fallback; Pods, apps/v1 Deployments and v2
+    Services are evaluated on the GPU, bit-exact with the oracle."""
+    ts, cs = W.config2()
+    ts = ts + [GUARDED]
+    cs = cs + [{"apiVersion": "constraints.gatekeeper.sh/v1beta1", "kind": "K8sGuardedEncode",
+                "metadata": {"name": "guarded"}}]
+    pods, svcs, objs, nss = _pods_services_deployments()
+    n_svc = sum(1 for s in svcs if s["apiVersion"] == "v1")
     drv = Driver()
     rep, res = run_objects(drv, ts, cs, objs, nss)
     assert not rep.mismatches, rep.mismatches[:3]
@@ -119,7 +184,7 @@ def test_config2_guard_program_routes_only_services_to_cpu():
     assert all(res.status[i] == 0 for i in range(len(pods)))
     assert all(res.reason[i] == 12 for i in range(len(objs)) if res.status[i] & 2)  # FB_TEMPLATE
     assert rep.violations > 5000
-    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
+    _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts], guard=("K8sGuardedEncode",))
 
 
 def test_config2_in_kernel_formatting(monkeypatch):
