@@ -95,11 +95,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    xdev = "cuda"  # device of the exchange / timing tensors
     if world > 1:
         import torch
         import torch.distributed as dist  # noqa: F811
+        # GKGPU_DIST_BACKEND=gloo: rehearsal of the multi-rank path on fewer
+        # GPUs than ranks (ranks share devices round-robin; RCCL refuses two
+        # ranks on one GPU), exchange tensors on the host.  Default: RCCL.
+        backend = os.environ.get("GKGPU_DIST_BACKEND", "nccl")
+        if backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
+            xdev = "cpu"
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
 
     import gkgpu
     from gkgpu import workloads as W
@@ -143,7 +151,7 @@ def main():
     t_stage_max = t_stage
     if dist is not None:
         import torch
-        t = torch.tensor([t_stage], dtype=torch.float64, device="cuda")
+        t = torch.tensor([t_stage], dtype=torch.float64, device=xdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_stage_max = float(t.item())
 
@@ -168,7 +176,7 @@ def main():
         from gkgpu.parallel import exchange_audit
         t0 = time.perf_counter()
         writer[0] = exchange_audit(sweep, base, resource, cons_ids, limit=20, dst=0,
-                                   device=torch.device("cuda", local))
+                                   device=torch.device("cuda", local) if xdev == "cuda" else torch.device("cpu"))
         exch_ms.append((time.perf_counter() - t0) * 1000.0)
         return sweep
 
@@ -190,7 +198,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1000.0
@@ -311,6 +319,7 @@ def main():
                 "kernel_templates": kinds_of,
                 "sclk_mhz_measured": sclk_mhz,
                 "device": device_info(local),
+                "dist_backend": (os.environ.get("GKGPU_DIST_BACKEND", "nccl") if dist is not None else None),
                 "stage_s": round(t_stage, 3),
                 "stage_s_max_over_ranks": round(t_stage_max, 3),
                 "stage_ms": {"parse": round(stage_ms[0], 1), "flatten": round(stage_ms[1], 1),

@@ -68,7 +68,7 @@ static_assert(GK_LDS_HWORDS < GK_HCAP, "LDS heap words must leave a private-segm
 constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
 constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged messages)
 #ifndef GK_EMCAP
-#define GK_EMCAP 32
+#define GK_EMCAP 64  // (32 sent dense unique-service-selector joins to the CPU fallback)
 #endif
 constexpr int EMCAP = GK_EMCAP;  // staged violation tuples per lane
 

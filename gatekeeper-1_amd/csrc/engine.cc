@@ -87,10 +87,16 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
   }
   if (!ok) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess;
   const int T = std::max(1, std::min(16, default_threads()));
+  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  double ms_copy = 0, ms_wait = 0;
+  auto t_all = std::chrono::steady_clock::now();
   for (size_t off = 0, k = 0; off < n; off += CH, ++k) {
     const size_t len = std::min(CH, n - off);
     const int b = (int)(k & 1);
+    auto tw = std::chrono::steady_clock::now();
     if (k >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) return false;
+    auto tc = std::chrono::steady_clock::now();
+    ms_wait += std::chrono::duration<double, std::milli>(tc - tw).count();
     char* dstp = pin[b];
     const char* srcp = src + off;
     std::vector<std::thread> th;
@@ -101,10 +107,15 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
     for (int t = 1; t < T; ++t) th.emplace_back(part, t);
     part(0);
     for (auto& x : th) x.join();
+    ms_copy += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
     if (hipMemcpyAsync((char*)dst + off, dstp, len, hipMemcpyHostToDevice, st) != hipSuccess) return false;
     if (hipEventRecord(ev[b], st) != hipSuccess) return false;
   }
-  return hipStreamSynchronize(st) == hipSuccess;
+  const bool ok_sync = hipStreamSynchronize(st) == hipSuccess;
+  if (trace)
+    fprintf(stderr, "upload: %.1f MB in %.1f ms (host copies %.1f ms, DMA waits %.1f ms, %d threads)\n", n / 1e6,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_all).count(), ms_copy, ms_wait, T);
+  return ok_sync;
 }
 
 struct DBuf {
@@ -740,6 +751,14 @@ static bool up(DBuf& b, const std::vector<T>& v, bool append_only) {
 static bool sync_tables(gk_engine* e, bool nodes = true) {
   Store& st = e->st;
   bool ok = true;
+  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!trace) return;
+    auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "sync_tables: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  };
   if (nodes) {
     // only the nodes appended (or rewritten after a transient reset) since the
     // last upload travel: a staged 1M-review batch is not re-sent per call
@@ -750,13 +769,17 @@ static bool sync_tables(gk_engine* e, bool nodes = true) {
                       (n - e->dev_nodes_ok) * sizeof(Node), hipMemcpyHostToDevice) == hipSuccess;
     if (ok) { e->dev_nodes_ok = (uint32_t)n; e->d_nodes.used = n * sizeof(Node); }
   }
+  lap("nodes");
   ok &= up(e->d_strs, st.strings(), true);
+  lap("strs");
   // +16: the device reads string bytes a dword at a time (devrt.h ByteRd) and may
   // touch up to 3 bytes past the last string
   ok &= e->d_pool.reserve(st.pool().size() + 16);
   ok &= e->d_pool.upload(st.pool().data(), st.pool().size(), true);
+  lap("pool");
   ok &= up(e->d_sflags, st.str_flags(), true);
   ok &= up(e->d_nums, st.numbers(), true);
+  lap("flags+nums");
   ok &= up(e->d_code, e->bank.code, false);
   ok &= up(e->d_K, e->bank.consts, false);
   std::vector<uint32_t> fmt = e->bank.fmt;
@@ -779,6 +802,7 @@ static bool sync_tables(gk_engine* e, bool nodes = true) {
   ok &= up(e->d_dfa_keys, dk, false);
   ok &= up(e->d_dfa_meta, dm, false);
   ok &= up(e->d_dfa_words, dw, false);
+  lap("rest");
   return ok;
 }
 
@@ -1596,8 +1620,18 @@ static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
     return GK_OK;
   }
   if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
-  if (!sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
-      !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
+  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  bool up_ok = sync_tables(e, false);
+  const double ms_tables = ms_since(t1);
+  up_ok = up_ok && up(b->d_revs, b->cols, false);
+  const double ms_cols = ms_since(t1);
+  up_ok = up_ok && b->d_nodes.reserve((size_t)b->node_end * sizeof(Node));
+  const double ms_alloc = ms_since(t1);
+  up_ok = up_ok && b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false);
+  if (trace)
+    fprintf(stderr, "stage upload: tables %.1f ms, columns %.1f ms, node alloc %.1f ms, nodes %.1f ms\n", ms_tables,
+            ms_cols - ms_tables, ms_alloc - ms_cols, ms_since(t1) - ms_alloc);
+  if (!up_ok) {
     b->d_revs.free_();
     b->d_nodes.free_();
     delete b;

