@@ -269,5 +269,9 @@ struct DevArgs {
 // deferred-message record: w[0] = fidx | nargs << 24 | FREC_LIVE, w[1..nargs] = args
 constexpr uint32_t FREC_WORDS = 8;
 constexpr uint64_t FREC_LIVE = 1ull << 63;
+// the tuple's details are `{}` (the hook default for a result without
+// details): the format pass writes them after the message, the audit kernel
+// writes no bytes for it
+constexpr uint64_t FREC_DET_OBJ = 1ull << 62;
 
 }  // namespace gk

@@ -1184,11 +1184,15 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
       const uint64_t* rec = (const uint64_t*)(L.B + o);
       uint32_t na = (uint32_t)rec[0] >> 24;
       uint64_t* w = gk_args.frec + (uint64_t)(bt + i) * FREC_WORDS;
-      w[0] = rec[0] | FREC_LIVE;
+      const char* det = L.B + o + 8 * (1 + na);
+      const bool obj = dl == 2 && det[0] == '{' && det[1] == '}';
+      w[0] = rec[0] | FREC_LIVE | (obj ? FREC_DET_OBJ : 0);
       for (uint32_t j = 0; j < na; ++j) w[1 + j] = rec[1 + j];
-      GOut gd{(uint8_t*)gk_args.bytes, bb + ml, bb + ml, 0, false};
-      puts_(gd, L.B + o + 8 * (1 + na), dl);
-      gd.finish();
+      if (!obj) {
+        GOut gd{(uint8_t*)gk_args.bytes, bb + ml, bb + ml, 0, false};
+        puts_(gd, det, dl);
+        gd.finish();
+      }
     } else if (dw & 0x8000u) {
       // deferred message (op_emit): record [fidx | nargs << 24, args...], then details
       const uint64_t* rec = (const uint64_t*)(L.B + o);

@@ -168,12 +168,18 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
     uint64_t lo4 = lo & ~(uint64_t)3, hi4 = (hi + 3) & ~(uint64_t)3;
     if (tot == hi - lo && hi4 - lo4 <= FSTAGE && hi4 <= gk_args.bytes_cap) {
       uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
-      for (uint32_t k = lane; k < nw; k += 64) st[k] = gw[(lo4 >> 2) + k];
+      // the range's bytes are read first unless this pass writes all of them:
+      // every tuple live with no details bytes from the audit kernel
+      // (FREC_DET_OBJ or none); the edge dwords are written bytewise anyway
+      const bool whole = __all(!valid || (live && ((h & FREC_DET_OBJ) || v.det_len == 0)));
+      if (!whole)
+        for (uint32_t k = lane; k < nw; k += 64) st[k] = gw[(lo4 >> 2) + k];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       if (live) {
         LOut o{stb + (v.msg_off - lo4), 0};
         fmt_run(L, o, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
+        if (h & FREC_DET_OBJ) { o.put('{'); o.put('}'); }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -189,6 +195,7 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
     } else if (live) {
       GOut g{(uint8_t*)gk_args.bytes, v.msg_off, v.msg_off, 0, false};
       fmt_run(L, g, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
+      if (h & FREC_DET_OBJ) { g.put('{'); g.put('}'); }
       g.finish();
     }
   }
