@@ -2017,6 +2017,25 @@ int gk_results_get(const gk_results* r, size_t i, gk_result_view* out) {
   return GK_OK;
 }
 
+int gk_results_export(const gk_results* r, void* buf, size_t cap, size_t* needed) {
+  if (!r) return GK_EINVAL;
+  size_t n = 0;
+  for (const ResultRow& row : r->rows) n += 16 + row.msg.size() + row.details.size();
+  if (needed) *needed = n;
+  if (!buf || cap < n) return buf ? GK_EINVAL : GK_OK;
+  char* p = (char*)buf;
+  for (const ResultRow& row : r->rows) {
+    const uint32_t h[4] = {row.review, row.constraint, (uint32_t)row.msg.size(), (uint32_t)row.details.size()};
+    memcpy(p, h, 16);
+    p += 16;
+    if (!row.msg.empty()) memcpy(p, row.msg.data(), row.msg.size());
+    p += row.msg.size();
+    if (!row.details.empty()) memcpy(p, row.details.data(), row.details.size());
+    p += row.details.size();
+  }
+  return GK_OK;
+}
+
 size_t gk_results_reviews(const gk_results* r) { return r ? std::max<size_t>(r->nrev, r->status.size()) : 0; }
 uint32_t gk_results_review_status(const gk_results* r, size_t i) { return r && i < r->status.size() ? r->status[i] : 0; }
 uint32_t gk_results_review_reason(const gk_results* r, size_t i) { return r && i < r->reason.size() ? r->reason[i] : 0; }

@@ -31,6 +31,7 @@ EXPORTS = [
     "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
+    "gk_results_export",
 ]
 
 
@@ -124,6 +125,7 @@ def load_library():
     lib.gk_results_count.argtypes = [vp]
     lib.gk_results_count.restype = sz
     lib.gk_results_get.argtypes = [vp, sz, C.POINTER(_View)]
+    lib.gk_results_export.argtypes = [vp, vp, sz, C.POINTER(sz)]
     lib.gk_results_reviews.argtypes = [vp]
     lib.gk_results_reviews.restype = sz
     lib.gk_results_review_status.argtypes = [vp, sz]
@@ -538,6 +540,28 @@ class Driver:
         self._check(self._lib.gk_query_batch(self._e, arr, lens, len(strs), C.byref(out)))
         return _collect(self._lib, out)
 
+    def query_batch_export(self, inputs: Sequence):
+        """gk_query_batch, then every result row copied out in one call
+        (gk_results_export) -- what a native caller does with the result views
+        -- plus the per-review status words.  Returns (blob, status); parse
+        the rows with export_rows(blob)."""
+        strs = [x if isinstance(x, str) else json.dumps(x) for x in inputs]
+        arr, lens, _keep = _arr(strs)
+        out = C.c_void_p()
+        self._check(self._lib.gk_query_batch(self._e, arr, lens, len(strs), C.byref(out)))
+        h = out
+        try:
+            need = C.c_size_t()
+            self._lib.gk_results_export(h, None, 0, C.byref(need))
+            buf = C.create_string_buffer(max(1, need.value))
+            self._check(self._lib.gk_results_export(h, buf, need.value, C.byref(need)))
+            nr = self._lib.gk_results_reviews(h)
+            st = (C.c_uint32 * max(1, nr))()
+            self._lib.gk_results_copy_status(h, st, None)
+            return buf.raw[:need.value], st[:nr]
+        finally:
+            self._lib.gk_results_free(h)
+
     def review_objects(self, objs: Sequence, namespaces: Sequence) -> Results:
         o = [x if isinstance(x, str) else json.dumps(x) for x in objs]
         n = [None if x is None else (x if isinstance(x, str) else json.dumps(x)) for x in namespaces]
@@ -651,3 +675,20 @@ class Driver:
             self._lib.gk_constraint_info(self._e, i, C.byref(k), C.byref(nm))
             out.append((k.value.decode(), nm.value.decode()))
         return out
+
+
+def export_rows(blob: bytes):
+    """(review, constraint index, msg, details JSON) of every row of a
+    gk_results_export buffer, in result order."""
+    import struct
+    out = []
+    i, n = 0, len(blob)
+    while i < n:
+        rv, c, ml, dl = struct.unpack_from("<IIII", blob, i)
+        i += 16
+        msg = blob[i:i + ml].decode("utf-8", "surrogateescape")
+        i += ml
+        det = blob[i:i + dl].decode("utf-8", "surrogateescape")
+        i += dl
+        out.append((rv, c, msg, det))
+    return out

@@ -185,6 +185,11 @@ typedef struct {
 
 size_t gk_results_count(const gk_results* r);
 int gk_results_get(const gk_results* r, size_t i, gk_result_view* out);
+/* every result row in one buffer (a caller's bulk copy instead of one
+ * gk_results_get per row): per row, u32 review, u32 constraint, u32 msg_len,
+ * u32 details_len, then the message and details bytes, unpadded.  *needed
+ * receives the byte size; GK_EINVAL when cap is smaller (nothing written). */
+int gk_results_export(const gk_results* r, void* buf, size_t cap, size_t* needed);
 size_t gk_results_reviews(const gk_results* r);
 uint32_t gk_results_review_status(const gk_results* r, size_t review);
 uint32_t gk_results_review_reason(const gk_results* r, size_t review);

@@ -564,6 +564,12 @@ def test_config5_webhook_micro_batch():
     assert rep.violations >= 256 * 10
     resp = handle_batch(drv, ins)
     assert all(r.code == DENIED for r in resp)
+    # the bulk export (gk_results_export) carries exactly the per-row views
+    from gkgpu.driver import export_rows
+    blob, st = drv.query_batch_export(ins)
+    rows = export_rows(blob)
+    assert [(r[0], r[2], r[3]) for r in rows] == [(x.review, x.msg, x.details_json) for x in res.results]
+    assert list(st) == list(res.status)
 
 
 STR_BUILTINS = W._tmpl("K8sStrBuiltins", """package k8sstrbuiltins
