@@ -1,3 +1,4 @@
+#include <algorithm>
 // Template JIT (see jit.h).
 #include "jit.h"
 
@@ -130,6 +131,137 @@ FmtFlow fmt_flow(const Program& p, const CodeBank& bank) {
   return F;
 }
 
+// Available lookups: which registers already hold R[base][K[x]] on entry to
+// each instruction, on every path (forward must-analysis over the template's
+// control-flow graph).  Rego values are immutable and rule bodies have no side
+// effects, so a lookup whose base and result registers are unchanged since
+// can be replaced by a copy.  This reaches across inlined function calls:
+// K8sContainerLimits' missing(container.resources.limits, "cpu") reads
+// limits["cpu"], which the group prologue already looked up (compiler.cc
+// group_prologue).  A fact dies when its base or result register is written
+// (or forced from a deferred sprintf), and all facts die at OP_ITER_NEXT, where
+// the lane heap of the previous iteration is reclaimed.
+struct LookFlow {
+  struct Fact { uint16_t base; uint32_t kidx; uint16_t res; };
+  struct State {
+    bool top = true;                     // not reached yet (identity of the meet)
+    std::vector<Fact> facts;             // sorted by (base, kidx)
+    std::map<uint16_t, uint32_t> konst;  // register -> constant index (OP_LOADK)
+  };
+  std::vector<State> in;
+  // register holding R[base][K[kidx]] on entry to instruction k, or -1
+  int find(uint32_t k, uint16_t base, uint32_t kidx) const {
+    if (k >= in.size() || in[k].top) return -1;
+    for (const Fact& f : in[k].facts) if (f.base == base && f.kidx == kidx) return f.res;
+    return -1;
+  }
+  int konst(uint32_t k, uint16_t r) const {
+    if (k >= in.size() || in[k].top) return -1;
+    auto it = in[k].konst.find(r);
+    return it == in[k].konst.end() ? -1 : (int)it->second;
+  }
+};
+
+static bool lookflow_on() {
+  const char* v = getenv("GKGPU_JIT_CSE");  // A/B switch, default on
+  return !v || atoi(v) != 0;
+}
+
+LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
+  const uint32_t b0 = p.code_off, n = p.code_len;
+  LookFlow LF;
+  LF.in.assign(n, LookFlow::State{});
+  if (!lookflow_on()) return LF;
+  using State = LookFlow::State;
+  auto kill = [](State& s, uint32_t r) {
+    if (r == 0xffff) return;
+    s.facts.erase(std::remove_if(s.facts.begin(), s.facts.end(),
+                                 [&](const LookFlow::Fact& f) { return f.base == r || f.res == r; }),
+                  s.facts.end());
+    s.konst.erase((uint16_t)r);
+  };
+  auto add = [](State& s, uint16_t base, uint32_t kidx, uint16_t res) {
+    if (base == res) return;
+    for (auto& f : s.facts)
+      if (f.base == base && f.kidx == kidx) { f.res = res; return; }
+    s.facts.push_back({base, kidx, res});
+    std::sort(s.facts.begin(), s.facts.end(), [](const LookFlow::Fact& x, const LookFlow::Fact& y) {
+      return x.base != y.base ? x.base < y.base : x.kidx < y.kidx;
+    });
+  };
+  std::vector<uint32_t> work;
+  auto flow = [&](uint32_t to, const State& s) {
+    if (to < b0 || to >= b0 + n) return;
+    State& d = LF.in[to - b0];
+    if (d.top) { d = s; d.top = false; work.push_back(to - b0); return; }
+    // meet: facts and constants present (identically) on both sides
+    std::vector<LookFlow::Fact> nf;
+    for (const auto& f : d.facts)
+      for (const auto& g : s.facts)
+        if (f.base == g.base && f.kidx == g.kidx && f.res == g.res) { nf.push_back(f); break; }
+    std::map<uint16_t, uint32_t> nk;
+    for (const auto& kv : d.konst) {
+      auto it = s.konst.find(kv.first);
+      if (it != s.konst.end() && it->second == kv.second) nk.insert(kv);
+    }
+    if (nf.size() != d.facts.size() || nk.size() != d.konst.size()) {
+      d.facts.swap(nf);
+      d.konst.swap(nk);
+      work.push_back(to - b0);
+    }
+  };
+  if (n) { LF.in[0].top = false; work.push_back(0); }
+  while (!work.empty()) {
+    uint32_t k = work.back();
+    work.pop_back();
+    const Ins& in = bank.code[b0 + k];
+    State s = LF.in[k];
+    for (uint32_t r : fmt_reads(in)) if (F.has(k, r)) kill(s, r);  // forced here
+    const uint32_t next = b0 + k + 1;
+    switch (in.op) {
+      case OP_END: case OP_FAIL_FALLBACK: continue;
+      case OP_JMP: flow(in.x, s); continue;
+      case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: flow(in.x, s); flow(next, s); continue;
+      case OP_ITER_NEXT: {
+        s.facts.clear();
+        flow(in.x, s);
+        kill(s, in.b);
+        kill(s, in.c);
+        flow(next, s);
+        continue;
+      }
+      case OP_MEMO_GET: {
+        State t = s;
+        kill(t, in.a);
+        flow(in.x, t);
+        flow(next, s);
+        continue;
+      }
+      case OP_LOADK: kill(s, in.a); s.konst[in.a] = in.x; break;
+      case OP_MOV: {
+        auto it = s.konst.find(in.b);
+        const int kb = it == s.konst.end() ? -1 : (int)it->second;
+        kill(s, in.a);
+        if (kb >= 0) s.konst[in.a] = (uint32_t)kb;
+        break;
+      }
+      case OP_GETK: kill(s, in.a); add(s, in.b, in.x, in.a); break;
+      case OP_GET: {
+        auto it = s.konst.find(in.c);
+        const int kc = it == s.konst.end() ? -1 : (int)it->second;
+        kill(s, in.a);
+        if (kc >= 0 && in.a != in.c) add(s, in.b, (uint32_t)kc, in.a);
+        break;
+      }
+      case OP_ITER_INIT: kill(s, in.a); kill(s, in.a + 1u); break;
+      case OP_EMIT: case OP_MEMO_PUT: case OP_ORD: break;
+      default: kill(s, in.a); break;
+    }
+    flow(next, s);
+  }
+  return LF;
+}
+
 // A literal re_match pattern's DFA (regex.cc layout; the semantics of re_run /
 // run_regex_dfa) as code: a switch over states with byte ranges as compares,
 // so matching loads only the subject's bytes.  "" when too large to inline.
@@ -246,6 +378,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   const char* lm = getenv("GKGPU_JIT_LMEMO");
   if (!lm || atoi(lm) == 0) for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
   FmtFlow F = fmt_flow(p, bank);
+  LookFlow LK = look_flow(p, bank, F);
   Gen g;
   // literal re_match patterns compiled to code
   std::vector<std::pair<uint64_t, std::string>> relits;  // (pattern value, function)
@@ -307,8 +440,21 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       case OP_LOADREV: o << a << " = review;"; break;
       case OP_LOADPARAM: o << a << " = params;"; break;
       case OP_MOV: o << a << " = " << b << ";"; break;
-      case OP_GET: o << a << " = vget(L, " << b << ", " << c << ");"; break;
-      case OP_GETK: o << a << " = vget(L, " << b << ", " << lit(bank.consts[in.x]) << ");"; break;
+      case OP_GET: {
+        const int kc = LK.konst(k, in.c);
+        const int have = kc >= 0 ? LK.find(k, in.b, (uint32_t)kc) : -1;
+        if (have == (int)in.a) o << "/* " << a << " holds " << b << "[" << c << "] */";
+        else if (have >= 0) o << a << " = " << R((uint32_t)have) << ";  // = vget(L, " << b << ", " << c << ")";
+        else o << a << " = vget(L, " << b << ", " << c << ");";
+        break;
+      }
+      case OP_GETK: {
+        const int have = LK.find(k, in.b, in.x);
+        if (have == (int)in.a) o << "/* " << a << " holds " << b << "[K" << in.x << "] */";
+        else if (have >= 0) o << a << " = " << R((uint32_t)have) << ";  // = vget(L, " << b << ", K" << in.x << ")";
+        else o << a << " = vget(L, " << b << ", " << lit(bank.consts[in.x]) << ");";
+        break;
+      }
       case OP_ITER_INIT: o << "op_iter_init(L, " << a << ", " << R(in.a + 1) << ", " << b << ", " << y << ");"; break;
       case OP_ITER_NEXT:
         o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next(L, " << a << ", " << R(in.a + 1)
