@@ -122,7 +122,7 @@ enum Builtin : uint32_t {
   BI_COUNT = 0, BI_ANY, BI_ALL, BI_STARTSWITH, BI_ENDSWITH, BI_CONTAINS, BI_RE_MATCH, BI_TO_NUMBER,
   BI_REPLACE, BI_SUBSTRING, BI_IS_NUMBER, BI_IS_STRING, BI_IS_BOOLEAN, BI_IS_ARRAY, BI_IS_OBJECT,
   BI_IS_SET, BI_IS_NULL, BI_LOWER, BI_UPPER, BI_TRIM, BI_SPLIT, BI_CONCAT, BI_INDEXOF,
-  BI_TRIM_PREFIX, BI_TRIM_SUFFIX, BI_SORT, BI_COUNT_
+  BI_TRIM_PREFIX, BI_TRIM_SUFFIX, BI_SORT, BI_ARRAY_CONCAT, BI_COUNT_
 };
 
 // per-(review) outcome flags

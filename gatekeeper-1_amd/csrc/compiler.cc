@@ -55,14 +55,14 @@ const std::map<std::string, uint32_t> kBuiltins = {
     {"is_array", BI_IS_ARRAY}, {"is_object", BI_IS_OBJECT}, {"is_set", BI_IS_SET}, {"is_null", BI_IS_NULL},
     {"lower", BI_LOWER}, {"upper", BI_UPPER}, {"trim", BI_TRIM}, {"split", BI_SPLIT}, {"concat", BI_CONCAT},
     {"indexof", BI_INDEXOF}, {"trim_prefix", BI_TRIM_PREFIX}, {"trim_suffix", BI_TRIM_SUFFIX},
-    {"sort", BI_SORT},
+    {"sort", BI_SORT}, {"array.concat", BI_ARRAY_CONCAT},
 };
 const std::map<uint32_t, int> kArity = {
     {BI_COUNT, 1}, {BI_ANY, 1}, {BI_ALL, 1}, {BI_STARTSWITH, 2}, {BI_ENDSWITH, 2}, {BI_CONTAINS, 2},
     {BI_RE_MATCH, 2}, {BI_TO_NUMBER, 1}, {BI_REPLACE, 3}, {BI_SUBSTRING, 3}, {BI_IS_NUMBER, 1},
     {BI_IS_STRING, 1}, {BI_IS_BOOLEAN, 1}, {BI_IS_ARRAY, 1}, {BI_IS_OBJECT, 1}, {BI_IS_SET, 1},
     {BI_IS_NULL, 1}, {BI_LOWER, 1}, {BI_UPPER, 1}, {BI_TRIM, 2}, {BI_SPLIT, 2}, {BI_CONCAT, 2},
-    {BI_INDEXOF, 2}, {BI_TRIM_PREFIX, 2}, {BI_TRIM_SUFFIX, 2}, {BI_SORT, 1},
+    {BI_INDEXOF, 2}, {BI_TRIM_PREFIX, 2}, {BI_TRIM_SUFFIX, 2}, {BI_SORT, 1}, {BI_ARRAY_CONCAT, 2},
 };
 const std::map<std::string, uint32_t> kCmp = {{"equal", CMP_EQ}, {"neq", CMP_NE}, {"lt", CMP_LT},
                                               {"lte", CMP_LE}, {"gt", CMP_GT}, {"gte", CMP_GE}};

@@ -1511,6 +1511,25 @@ __device__ uint64_t bi_sort(PLane& L, uint64_t a) {
   return out;
 }
 
+// array.concat (topdown/array.go builtinArrayConcat): two arrays -> one new
+// heap array (a type error otherwise)
+__device__ uint64_t bi_array_concat(PLane& L, uint64_t a, uint64_t b) {
+  const uint64_t UND = mkv(V_UNDEF, 0);
+  if (tclass(a) != 7 || tclass(b) != 7) { lane_error(L); return UND; }
+  const uint32_t na = coll_len(L, a), nb = coll_len(L, b);
+  uint64_t out = list_new(L, LK_ARR, na + nb);
+  if (vtag(out) == V_UNDEF) return UND;
+  const uint32_t o = list_off(out);
+  for (uint32_t i = 0; i < na + nb; ++i) {
+    uint64_t k, v;
+    if (i < na) coll_at(L, a, i, k, v);
+    else coll_at(L, b, i - na, k, v);
+    hset(L, o + 2 + i, v);
+  }
+  hset(L, o, na + nb);
+  return out;
+}
+
 __device__ uint64_t call_builtin(PLane& L, uint32_t id, const uint64_t* a) {
   switch (id) {
     case BI_COUNT: return bi_count(L, a[0]);
@@ -1534,6 +1553,7 @@ __device__ uint64_t call_builtin(PLane& L, uint32_t id, const uint64_t* a) {
     case BI_CONCAT: return bi_concat(L, a[0], a[1]);
     case BI_INDEXOF: return bi_indexof(L, a[0], a[1]);
     case BI_SORT: return bi_sort(L, a[0]);
+    case BI_ARRAY_CONCAT: return bi_array_concat(L, a[0], a[1]);
     default: break;
   }
   lane_fallback(L, FB_UNSUPPORTED);
@@ -1964,8 +1984,14 @@ __device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, 
   for (uint32_t s = 0; s < nseg; ++s) {
     const uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
     if (kind == 0) { put_sid(o, a); continue; }
-    const uint64_t v = args[a & 0xffff];
     const uint32_t verb = a >> 16;
+#ifdef GK_DIAG_SIZE_BOUND
+    // diagnostics only (cost of the sizing loads): a 64-byte over-estimate
+    // per argument, no loads; messages come out padded, not comparable
+    o.n += 64;
+    continue;
+#endif
+    const uint64_t v = args[a & 0xffff];
     if (vtag(v) == V_STR) {
       const uint32_t n = gk_args.strs[(uint32_t)vpay(v)].len;
       GK_TOUCH_STR((uint32_t)vpay(v));

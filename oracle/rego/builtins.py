@@ -347,6 +347,15 @@ def sort(a):
     _err(1, a, "array", "set")
 
 
+def array_concat(a, b):
+    """topdown/array.go builtinArrayConcat: both operands arrays."""
+    if not isinstance(a, Arr):
+        _err(1, a, "array")
+    if not isinstance(b, Arr):
+        _err(2, b, "array")
+    return Arr(list(a) + list(b))
+
+
 def abs_(a):
     n = _num(a, 1)
     return Num.from_bf(bf_round(abs(bf_to_fraction(n.bf))))
@@ -400,6 +409,7 @@ BUILTINS = {
     "re_match": re_match, "regex.match": re_match, "to_number": to_number,
     "is_number": is_number, "is_string": is_string, "is_boolean": is_boolean, "is_array": is_array,
     "is_set": is_set, "is_object": is_object, "is_null": is_null, "type_name": type_name, "sort": sort,
+    "array.concat": array_concat,
 }
 BUILTINS = {k: v for k, v in BUILTINS.items() if v is not None}
 
@@ -409,5 +419,5 @@ ARITY = {
     "startswith": 2, "endswith": 2, "contains": 2, "replace": 3, "substring": 3, "split": 2, "concat": 2,
     "trim": 2, "trim_prefix": 2, "trim_suffix": 2, "lower": 1, "upper": 1, "indexof": 2, "sprintf": 2,
     "re_match": 2, "regex.match": 2, "to_number": 1, "is_number": 1, "is_string": 1, "is_boolean": 1,
-    "is_array": 1, "is_set": 1, "is_object": 1, "is_null": 1, "type_name": 1, "sort": 1,
+    "is_array": 1, "is_set": 1, "is_object": 1, "is_null": 1, "type_name": 1, "sort": 1, "array.concat": 2,
 }

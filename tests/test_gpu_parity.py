@@ -165,6 +165,34 @@ def test_unique_service_selector_inventory_changes():
         _assert_clean(rep)
 
 
+def test_unique_label_join_on_gpu():
+    """demo/basic's K8sUniqueLabel (data.inventory over both scopes,
+    array.concat, negated helper calls) over Namespaces synced as inventory:
+    results equal the oracle's.  The template materialises every inventory
+    object in lane-heap arrays, so beyond a few dozen objects the lanes go to
+    the CPU fallback (FB_HEAP) -- still bit-exact for the rest."""
+    import random
+    from gkgpu.client import data_path
+    ts = [W.UNIQUE_LABEL]
+    cs = [W.constraint("K8sUniqueLabel", "ns-gk-label-unique",
+                       match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
+                       parameters={"label": "gatekeeper"})]
+    for n, want_fb in ((12, False), (60, True)):
+        rng = random.Random(n)
+        nss = []
+        for i in range(n):
+            labels = {"gatekeeper": "v%d" % rng.randint(0, n // 3)} if rng.random() < 0.7 else {}
+            nss.append({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns-%03d" % i, "labels": labels}})
+        drv = Driver()
+        rep, res = run_objects(drv, ts, cs, nss, [None] * n, extra_data=[(data_path(o), o) for o in nss])
+        assert not rep.mismatches, rep.mismatches[:3]
+        if want_fb:
+            assert rep.fallback > 0 and all(res.reason[i] == 1 for i in range(n) if res.status[i] & 2), rep
+        else:
+            assert rep.fallback == 0 and rep.violations >= 2, rep
+        _assert_backend(drv, ["K8sUniqueLabel"])
+
+
 GUARDED = W._tmpl("K8sGuardedEncode", """package k8sguardedencode
 
 violation[{"msg": msg}] {

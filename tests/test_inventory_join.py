@@ -119,3 +119,45 @@ def test_inventory_tree_follows_puts_and_deletes():
         assert viol == _oracle_count(od, objs, objns), step
         seen.append(viol)
     assert seen[0] == 0 and seen[3] > seen[1] > 0
+
+
+def _namespaces(n, seed=7):
+    import random
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        labels = {}
+        if rng.random() < 0.7:
+            labels["gatekeeper"] = "v%d" % rng.randint(0, n // 3)
+        out.append({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns-%03d" % i, "labels": labels}})
+    return out
+
+
+def test_unique_label_counts_match_oracle():
+    """demo/basic's K8sUniqueLabel (array.concat over both inventory scopes,
+    `not identical_*` negations) on the host runtime vs the oracle, with the
+    Namespaces synced as cluster-scoped inventory."""
+    ts = [W.UNIQUE_LABEL]
+    cs = [W.constraint("K8sUniqueLabel", "ns-gk-label-unique",
+                       match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
+                       parameters={"label": "gatekeeper"})]
+    # the template materialises every inventory object in two lane-heap arrays
+    # and their concatenation: small inventories fit the 128-word lane heap
+    # (larger ones go to the CPU fallback, FB_HEAP)
+    nss = _namespaces(12)
+    extra = [(data_path(o), o) for o in nss]
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    for p, o in extra:
+        d.put_data(p, o)
+    assert d.template_status("K8sUniqueLabel")[0] == 1, d.template_status("K8sUniqueLabel")
+    b = d.stage_objects(nss, [None] * len(nss))
+    _, _, viol, _, flagged = cpu_baseline.sweep(d, b, threads=2)
+    want = _oracle_count(oracle_for(ts, cs, extra), nss, [None] * len(nss))
+    assert flagged == 0
+    assert want >= 2
+    assert viol == want
