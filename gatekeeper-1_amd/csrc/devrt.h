@@ -1692,6 +1692,17 @@ __device__ __forceinline__ uint64_t lazy_sprintf(PLane& L, uint32_t fidx, uint64
   return mkv(V_FMT, ((uint64_t)fidx << 32) | idx);
 }
 
+// lazy_sprintf with the format's argument count known at compile time (jit.cc)
+__device__ __forceinline__ uint64_t lazy_sprintf_n(PLane& L, uint32_t fidx, uint64_t args, uint32_t want) {
+  if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
+  uint32_t t = vtag(args);
+  if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
+  uint32_t idx = t == V_NODE ? ((uint32_t)vpay(args) | 0x80000000u) : list_off(args);
+  if (t == V_NODE && (uint32_t)vpay(args) >= 0x80000000u) return do_sprintf(L, fidx, args);
+  if (coll_len(L, args) != want) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
+  return mkv(V_FMT, ((uint64_t)fidx << 32) | idx);
+}
+
 // the string a deferred sprintf denotes, built in the lane buffer
 __device__ uint64_t force_fmt(PLane& L, uint64_t v) {
   if (vtag(v) != V_FMT) return v;

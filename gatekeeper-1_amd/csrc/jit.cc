@@ -503,7 +503,10 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         break;
       }
       case OP_SPRINTF:
-        o << a << " = " << (lazy_fmt(in) ? "lazy_sprintf" : "do_sprintf") << "(L, " << in.x << "u, " << b << ");";
+        if (lazy_fmt(in) && in.x + 1 < bank.fmt.size())  // argument count as an immediate (no table load)
+          o << a << " = lazy_sprintf_n(L, " << in.x << "u, " << b << ", " << bank.fmt[in.x + 1] << "u);";
+        else
+          o << a << " = " << (lazy_fmt(in) ? "lazy_sprintf" : "do_sprintf") << "(L, " << in.x << "u, " << b << ");";
         break;
       case OP_LEN_EQ: o << a << " = op_len_eq(L, " << b << ", " << y << ");"; break;
       case OP_EMIT:
