@@ -691,6 +691,10 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
   if (const char* dd = getenv("GKGPU_JIT_DUMP")) {  // diagnostics: keep the generated source
     if (*dd) write_file_atomic(dd, key + ".hip", src);
   }
+  if (getenv("GKGPU_JIT_DUMP_ONLY")) {  // host tests of the generator: no hipRTC (the template stays on the VM)
+    log = "GKGPU_JIT_DUMP_ONLY";
+    return false;
+  }
   hiprtcProgram prog;
   const char* hs[] = {gk_rt_common_h, gk_rt_devrt_h};
   const char* hn[] = {"common.h", "devrt.h"};
