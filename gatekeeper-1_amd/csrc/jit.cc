@@ -479,13 +479,27 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           case BI_STARTSWITH: case BI_ENDSWITH: case BI_CONTAINS:
             o << a << " = bi_strpred(L, " << in.y << "u, " << A0 << ", " << A1 << ");";
             break;
-          case BI_RE_MATCH:
+          case BI_RE_MATCH: {
+            // re_match is pure: with interned pattern and subject (the usual
+            // case: a constraint parameter against a document value) the
+            // cross-lane memo answers repeats of the pair from L2 instead of
+            // stepping the DFA over the subject's bytes again (gm_put keeps
+            // only successful booleans).  GKGPU_RE_MEMO=0: A/B switch.
+            const char* rm = getenv("GKGPU_RE_MEMO");
+            const bool memo_re = !rm || atoi(rm) != 0;
+            const std::string site = std::to_string(0x10000u + k) + "u";
             o << "{ uint64_t p_ = " << A0 << ", s_ = " << A1 << "; if (!is_strv(p_) || !is_strv(s_)) { lane_error(L); "
               << a << " = " << UND << "; }";
-            for (auto& rl : relits)
-              o << " else if (p_ == " << lit(rl.first) << ") " << a << " = re_result(L, " << rl.second << "(sview(L, s_)));";
-            o << " else " << a << " = re_result(L, re_run(L, p_, s_)); }";
+            if (memo_re) o << " else if (gm_get(" << site << ", p_, s_, " << a << ")) {}";
+            o << " else {";
+            for (size_t i = 0; i < relits.size(); ++i)
+              o << (i ? " else if (p_ == " : " if (p_ == ") << lit(relits[i].first) << ") " << a << " = re_result(L, "
+                << relits[i].second << "(sview(L, s_)));";
+            o << (relits.empty() ? " " : " else ") << a << " = re_result(L, re_run(L, p_, s_));";
+            if (memo_re) o << " gm_put(L, " << site << ", p_, s_, " << a << ");";
+            o << " } }";
             break;
+          }
           case BI_TO_NUMBER: o << a << " = bi_to_number(L, " << A0 << ");"; break;
           case BI_REPLACE: o << a << " = bi_replace(L, " << A0 << ", " << A1 << ", " << A2 << ");"; break;
           case BI_SUBSTRING: o << a << " = bi_substring(L, " << A0 << ", " << A1 << ", " << A2 << ");"; break;
