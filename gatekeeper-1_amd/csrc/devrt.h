@@ -71,6 +71,10 @@ constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged
 #define GK_EMCAP 64  // (32 sent dense unique-service-selector joins to the CPU fallback)
 #endif
 constexpr int EMCAP = GK_EMCAP;  // staged violation tuples per lane
+// em_dlen of a deferred record: 0x8000 | details length (< 0x4000); with
+// EM_DET_OBJ the details are the hook default `{}` and were not staged
+constexpr uint16_t EM_DET_OBJ = 0x4000u;
+__device__ __forceinline__ uint32_t em_dl(uint32_t dw) { return (dw & EM_DET_OBJ) ? 2u : (dw & 0x3fffu); }
 
 
 
@@ -1146,7 +1150,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
   uint32_t nt = keep ? L.en : 0, nb = 0;
   if (keep)
-    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + (L.em_dlen[i] & 0x7fffu);
+    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + em_dl(L.em_dlen[i]);
   uint32_t tt, tb;
   uint32_t pt = wave_excl_scan(nt, lane, tt);
   uint32_t pb = wave_excl_scan(nb, lane, tb);
@@ -1166,7 +1170,7 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
   }
   const bool fused = L.ord_base != 0;  // an OP_ORD group ran: number by (key, index)
   for (uint32_t i = 0; i < nt; ++i) {
-    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = dw & 0x7fffu, o = L.em_off[i];
+    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = em_dl(dw), o = L.em_off[i];
     uint32_t seq = i;
     if (fused) {
       const uint32_t oi = L.em_ord[i];
@@ -1185,7 +1189,7 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
       uint32_t na = (uint32_t)rec[0] >> 24;
       uint64_t* w = gk_args.frec + (uint64_t)(bt + i) * FREC_WORDS;
       const char* det = L.B + o + 8 * (1 + na);
-      const bool obj = dl == 2 && det[0] == '{' && det[1] == '}';
+      const bool obj = (dw & EM_DET_OBJ) || (dl == 2 && det[0] == '{' && det[1] == '}');
       w[0] = rec[0] | FREC_LIVE | (obj ? FREC_DET_OBJ : 0);
       for (uint32_t j = 0; j < na; ++j) w[1 + j] = rec[1 + j];
       if (!obj) {
@@ -1198,7 +1202,8 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
       const uint64_t* rec = (const uint64_t*)(L.B + o);
       uint32_t h = (uint32_t)rec[0], na = h >> 24;
       fmt_run(L, g, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
-      puts_(g, L.B + o + 8 * (1 + na), dl);
+      if (dw & EM_DET_OBJ) { put(g, '{'); put(g, '}'); }
+      else puts_(g, L.B + o + 8 * (1 + na), dl);
       g.finish();
     } else {
       if (gk_args.frec) gk_args.frec[(uint64_t)(bt + i) * FREC_WORDS] = 0;
@@ -1903,7 +1908,7 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
       uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
       if (cn.n > 0x7fffu || L.en >= EMCAP || off + rec > BCAP) { lane_fallback(L, FB_MSG_LEN); return false; }
       Out o{L.B + off + rec, 0, (uint32_t)(BCAP - off - rec), false};
-      if (!put_json(L, o, d) || o.ovf || o.n > 0x7fffu) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
+      if (!put_json(L, o, d) || o.ovf || o.n > 0x3fffu) { lane_fallback(L, o.ovf || o.n > 0x3fffu ? FB_MSG_LEN : FB_PRINT); return false; }
       uint64_t* w = (uint64_t*)(L.B + off);
       w[0] = fidx | (n << 24);
       for (uint32_t i = 0; i < n; ++i) w[1 + i] = arg(i);
@@ -1951,7 +1956,7 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
     if (vtag(args) == V_LIST) {
       const uint32_t n = list_len(L, args);
       const uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
-      if (n <= FMT_MAXARGS && off + rec + 2 <= BCAP) {
+      if (n <= FMT_MAXARGS && off + rec <= BCAP) {
         uint64_t* w = (uint64_t*)(L.B + off);
         bool ok = true;
         for (uint32_t i = 0; i < n && ok; ++i) {
@@ -1961,14 +1966,13 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
         }
         if (ok) {
           w[0] = fmt_fidx(m) | (n << 24);
-          // absent details print as the hook's default "{}" (put_json of undefined)
-          L.B[off + rec] = '{';
-          L.B[off + rec + 1] = '}';
-          L.bp = off + rec + 2;
+          // absent details print as the hook's default "{}" (put_json of
+          // undefined): flagged, written by the format pass / flush
+          L.bp = off + rec;
           L.em_rule[L.en] = (uint16_t)rule;
           L.em_off[L.en] = (uint16_t)off;
           L.em_mlen[L.en] = EM_UNSIZED;
-          L.em_dlen[L.en] = 0x8000u | 2u;
+          L.em_dlen[L.en] = 0x8000u | EM_DET_OBJ | 2u;
           L.em_ord[L.en] = L.ord;
           ++L.en;
           L.nsz = 1;
