@@ -485,8 +485,11 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
             // cross-lane memo answers repeats of the pair from L2 instead of
             // stepping the DFA over the subject's bytes again (gm_put keeps
             // only successful booleans).  GKGPU_RE_MEMO=0: A/B switch.
+            // Not for a literal pattern (an inlined DFA, typically inside a
+            // pure function the memo already answers: K8sContainerLimits'
+            // canonify_cpu ran 4.48 -> 4.73 ms with it).
             const char* rm = getenv("GKGPU_RE_MEMO");
-            const bool memo_re = !rm || atoi(rm) != 0;
+            const bool memo_re = (!rm || atoi(rm) != 0) && LK.konst(k, in.b) < 0;
             const std::string site = std::to_string(0x10000u + k) + "u";
             o << "{ uint64_t p_ = " << A0 << ", s_ = " << A1 << "; if (!is_strv(p_) || !is_strv(s_)) { lane_error(L); "
               << a << " = " << UND << "; }";
