@@ -189,6 +189,7 @@ struct gk_results {
   std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
   struct Sample { uint32_t review, constraint; uint16_t seq, rule; uint32_t msg_len; std::string msg; };
   std::vector<Sample> samples;             // gk_batch_eval_audit: first `limit` per constraint, in order
+  uint64_t failed_lanes = 0;               // (review, constraint) lanes flagged error / fallback on the device
   bool audited = false;
   struct Launch { std::string kernel; double ms; uint32_t nconstraints; uint64_t tuples, bytes; };
   std::vector<Launch> launches;            // kernels of the last attempt, in launch order
@@ -1017,6 +1018,7 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     res->dev_tuples = counters[0];
     res->dev_bytes = counters[1];
+    res->failed_lanes = counters[2];
     res->d_tuples = e->d_out.p;
     res->d_bytes = e->d_bytes.p;
     res->epoch = ++e->eval_epoch;
@@ -1735,7 +1737,10 @@ int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** 
   hipEventRecord(ev0, e->stream);
   unsigned int ncand = 0;
   for (int pass = 0; pass < 3; ++pass) {
-    int lr = gk_launch_sample((const Viol*)e->d_out.p, res->dev_tuples, (uint32_t*)e->d_rflags.p, nrev,
+    // no lane failed and no enforcementAction error: every review counts, and
+    // the sampling passes skip the per-tuple review-flag reads
+    uint32_t* rf = (any_err || res->failed_lanes) ? (uint32_t*)e->d_rflags.p : nullptr;
+    int lr = gk_launch_sample((const Viol*)e->d_out.p, res->dev_tuples, rf, nrev,
                               any_err ? (const uint8_t*)e->d_cerr.p : nullptr, ncons, nb, std::max<uint32_t>(limit, 1),
                               (uint32_t*)e->d_hist.p, (uint32_t*)e->d_cut.p, (unsigned long long*)e->d_ftot.p,
                               (const char*)e->d_bytes.p, (SampleRec*)e->d_cand.p, (uint32_t)e->cand_cap,

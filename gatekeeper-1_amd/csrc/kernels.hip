@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(256) gk_sample_hist(const Viol* out, uint64_t 
                                                       uint32_t nb, uint32_t* hist) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Viol v = out[i];
-    if (rflags[v.review] & (RF_ERROR | RF_FALLBACK)) continue;
+    if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
     atomicAdd(&hist[(uint64_t)v.constraint * nb + sample_bucket(v.review, nrev, nb)], 1u);
   }
 }
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(256) gk_sample_select(const Viol* out, uint64_
                                                         SampleRec* cand, uint32_t cap, unsigned int* ncand) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Viol v = out[i];
-    if (rflags[v.review] & (RF_ERROR | RF_FALLBACK)) continue;
+    if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
     if (sample_bucket(v.review, nrev, nb) > cut[v.constraint]) continue;
     uint32_t slot = atomicAdd(ncand, 1u);
     if (slot >= cap) continue;  // the host grows the buffer and runs this pass again
