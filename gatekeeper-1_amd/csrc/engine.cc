@@ -1806,6 +1806,27 @@ int gk_results_sample_get(const gk_results* r, size_t i, gk_sample_view* out) {
   return GK_OK;
 }
 
+int gk_results_samples_export(const gk_results* r, void* buf, size_t cap, size_t* needed) {
+  if (!r) return GK_EINVAL;
+  size_t n = 0;
+  for (const auto& smp : r->samples) n += 20 + smp.msg.size();
+  if (needed) *needed = n;
+  if (!buf || cap < n) return buf ? GK_EINVAL : GK_OK;
+  char* p = (char*)buf;
+  for (const auto& smp : r->samples) {
+    const uint32_t a[2] = {smp.review, smp.constraint};
+    const uint16_t b[2] = {smp.seq, smp.rule};
+    const uint32_t c[2] = {smp.msg_len, (uint32_t)smp.msg.size()};
+    memcpy(p, a, 8);
+    memcpy(p + 8, b, 4);
+    memcpy(p + 12, c, 8);
+    p += 20;
+    if (!smp.msg.empty()) memcpy(p, smp.msg.data(), smp.msg.size());
+    p += smp.msg.size();
+  }
+  return GK_OK;
+}
+
 const char* gk_results_constraint_action(const gk_results* r, size_t c) {
   return r && c < r->cea.size() ? r->cea[c].c_str() : nullptr;
 }

@@ -31,7 +31,7 @@ EXPORTS = [
     "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
-    "gk_results_export",
+    "gk_results_export", "gk_results_samples_export",
 ]
 
 
@@ -126,6 +126,7 @@ def load_library():
     lib.gk_results_count.restype = sz
     lib.gk_results_get.argtypes = [vp, sz, C.POINTER(_View)]
     lib.gk_results_export.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    lib.gk_results_samples_export.argtypes = [vp, vp, sz, C.POINTER(sz)]
     lib.gk_results_reviews.argtypes = [vp]
     lib.gk_results_reviews.restype = sz
     lib.gk_results_review_status.argtypes = [vp, sz]
@@ -280,13 +281,22 @@ def _collect_audit(lib, h) -> AuditSweep:
         nc = lib.gk_results_constraints(h)
         totals = [lib.gk_results_constraint_total(h, i) for i in range(nc)]
         actions = [(lib.gk_results_constraint_action(h, i) or b"").decode("utf-8", "surrogateescape") for i in range(nc)]
-        v = _SampleView()
+        # one bulk copy of the samples (gk_results_samples_export) instead of
+        # a ctypes call per sample
+        import struct
         samples = []
-        for i in range(lib.gk_results_sample_count(h)):
-            lib.gk_results_sample_get(h, i, C.byref(v))
-            samples.append(Sample(v.review, v.constraint, v.seq, v.rule, v.msg_len,
-                                  C.string_at(v.msg, v.msg_stored) if v.msg_stored else b"",
-                                  v.enforcement_action.decode("utf-8", "surrogateescape")))
+        need = C.c_size_t()
+        lib.gk_results_samples_export(h, None, 0, C.byref(need))
+        if need.value:
+            buf = C.create_string_buffer(need.value)
+            lib.gk_results_samples_export(h, buf, need.value, C.byref(need))
+            raw = buf.raw
+            i = 0
+            while i < need.value:
+                rv, c, seq, rule, ml, st = struct.unpack_from("<IIHHII", raw, i)
+                i += 20
+                samples.append(Sample(rv, c, seq, rule, ml, raw[i:i + st], actions[c] if c < nc else ""))
+                i += st
         t = (C.c_double * 5)()
         lib.gk_results_timing(h, t)
         dt, db = C.c_uint64(), C.c_uint64()

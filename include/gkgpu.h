@@ -154,6 +154,10 @@ typedef struct {
 } gk_sample_view;
 size_t gk_results_sample_count(const gk_results* r);
 int gk_results_sample_get(const gk_results* r, size_t i, gk_sample_view* out);
+/* every sample in one buffer: per sample u32 review, u32 constraint, u16 seq,
+ * u16 rule, u32 msg_len, u32 stored, then `stored` message bytes.  *needed
+ * receives the size; GK_EINVAL when cap is smaller (nothing written). */
+int gk_results_samples_export(const gk_results* r, void* buf, size_t cap, size_t* needed);
 /* the constraint's enforcementAction as results report it */
 const char* gk_results_constraint_action(const gk_results* r, size_t constraint);
 
