@@ -88,10 +88,13 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
   if (!ok) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess;
   const int T = std::max(1, std::min(16, default_threads()));
   const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  // GKGPU_BOUNCE_CHUNK (tests): a smaller chunk, to exercise many chunks
+  const char* bc = getenv("GKGPU_BOUNCE_CHUNK");
+  const size_t chunk = bc && atoll(bc) > 0 ? std::min<size_t>(CH, (size_t)atoll(bc)) : CH;
   double ms_copy = 0, ms_wait = 0;
   auto t_all = std::chrono::steady_clock::now();
-  for (size_t off = 0, k = 0; off < n; off += CH, ++k) {
-    const size_t len = std::min(CH, n - off);
+  for (size_t off = 0, k = 0; off < n; off += chunk, ++k) {
+    const size_t len = std::min(chunk, n - off);
     const int b = (int)(k & 1);
     auto tw = std::chrono::steady_clock::now();
     if (k >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) return false;
@@ -137,7 +140,10 @@ struct DBuf {
   bool upload(const void* src, size_t n, bool append_only) {
     if (!reserve(n)) return false;
     size_t from = append_only ? std::min(used, n) : 0;
-    if (n > from && n - from >= (256u << 20)) {
+    // GKGPU_BOUNCE_MIN (tests): the smallest copy that takes the bounce path
+    const char* bm = getenv("GKGPU_BOUNCE_MIN");
+    const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+    if (n > from && n - from >= bounce_min) {
       if (!upload_bounce((char*)p + from, (const char*)src + from, n - from)) return false;
     } else if (n > from && hipMemcpy((char*)p + from, (const char*)src + from, n - from, hipMemcpyHostToDevice) != hipSuccess)
       return false;

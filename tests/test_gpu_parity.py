@@ -393,6 +393,30 @@ def test_staged_batch_matches_direct_and_counts():
     assert sum(r1.totals) == len(r1.results)
 
 
+def test_staged_batch_through_the_pinned_bounce_upload(monkeypatch):
+    """The node arena of a staged batch goes to HBM through the pinned bounce
+    buffers (engine.cc upload_bounce; by default only copies >= 256 MB, i.e.
+    the bench's 1M Pods): with the threshold lowered, a multi-chunk upload of a
+    smaller batch gives the same results as the direct path."""
+    monkeypatch.setenv("GKGPU_BOUNCE_MIN", str(1 << 16))
+    monkeypatch.setenv("GKGPU_BOUNCE_CHUNK", str(1 << 18))  # ~14 chunks, both buffers reused
+    ts, cs = W.config2()
+    pods, ns_of, ns_objs = W.gen_pods(3000, seed=8, n_namespaces=40)
+    nss = [ns_objs[n] for n in ns_of]
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    direct = drv.review_objects(pods, nss)
+    b = drv.stage_objects(pods, nss)
+    r1 = b.eval(decode=True)
+    assert len(r1.results) > 5000
+    assert sorted((x.review, x.constraint_name, x.msg) for x in r1.results) == \
+        sorted((x.review, x.constraint_name, x.msg) for x in direct.results)
+
+
 def test_staged_batches_are_independent():
     """A staged batch keeps its own device documents: staging another batch or
     serving a Query in between does not change its results."""
