@@ -150,10 +150,7 @@ struct Lane {
   GK_LSCAL(uint32_t, nsz, 7);  // op_emit staged a record that size_deferred has not sized yet
   uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
   uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
-  // staged emission i: rule | off << 16 | mlen << 32 | dlen << 48 in one word
-  // (one store per emission site instead of four), order key beside it
-  uint64_t em[EMCAP];
-  uint16_t em_ord[EMCAP];
+  uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP], em_ord[EMCAP];
 };
 
 // A lane's state lives in private (scratch) memory.  Helpers take it through
@@ -166,17 +163,6 @@ struct Lane {
 #define GK_PRIV
 #endif
 typedef GK_PRIV Lane PLane;
-__device__ __forceinline__ void em_put(PLane& L, uint32_t i, uint32_t rule, uint32_t off, uint32_t mlen, uint32_t dlen) {
-  L.em[i] = (uint64_t)(rule & 0xffffu) | ((uint64_t)(off & 0xffffu) << 16) | ((uint64_t)(mlen & 0xffffu) << 32) |
-            ((uint64_t)(dlen & 0xffffu) << 48);
-}
-__device__ __forceinline__ uint32_t em_rule(const PLane& L, uint32_t i) { return (uint32_t)(L.em[i] & 0xffffu); }
-__device__ __forceinline__ uint32_t em_off(const PLane& L, uint32_t i) { return (uint32_t)((L.em[i] >> 16) & 0xffffu); }
-__device__ __forceinline__ uint32_t em_mlen(const PLane& L, uint32_t i) { return (uint32_t)((L.em[i] >> 32) & 0xffffu); }
-__device__ __forceinline__ uint32_t em_dlen(const PLane& L, uint32_t i) { return (uint32_t)(L.em[i] >> 48); }
-__device__ __forceinline__ void em_set_mlen(PLane& L, uint32_t i, uint32_t m) {
-  L.em[i] = (L.em[i] & ~(0xffffull << 32)) | ((uint64_t)(m & 0xffffu) << 32);
-}
 
 // The first GK_LDS_HWORDS words of each lane's heap live in LDS (template and
 // VM kernels; 0 = all in the private segment, as in the CPU build).  Lists and
@@ -1138,7 +1124,10 @@ __device__ void stage_tuple(PLane& L, uint32_t rule, const char* msg, uint32_t m
   }
   for (uint32_t i = 0; i < mlen; ++i) B[off + i] = msg[i];
   L.bp = off + mlen + dlen;
-  em_put(L, L.en, rule, off, mlen, dlen);
+  L.em_rule[L.en] = (uint16_t)rule;
+  L.em_off[L.en] = (uint16_t)off;
+  L.em_mlen[L.en] = (uint16_t)mlen;
+  L.em_dlen[L.en] = (uint16_t)dlen;
   L.em_ord[L.en] = L.ord;
   ++L.en;
   // only the staged bytes escape: the iteration's list heap stays reclaimable
@@ -1161,7 +1150,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
   uint32_t nt = keep ? L.en : 0, nb = 0;
   if (keep)
-    for (uint32_t i = 0; i < nt; ++i) nb += em_mlen(L, i) + em_dl(em_dlen(L, i));
+    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + em_dl(L.em_dlen[i]);
   uint32_t tt, tb;
   uint32_t pt = wave_excl_scan(nt, lane, tt);
   uint32_t pb = wave_excl_scan(nb, lane, tb);
@@ -1181,7 +1170,7 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
   }
   const bool fused = L.ord_base != 0;  // an OP_ORD group ran: number by (key, index)
   for (uint32_t i = 0; i < nt; ++i) {
-    uint32_t ml = em_mlen(L, i), dw = em_dlen(L, i), dl = em_dl(dw), o = em_off(L, i);
+    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = em_dl(dw), o = L.em_off[i];
     uint32_t seq = i;
     if (fused) {
       const uint32_t oi = L.em_ord[i];
@@ -1225,7 +1214,7 @@ __device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool
     v.review = r;
     v.constraint = c;
     v.seq = (uint16_t)seq;
-    v.rule = (uint16_t)em_rule(L, i);
+    v.rule = L.em_rule[i];
     v.msg_off = bb;
     v.msg_len = ml;
     v.det_len = dl;
@@ -1924,7 +1913,10 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
       w[0] = fidx | (n << 24);
       for (uint32_t i = 0; i < n; ++i) w[1 + i] = arg(i);
       L.bp = off + rec + o.n;
-      em_put(L, L.en, rule, off, cn.n, o.n | 0x8000u);
+      L.em_rule[L.en] = (uint16_t)rule;
+      L.em_off[L.en] = (uint16_t)off;
+      L.em_mlen[L.en] = (uint16_t)cn.n;
+      L.em_dlen[L.en] = (uint16_t)(o.n | 0x8000u);
       L.em_ord[L.en] = L.ord;
       ++L.en;
       for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
@@ -1977,7 +1969,10 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
           // absent details print as the hook's default "{}" (put_json of
           // undefined): flagged, written by the format pass / flush
           L.bp = off + rec;
-          em_put(L, L.en, rule, off, EM_UNSIZED, 0x8000u | EM_DET_OBJ | 2u);
+          L.em_rule[L.en] = (uint16_t)rule;
+          L.em_off[L.en] = (uint16_t)off;
+          L.em_mlen[L.en] = EM_UNSIZED;
+          L.em_dlen[L.en] = 0x8000u | EM_DET_OBJ | 2u;
           L.em_ord[L.en] = L.ord;
           ++L.en;
           L.nsz = 1;
@@ -2032,8 +2027,8 @@ __device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, 
 // inlined into finish_lane, out of line, where no predicate registers are live)
 __device__ __forceinline__ void size_deferred(PLane& L) {
   for (uint32_t i = 0; i < L.en; ++i) {
-    if (em_mlen(L, i) != EM_UNSIZED) continue;
-    const uint64_t* rec = (const uint64_t*)(L.B + em_off(L, i));
+    if (L.em_mlen[i] != EM_UNSIZED) continue;
+    const uint64_t* rec = (const uint64_t*)(L.B + L.em_off[i]);
     uint32_t n = 0;
     const bool ok = size_plain((uint32_t)rec[0] & 0xffffffu, rec + 1, n);
     if (!ok || n > 0x7fffu) {
@@ -2042,7 +2037,7 @@ __device__ __forceinline__ void size_deferred(PLane& L) {
       L.reason = ok ? FB_MSG_LEN : FB_PRINT;
       return;
     }
-    em_set_mlen(L, i, n);
+    L.em_mlen[i] = (uint16_t)n;
   }
   L.nsz = 0;
 }

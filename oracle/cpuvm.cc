@@ -173,7 +173,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
   }
   if (L.fail) { ++k.flagged; return; }
   for (uint32_t i = 0; i < L.en; ++i) {
-    uint32_t ml = em_mlen(L, i), dw = em_dlen(L, i), o = em_off(L, i);
+    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], o = L.em_off[i];
     if (dw & 0x8000u) {
       const uint64_t* rec = (const uint64_t*)(L.B + o);
       uint32_t h = (uint32_t)rec[0];
