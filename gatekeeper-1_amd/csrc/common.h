@@ -263,15 +263,26 @@ struct DevArgs {
   unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]
   uint64_t* gmemo;            // template kernels: cross-lane memo of pure function calls (4 words per entry)
   uint32_t gmemo_mask;        // entries - 1 (power of two)
-  uint64_t* frec;             // optional: per output tuple, a deferred-message record
-                              // (FREC_WORDS words) formatted by the format pass
+  uint64_t* frec;             // per output tuple, a deferred message's argument words, structure
+                              // of arrays: word j of tuple i at frec[j * out_cap + i]
+  char* ebytes;               // bytes that existed at emission (eager messages, details JSON)
+  uint64_t ebytes_cap;
+  uint32_t* lens;             // size pass: output bytes per tuple (message + details)
+  unsigned long long* part;   // size pass: per tile of FTILE tuples, its bytes; then the
+                              // exclusive prefix over tiles (spine)
 };
-// deferred-message record: w[0] = fidx | nargs << 24 | FREC_LIVE, w[1..nargs] = args
-constexpr uint32_t FREC_WORDS = 8;
-constexpr uint64_t FREC_LIVE = 1ull << 63;
-// the tuple's details are `{}` (the hook default for a result without
-// details): the format pass writes them after the message, the audit kernel
-// writes no bytes for it
-constexpr uint64_t FREC_DET_OBJ = 1ull << 62;
+// A deferred message's sprintf takes at most FMT_MAXARGS arguments (the
+// argument words a tuple carries in frec)
+constexpr uint32_t FMT_MAXARGS = 6;
+// Viol.pad while the predicate kernels run (the format pass clears it):
+//   VF_DEFER   msg_len = fidx | nargs << 24, the arguments in frec; the size
+//              pass prints its length, the format pass the bytes
+//   VF_DET_OBJ the details are the hook default `{}` (no staged bytes)
+// otherwise msg_len is the message length and ebytes[msg_off, ...) holds the
+// message (eager) followed by the details (unless VF_DET_OBJ); a deferred
+// message's details (unless VF_DET_OBJ) are at ebytes[msg_off, +det_len)
+constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2;
+// the size / format passes work in tiles of FTILE consecutive tuples
+constexpr uint32_t FTILE = 4096;
 
 }  // namespace gk

@@ -16,13 +16,25 @@
 
 #include "common.h"
 
-// Launch arguments: ONE copy in constant memory, set before every launch
-// (hipMemcpyToSymbolAsync for the VM kernel, hipModuleGetGlobal + copy for a
-// template kernel) and read with wave-uniform scalar loads.  Passing them by
+// Launch arguments: every kernel takes the DevArgs BY VALUE as its ONLY
+// parameter, so they sit at the start of the dispatch's kernarg segment,
+// immediately followed by the hidden (implicit) kernel arguments.  Device
+// functions receive the implicit-argument pointer as an SGPR input (the
+// kernarg segment pointer itself reads as null outside the kernel), so every
+// helper reads the launch arguments at implicitarg_ptr - sizeof(DevArgs), with
+// wave-uniform scalar loads.  Per-launch arguments: concurrent evaluations on
+// different streams never share them (a __constant__ copy per code object is
+// overwritten by the next launch of the same kernel).  Passing them by
 // reference to non-inlined helpers would copy them into every lane's scratch.
-extern "C" {
-__constant__ gk::DevArgs gk_args;
-}
+// The host build of this runtime (oracle/cpuvm.cc) declares a variable of that
+// name instead.
+#ifndef GK_HOST
+static_assert(sizeof(gk::DevArgs) % 8 == 0, "the hidden kernel arguments follow DevArgs at an 8-byte boundary");
+#define gk_args                                                                                                     \
+  (*(const __attribute__((address_space(4))) gk::DevArgs*)((const __attribute__((address_space(4))) char*)        \
+                                                              __builtin_amdgcn_implicitarg_ptr() -                 \
+                                                          sizeof(gk::DevArgs)))
+#endif
 
 // Reference accounting hooks (empty on the device): the CPU build of this
 // runtime (oracle/cpuvm.cc) defines them to record which document nodes and
@@ -66,16 +78,25 @@ constexpr int HCAP = GK_HCAP;  // heap words per lane (lists, big floats)
 #define GK_LDS_HWORDS_DEF GK_LDS_HWORDS
 static_assert(GK_LDS_HWORDS < GK_HCAP, "LDS heap words must leave a private-segment tail");
 constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
-constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings, staged messages)
-#ifndef GK_EMCAP
-#define GK_EMCAP 64  // (32 sent dense unique-service-selector joins to the CPU fallback)
-#endif
-constexpr int EMCAP = GK_EMCAP;  // staged violation tuples per lane
-// em_dlen of a deferred record: 0x8000 | details length (< 0x4000); with
-// EM_DET_OBJ the details are the hook default `{}` and were not staged
-constexpr uint16_t EM_DET_OBJ = 0x4000u;
-__device__ __forceinline__ uint32_t em_dl(uint32_t dw) { return (dw & EM_DET_OBJ) ? 2u : (dw & 0x3fffu); }
+constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings; an emission's bytes in transit)
+// emission order key of a tuple (Viol.seq): (OP_ORD key << 8) | the lane's
+// emission index; a lane past either limit goes to the CPU fallback
+constexpr uint32_t EM_MAXIDX = 256, EM_MAXORD = 256;
 
+// Wave-level primitives of the emission path.  The host build of this runtime
+// (oracle/cpuvm.cc, GK_HOST) evaluates one lane at a time: a wave of one.
+#ifdef GK_HOST
+__device__ __forceinline__ uint64_t gk_ballot(bool p) { return p ? 1ull : 0ull; }
+__device__ __forceinline__ uint32_t gk_lane_id() { return 0u; }
+__device__ __forceinline__ uint32_t gk_lanes_below(uint64_t) { return 0u; }
+#else
+__device__ __forceinline__ uint64_t gk_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t gk_lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// set bits of m below this lane
+__device__ __forceinline__ uint32_t gk_lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+#endif
 
 
 // ------------------------------------------------------------------ values
@@ -113,7 +134,7 @@ __device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); retu
 #define GK_LDS_SCALARS 0
 #endif
 #if GK_LDS_SCALARS
-constexpr int LDS_NSCAL = 8;
+constexpr int LDS_NSCAL = 9;
 __shared__ uint32_t gk_lds_scal[LDS_NSCAL][256];
 template <class T, int F>
 struct LdsField {
@@ -144,13 +165,12 @@ struct Lane {
   GK_LSCAL(uint32_t, reason, 5);
   // per loop depth: heap / byte watermarks that values escaping the loop pinned
   uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
-  // staged emissions: msg bytes then details JSON at B[off..off+mlen+dlen)
-  GK_LSCAL(uint32_t, en, 6);
+  GK_LSCAL(uint32_t, en, 6);  // tuples this lane emitted (written straight to the output)
   uint32_t steps;
-  GK_LSCAL(uint32_t, nsz, 7);  // op_emit staged a record that size_deferred has not sized yet
+  GK_LSCAL(uint32_t, rv, 7);  // the review's index in the caller's batch (Viol.review)
+  GK_LSCAL(uint32_t, cn, 8);  // the constraint (Viol.constraint)
   uint32_t memo_ok;  // VM memo slots holding a value (bit per slot)
   uint64_t memo_k0[MEMO_SLOTS], memo_k1[MEMO_SLOTS], memo_v[MEMO_SLOTS];
-  uint16_t em_rule[EMCAP], em_off[EMCAP], em_mlen[EMCAP], em_dlen[EMCAP], em_ord[EMCAP];
 };
 
 // A lane's state lives in private (scratch) memory.  Helpers take it through
@@ -1107,121 +1127,91 @@ __device__ int match_constraint(const MatchSpec& m, const ReviewCol& rc) {
 }
 
 // ------------------------------------------------------------------ emit
-// A violation is staged in the lane (bytes pinned in L.B against every
-// enclosing loop's per-iteration reset); output space is reserved once per
-// wavefront at the end of the kernel (flush_wave), so the global tuple/byte
-// cursors see one atomic per wave instead of one per violation.
-__device__ void stage_tuple(PLane& L, uint32_t rule, const char* msg, uint32_t mlen, const char* det, uint32_t dlen,
-                            uint32_t depth) {
-  if (L.en >= EMCAP || L.bp + mlen + dlen > BCAP) { lane_fallback(L, FB_MSG_LEN); return; }
-  uint32_t off = L.bp;
-  // det may already sit at B[bp + ...] (formatted in place): move it up first
-  char* B = L.B;
-  if (det == B + off) {
-    for (uint32_t i = dlen; i-- > 0;) B[off + mlen + i] = det[i];
-  } else {
-    for (uint32_t i = 0; i < dlen; ++i) B[off + mlen + i] = det[i];
-  }
-  for (uint32_t i = 0; i < mlen; ++i) B[off + i] = msg[i];
-  L.bp = off + mlen + dlen;
-  L.em_rule[L.en] = (uint16_t)rule;
-  L.em_off[L.en] = (uint16_t)off;
-  L.em_mlen[L.en] = (uint16_t)mlen;
-  L.em_dlen[L.en] = (uint16_t)dlen;
-  L.em_ord[L.en] = L.ord;
-  ++L.en;
-  // only the staged bytes escape: the iteration's list heap stays reclaimable
-  for (uint32_t d = 1; d <= depth && d < MAXLOOP; ++d)
-    if (L.keepB[d] < L.bp) L.keepB[d] = (uint16_t)L.bp;
+// Violations go straight to the output at the emission site.  The lanes of a
+// wavefront that emit at one site take consecutive tuple slots (one ballot +
+// one atomic per wave and site), so their 32-B tuples land as one coalesced
+// run; a deferred message's argument record goes to the structure-of-arrays
+// `frec` at the same slot (word j of tuple i at frec[j * out_cap + i]).
+// Message bytes that exist at emission time (an eager message, a details
+// JSON) are copied to `ebytes`, reserved the same way.  The final byte layout
+// (message, then details) is produced after the predicate kernels by the size
+// and format passes (kernels.hip), which also size deferred messages.  A lane
+// that fails after emitting leaves its tuples behind: the review's flag word
+// (rflags) drops them in every consumer, as it drops the rows of reviews
+// another constraint's lane flagged.
+
+// one slot per active lane with `want`, in lane order; one atomic per wave
+__device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, bool want) {
+  const uint64_t m = gk_ballot(want);
+  if (!want) return 0;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint64_t base = 0;
+  if (gk_lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__builtin_popcountll(m));
+  base = __shfl(base, (int)leader, 64);
+  return base + gk_lanes_below(m);
 }
 
-// wave-wide exclusive prefix sum (all 64 lanes must be active)
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t& total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
+// `n` bytes per active lane with `want` (n may differ per lane), in lane order
+__device__ __forceinline__ uint64_t wave_reserve_bytes(unsigned long long* ctr, bool want, uint32_t n) {
+  const uint64_t m = gk_ballot(want && n > 0);
+  if (!m) return 0;
+  uint64_t below = 0, tot = 0;
+  const uint32_t me = gk_lane_id();
+  for (uint64_t mm = m; mm; mm &= mm - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+    const uint32_t v = (uint32_t)__shfl(n, (int)l, 64);
+    if (l < me) below += v;
+    tot += v;
   }
-  total = __shfl(x, 63, 64);
-  return x - v;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint64_t base = 0;
+  if (me == leader) base = atomicAdd(ctr, (unsigned long long)tot);
+  base = __shfl(base, (int)leader, 64);
+  return base + below;
 }
 
-__device__ void flush_wave(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool keep) {
-  uint32_t nt = keep ? L.en : 0, nb = 0;
-  if (keep)
-    for (uint32_t i = 0; i < nt; ++i) nb += (uint32_t)L.em_mlen[i] + em_dl(L.em_dlen[i]);
-  uint32_t tt, tb;
-  uint32_t pt = wave_excl_scan(nt, lane, tt);
-  uint32_t pb = wave_excl_scan(nb, lane, tb);
-  uint64_t bt = 0, bb = 0;
-  if (lane == 63 && tt) {
-    bt = atomicAdd(&gk_args.counters[0], (unsigned long long)tt);
-    bb = atomicAdd(&gk_args.counters[1], (unsigned long long)tb);
-    atomicAdd(&gk_args.totals[c], (unsigned long long)tt);
-  }
-  if (!tt) return;
-  bt = __shfl(bt, 63, 64) + pt;
-  bb = __shfl(bb, 63, 64) + pb;
-  if (!nt) return;
-  if (bt + nt > gk_args.out_cap || bb + nb > gk_args.bytes_cap) {
-    atomicOr(&gk_args.rflags[r], (uint32_t)RF_OVERFLOW);
-    return;
-  }
-  const bool fused = L.ord_base != 0;  // an OP_ORD group ran: number by (key, index)
-  for (uint32_t i = 0; i < nt; ++i) {
-    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], dl = em_dl(dw), o = L.em_off[i];
-    uint32_t seq = i;
-    if (fused) {
-      const uint32_t oi = L.em_ord[i];
-      seq = 0;
-      for (uint32_t j = 0; j < nt; ++j) {
-        const uint32_t oj = L.em_ord[j];
-        seq += (oj < oi || (oj == oi && j < i)) ? 1u : 0u;
-      }
-    }
-    GOut g{(uint8_t*)gk_args.bytes, bb, bb, 0, false};
-    if ((dw & 0x8000u) && gk_args.frec) {
-      // deferred message: hand the record to the format pass (gk_format_kernel),
-      // which formats it into [bb, bb + ml) one lane per tuple; only the details
-      // bytes are written here
-      const uint64_t* rec = (const uint64_t*)(L.B + o);
-      uint32_t na = (uint32_t)rec[0] >> 24;
-      uint64_t* w = gk_args.frec + (uint64_t)(bt + i) * FREC_WORDS;
-      const char* det = L.B + o + 8 * (1 + na);
-      const bool obj = (dw & EM_DET_OBJ) || (dl == 2 && det[0] == '{' && det[1] == '}');
-      w[0] = rec[0] | FREC_LIVE | (obj ? FREC_DET_OBJ : 0);
-      for (uint32_t j = 0; j < na; ++j) w[1 + j] = rec[1 + j];
-      if (!obj) {
-        GOut gd{(uint8_t*)gk_args.bytes, bb + ml, bb + ml, 0, false};
-        puts_(gd, det, dl);
-        gd.finish();
-      }
-    } else if (dw & 0x8000u) {
-      // deferred message (op_emit): record [fidx | nargs << 24, args...], then details
-      const uint64_t* rec = (const uint64_t*)(L.B + o);
-      uint32_t h = (uint32_t)rec[0], na = h >> 24;
-      fmt_run(L, g, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
-      if (dw & EM_DET_OBJ) { put(g, '{'); put(g, '}'); }
-      else puts_(g, L.B + o + 8 * (1 + na), dl);
-      g.finish();
-    } else {
-      if (gk_args.frec) gk_args.frec[(uint64_t)(bt + i) * FREC_WORDS] = 0;
-      puts_(g, L.B + o, ml + dl);
-      g.finish();
-    }
-    Viol v;
-    v.review = r;
-    v.constraint = c;
-    v.seq = (uint16_t)seq;
-    v.rule = L.em_rule[i];
-    v.msg_off = bb;
-    v.msg_len = ml;
-    v.det_len = dl;
-    v.pad = 0;
-    gk_args.out[bt + i] = v;
-    bb += ml + dl;
-  }
+// the tuple order key of the lane's next emission; false = over the limits
+__device__ __forceinline__ bool next_seq(PLane& L, uint32_t& seq) {
+  const uint32_t en = L.en, ord = L.ord;
+  if (en >= EM_MAXIDX || ord >= EM_MAXORD) { lane_fallback(L, FB_MSG_LEN); return false; }
+  seq = (ord << 8) | en;
+  return true;
+}
+
+// an emission's bytes into the global staging buffer (slow path only)
+__device__ __forceinline__ void copy_out(char* dst, const char* src, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
+}
+
+__device__ __forceinline__ void slot_overflow(const PLane& L) { atomicOr(&gk_args.rflags[L.rv], (uint32_t)RF_OVERFLOW); }
+
+// An emission whose message and details bytes exist now (an eager message,
+// e.g. autoreject's constant or a string sprintf built in the lane buffer).
+// det == nullptr: the details are the hook default `{}`.  Every active lane
+// calls it (want = this lane emits).
+__device__ __noinline__ void emit_eager(PLane& L, bool want, uint32_t rule, const char* msg, uint32_t mlen,
+                                        const char* det, uint32_t dlen) {
+  uint32_t seq = 0;
+  if (want) want = next_seq(L, seq);
+  const bool detobj = det == nullptr;
+  const uint32_t eb = want ? mlen + (detobj ? 0u : dlen) : 0u;
+  const uint64_t eoff = wave_reserve_bytes(&gk_args.counters[1], want, eb);
+  const uint64_t slot = wave_reserve(&gk_args.counters[0], want);
+  if (!want) return;
+  L.en = L.en + 1u;
+  if (slot >= gk_args.out_cap || eoff + eb > gk_args.ebytes_cap) { slot_overflow(L); return; }
+  copy_out(gk_args.ebytes + eoff, msg, mlen);
+  if (!detobj) copy_out(gk_args.ebytes + eoff + mlen, det, dlen);
+  Viol v;
+  v.review = L.rv;
+  v.constraint = L.cn;
+  v.seq = (uint16_t)seq;
+  v.rule = (uint16_t)rule;
+  v.msg_len = mlen;
+  v.msg_off = eoff;
+  v.det_len = detobj ? 2u : dlen;
+  v.pad = detobj ? VF_DET_OBJ : 0u;
+  gk_args.out[slot] = v;
 }
 
 // ------------------------------------------------------------------ builtins
@@ -1674,12 +1664,12 @@ __device__ __noinline__ uint64_t do_sprintf(PLane& L, uint32_t fidx, uint64_t ar
 }
 
 // Deferred sprintf (template kernels): the message is not built in the lane
-// buffer; the value records (format, argument array) and is formatted straight
-// into the output bytes when the violation is flushed (flush_wave), or forced
-// into the lane buffer where anything else reads it (jit.cc inserts force_fmt).
+// buffer; the value records (format, argument array).  An emission hands the
+// record to the format pass (kernels.hip), which prints it into the output
+// bytes; anywhere else that reads the value forces it into the lane buffer
+// first (jit.cc inserts force_fmt).
 // The argument array is the heap list / document array sprintf received, so a
 // V_FMT lives exactly as long as that array (heap_val: pinned like a list).
-constexpr uint32_t FMT_MAXARGS = 6;
 __device__ __forceinline__ uint64_t fmt_args(uint64_t f) {
   uint64_t p = vpay(f);
   uint32_t lo = (uint32_t)p;
@@ -1819,8 +1809,9 @@ __device__ __forceinline__ uint64_t op_len_eq(PLane& L, uint64_t v, uint32_t y) 
 // expression are evaluated in one pass over its solutions, body after body for
 // each solution; the reference evaluates them body by body (topdown
 // evalOneRule per rule), so each fused body's emissions carry key base + j and
-// the group's exit moves the base past them.  flush_wave numbers a lane's
-// emissions by (key, emission index), which restores the reference's order.
+// the group's exit moves the base past them.  A tuple's order key is
+// (key, the lane's emission index) (next_seq), which sorts the lane's
+// emissions in the reference's order.
 __device__ __forceinline__ void op_ord(PLane& L, uint32_t y) {
   const uint32_t k = (uint32_t)L.ord_base + (y & 0x7fffffffu);
   if (k > 0xffffu) { lane_fallback(L, FB_MSG_LEN); return; }
@@ -1891,107 +1882,114 @@ __device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k
   e[0] = k0; e[1] = k1; e[2] = v; e[3] = gm_check(h, v);
 }
 
-// m: message register, d: details register (undefined when absent)
+// m: message register, d: details register (undefined when absent).  Every
+// active lane at the emission site calls it (the output reservations are
+// wave-level); a lane that already failed emits nothing.
 __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
-  if (vtag(m) == V_FMT) {
-    // deferred message: size it now, format it into the output at flush_wave.
-    // Only heap-free arguments are recorded (the record outlives this
-    // iteration's heap); otherwise the message is built here as before.
-    uint64_t args = fmt_args(m);
-    uint32_t fidx = fmt_fidx(m), n = coll_len(L, args);
-    bool ok = n <= FMT_MAXARGS;
-    for (uint32_t i = 0; i < n && ok; ++i) { uint64_t k, v; coll_at(L, args, i, k, v); ok = memo_stable(v); }
-    if (ok) {
-      auto arg = [&](uint32_t i) { uint64_t k, v; coll_at(L, args, i, k, v); return v; };
-      Cnt cn{0, false};
-      if (!fmt_run(L, cn, fidx, arg)) { lane_fallback(L, FB_PRINT); return false; }
-      uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
-      if (cn.n > 0x7fffu || L.en >= EMCAP || off + rec > BCAP) { lane_fallback(L, FB_MSG_LEN); return false; }
-      Out o{L.B + off + rec, 0, (uint32_t)(BCAP - off - rec), false};
-      if (!put_json(L, o, d) || o.ovf || o.n > 0x3fffu) { lane_fallback(L, o.ovf || o.n > 0x3fffu ? FB_MSG_LEN : FB_PRINT); return false; }
-      uint64_t* w = (uint64_t*)(L.B + off);
-      w[0] = fidx | (n << 24);
-      for (uint32_t i = 0; i < n; ++i) w[1 + i] = arg(i);
-      L.bp = off + rec + o.n;
-      L.em_rule[L.en] = (uint16_t)rule;
-      L.em_off[L.en] = (uint16_t)off;
-      L.em_mlen[L.en] = (uint16_t)cn.n;
-      L.em_dlen[L.en] = (uint16_t)(o.n | 0x8000u);
-      L.em_ord[L.en] = L.ord;
-      ++L.en;
-      for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
-        if (L.keepB[dd] < L.bp) L.keepB[dd] = (uint16_t)L.bp;
-      return !L.fail;
-    }
-    m = force_fmt(L, m);
-    if (L.fail) return false;
+  bool ok = !L.fail;
+  bool defer = false;
+  uint32_t fidx = 0, n = 0;
+  uint64_t args = 0;
+  if (ok && vtag(m) == V_FMT) {
+    // a deferred message whose arguments are heap-free values (the record
+    // outlives this iteration's heap) goes to the format pass as its record;
+    // otherwise it is built in the lane buffer now
+    args = fmt_args(m);
+    fidx = fmt_fidx(m);
+    n = coll_len(L, args);
+    defer = n <= FMT_MAXARGS;
+    for (uint32_t i = 0; i < n && defer; ++i) { uint64_t k, v; coll_at(L, args, i, k, v); defer = memo_stable(v); }
+    if (!defer) { m = force_fmt(L, m); ok = !L.fail; }
   }
-  if (!is_strv(m)) { lane_error(L); return false; }  // types.Result.msg must unmarshal as a string
-  SView ms = sview(L, m);
-  char* dbuf = L.B + L.bp;
-  Out o{dbuf, 0, (uint32_t)(BCAP - L.bp), false};
-  if (!put_json(L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); return false; }
-  stage_tuple(L, rule, ms.p, ms.n, dbuf, o.n, depth);
-  return !L.fail;
+  if (ok && !defer && !is_strv(m)) { lane_error(L); ok = false; }  // types.Result.msg must unmarshal as a string
+  // details JSON in the lane buffer above everything live (not kept: copied out below)
+  const char* det = nullptr;
+  uint32_t dlen = 2;
+  if (ok && vtag(d) != V_UNDEF) {
+    Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
+    if (!put_json(L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); ok = false; }
+    else if (!(o.n == 2 && o.p[0] == '{' && o.p[1] == '}')) { det = o.p; dlen = o.n; }
+  }
+  SView ms{nullptr, 0};
+  if (ok && !defer) ms = sview(L, m);
+  uint32_t seq = 0;
+  if (ok) ok = next_seq(L, seq);
+  const uint32_t eb = ok ? (defer ? 0u : ms.n) + (det ? dlen : 0u) : 0u;
+  const uint64_t eoff = wave_reserve_bytes(&gk_args.counters[1], ok, eb);
+  const uint64_t slot = wave_reserve(&gk_args.counters[0], ok);
+  if (!ok) return false;
+  L.en = L.en + 1u;
+  if (slot >= gk_args.out_cap || eoff + eb > gk_args.ebytes_cap) { slot_overflow(L); return true; }
+  if (!defer) copy_out(gk_args.ebytes + eoff, ms.p, ms.n);
+  if (det) copy_out(gk_args.ebytes + eoff + (defer ? 0u : ms.n), det, dlen);
+  Viol v;
+  v.review = L.rv;
+  v.constraint = L.cn;
+  v.seq = (uint16_t)seq;
+  v.rule = (uint16_t)rule;
+  v.msg_len = defer ? (fidx | (n << 24)) : ms.n;
+  v.msg_off = eoff;
+  v.det_len = dlen;
+  v.pad = (defer ? VF_DEFER : 0u) | (det ? 0u : VF_DET_OBJ);
+  gk_args.out[slot] = v;
+  if (defer)
+    for (uint32_t i = 0; i < n; ++i) {
+      uint64_t k, a;
+      coll_at(L, args, i, k, a);
+      gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = a;
+    }
+  return true;
 }
 
 // Emission fast path, inlined at every emission site: a deferred sprintf
 // message without details whose arguments are plain scalars (interned
-// strings, ints) is staged as its argument record only; its
-// printed length is computed once per lane by size_deferred at the end of the
-// program, where no predicate registers are live.  An out-of-line op_emit per
-// violation made every emission save and restore the predicate's live VGPRs
-// in scratch.  Printing such arguments can only fail on an over-long message
-// (FB_MSG_LEN) or a verb/argument mismatch (FB_PRINT); size_deferred then
-// marks the lane as the reference-equivalent emission-time fallback.
+// strings, ints) -- the common case -- is written as its 32-B tuple and its
+// argument words, nothing else: no bytes, no sizing (the size pass prints
+// its length, kernels.hip).  Lanes on other paths take op_emit_slow, which
+// is out of line: a call saves and restores the predicate's live VGPRs in
+// scratch.
 #ifndef GK_EMIT_FAST
 #define GK_EMIT_FAST 1
 #endif
-constexpr uint16_t EM_UNSIZED = 0xffffu;  // em_mlen of a record size_deferred has not sized yet
 __device__ __forceinline__ bool plain_scalar(uint64_t v) { return vtag(v) == V_STR || vtag(v) == V_INT; }
 __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
 #if GK_EMIT_FAST
-  if (vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EMCAP) {
-    const uint64_t args = fmt_args(m);
+  bool fast = false;
+  uint32_t n = 0, seq = 0;
+  uint64_t args = 0;
+  if (vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX && L.ord < EM_MAXORD) {
+    args = fmt_args(m);
     if (vtag(args) == V_LIST) {
-      const uint32_t n = list_len(L, args);
-      const uint32_t off = (L.bp + 7) & ~7u, rec = 8 * (1 + n);
-      if (n <= FMT_MAXARGS && off + rec <= BCAP) {
-        uint64_t* w = (uint64_t*)(L.B + off);
-        bool ok = true;
-        for (uint32_t i = 0; i < n && ok; ++i) {
-          const uint64_t v = list_at(L, args, i);
-          ok = plain_scalar(v);
-          w[1 + i] = v;
-        }
-        if (ok) {
-          w[0] = fmt_fidx(m) | (n << 24);
-          // absent details print as the hook's default "{}" (put_json of
-          // undefined): flagged, written by the format pass / flush
-          L.bp = off + rec;
-          L.em_rule[L.en] = (uint16_t)rule;
-          L.em_off[L.en] = (uint16_t)off;
-          L.em_mlen[L.en] = EM_UNSIZED;
-          L.em_dlen[L.en] = 0x8000u | EM_DET_OBJ | 2u;
-          L.em_ord[L.en] = L.ord;
-          ++L.en;
-          L.nsz = 1;
-          for (uint32_t dd = 1; dd <= depth && dd < MAXLOOP; ++dd)
-            if (L.keepB[dd] < L.bp) L.keepB[dd] = (uint16_t)L.bp;
-          return true;
-        }
-      }
+      n = list_len(L, args);
+      fast = n <= FMT_MAXARGS;
+      for (uint32_t i = 0; i < n && fast; ++i) fast = plain_scalar(list_at(L, args, i));
     }
+  }
+  if (fast) {
+    seq = ((uint32_t)L.ord << 8) | (uint32_t)L.en;
+    const uint64_t slot = wave_reserve(&gk_args.counters[0], true);
+    L.en = L.en + 1u;
+    if (slot >= gk_args.out_cap) { slot_overflow(L); return true; }
+    Viol v;
+    v.review = L.rv;
+    v.constraint = L.cn;
+    v.seq = (uint16_t)seq;
+    v.rule = (uint16_t)rule;
+    v.msg_len = fmt_fidx(m) | (n << 24);
+    v.msg_off = 0;
+    v.det_len = 2;
+    v.pad = VF_DEFER | VF_DET_OBJ;
+    gk_args.out[slot] = v;
+    for (uint32_t i = 0; i < n; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = list_at(L, args, i);
+    return true;
   }
 #endif
   return op_emit_slow(L, m, d, depth, rule);
 }
 
 // Printed length of a deferred message whose arguments are plain scalars:
-// put_fmt_arg restricted to interned strings and ints, on a counter.  (Sizing
-// through the generic fmt_run here made this gfx950 toolchain emit an illegal
-// V_CMP on src_shared_base: the heap-value printing paths test the LDS
-// aperture of the lane pointer.)
+// put_fmt_arg restricted to interned strings and ints, on a counter (the size
+// pass's fast path; fmt_run on a counter serves every other record).
 __device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, uint32_t& len) {
   const uint32_t* f = gk_args.fmt + fidx;
   const uint32_t nseg = f[0];
@@ -2000,17 +1998,13 @@ __device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, 
     const uint32_t kind = f[2 + 2 * s], a = f[3 + 2 * s];
     if (kind == 0) { put_sid(o, a); continue; }
     const uint32_t verb = a >> 16;
-#ifdef GK_DIAG_SIZE_BOUND
-    // diagnostics only (cost of the sizing loads): a 64-byte over-estimate
-    // per argument, no loads; messages come out padded, not comparable
-    o.n += 64;
-    continue;
-#endif
     const uint64_t v = args[a & 0xffff];
     if (vtag(v) == V_STR) {
       const uint32_t n = gk_args.strs[(uint32_t)vpay(v)].len;
       GK_TOUCH_STR((uint32_t)vpay(v));
       if (verb == 'd') { put_cstr(o, "%!d(string="); o.n += n; put(o, ')'); } else o.n += n;
+    } else if (vtag(v) != V_INT) {
+      return false;
     } else if (intv_gform(v)) {
       if (verb != 'v') return false;
       put_intv(o, v);
@@ -2023,34 +2017,19 @@ __device__ __forceinline__ bool size_plain(uint32_t fidx, const uint64_t* args, 
   len = o.n;
   return true;
 }
-// sizes the records op_emit staged unsized (once per lane, after the program;
-// inlined into finish_lane, out of line, where no predicate registers are live)
-__device__ __forceinline__ void size_deferred(PLane& L) {
-  for (uint32_t i = 0; i < L.en; ++i) {
-    if (L.em_mlen[i] != EM_UNSIZED) continue;
-    const uint64_t* rec = (const uint64_t*)(L.B + L.em_off[i]);
-    uint32_t n = 0;
-    const bool ok = size_plain((uint32_t)rec[0] & 0xffffffu, rec + 1, n);
-    if (!ok || n > 0x7fffu) {
-      // the emission-time outcome: the program would have stopped here
-      L.fail = RF_FALLBACK;
-      L.reason = ok ? FB_MSG_LEN : FB_PRINT;
-      return;
-    }
-    L.em_mlen[i] = (uint16_t)n;
-  }
-  L.nsz = 0;
-}
 
-// end of a lane's evaluation (out of line: the predicate's registers are dead)
-__device__ __noinline__ void finish_lane(PLane& L, uint32_t lane, uint32_t r, uint32_t c, bool live) {
-  if (live && !L.fail && L.nsz) size_deferred(L);
+// end of a lane's evaluation (all 64 lanes of the wave, reconverged): flag a
+// failed review, add the wave's clean emissions to the constraint's total
+__device__ __noinline__ void finish_lane(PLane& L, uint32_t lane, uint32_t c, bool live) {
   if (live && L.fail) {
     atomicAdd(&gk_args.counters[2], 1ull);
-    atomicOr(&gk_args.rflags[r], L.fail);
-    if (gk_args.rreason) atomicMax(&gk_args.rreason[r], L.reason);
+    atomicOr(&gk_args.rflags[L.rv], L.fail);
+    if (gk_args.rreason) atomicMax(&gk_args.rreason[L.rv], L.reason);
   }
-  flush_wave(L, lane, r, c, live && !L.fail);
+  uint32_t k = (live && !L.fail) ? (uint32_t)L.en : 0u;
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) k += (uint32_t)__shfl_xor(k, dd, 64);
+  if (lane == 0 && k) atomicAdd(&gk_args.totals[c], (unsigned long long)k);
 }
 
 // ------------------------------------------------------------------ kernel body
@@ -2071,22 +2050,26 @@ __device__ __forceinline__ void audit_body(Run run) {
   Lane L0;
   PLane& L = *(PLane*)&L0;
   L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
-  L.nsz = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   bool live = rp < gk_args.nrev;
+  ReviewCol rc{};
   if (live) {
-    const ReviewCol rc = gk_args.revs[rp];
+    rc = gk_args.revs[rp];
     if (rc.orig != NO_ID) r = rc.orig;
-    const MatchSpec m = gk_args.cons[c];
+  }
+  L.rv = r;
+  L.cn = c;
+  const MatchSpec m = gk_args.cons[c];
+  // autoreject_review (target_template_source.go:12-25)
+  const bool autorej = live && !(rc.flags & RC_FALLBACK) && (m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) &&
+                       rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) &&
+                       !(rc.flags & RC_UNSTABLE_NS);
+  if (__builtin_expect(gk_ballot(autorej) != 0, 0))
+    emit_eager(L, autorej, RULE_AUTOREJECT, "Namespace is not cached in OPA.", 31, nullptr, 2);
+  if (live) {
     if (rc.flags & RC_FALLBACK) {
       L.fail = RF_FALLBACK;
     } else {
-      // autoreject_review (target_template_source.go:12-25)
-      if ((m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID &&
-          !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS)) {
-        const char* msg = "Namespace is not cached in OPA.";
-        stage_tuple(L, RULE_AUTOREJECT, msg, 31, "{}", 2, 0);
-      }
       int mr = match_constraint(m, rc);
       if (mr == -1) L.fail = RF_ERROR;
       else if (mr == -2) L.fail = RF_FALLBACK;
@@ -2097,9 +2080,9 @@ __device__ __forceinline__ void audit_body(Run run) {
       }
     }
   }
-  // every lane of the wave reaches here (reconverged): size deferred records,
-  // flag failed reviews, reserve + write output
-  finish_lane(L, lane, r, c, live);
+  // every lane of the wave reaches here (reconverged): flag failed reviews,
+  // count the clean emissions
+  finish_lane(L, lane, c, live);
   if (gk_args.prof) {
     uint32_t mx = L.steps;
 #pragma unroll

@@ -10,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -29,7 +30,7 @@
 namespace gk {
 }
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
-extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream);
+extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev);
 extern "C" size_t gk_devargs_size();
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
@@ -125,6 +126,11 @@ struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
   size_t used = 0;  // bytes uploaded (append-only arrays upload the tail)
+  // Shared append-only tables (strings, pool, numbers) are read by kernels of
+  // concurrent evaluations while another evaluation appends to them: a grown
+  // table keeps its predecessor alive here (freed with the engine), so a
+  // pointer an in-flight launch holds stays valid.
+  std::vector<void*>* graveyard = nullptr;
   bool reserve(size_t n) {
     if (n <= cap) return true;
     size_t nc = std::max(n, cap * 2);
@@ -132,7 +138,10 @@ struct DBuf {
     void* q = nullptr;
     if (hipMalloc(&q, nc) != hipSuccess) return false;
     if (p && used) hipMemcpy(q, p, used, hipMemcpyDeviceToDevice);
-    if (p) hipFree(p);
+    if (p) {
+      if (graveyard) graveyard->push_back(p);
+      else hipFree(p);
+    }
     p = q;
     cap = nc;
     return true;
@@ -165,7 +174,9 @@ struct TemplateEnt {
 
 struct ConstraintEnt {
   std::string kind, name;
+  std::string json;        // the PutData document (kept to re-place it when the permanent region is compacted)
   uint32_t root = NO_ID;   // node of the whole constraint (permanent region)
+  uint32_t nnodes = 0;     // nodes of its document
   MatchSpec spec{};
   std::string ea;          // enforcementAction as returned in results
   bool ea_error = false;   // non-string enforcementAction: Query fails
@@ -175,6 +186,36 @@ struct ConstraintEnt {
 struct ResultRow {
   uint32_t review, constraint, seq, rule;
   std::string msg, details;
+};
+
+// One evaluation's device state: its stream, its launch events and every
+// buffer a call writes (review columns and documents of a query, output
+// tuples and bytes, flags, totals, sampling).  Concurrent evaluations
+// (drivers.Driver.Query under local.go's read lock) each hold one; a pool
+// keeps them for reuse.  The engine's permanent tables (constraint match
+// words, bytecode, templates' kernels, the permanent node region, strings)
+// are shared and read-only while evaluations run.
+struct EvalCtx {
+  std::mutex busy;  // held by the evaluation using it (and by a raw-output copy of its results)
+  hipStream_t stream = nullptr;
+  std::vector<hipEvent_t> events;
+  DBuf d_nodes, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist, d_gmemo,
+      d_frec, d_hist, d_cut, d_ftot, d_cand, d_ncand, d_cerr, d_ebytes, d_lens, d_part;
+  size_t out_cap = 1 << 20, bytes_cap = 64u << 20, ebytes_cap = 16u << 20, cand_cap = 1 << 14;
+  uint64_t eval_epoch = 0;   // bumps on every evaluation (output buffers reused)
+  uint64_t perm_gen = 0;     // engine generation whose permanent nodes d_nodes holds below perm_nodes
+  uint32_t perm_nodes = 0;
+  NodeArena arena;           // host documents of the current query (node id perm_nodes + k)
+  void release_all() {
+    for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
+                    &d_clist, &d_gmemo, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
+                    &d_part})
+      b->free_();
+    for (hipEvent_t x : events) hipEventDestroy(x);
+    events.clear();
+    if (stream) hipStreamDestroy(stream);
+    stream = nullptr;
+  }
 };
 
 }  // namespace gk
@@ -188,10 +229,10 @@ struct gk_results {
   std::vector<uint8_t> cea_error;          // per constraint: non-string enforcementAction (Query error)
   uint64_t excluded = 0;                   // reviews skipped by the process excluder
   double ms[5] = {0, 0, 0, 0, 0};
-  uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernel wrote
-  const void* d_tuples = nullptr;          // engine-owned device output of this call (valid
-  const void* d_bytes = nullptr;           // until the engine's next evaluation)
-  uint64_t epoch = 0;
+  uint64_t dev_tuples = 0, dev_bytes = 0;  // tuples / message bytes the kernels wrote
+  gk::EvalCtx* ctx = nullptr;              // the evaluation context holding the device output
+  uint64_t epoch = 0;                      // ... while its eval_epoch equals this
+  uint64_t gen = 0;                        // engine generation (state of modules / data) evaluated
   std::vector<uint64_t> prof;              // GKGPU_PROFILE=1: per constraint VM step stats
   struct Sample { uint32_t review, constraint; uint16_t seq, rule; uint32_t msg_len; std::string msg; };
   std::vector<Sample> samples;             // gk_batch_eval_audit: first `limit` per constraint, in order
@@ -207,37 +248,52 @@ struct gk_batch {
   bool str_bytes_done = false;
   uint64_t gen = 0;
   uint32_t nrev = 0;
-  uint32_t node_begin = 0, node_end = 0;
+  uint32_t node_begin = 0, node_end = 0;    // node ids of the batch's documents
   uint64_t excluded = 0;                    // reviews skipped by the process excluder
   double ms_parse = 0, ms_flatten = 0, ms_upload = 0;
   std::vector<gk::ReviewCol> cols;
   std::vector<gk::ResourceIds> resources;   // HandleViolation identity per batch index
+  gk::NodeArena arena;                      // host copy of the documents (node id node_begin + k)
   gk::DBuf d_revs;
   gk::DBuf d_nodes;  // the batch's own device node array: permanent region + its documents
   uint64_t dev_bytes = 0;
 };
 
 struct gk_engine {
-  std::mutex mu;
-  std::string err;
+  // drivers.Driver's locking (local.go:62-68, 117, 303-304): evaluations
+  // (Query and the batch calls) share `rw`; mutations (Put/Delete of modules
+  // and data, excluder changes) take it exclusively, so an evaluation sees one
+  // engine state from start to end.  `turn` makes a waiting mutation block new
+  // readers (no writer starvation under a stream of queries).  `smu` guards
+  // the string / number tables, which evaluations append to while they
+  // flatten their documents.
+  std::shared_mutex rw;
+  std::mutex turn;
+  std::mutex smu;
+  std::mutex pool_mu;
+  std::vector<std::unique_ptr<gk::EvalCtx>> ctxs;  // evaluation contexts (pool)
+  std::vector<void*> graveyard;                     // superseded shared device tables
+  uint64_t prepared_gen = 0;  // generation the compiled state and device tables were prepared for
+  bool prepared_dev = false;
   int device = 0;
   bool dev_ok = false;
+  std::mutex dbg_mu;
   std::vector<uint32_t> pchist;  // last launch's per-pc execution counts (GKGPU_PROFILE=2)
   int profile = 0;  // GKGPU_PROFILE=1: VM step statistics per launch; 2: + per-pc histogram
-  hipStream_t stream = nullptr;
   gk::Store st;
+  uint32_t base_nodes = 0;  // the store's fixed nodes
   // modules
   std::map<std::string, std::string> modules;  // name -> source
   gk::ModuleSet mods;
   gk::CodeBank bank;
   std::vector<gk::Program> progs;
+  uint64_t module_nodes = 0;  // permanent nodes the compiled templates' constants occupy
   // per-template kernels (jit.cc), parallel to progs
   struct Jit {
     std::string name, src, code, log;
     int state = 0;  // 0 not compiled, 1 code ready, -1 compile failed
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
-    hipDeviceptr_t args = nullptr;  // the module's gk_args (constant memory)
   };
   std::vector<Jit> jits;
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
@@ -250,14 +306,16 @@ struct gk_engine {
   std::vector<uint32_t> mwords;
   bool constraints_dirty = true;
   std::map<std::string, std::string> inventory;  // external path -> json
-  std::map<std::string, uint32_t> ns_cache;       // namespace name -> node (permanent)
+  std::map<std::string, std::pair<uint32_t, uint32_t>> ns_nodes;  // namespace name -> (node, node count)
+  gk::NsCache ns_cache;                           // namespace name -> node (permanent)
   std::map<std::string, std::string> other_data;
   // process excluder (pkg/controller/config/process/excluder.go): process -> namespaces
   std::map<std::string, std::set<std::string>> excluded;
-  uint32_t perm_nodes = 0;                        // nodes below this are permanent
+  uint32_t perm_nodes = 0;                        // nodes of the permanent region
   // data.inventory (templates' cross-resource joins): one permanent object
   // node whose members sync_inventory points at the current inventory tree
   uint32_t inv_node = gk::NO_ID;
+  uint32_t inv_lo = 0, inv_hi = 0;  // node range of the current inventory tree
   bool inv_dirty = true;        // /external/ data changed since the tree was built
   bool uses_inventory = false;  // some compiled template reads data.inventory
   uint64_t gen = 1;                               // bumps on any mutation
@@ -265,20 +323,35 @@ struct gk_engine {
   std::map<uint32_t, std::pair<uint32_t, uint32_t>> dfa_index;  // pattern sid -> (word offset, status)
   std::vector<uint32_t> dfa_words;
   std::vector<uint32_t> dfa_keys, dfa_meta;
-  // device mirrors
+  // device mirrors of the permanent tables (written under the exclusive lock,
+  // except the append-only string / number tables: under smu, graveyard kept)
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
-      d_dfa_meta, d_dfa_words, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist,
-      d_gmemo, d_frec, d_hist, d_cut, d_ftot, d_cand, d_ncand, d_cerr;
-  size_t cand_cap = 1 << 14;
+      d_dfa_meta, d_dfa_words;
   // gk_debug_host_args: host copies of the per-call tables (diagnostics / CPU baseline)
   std::vector<gk::MatchSpec> dbg_cons;
   std::vector<uint32_t> dbg_progoff, dbg_mwords, dbg_dfa_keys, dbg_dfa_meta, dbg_dfa_words, dbg_fmt;
+  std::vector<gk::Node> dbg_nodes;
+  std::vector<gk::StrEnt> dbg_strs;
+  std::vector<uint8_t> dbg_sflags;
+  std::vector<gk::NumEnt> dbg_nums;
   std::string dbg_pool;
-  size_t out_cap = 1 << 20, bytes_cap = 64u << 20;
-  std::vector<hipEvent_t> events;  // per-launch timing events, reused across calls
-  uint32_t dev_nodes_ok = 0;       // leading nodes whose d_nodes copy matches the host arena
-  uint64_t eval_epoch = 0;         // bumps on every evaluation (device output buffers reused)
+  uint32_t dev_nodes_ok = 0;       // leading permanent nodes whose d_nodes copy matches the host arena
+  size_t out_cap0 = 1 << 20;       // initial tuple capacity of a new context (opts max_violations)
 };
+
+namespace gk {
+
+// The device string / number tables as one evaluation uses them: the current
+// pointers, snapshotted under smu right after the evaluation's own strings
+// were uploaded (grown tables keep their predecessors: DBuf::graveyard).
+struct TablePtrs {
+  const StrEnt* strs = nullptr;
+  const uint8_t* pool = nullptr;
+  const uint8_t* sflags = nullptr;
+  const NumEnt* nums = nullptr;
+};
+
+}  // namespace gk
 
 // Drops the transient node region (review documents of the last call).  The
 // device mirror stays valid below the cut, so the next upload is incremental.
@@ -339,8 +412,11 @@ static std::vector<std::string> pkg_path(const std::string& name) {
 
 using namespace gk;
 
-static int fail(gk_engine* e, int code, const std::string& m) {
-  e->err = m;
+// gk_last_error: the message of this thread's last failed call (concurrent
+// callers do not see each other's errors)
+static thread_local std::string tl_err;
+static int fail(gk_engine*, int code, const std::string& m) {
+  tl_err = m;
   return code;
 }
 
@@ -363,6 +439,7 @@ static void rebuild_modules(gk_engine* e) {
   }
   e->bank.inventory_node = e->inv_node;
   e->uses_inventory = false;
+  const size_t n_before = e->st.nodes().size();
   std::vector<std::shared_ptr<rego::Module>> parsed;
   for (auto& kv : e->modules) {
     auto m = rego::parse_module(kv.second);
@@ -431,6 +508,7 @@ static void rebuild_modules(gk_engine* e) {
     e->templates[kind] = te;
   }
   e->perm_nodes = (uint32_t)e->st.nodes().size();
+  e->module_nodes = e->st.nodes().size() - n_before;
   e->modules_dirty = false;
   e->constraints_dirty = true;
   e->gen++;
@@ -626,8 +704,10 @@ static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
 // are assembled into one JSON tree by path segment, parsed into the permanent
 // node region, and the engine's inventory node is pointed at its members, so
 // compiled templates (a constant V_NODE of that node) see the current tree.
-// Rebuilt lazily, only when a compiled template reads data.inventory; the
-// previous tree's nodes stay behind in the permanent region.
+// Rebuilt lazily, only when a compiled template reads data.inventory.  The
+// new tree replaces the previous one in place when that was the last thing in
+// the permanent region; otherwise the old tree's nodes are garbage until the
+// region is compacted (maybe_compact).
 static void sync_inventory(gk_engine* e) {
   if (!e->uses_inventory || !e->inv_dirty || e->inv_node == NO_ID) return;
   std::vector<std::pair<std::vector<std::string>, const std::string*>> ents;
@@ -670,7 +750,14 @@ static void sync_inventory(gk_engine* e) {
   int root = rd.parse();
   if (root < 0) throw std::runtime_error("inventory tree: " + d.err);
   reset_transient(e);
+  if (e->inv_hi > e->inv_lo && e->inv_hi == e->perm_nodes) {
+    // the previous tree is the region's tail: reuse its space
+    e->st.nodes().resize(e->inv_lo);
+    e->perm_nodes = e->inv_lo;
+  }
+  e->inv_lo = (uint32_t)e->st.nodes().size();
   const uint32_t r = e->st.add_doc(d, root);
+  e->inv_hi = (uint32_t)e->st.nodes().size();
   Node& slot = e->st.nodes()[e->inv_node];
   const Node& t = e->st.nodes()[r];
   slot.type = t.type;
@@ -678,8 +765,59 @@ static void sync_inventory(gk_engine* e) {
   slot.n = t.n;
   slot.flags = t.flags;
   e->perm_nodes = (uint32_t)e->st.nodes().size();
-  e->dev_nodes_ok = std::min<uint32_t>(e->dev_nodes_ok, e->inv_node);
+  e->dev_nodes_ok = std::min<uint32_t>(e->dev_nodes_ok, std::min(e->inv_node, e->inv_lo));
   e->inv_dirty = false;
+}
+
+// Compaction of the permanent node region (under the exclusive lock): replaced
+// or deleted constraints, namespaces and inventory trees leave their nodes
+// behind (node ids are never reused while anything may refer to them).  When
+// that garbage outgrows the live documents, the region is rebuilt from the
+// kept JSON texts: constraints, cached namespaces, then the modules'
+// constants and the inventory tree (rebuild_modules / sync_inventory).
+static void maybe_compact(gk_engine* e, bool force = false) {
+  uint64_t live = e->base_nodes + e->module_nodes + (e->inv_hi - e->inv_lo);
+  for (auto& kv : e->constraints) live += kv.second.nnodes;
+  for (auto& kv : e->ns_nodes) live += kv.second.second;
+  const uint64_t garbage = e->perm_nodes > live ? e->perm_nodes - live : 0;
+  // GKGPU_COMPACT_MIN (tests): compact as soon as the garbage exceeds this
+  // many nodes (default: max(2^20, live nodes))
+  const char* cm = getenv("GKGPU_COMPACT_MIN");
+  const uint64_t limit = cm && *cm ? (uint64_t)atoll(cm) : std::max<uint64_t>(1u << 20, live);
+  if (!force && garbage <= limit) return;
+  e->st.nodes().resize(e->base_nodes);
+  e->perm_nodes = e->base_nodes;
+  e->dev_nodes_ok = 0;
+  e->inv_node = NO_ID;
+  e->inv_lo = e->inv_hi = 0;
+  e->inv_dirty = true;
+  e->modules_dirty = true;
+  e->constraints_dirty = true;
+  JDoc d;
+  for (auto& kv : e->constraints) {
+    ConstraintEnt& c = kv.second;
+    JsonReader rd(c.json.data(), c.json.size(), &d);
+    const int root = rd.parse();
+    const size_t n0 = e->st.nodes().size();
+    c.root = root >= 0 ? e->st.add_doc(d, root) : NO_ID;
+    c.nnodes = (uint32_t)(e->st.nodes().size() - n0);
+  }
+  for (auto& kv : e->ns_nodes) {
+    auto it = e->inventory.end();
+    for (auto jt = e->inventory.begin(); jt != e->inventory.end(); ++jt) {
+      auto q = split_path(jt->first);
+      if (q.size() == 6 && q[2] == "cluster" && q[3] == "v1" && q[4] == "Namespace" && q[5] == kv.first) { it = jt; }
+    }
+    if (it == e->inventory.end()) continue;
+    JsonReader rd(it->second.data(), it->second.size(), &d);
+    const int root = rd.parse();
+    const size_t n0 = e->st.nodes().size();
+    const uint32_t node = root >= 0 ? e->st.add_doc(d, root) : NO_ID;
+    kv.second = {node, (uint32_t)(e->st.nodes().size() - n0)};
+    e->ns_cache[kv.first] = node;
+  }
+  e->perm_nodes = (uint32_t)e->st.nodes().size();
+  e->gen++;
 }
 
 static void rebuild_constraints(gk_engine* e) {
@@ -745,7 +883,6 @@ static bool ensure_device(gk_engine* e) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= e->device) return false;
   if (hipSetDevice(e->device) != hipSuccess) return false;
-  if (hipStreamCreate(&e->stream) != hipSuccess) return false;
   e->dev_ok = true;
   return true;
 }
@@ -755,38 +892,42 @@ static bool up(DBuf& b, const std::vector<T>& v, bool append_only) {
   return b.upload(v.data(), v.size() * sizeof(T), append_only);
 }
 
-static bool sync_tables(gk_engine* e, bool nodes = true) {
+// The string / number tables' new tails to the device (append-only), and the
+// pointers an evaluation launches with.  Under smu: evaluations intern while
+// they flatten.
+static bool sync_strings(gk_engine* e, TablePtrs* out) {
+  std::lock_guard<std::mutex> g(e->smu);
+  if (hipSetDevice(e->device) != hipSuccess) return false;
+  Store& st = e->st;
+  bool ok = up(e->d_strs, st.strings(), true);
+  // +16: the device reads string bytes a dword at a time (devrt.h puts_) and may
+  // touch up to 3 bytes past the last string
+  ok = ok && e->d_pool.reserve(st.pool().size() + 16);
+  ok = ok && e->d_pool.upload(st.pool().data(), st.pool().size(), true);
+  ok = ok && up(e->d_sflags, st.str_flags(), true);
+  ok = ok && up(e->d_nums, st.numbers(), true);
+  if (out) {
+    out->strs = (const StrEnt*)e->d_strs.p;
+    out->pool = (const uint8_t*)e->d_pool.p;
+    out->sflags = (const uint8_t*)e->d_sflags.p;
+    out->nums = (const NumEnt*)e->d_nums.p;
+  }
+  return ok;
+}
+
+// The permanent tables to the device (under the exclusive lock: no evaluation
+// in flight): the permanent node region's new tail, bytecode, constants,
+// formats, constraints' match words, regex DFAs.
+static bool sync_tables(gk_engine* e) {
   Store& st = e->st;
   bool ok = true;
-  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
-  auto t0 = std::chrono::steady_clock::now();
-  auto lap = [&](const char* what) {
-    if (!trace) return;
-    auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "sync_tables: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
-    t0 = t;
-  };
-  if (nodes) {
-    // only the nodes appended (or rewritten after a transient reset) since the
-    // last upload travel: a staged 1M-review batch is not re-sent per call
-    size_t n = st.nodes().size();
-    ok &= e->d_nodes.reserve(std::max<size_t>(n, 1) * sizeof(Node));
-    if (ok && n > e->dev_nodes_ok)
-      ok &= hipMemcpy((char*)e->d_nodes.p + (size_t)e->dev_nodes_ok * sizeof(Node), st.nodes().data() + e->dev_nodes_ok,
-                      (n - e->dev_nodes_ok) * sizeof(Node), hipMemcpyHostToDevice) == hipSuccess;
-    if (ok) { e->dev_nodes_ok = (uint32_t)n; e->d_nodes.used = n * sizeof(Node); }
-  }
-  lap("nodes");
-  ok &= up(e->d_strs, st.strings(), true);
-  lap("strs");
-  // +16: the device reads string bytes a dword at a time (devrt.h ByteRd) and may
-  // touch up to 3 bytes past the last string
-  ok &= e->d_pool.reserve(st.pool().size() + 16);
-  ok &= e->d_pool.upload(st.pool().data(), st.pool().size(), true);
-  lap("pool");
-  ok &= up(e->d_sflags, st.str_flags(), true);
-  ok &= up(e->d_nums, st.numbers(), true);
-  lap("flags+nums");
+  const size_t n = st.nodes().size();
+  ok &= e->d_nodes.reserve(std::max<size_t>(n, 1) * sizeof(Node));
+  if (ok && n > e->dev_nodes_ok)
+    ok &= hipMemcpy((char*)e->d_nodes.p + (size_t)e->dev_nodes_ok * sizeof(Node), st.nodes().data() + e->dev_nodes_ok,
+                    (n - e->dev_nodes_ok) * sizeof(Node), hipMemcpyHostToDevice) == hipSuccess;
+  if (ok) { e->dev_nodes_ok = (uint32_t)n; e->d_nodes.used = n * sizeof(Node); }
+  ok &= sync_strings(e, nullptr);
   ok &= up(e->d_code, e->bank.code, false);
   ok &= up(e->d_K, e->bank.consts, false);
   std::vector<uint32_t> fmt = e->bank.fmt;
@@ -809,7 +950,6 @@ static bool sync_tables(gk_engine* e, bool nodes = true) {
   ok &= up(e->d_dfa_keys, dk, false);
   ok &= up(e->d_dfa_meta, dm, false);
   ok &= up(e->d_dfa_words, dw, false);
-  lap("rest");
   return ok;
 }
 
@@ -827,26 +967,146 @@ static void ensure_jit(gk_engine* e, bool load) {
   if (!load) return;
   for (auto& j : e->jits) {
     if (j.state != 1 || j.fn) continue;
-    size_t asz = 0;
     if (hipModuleLoadData(&j.mod, j.code.data()) != hipSuccess ||
-        hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess ||
-        hipModuleGetGlobal(&j.args, &asz, j.mod, "gk_args") != hipSuccess || asz != sizeof(DevArgs)) {
+        hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess) {
       if (j.mod) hipModuleUnload(j.mod);
       j.mod = nullptr;
       j.fn = nullptr;
-      j.args = nullptr;
       j.state = -1;
       j.log = "module load failed";
     }
   }
 }
 
-// runs the kernel over `cols` (already resident in d_revs when `resident`)
-static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, DBuf* revbuf, bool decode,
-                              gk_results* res, const void* nodes = nullptr, uint64_t n_excluded = 0) {
+// ------------------------------------------------------------------ locking
+// Brings the compiled state (templates, constraints' match words, inventory
+// tree, regex DFAs) and the device tables up to date with the last mutation.
+// Called with the exclusive lock held.
+static int prepare_locked(gk_engine* e, bool device) {
+  try {
+    maybe_compact(e);
+    rebuild_constraints(e);
+    rebuild_regex(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  if (device && ensure_device(e)) {
+    ensure_jit(e, true);
+    if (!sync_tables(e)) return fail(e, GK_EDEVICE, "device upload failed");
+  }
+  e->prepared_gen = e->gen;
+  // the device side was brought up to date, or there is no device to use
+  // (the evaluation then fails with GK_EDEVICE)
+  e->prepared_dev = device;
+  return GK_OK;
+}
+
+static bool prepared(const gk_engine* e, bool device) {
+  return e->prepared_gen == e->gen && (!device || e->prepared_dev);
+}
+
+// An evaluation's hold on the engine: the shared lock, taken once the engine
+// is prepared for this state (a stale engine is prepared under the exclusive
+// lock first, then the shared lock is taken again).
+struct ReadLock {
+  std::shared_lock<std::shared_mutex> lk;
+};
+// the shared lock without preparing (reads of the mutation-side state)
+static void read_lock_raw(gk_engine* e, ReadLock& r) {
+  { std::lock_guard<std::mutex> t(e->turn); }
+  r.lk = std::shared_lock<std::shared_mutex>(e->rw);
+}
+static int read_lock(gk_engine* e, ReadLock& r, bool device) {
+  for (;;) {
+    { std::lock_guard<std::mutex> t(e->turn); }
+    r.lk = std::shared_lock<std::shared_mutex>(e->rw);
+    if (prepared(e, device)) return GK_OK;
+    r.lk.unlock();
+    std::lock_guard<std::mutex> t(e->turn);
+    std::unique_lock<std::shared_mutex> w(e->rw);
+    if (!prepared(e, device)) {
+      int rc = prepare_locked(e, device);
+      if (rc != GK_OK) return rc;
+    }
+  }
+}
+
+// A mutation's hold: new readers queue behind it on `turn`
+struct WriteLock {
+  std::lock_guard<std::mutex> t;
+  std::unique_lock<std::shared_mutex> w;
+  explicit WriteLock(gk_engine* e) : t(e->turn), w(e->rw) {}
+};
+
+// An evaluation context from the pool (a new one when all are busy)
+struct CtxLease {
+  gk_engine* e;
+  EvalCtx* x = nullptr;
+  std::unique_lock<std::mutex> hold;
+  explicit CtxLease(gk_engine* eng) : e(eng) {
+    std::lock_guard<std::mutex> g(e->pool_mu);
+    for (auto& c : e->ctxs) {
+      std::unique_lock<std::mutex> h(c->busy, std::try_to_lock);
+      if (h.owns_lock()) { x = c.get(); hold = std::move(h); return; }
+    }
+    e->ctxs.push_back(std::make_unique<EvalCtx>());
+    x = e->ctxs.back().get();
+    x->out_cap = e->out_cap0;
+    if (const char* tc = getenv("GKGPU_TEST_CAPS")) {
+      // tests: initial tuple, staged-byte and output-byte capacities (overflow paths)
+      unsigned long long t = 0, eb = 0, b = 0;
+      if (sscanf(tc, "%llu,%llu,%llu", &t, &eb, &b) == 3 && t && eb && b) {
+        x->out_cap = t;
+        x->ebytes_cap = eb;
+        x->bytes_cap = b;
+      }
+    }
+    hold = std::unique_lock<std::mutex>(x->busy);
+  }
+};
+
+// device-to-host copy on the context's stream (concurrent evaluations do not
+// serialize on the null stream)
+static bool d2h(EvalCtx* x, void* dst, const void* src, size_t n) {
+  if (!n) return true;
+  return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, x->stream) == hipSuccess &&
+         hipStreamSynchronize(x->stream) == hipSuccess;
+}
+
+static bool ctx_device(gk_engine* e, EvalCtx* x) {
+  if (hipSetDevice(e->device) != hipSuccess) return false;
+  if (!x->stream && hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return false;
+  return true;
+}
+
+// The device node array of a query: the engine's permanent region (copied on
+// the device, once per engine state) followed by the call's documents.
+static bool ctx_nodes(gk_engine* e, EvalCtx* x, const NodeArena& arena) {
+  const size_t perm = e->perm_nodes;
+  if (!x->d_nodes.reserve((perm + arena.size() + 1) * sizeof(Node))) return false;
+  if (x->perm_gen != e->prepared_gen || x->perm_nodes != perm) {
+    if (perm && hipMemcpyAsync(x->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice, x->stream) != hipSuccess)
+      return false;
+    x->perm_gen = e->prepared_gen;
+    x->perm_nodes = (uint32_t)perm;
+  }
+  if (arena.size() &&
+      hipMemcpyAsync((char*)x->d_nodes.p + perm * sizeof(Node), arena.data(), arena.size() * sizeof(Node),
+                     hipMemcpyHostToDevice, x->stream) != hipSuccess)
+    return false;
+  return hipStreamSynchronize(x->stream) == hipSuccess;
+}
+
+// Runs the launch plan over `cols` on the evaluation context `x` (its stream
+// and output buffers): `revbuf` holds the columns on the device (uploaded here
+// when it is the context's own buffer), `nodes` the documents, `tp` the string
+// tables as of this call.  Shared lock held.
+static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, const std::vector<ReviewCol>& cols,
+                              DBuf* revbuf, bool decode, gk_results* res, const void* nodes, uint64_t n_excluded = 0) {
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
   res->nrev = nrev;
+  res->gen = e->gen;
   res->excluded = n_excluded;
   res->totals.assign(ncons, 0);
   for (auto* c : e->corder) {
@@ -872,23 +1132,27 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     mark_excluded();
     return GK_OK;
   }
-  if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
+  if (!e->dev_ok || !ctx_device(e, x)) return fail(e, GK_EDEVICE, "no HIP device available");
+  res->ctx = x;
   auto t0 = Clock::now();
-  if (!sync_tables(e, nodes == nullptr)) return fail(e, GK_EDEVICE, "device upload failed");
-  if (revbuf == &e->d_revs || !revbuf->p || revbuf->used != cols.size() * sizeof(ReviewCol)) {
+  if (revbuf == &x->d_revs || !revbuf->p || revbuf->used != cols.size() * sizeof(ReviewCol)) {
     if (!up(*revbuf, cols, false)) return fail(e, GK_EDEVICE, "device upload failed");
   }
-  bool ok = true;
-  ok &= e->d_rflags.reserve(nrev * 4) && e->d_rreason.reserve(nrev * 4) && e->d_totals.reserve(ncons * 8) &&
-        e->d_counters.reserve(64 + 16 * (e->progs.size() + 1)) && e->d_out.reserve(e->out_cap * sizeof(Viol)) && e->d_bytes.reserve(e->bytes_cap);
+  // output buffers: tuples + their deferred-argument words (frec, structure of
+  // arrays), bytes staged at emission (ebytes), per-tuple byte counts and tile
+  // sums of the size pass, final message bytes (+16: dword reads past the end)
+  auto reserve_out = [&]() {
+    return x->d_out.reserve(x->out_cap * sizeof(Viol)) && x->d_frec.reserve(x->out_cap * FMT_MAXARGS * 8) &&
+           x->d_lens.reserve(x->out_cap * 4) && x->d_part.reserve((x->out_cap / FTILE + 2) * 8) &&
+           x->d_ebytes.reserve(x->ebytes_cap + 16) && x->d_bytes.reserve(x->bytes_cap + 16);
+  };
+  bool ok = x->d_rflags.reserve(nrev * 4) && x->d_rreason.reserve(nrev * 4) && x->d_totals.reserve(ncons * 8) &&
+            x->d_counters.reserve(64 + 16 * (e->progs.size() + 1)) && reserve_out();
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
-  // deferred-message records for the format pass (GKGPU_FORMAT_PASS=0: format in the audit kernels)
-  const bool fpass = env_mode("GKGPU_FORMAT_PASS", 1, 1) != 0;
-  if (fpass && !e->d_frec.reserve(e->out_cap * FREC_WORDS * 8)) return fail(e, GK_EDEVICE, "device allocation failed");
   // launch plan: constraints grouped by template kernel (jit.cc); the bytecode
   // VM kernel takes every constraint whose template has no kernel / program
   ensure_jit(e, true);
-  struct Step { hipFunction_t fn; hipDeviceptr_t args; std::string name; uint32_t off, n; };
+  struct Step { hipFunction_t fn; std::string name; uint32_t off, n; };
   std::vector<Step> plan;
   {
     std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
@@ -901,32 +1165,31 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     for (size_t g = 0; g < groups.size(); ++g) {
       if (groups[g].empty()) continue;
       bool vm = g == e->progs.size();
-      plan.push_back({vm ? nullptr : e->jits[g].fn, vm ? nullptr : e->jits[g].args,
-                      vm ? std::string("audit_kernel") : e->jits[g].name,
+      plan.push_back({vm ? nullptr : e->jits[g].fn, vm ? std::string("audit_kernel") : e->jits[g].name,
                       (uint32_t)clist.size(), (uint32_t)groups[g].size()});
       clist.insert(clist.end(), groups[g].begin(), groups[g].end());
     }
-    if (!up(e->d_clist, clist, false)) return fail(e, GK_EDEVICE, "device upload failed");
+    if (!up(x->d_clist, clist, false)) return fail(e, GK_EDEVICE, "device upload failed");
   }
   res->ms[1] = ms_since(t0);
   for (int attempt = 0; attempt < 4; ++attempt) {
-    hipMemsetAsync(e->d_rflags.p, 0, nrev * 4, e->stream);
-    hipMemsetAsync(e->d_rreason.p, 0, nrev * 4, e->stream);
-    hipMemsetAsync(e->d_totals.p, 0, ncons * 8, e->stream);
-    hipMemsetAsync(e->d_counters.p, 0, 64 + 16 * plan.size(), e->stream);
-    bool prof = e->profile && e->d_prof.reserve(ncons * 32);
-    if (prof) hipMemsetAsync(e->d_prof.p, 0, ncons * 32, e->stream);
+    hipMemsetAsync(x->d_rflags.p, 0, nrev * 4, x->stream);
+    hipMemsetAsync(x->d_rreason.p, 0, nrev * 4, x->stream);
+    hipMemsetAsync(x->d_totals.p, 0, ncons * 8, x->stream);
+    hipMemsetAsync(x->d_counters.p, 0, 64 + 16 * plan.size(), x->stream);
+    bool prof = e->profile && x->d_prof.reserve(ncons * 32);
+    if (prof) hipMemsetAsync(x->d_prof.p, 0, ncons * 32, x->stream);
     DevArgs a{};
-    a.prof = prof ? (unsigned long long*)e->d_prof.p : nullptr;
+    a.prof = prof ? (unsigned long long*)x->d_prof.p : nullptr;
     uint32_t ncode = (uint32_t)e->bank.code.size();
-    bool hist = e->profile >= 2 && e->d_pchist.reserve(ncode * 4);
-    if (hist) hipMemsetAsync(e->d_pchist.p, 0, ncode * 4, e->stream);
-    a.pchist = hist ? (unsigned int*)e->d_pchist.p : nullptr;
-    a.nodes = (const Node*)(nodes ? nodes : e->d_nodes.p);
-    a.strs = (const StrEnt*)e->d_strs.p;
-    a.pool = (const uint8_t*)e->d_pool.p;
-    a.sflags = (const uint8_t*)e->d_sflags.p;
-    a.nums = (const NumEnt*)e->d_nums.p;
+    bool hist = e->profile >= 2 && x->d_pchist.reserve(ncode * 4);
+    if (hist) hipMemsetAsync(x->d_pchist.p, 0, ncode * 4, x->stream);
+    a.pchist = hist ? (unsigned int*)x->d_pchist.p : nullptr;
+    a.nodes = (const Node*)nodes;
+    a.strs = tp.strs;
+    a.pool = tp.pool;
+    a.sflags = tp.sflags;
+    a.nums = tp.nums;
     a.code = (const Ins*)e->d_code.p;
     a.K = (const uint64_t*)e->d_K.p;
     a.fmt = (const uint32_t*)e->d_fmt.p;
@@ -942,61 +1205,82 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     a.ncons = ncons;
     a.nrev = nrev;
     a.ntiles = (nrev + 63) / 64;
-    a.out = (Viol*)e->d_out.p;
-    a.out_cap = e->out_cap;
-    a.counters = (unsigned long long*)e->d_counters.p;
-    a.bytes = (char*)e->d_bytes.p;
-    a.bytes_cap = e->bytes_cap;
-    a.rflags = (uint32_t*)e->d_rflags.p;
-    a.totals = (unsigned long long*)e->d_totals.p;
-    a.rreason = (uint32_t*)e->d_rreason.p;
-    a.frec = fpass ? (uint64_t*)e->d_frec.p : nullptr;
-    while (e->events.size() < plan.size() + 2) {
-      hipEvent_t x;
-      if (hipEventCreate(&x) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
-      e->events.push_back(x);
+    a.out = (Viol*)x->d_out.p;
+    a.out_cap = x->out_cap;
+    a.counters = (unsigned long long*)x->d_counters.p;
+    a.bytes = (char*)x->d_bytes.p;
+    a.bytes_cap = x->bytes_cap;
+    a.rflags = (uint32_t*)x->d_rflags.p;
+    a.totals = (unsigned long long*)x->d_totals.p;
+    a.rreason = (uint32_t*)x->d_rreason.p;
+    a.frec = (uint64_t*)x->d_frec.p;
+    a.ebytes = (char*)x->d_ebytes.p;
+    a.ebytes_cap = x->ebytes_cap;
+    a.lens = (uint32_t*)x->d_lens.p;
+    a.part = (unsigned long long*)x->d_part.p;
+    while (x->events.size() < plan.size() + 4) {
+      hipEvent_t ev1;
+      if (hipEventCreate(&ev1) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
+      x->events.push_back(ev1);
     }
-    const std::vector<hipEvent_t>& ev = e->events;
-    hipEventRecord(ev[0], e->stream);
+    const std::vector<hipEvent_t>& ev = x->events;
+    hipEventRecord(ev[0], x->stream);
     std::vector<DevArgs> argv(plan.size(), a);  // live until the stream sync below
     for (size_t i = 0; i < plan.size(); ++i) {
-      argv[i].clist = (const uint32_t*)e->d_clist.p + plan[i].off;
+      argv[i].clist = (const uint32_t*)x->d_clist.p + plan[i].off;
       argv[i].nclist = plan[i].n;
       const DevArgs& a = argv[i];
       int lr;
       if (plan[i].fn) {
         // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
         const bool gm_on = env_mode("GKGPU_GMEMO", 1, 1) != 0;  // A/B switch
-        if (gm_on && e->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
-          argv[i].gmemo = (uint64_t*)e->d_gmemo.p;
+        if (gm_on && x->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
+          argv[i].gmemo = (uint64_t*)x->d_gmemo.p;
           argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
-          hipMemsetAsync(e->d_gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, e->stream);
+          hipMemsetAsync(x->d_gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, x->stream);
         }
         uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
         uint32_t blocks = (uint32_t)((threads + 255) / 256);
-        lr = (int)hipMemcpyHtoDAsync(plan[i].args, (void*)&a, sizeof(a), e->stream);
-        if (lr == 0)
-          lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, e->stream, nullptr, nullptr);
+        // the arguments travel in the dispatch's kernarg segment (devrt.h gk_args)
+        void* params[] = {(void*)&argv[i]};
+        lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, x->stream, params, nullptr);
       } else {
-        lr = gk_launch_audit(&a, e->stream);
+        lr = gk_launch_audit(&a, x->stream);
       }
-      hipEventRecord(ev[i + 1], e->stream);
+      hipEventRecord(ev[i + 1], x->stream);
       // cumulative (tuples, bytes) after this launch -> per-launch output counts
-      hipMemcpyAsync((char*)e->d_counters.p + 64 + 16 * i, e->d_counters.p, 16, hipMemcpyDeviceToDevice, e->stream);
+      hipMemcpyAsync((char*)x->d_counters.p + 64 + 16 * i, x->d_counters.p, 16, hipMemcpyDeviceToDevice, x->stream);
       if (lr != 0) {
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
     }
-    // format pass over the deferred messages of every launch above
-    if (fpass) {
-      int lr = gk_launch_format(&a, e->stream);
-      hipEventRecord(ev[plan.size() + 1], e->stream);
-      if (lr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)lr));
+    // size, spine and format passes over the tuples of every launch above
+    int flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 1]);
+    if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)flr));
+    if (hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
+    // [0] tuples, [1] staged bytes, [2] lanes that flagged their review (error/fallback), [3] output bytes
+    uint64_t counters[4];
+    d2h(x, counters, x->d_counters.p, 32);
+    if (counters[0] > x->out_cap || counters[1] > x->ebytes_cap) {
+      x->out_cap = std::max<size_t>(x->out_cap * 2, counters[0] + 1024);
+      x->ebytes_cap = std::max<size_t>(x->ebytes_cap * 2, (size_t)counters[1] + 65536);
+      if (!reserve_out()) return fail(e, GK_EDEVICE, "device allocation failed");
+      continue;
     }
-    if (hipStreamSynchronize(e->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
+    if (counters[3] > x->bytes_cap) {
+      // the tuples are complete; only the output bytes did not fit: grow them
+      // and run the passes again
+      x->bytes_cap = std::max<size_t>(x->bytes_cap * 2, (size_t)counters[3] + 65536);
+      if (!reserve_out()) return fail(e, GK_EDEVICE, "device allocation failed");
+      a.bytes = (char*)x->d_bytes.p;
+      a.bytes_cap = x->bytes_cap;
+      flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 1]);
+      if (flr != 0 || hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "format pass failed");
+      d2h(x, counters, x->d_counters.p, 32);
+    }
     res->launches.clear();
     std::vector<uint64_t> snap(2 * plan.size());
-    hipMemcpy(snap.data(), (char*)e->d_counters.p + 64, 16 * plan.size(), hipMemcpyDeviceToHost);
+    d2h(x, snap.data(), (char*)x->d_counters.p + 64, 16 * plan.size());
     for (size_t i = 0; i < plan.size(); ++i) {
       float kms = 0;
       hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
@@ -1004,32 +1288,23 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
       uint64_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
       res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
-    if (fpass) {
-      float kms = 0;
-      hipEventElapsedTime(&kms, ev[plan.size()], ev[plan.size() + 1]);
-      res->ms[2] += kms;
-      res->launches.push_back({"gk_format_kernel", (double)kms, 0, 0, 0});
+    {
+      float k_size = 0, k_spine = 0, k_fmt = 0;
+      hipEventElapsedTime(&k_size, ev[plan.size()], ev[plan.size() + 1]);
+      hipEventElapsedTime(&k_spine, ev[plan.size() + 1], ev[plan.size() + 2]);
+      hipEventElapsedTime(&k_fmt, ev[plan.size() + 2], ev[plan.size() + 3]);
+      res->ms[2] += k_size + k_spine + k_fmt;
+      res->launches.push_back({"gk_size_kernel", (double)k_size, 0, 0, 0});
+      res->launches.push_back({"gk_scan_spine", (double)k_spine, 0, 0, 0});
+      res->launches.push_back({"gk_format_kernel", (double)k_fmt, 0, 0, counters[3]});
     }
     auto t1 = Clock::now();
-    // [0] tuples, [1] message bytes, [2] lanes that flagged their review (error/fallback)
-    uint64_t counters[3];
-    hipMemcpy(counters, e->d_counters.p, 24, hipMemcpyDeviceToHost);
-    if (counters[0] > e->out_cap || counters[1] > e->bytes_cap) {
-      e->out_cap = std::max<size_t>(e->out_cap * 2, counters[0] + 1024);
-      e->bytes_cap = std::max<size_t>(e->bytes_cap * 2, (size_t)counters[1] + 65536);
-      if (!e->d_out.reserve(e->out_cap * sizeof(Viol)) || !e->d_bytes.reserve(e->bytes_cap) ||
-          (fpass && !e->d_frec.reserve(e->out_cap * FREC_WORDS * 8)))
-        return fail(e, GK_EDEVICE, "device allocation failed");
-      continue;
-    }
     res->dev_tuples = counters[0];
-    res->dev_bytes = counters[1];
+    res->dev_bytes = counters[3];
     res->failed_lanes = counters[2];
-    res->d_tuples = e->d_out.p;
-    res->d_bytes = e->d_bytes.p;
-    res->epoch = ++e->eval_epoch;
+    res->epoch = ++x->eval_epoch;
     std::vector<uint64_t> tot(ncons);
-    hipMemcpy(tot.data(), e->d_totals.p, ncons * 8, hipMemcpyDeviceToHost);
+    d2h(x, tot.data(), x->d_totals.p, ncons * 8);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
     bool ea_err = false;
     for (auto* c : e->corder) ea_err |= c->ea_error;
@@ -1042,25 +1317,26 @@ static int launch_and_collect(gk_engine* e, const std::vector<ReviewCol>& cols, 
     }
     res->status.assign(nrev, 0);
     res->reason.assign(nrev, 0);
-    hipMemcpy(res->status.data(), e->d_rflags.p, nrev * 4, hipMemcpyDeviceToHost);
-    hipMemcpy(res->reason.data(), e->d_rreason.p, nrev * 4, hipMemcpyDeviceToHost);
+    d2h(x, res->status.data(), x->d_rflags.p, nrev * 4);
+    d2h(x, res->reason.data(), x->d_rreason.p, nrev * 4);
     if (hist) {
+      std::lock_guard<std::mutex> g(e->dbg_mu);
       e->pchist.assign(ncode, 0);
-      hipMemcpy(e->pchist.data(), e->d_pchist.p, ncode * 4, hipMemcpyDeviceToHost);
+      d2h(x, e->pchist.data(), x->d_pchist.p, ncode * 4);
     }
     if (prof) {
       res->prof.assign(ncons * 4, 0);
-      hipMemcpy(res->prof.data(), e->d_prof.p, ncons * 32, hipMemcpyDeviceToHost);
+      d2h(x, res->prof.data(), x->d_prof.p, ncons * 32);
     }
     bool flagged = false;
     for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
     if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); mark_excluded(); return GK_OK; }
     std::vector<Viol> vs(counters[0]);
     std::string bytes;
-    if (counters[0]) hipMemcpy(vs.data(), e->d_out.p, counters[0] * sizeof(Viol), hipMemcpyDeviceToHost);
+    if (counters[0]) d2h(x, vs.data(), x->d_out.p, counters[0] * sizeof(Viol));
     if (decode) {
-      bytes.assign(counters[1], '\0');
-      if (counters[1]) hipMemcpy(&bytes[0], e->d_bytes.p, counters[1], hipMemcpyDeviceToHost);
+      bytes.assign(counters[3], '\0');
+      if (counters[3]) d2h(x, &bytes[0], x->d_bytes.p, counters[3]);
     }
     res->ms[3] = ms_since(t1);
     auto t2 = Clock::now();
@@ -1130,7 +1406,7 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
       int hv = d.get(r, "host_only");
       if (hv >= 0 && d.nodes[hv].type == NT_TRUE) e->host_only = true;
       int mv = d.get(r, "max_violations");
-      if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap = (size_t)atoll(d.str(d.nodes[mv]));
+      if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap0 = std::max<size_t>(64, (size_t)atoll(d.str(d.nodes[mv])));
     }
   }
   {
@@ -1140,23 +1416,24 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
     if (je && *je == '0') e->jit_enabled = false;
   }
   e->perm_nodes = (uint32_t)e->st.nodes().size();
+  e->base_nodes = e->perm_nodes;
+  e->d_strs.graveyard = e->d_pool.graveyard = e->d_sflags.graveyard = e->d_nums.graveyard = &e->graveyard;
   *out = e;
   return GK_OK;
 }
 
 void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
+  for (auto& x : e->ctxs) x->release_all();
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
-                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
-                  &e->d_revs, &e->d_out, &e->d_bytes, &e->d_counters, &e->d_rflags, &e->d_totals, &e->d_rreason, &e->d_prof, &e->d_pchist, &e->d_clist, &e->d_gmemo, &e->d_frec, &e->d_hist, &e->d_cut, &e->d_ftot, &e->d_cand, &e->d_ncand, &e->d_cerr})
+                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words})
     b->free_();
+  for (void* p : e->graveyard) hipFree(p);
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
-  for (hipEvent_t x : e->events) hipEventDestroy(x);
-  if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
 
-const char* gk_last_error(gk_engine* e) { return e ? e->err.c_str() : "null engine"; }
+const char* gk_last_error(gk_engine* e) { return e ? tl_err.c_str() : "null engine"; }
 
 int gk_init(gk_engine* e) {
   if (!e) return GK_EINVAL;
@@ -1165,7 +1442,7 @@ int gk_init(gk_engine* e) {
 
 int gk_put_module(gk_engine* e, const char* name, const char* src, size_t len) {
   if (!e || !name || !src) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   std::string s(src, len);
   try {
     rego::parse_module(s);
@@ -1191,7 +1468,7 @@ static int delete_modules_locked(gk_engine* e, const std::string& prefix) {
 
 int gk_put_modules(gk_engine* e, const char* prefix, const char* const* srcs, const size_t* lens, size_t n) {
   if (!e || !prefix) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   std::vector<std::string> ss;
   for (size_t i = 0; i < n; ++i) {
     std::string s(srcs[i], lens ? lens[i] : strlen(srcs[i]));
@@ -1212,7 +1489,7 @@ int gk_put_modules(gk_engine* e, const char* prefix, const char* const* srcs, co
 
 int gk_delete_module(gk_engine* e, const char* name, int* deleted) {
   if (!e || !name) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   int d = (int)e->modules.erase(name);
   if (d) { e->modules_dirty = true; e->gen++; }
   if (deleted) *deleted = d;
@@ -1221,7 +1498,7 @@ int gk_delete_module(gk_engine* e, const char* name, int* deleted) {
 
 int gk_delete_modules(gk_engine* e, const char* prefix, int* count) {
   if (!e || !prefix) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   int n = delete_modules_locked(e, prefix);
   if (count) *count = n;
   return GK_OK;
@@ -1229,7 +1506,7 @@ int gk_delete_modules(gk_engine* e, const char* prefix, int* count) {
 
 int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
   if (!e || !path || !json) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   auto p = split_path(path);
   JDoc d;
   JsonReader rd(json, len, &d);
@@ -1242,7 +1519,10 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
     ConstraintEnt c;
     c.kind = p[4];
     c.name = p[5];
+    c.json.assign(json, len);
+    const size_t n0 = e->st.nodes().size();
     c.root = e->st.add_doc(d, root);
+    c.nnodes = (uint32_t)(e->st.nodes().size() - n0);
     e->perm_nodes = (uint32_t)e->st.nodes().size();
     e->constraints[{c.kind, c.name}] = c;
     e->constraints_dirty = true;
@@ -1255,7 +1535,10 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
     if (p.size() == 6 && p[2] == "cluster" && p[3] == "v1" && p[4] == "Namespace") {
       rebuild_modules(e);
       reset_transient(e);
-      e->ns_cache[p[5]] = e->st.add_doc(d, root);
+      const size_t n0 = e->st.nodes().size();
+      const uint32_t node = e->st.add_doc(d, root);
+      e->ns_cache[p[5]] = node;
+      e->ns_nodes[p[5]] = {node, (uint32_t)(e->st.nodes().size() - n0)};
       e->perm_nodes = (uint32_t)e->st.nodes().size();
     }
     return GK_OK;
@@ -1266,7 +1549,7 @@ int gk_put_data(gk_engine* e, const char* path, const char* json, size_t len) {
 
 int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
   if (!e || !path) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   auto p = split_path(path);
   int d = 0;
   e->gen++;
@@ -1286,59 +1569,54 @@ int gk_delete_data(gk_engine* e, const char* path, int* deleted) {
   }
   for (auto it = e->ns_cache.begin(); it != e->ns_cache.end();) {
     std::vector<std::string> q{"external", TARGET, "cluster", "v1", "Namespace", it->first};
-    if (prefix_match(q)) { it = e->ns_cache.erase(it); d = 1; }
+    if (prefix_match(q)) { e->ns_nodes.erase(it->first); it = e->ns_cache.erase(it); d = 1; }
     else ++it;
   }
   for (auto it = e->other_data.begin(); it != e->other_data.end();) {
     if (prefix_match(split_path(it->first))) { it = e->other_data.erase(it); d = 1; }
     else ++it;
   }
-  if (p.empty()) { e->constraints.clear(); e->inventory.clear(); e->ns_cache.clear(); e->other_data.clear(); d = 1; e->inv_dirty = true; }
+  if (p.empty()) {
+    e->constraints.clear();
+    e->inventory.clear();
+    e->ns_cache.clear();
+    e->ns_nodes.clear();
+    e->other_data.clear();
+    d = 1;
+    e->inv_dirty = true;
+  }
   if (deleted) *deleted = d;
   return GK_OK;
 }
 
-// Query inputs ({"review": ...} documents) into the transient region
-static int flatten_inputs(gk_engine* e, const std::vector<std::pair<const char*, size_t>>& inputs,
-                          std::vector<ReviewCol>& cols) {
-  cols.reserve(inputs.size());
-  JDoc d;
-  for (auto& in : inputs) {
-    JsonReader rd(in.first, in.second, &d);
-    int root = rd.parse();
-    if (root < 0) return fail(e, GK_EINVAL, "invalid input JSON: " + d.err);
-    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
-    uint32_t rn = rv >= 0 ? e->st.add_doc(d, rv) : NO_ID;
-    bool glob = false;
-    cols.push_back(review_columns(e->st, e->st, e->ns_cache, rn, &glob));
-  }
-  return GK_OK;
-}
-
+// n independent Query(violation, input) calls (drivers/local/local.go:302-359)
+// evaluated in one launch.  Shared lock: concurrent callers each flatten
+// their documents into their own evaluation context and run on its stream.
 static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, size_t>>& inputs, gk_results** out) {
-  auto* res = new gk_results();
-  try {
-    rebuild_constraints(e);
-    rebuild_regex(e);
-  } catch (const std::exception& ex) {
-    delete res;
-    return fail(e, GK_EPARSE, ex.what());
-  }
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  if (!e->dev_ok) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  EvalCtx* x = lease.x;
+  auto res = std::make_unique<gk_results>();
   auto t0 = Clock::now();
-  reset_transient(e);
   std::vector<ReviewCol> cols;
-  int frc = flatten_inputs(e, inputs, cols);
-  if (frc != GK_OK) { delete res; return frc; }
+  std::string err;
+  if (!flatten_reviews(e->st, e->smu, e->ns_cache, inputs, e->perm_nodes, x->arena, cols, err))
+    return fail(e, GK_EINVAL, err);
   res->ms[0] = ms_since(t0);
-  int rc = launch_and_collect(e, cols, &e->d_revs, true, res);
-  if (rc != GK_OK) { delete res; return rc; }
-  *out = res;
+  TablePtrs tp;
+  if (!ctx_device(e, x) || !sync_strings(e, &tp) || !ctx_nodes(e, x, x->arena))
+    return fail(e, GK_EDEVICE, "device upload failed");
+  rc = launch_and_collect(e, x, tp, cols, &x->d_revs, true, res.get(), x->d_nodes.p);
+  if (rc != GK_OK) return rc;
+  *out = res.release();
   return GK_OK;
 }
 
 int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len, gk_results** out) {
   if (!e || !path || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   std::string p(path);
   std::string viol = std::string("hooks[\"") + TARGET + "\"].violation";
   std::string aud = std::string("hooks[\"") + TARGET + "\"].audit";
@@ -1349,8 +1627,13 @@ int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len,
   }
   if (p == aud) {
     // hooks.audit: reviews synthesized from the synced inventory
-    // (target_template_source.go:46-89: make_review / add_field)
+    // (target_template_source.go:46-89: make_review / add_field); the
+    // inventory is read under the shared lock, evaluated in a second hold
+    // (a mutation in between is a later state, as for two Queries)
     std::vector<std::string> docs;
+    ReadLock rl;
+    int rc = read_lock(e, rl, false);
+    if (rc != GK_OK) return rc;
     std::string prefix = std::string("/external/") + TARGET + "/";
     for (auto& kv : e->inventory) {
       auto q = split_path(kv.first);
@@ -1373,6 +1656,7 @@ int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len,
                       (q.size() == 7 ? ",\"namespace\":" + js(ns) : std::string()) + "}}";
       docs.push_back(r);
     }
+    rl.lk.unlock();
     std::vector<std::pair<const char*, size_t>> in;
     for (auto& s : docs) in.push_back({s.data(), s.size()});
     return eval_inputs(e, in, out);
@@ -1382,7 +1666,6 @@ int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len,
 
 int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n, gk_results** out) {
   if (!e || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   std::vector<std::pair<const char*, size_t>> in;
   for (size_t i = 0; i < n; ++i) in.push_back({inputs[i], lens ? lens[i] : strlen(inputs[i])});
   return eval_inputs(e, in, out);
@@ -1393,13 +1676,15 @@ int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, 
 // columns (in evaluation order; each carries its batch index in `orig` when
 // reordered), the HandleViolation resource identity per batch index and the
 // number of reviews the process excluder skipped.
-static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size, std::vector<ReviewCol>& cols,
-                             std::vector<ResourceIds>* resources, uint64_t* excluded, double* ms_parse = nullptr) {
+static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size, NodeArena& arena,
+                             std::vector<ReviewCol>& cols, std::vector<ResourceIds>* resources, uint64_t* excluded,
+                             double* ms_parse = nullptr) {
   FlatResult fr;
   std::string err;
   auto exit_ = e->excluded.find("audit");
   const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
-  if (!flatten_page(e->st, e->ns_cache, ex, page, default_threads(), fr, err)) return fail(e, GK_EINVAL, err);
+  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, page, default_threads(), e->perm_nodes, arena, fr, err))
+    return fail(e, GK_EINVAL, err);
   if (ms_parse) *ms_parse = fr.ms_parse;
   if (resources) resources->swap(fr.resources);
   if (excluded) *excluded = fr.excluded;
@@ -1564,31 +1849,31 @@ static void page_from_arrays(const char* const* objs, const size_t* obj_lens, co
 }
 
 static int review_page(gk_engine* e, const Page& page, gk_results** out) {
-  auto* res = new gk_results();
-  try {
-    rebuild_constraints(e);
-    rebuild_regex(e);
-  } catch (const std::exception& ex) {
-    delete res;
-    return fail(e, GK_EPARSE, ex.what());
-  }
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  if (!e->dev_ok) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  EvalCtx* x = lease.x;
+  auto res = std::make_unique<gk_results>();
   auto t0 = Clock::now();
-  reset_transient(e);
   std::vector<ReviewCol> cols;
   uint64_t excluded = 0;
-  int rc = flatten_page_into(e, page, false, cols, nullptr, &excluded);
-  if (rc != GK_OK) { delete res; return rc; }
+  rc = flatten_page_into(e, page, false, x->arena, cols, nullptr, &excluded);
+  if (rc != GK_OK) return rc;
   res->ms[0] = ms_since(t0);
-  rc = launch_and_collect(e, cols, &e->d_revs, true, res, nullptr, excluded);
-  if (rc != GK_OK) { delete res; return rc; }
-  *out = res;
+  TablePtrs tp;
+  if (!ctx_device(e, x) || !sync_strings(e, &tp) || !ctx_nodes(e, x, x->arena))
+    return fail(e, GK_EDEVICE, "device upload failed");
+  rc = launch_and_collect(e, x, tp, cols, &x->d_revs, true, res.get(), x->d_nodes.p, excluded);
+  if (rc != GK_OK) return rc;
+  *out = res.release();
   return GK_OK;
 }
 
 int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
                       const size_t* ns_lens, size_t n, gk_results** out) {
   if (!e || !out || (n && !objs)) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   PageBuf pb;
   page_from_arrays(objs, obj_lens, ns_json, ns_lens, n, pb);
   return review_page(e, pb.page, out);
@@ -1597,65 +1882,76 @@ int gk_review_objects(gk_engine* e, const char* const* objs, const size_t* obj_l
 int gk_review_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
                    const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_results** out) {
   if (!e || !out || (n && (!objs || !obj_offs)) || (n_ns && (!nss || !ns_offs))) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
   return review_page(e, pg, out);
 }
 
-static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
-  try {
-    rebuild_constraints(e);
-    rebuild_regex(e);
-  } catch (const std::exception& ex) {
-    return fail(e, GK_EPARSE, ex.what());
+// A staged batch's device node array: the engine's permanent region (copied on
+// the device) followed by the batch's documents (large ones through the
+// pinned bounce buffers, engine.cc upload_bounce).
+static bool batch_upload(gk_engine* e, gk_batch* b) {
+  const size_t perm = b->node_begin, docs = b->arena.size();
+  if (!b->d_nodes.reserve((perm + docs + 1) * sizeof(Node))) return false;
+  if (perm && hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess)
+    return false;
+  const size_t bytes = docs * sizeof(Node);
+  char* dst = (char*)b->d_nodes.p + perm * sizeof(Node);
+  const char* bm = getenv("GKGPU_BOUNCE_MIN");  // tests: the smallest copy that takes the bounce path
+  const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+  if (bytes >= bounce_min) {
+    if (!upload_bounce(dst, (const char*)b->arena.data(), bytes)) return false;
+  } else if (bytes && hipMemcpy(dst, b->arena.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    return false;
   }
+  b->d_nodes.used = (perm + docs) * sizeof(Node);
+  return true;
+}
+
+static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
+  ReadLock rl;
+  int rc = read_lock(e, rl, !e->host_only);
+  if (rc != GK_OK) return rc;
   auto t0 = Clock::now();
-  auto* b = new gk_batch();
+  auto b = std::make_unique<gk_batch>();
   b->eng = e;
-  reset_transient(e);
-  b->node_begin = (uint32_t)e->st.nodes().size();
+  b->node_begin = e->perm_nodes;
   const bool size_order = env_mode("GKGPU_SIZE_ORDER", 1, 1) != 0;  // A/B switch (default on)
-  int rc = flatten_page_into(e, page, size_order, b->cols, &b->resources, &b->excluded, &b->ms_parse);
-  if (rc != GK_OK) { delete b; return rc; }
+  rc = flatten_page_into(e, page, size_order, b->arena, b->cols, &b->resources, &b->excluded, &b->ms_parse);
+  if (rc != GK_OK) return rc;
   b->ms_flatten = ms_since(t0);
-  b->node_end = (uint32_t)e->st.nodes().size();
+  b->node_end = b->node_begin + (uint32_t)b->arena.size();
   b->nrev = (uint32_t)page.n;
   b->gen = e->gen;
+  b->node_count = b->node_end - b->node_begin;
   auto t1 = Clock::now();
   if (e->host_only) {  // documents stay in the host arena only (gk_debug_host_args)
-    b->node_count = b->node_end - b->node_begin;
-    *out = b;
+    *out = b.release();
     return GK_OK;
   }
-  if (!ensure_device(e)) { delete b; return fail(e, GK_EDEVICE, "no HIP device available"); }
+  if (!e->dev_ok) return fail(e, GK_EDEVICE, "no HIP device available");
   const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
-  bool up_ok = sync_tables(e, false);
+  bool up_ok = sync_strings(e, nullptr);
   const double ms_tables = ms_since(t1);
   up_ok = up_ok && up(b->d_revs, b->cols, false);
   const double ms_cols = ms_since(t1);
-  up_ok = up_ok && b->d_nodes.reserve((size_t)b->node_end * sizeof(Node));
-  const double ms_alloc = ms_since(t1);
-  up_ok = up_ok && b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false);
+  up_ok = up_ok && batch_upload(e, b.get());
   if (trace)
-    fprintf(stderr, "stage upload: tables %.1f ms, columns %.1f ms, node alloc %.1f ms, nodes %.1f ms\n", ms_tables,
-            ms_cols - ms_tables, ms_alloc - ms_cols, ms_since(t1) - ms_alloc);
+    fprintf(stderr, "stage upload: strings %.1f ms, columns %.1f ms, nodes %.1f ms\n", ms_tables, ms_cols - ms_tables,
+            ms_since(t1) - ms_cols);
   if (!up_ok) {
     b->d_revs.free_();
     b->d_nodes.free_();
-    delete b;
     return fail(e, GK_EDEVICE, "upload failed");
   }
   b->ms_upload = ms_since(t1);
   b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
-  b->node_count = b->node_end - b->node_begin;
-  *out = b;
+  *out = b.release();
   return GK_OK;
 }
 
 int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* obj_lens, const char* const* ns_json,
                            const size_t* ns_lens, size_t n, gk_batch** out) {
   if (!e || !out || (n && !objs)) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   PageBuf pb;
   page_from_arrays(objs, obj_lens, ns_json, ns_lens, n, pb);
   return stage_page(e, pb.page, out);
@@ -1664,7 +1960,6 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
 int gk_batch_stage_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
                         const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_batch** out) {
   if (!e || !out || (n && (!objs || !obj_offs)) || (n_ns && (!nss || !ns_offs))) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
   Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
   return stage_page(e, pg, out);
 }
@@ -1681,7 +1976,7 @@ uint64_t gk_batch_excluded(const gk_batch* b) { return b ? b->excluded : 0; }
 
 int gk_batch_resource(gk_engine* e, const gk_batch* b, size_t review, gk_resource* out) {
   if (!e || !b || !out || review >= b->resources.size()) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  std::lock_guard<std::mutex> g(e->smu);  // string table (appended to by concurrent evaluations)
   const ResourceIds& r = b->resources[review];
   auto put = [&](char* dst, uint32_t sid) {
     std::string_view v = e->st.str(sid);
@@ -1700,13 +1995,18 @@ int gk_batch_resource(gk_engine* e, const gk_batch* b, size_t review, gk_resourc
 
 int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   if (!e || !b || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
-  auto* res = new gk_results();
-  const void* nodes = b->d_nodes.p;
-  int rc = launch_and_collect(e, b->cols, &b->d_revs, decode != 0, res, nodes, b->excluded);
-  if (rc != GK_OK) { delete res; return rc; }
-  *out = res;
+  if (!e->dev_ok || !b->d_nodes.p) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  TablePtrs tp;
+  if (!ctx_device(e, lease.x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
+  auto res = std::make_unique<gk_results>();
+  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, decode != 0, res.get(), b->d_nodes.p, b->excluded);
+  if (rc != GK_OK) return rc;
+  *out = res.release();
   return GK_OK;
 }
 
@@ -1717,58 +2017,64 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
 // gk_sample_*) so only O(constraints x limit) records reach the host.
 int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out) {
   if (!e || !b || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
-  auto* res = new gk_results();
-  int rc = launch_and_collect(e, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded);
-  if (rc != GK_OK) { delete res; return rc; }
+  if (!e->dev_ok || !b->d_nodes.p) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  EvalCtx* x = lease.x;
+  TablePtrs tp;
+  if (!ctx_device(e, x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
+  auto resp = std::make_unique<gk_results>();
+  gk_results* res = resp.get();
+  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded);
+  if (rc != GK_OK) return rc;
   res->audited = true;
   const uint32_t ncons = (uint32_t)e->corder.size(), nrev = b->nrev;
-  if (ncons == 0 || nrev == 0) { *out = res; return GK_OK; }
+  if (ncons == 0 || nrev == 0) { *out = resp.release(); return GK_OK; }
   if (res->dev_tuples == 0) {
     std::fill(res->totals.begin(), res->totals.end(), 0);
-    *out = res;
+    *out = resp.release();
     return GK_OK;
   }
   const uint32_t nb = std::min<uint32_t>(8192, nrev);
   bool any_err = false;
   std::vector<uint8_t> cerr(ncons, 0);
   for (uint32_t c = 0; c < ncons; ++c) { cerr[c] = e->corder[c]->ea_error; any_err |= cerr[c] != 0; }
-  bool ok = e->d_hist.reserve((size_t)ncons * nb * 4) && e->d_cut.reserve(ncons * 4) && e->d_ftot.reserve(ncons * 8) &&
-            e->d_ncand.reserve(16) && e->d_cand.reserve(e->cand_cap * sizeof(SampleRec)) &&
-            (!any_err || up(e->d_cerr, cerr, false));
-  if (!ok) { delete res; return fail(e, GK_EDEVICE, "device allocation failed"); }
+  bool ok = x->d_hist.reserve((size_t)ncons * nb * 4) && x->d_cut.reserve(ncons * 4) && x->d_ftot.reserve(ncons * 8) &&
+            x->d_ncand.reserve(16) && x->d_cand.reserve(x->cand_cap * sizeof(SampleRec)) &&
+            (!any_err || up(x->d_cerr, cerr, false));
+  if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");
   auto t0 = Clock::now();
-  hipEvent_t ev0 = e->events[0], ev1 = e->events[1];
-  hipEventRecord(ev0, e->stream);
+  hipEvent_t ev0 = x->events[0], ev1 = x->events[1];
+  hipEventRecord(ev0, x->stream);
   unsigned int ncand = 0;
   for (int pass = 0; pass < 3; ++pass) {
     // no lane failed and no enforcementAction error: every review counts, and
     // the sampling passes skip the per-tuple review-flag reads
-    uint32_t* rf = (any_err || res->failed_lanes) ? (uint32_t*)e->d_rflags.p : nullptr;
-    int lr = gk_launch_sample((const Viol*)e->d_out.p, res->dev_tuples, rf, nrev,
-                              any_err ? (const uint8_t*)e->d_cerr.p : nullptr, ncons, nb, std::max<uint32_t>(limit, 1),
-                              (uint32_t*)e->d_hist.p, (uint32_t*)e->d_cut.p, (unsigned long long*)e->d_ftot.p,
-                              (const char*)e->d_bytes.p, (SampleRec*)e->d_cand.p, (uint32_t)e->cand_cap,
-                              (unsigned int*)e->d_ncand.p, pass > 0, e->stream);
-    if (lr != 0) { delete res; return fail(e, GK_EDEVICE, std::string("sample launch failed: ") + hipGetErrorString((hipError_t)lr)); }
-    if (pass == 0) hipEventRecord(ev1, e->stream);
-    if (hipMemcpyAsync(&ncand, e->d_ncand.p, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess) {
-      delete res;
+    uint32_t* rf = (any_err || res->failed_lanes) ? (uint32_t*)x->d_rflags.p : nullptr;
+    int lr = gk_launch_sample((const Viol*)x->d_out.p, res->dev_tuples, rf, nrev,
+                              any_err ? (const uint8_t*)x->d_cerr.p : nullptr, ncons, nb, std::max<uint32_t>(limit, 1),
+                              (uint32_t*)x->d_hist.p, (uint32_t*)x->d_cut.p, (unsigned long long*)x->d_ftot.p,
+                              (const char*)x->d_bytes.p, (SampleRec*)x->d_cand.p, (uint32_t)x->cand_cap,
+                              (unsigned int*)x->d_ncand.p, pass > 0, x->stream);
+    if (lr != 0) return fail(e, GK_EDEVICE, std::string("sample launch failed: ") + hipGetErrorString((hipError_t)lr));
+    if (pass == 0) hipEventRecord(ev1, x->stream);
+    if (hipMemcpyAsync(&ncand, x->d_ncand.p, 4, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipStreamSynchronize(x->stream) != hipSuccess)
       return fail(e, GK_EDEVICE, "sample pass failed");
-    }
-    if (ncand <= e->cand_cap) break;
-    e->cand_cap = std::max<size_t>(e->cand_cap * 2, (size_t)ncand + 1024);
-    if (!e->d_cand.reserve(e->cand_cap * sizeof(SampleRec))) { delete res; return fail(e, GK_EDEVICE, "device allocation failed"); }
+    if (ncand <= x->cand_cap) break;
+    x->cand_cap = std::max<size_t>(x->cand_cap * 2, (size_t)ncand + 1024);
+    if (!x->d_cand.reserve(x->cand_cap * sizeof(SampleRec))) return fail(e, GK_EDEVICE, "device allocation failed");
   }
   float kms = 0;
   hipEventElapsedTime(&kms, ev0, ev1);
   res->launches.push_back({"gk_sample", (double)kms, ncons, 0, 0});
   std::vector<uint64_t> ftot(ncons);
   std::vector<SampleRec> cand(ncand);
-  hipMemcpy(ftot.data(), e->d_ftot.p, ncons * 8, hipMemcpyDeviceToHost);
-  if (ncand) hipMemcpy(cand.data(), e->d_cand.p, (size_t)ncand * sizeof(SampleRec), hipMemcpyDeviceToHost);
+  if (!d2h(x, ftot.data(), x->d_ftot.p, ncons * 8) || !d2h(x, cand.data(), x->d_cand.p, (size_t)ncand * sizeof(SampleRec)))
+    return fail(e, GK_EDEVICE, "sample copy failed");
   for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = ftot[c];
   std::sort(cand.begin(), cand.end(), [](const SampleRec& x, const SampleRec& y) {
     if (x.constraint != y.constraint) return x.constraint < y.constraint;
@@ -1792,7 +2098,7 @@ int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** 
     res->samples.push_back(std::move(sm));
   }
   res->ms[4] += ms_since(t0);
-  *out = res;
+  *out = resp.release();
   return GK_OK;
 }
 
@@ -1849,19 +2155,15 @@ uint64_t gk_batch_device_bytes(const gk_batch* b) { return b ? b->dev_bytes : 0;
 int gk_batch_stats(const gk_batch* cb, uint64_t* reviews, uint64_t* nodes, uint64_t* str_bytes, uint64_t* col_bytes) {
   if (!cb) return GK_EINVAL;
   gk_batch* b = const_cast<gk_batch*>(cb);
-  if (str_bytes && !b->str_bytes_done && b->eng && b->gen == b->eng->gen) {
+  if (str_bytes && !b->str_bytes_done && b->eng) {
     // one pass over every staged document node and each distinct string value
     // it references (computed on first request: not part of staging)
-    std::lock_guard<std::mutex> g(b->eng->mu);
+    std::lock_guard<std::mutex> g(b->eng->smu);
     const Store& st = b->eng->st;
-    if (b->node_end <= st.nodes().size()) {
-      std::vector<uint8_t> seen(st.nstrings(), 0);
-      for (uint32_t k = b->node_begin; k < b->node_end; ++k) {
-        const Node& nd = st.nodes()[k];
-        if (nd.type == NT_STR && !seen[nd.val]) { seen[nd.val] = 1; b->str_bytes += st.strings()[nd.val].len; }
-      }
-      b->str_bytes_done = true;
-    }
+    std::vector<uint8_t> seen(st.nstrings(), 0);
+    for (const Node& nd : b->arena)
+      if (nd.type == NT_STR && nd.val < seen.size() && !seen[nd.val]) { seen[nd.val] = 1; b->str_bytes += st.strings()[nd.val].len; }
+    b->str_bytes_done = true;
   }
   if (reviews) *reviews = b->nrev;
   if (nodes) *nodes = b->node_count;
@@ -1915,8 +2217,12 @@ int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double
 
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail) {
   if (!e || !kind) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  rebuild_modules(e);
+  WriteLock g(e);  // compiles on demand
+  try {
+    rebuild_modules(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
   auto it = e->templates.find(kind);
   if (it == e->templates.end()) return GK_ENOTFOUND;
   int b = 0;
@@ -1941,8 +2247,13 @@ int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char
 int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuples_dst, void* bytes_dst,
                                   uint64_t* n_tuples) {
   if (!e || !r) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  if (r->epoch == 0 || r->epoch != e->eval_epoch)
+  EvalCtx* x = r->ctx;
+  if (!x || r->epoch == 0) return fail(e, GK_EINVAL, "the results hold no device output");
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  std::lock_guard<std::mutex> hold(x->busy);  // the context may not start another evaluation meanwhile
+  if (r->epoch != x->eval_epoch || r->gen != e->gen)
     return fail(e, GK_EINVAL, "device output was overwritten by a later evaluation on this engine");
   uint64_t kept = 0;
   if (tuples_dst && r->dev_tuples) {
@@ -1953,16 +2264,18 @@ int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuple
     bool any_err = false;
     std::vector<uint8_t> cerr(ncons, 0);
     for (uint32_t c = 0; c < ncons; ++c) { cerr[c] = e->corder[c]->ea_error; any_err |= cerr[c] != 0; }
-    if (!e->d_ncand.reserve(16) || (any_err && !up(e->d_cerr, cerr, false)))
+    if (!x->d_ncand.reserve(16) || (any_err && !up(x->d_cerr, cerr, false)))
       return fail(e, GK_EDEVICE, "device allocation failed");
-    int lr = gk_launch_filter((const Viol*)r->d_tuples, r->dev_tuples, (uint32_t*)e->d_rflags.p,
-                              any_err ? (const uint8_t*)e->d_cerr.p : nullptr, (Viol*)tuples_dst,
-                              (unsigned long long*)e->d_ncand.p, e->stream);
-    if (lr != 0 || hipMemcpyAsync(&kept, e->d_ncand.p, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess)
+    int lr = gk_launch_filter((const Viol*)x->d_out.p, r->dev_tuples, (uint32_t*)x->d_rflags.p,
+                              any_err ? (const uint8_t*)x->d_cerr.p : nullptr, (Viol*)tuples_dst,
+                              (unsigned long long*)x->d_ncand.p, x->stream);
+    if (lr != 0 || hipMemcpyAsync(&kept, x->d_ncand.p, 8, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipStreamSynchronize(x->stream) != hipSuccess)
       return fail(e, GK_EDEVICE, "device copy failed");
   }
-  if (bytes_dst && r->dev_bytes && hipMemcpy(bytes_dst, r->d_bytes, r->dev_bytes, hipMemcpyDeviceToDevice) != hipSuccess)
+  if (bytes_dst && r->dev_bytes &&
+      (hipMemcpyAsync(bytes_dst, x->d_bytes.p, r->dev_bytes, hipMemcpyDeviceToDevice, x->stream) != hipSuccess ||
+       hipStreamSynchronize(x->stream) != hipSuccess))
     return fail(e, GK_EDEVICE, "device copy failed");
   if (n_tuples) *n_tuples = kept;
   return GK_OK;
@@ -1977,7 +2290,7 @@ int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* by
 
 int gk_excluder_add(gk_engine* e, const char* const* processes, size_t np, const char* const* namespaces, size_t nn) {
   if (!e || (np && !processes) || (nn && !namespaces)) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   static const char* all[] = {"audit", "webhook", "sync"};  // excluder.go allProcesses
   for (size_t i = 0; i < nn; ++i)
     for (size_t j = 0; j < np; ++j) {
@@ -1991,7 +2304,7 @@ int gk_excluder_add(gk_engine* e, const char* const* processes, size_t np, const
 
 int gk_excluder_clear(gk_engine* e) {
   if (!e) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);
   e->excluded.clear();
   e->gen++;
   return GK_OK;
@@ -1999,7 +2312,8 @@ int gk_excluder_clear(gk_engine* e) {
 
 int gk_excluder_is_excluded(gk_engine* e, const char* process, const char* ns) {
   if (!e || !process || !ns) return 0;
-  std::lock_guard<std::mutex> g(e->mu);
+  ReadLock rl;
+  read_lock_raw(e, rl);
   auto it = e->excluded.find(process);
   return it != e->excluded.end() && it->second.count(ns) ? 1 : 0;
 }
@@ -2008,7 +2322,8 @@ uint64_t gk_results_excluded(const gk_results* r) { return r ? r->excluded : 0; 
 
 int gk_dump(gk_engine* e, char** out) {
   if (!e || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  ReadLock rl;
+  read_lock_raw(e, rl);
   std::string s = "{\"modules\":[";
   bool first = true;
   for (auto& kv : e->modules) {
@@ -2079,14 +2394,15 @@ int gk_results_timing(const gk_results* r, double* ms5) {
   return GK_OK;
 }
 void gk_results_free(gk_results* r) { delete r; }
+uint64_t gk_results_generation(const gk_results* r) { return r ? r->gen : 0; }
 
 int gk_template_status(gk_engine* e, const char* kind, const char** reason) {
   if (!e || !kind) return -1;
-  std::lock_guard<std::mutex> g(e->mu);
+  WriteLock g(e);  // compiles on demand
   try {
     rebuild_modules(e);
   } catch (const std::exception& ex) {
-    e->err = ex.what();
+    fail(e, GK_EPARSE, ex.what());
     return -1;
   }
   auto it = e->templates.find(kind);
@@ -2097,15 +2413,16 @@ int gk_template_status(gk_engine* e, const char* kind, const char** reason) {
 
 size_t gk_constraint_count(gk_engine* e) {
   if (!e) return 0;
-  std::lock_guard<std::mutex> g(e->mu);
-  rebuild_constraints(e);
+  ReadLock rl;
+  if (read_lock(e, rl, false) != GK_OK) return 0;
   return e->corder.size();
 }
 
 int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name) {
   if (!e) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  rebuild_constraints(e);
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);
+  if (rc != GK_OK) return rc;
   if (i >= e->corder.size()) return GK_EINVAL;
   if (kind) *kind = e->corder[i]->kind.c_str();
   if (name) *name = e->corder[i]->name.c_str();
@@ -2117,7 +2434,10 @@ int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** n
 // ------------------------------------------------------------------ diagnostics
 extern "C" int gk_debug_store_sizes(gk_engine* e, uint64_t* nodes, uint64_t* strings) {
   if (!e) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);  // permanent region as the next evaluation sees it
+  if (rc != GK_OK) return rc;
+  std::lock_guard<std::mutex> g(e->smu);
   if (nodes) *nodes = e->st.nodes().size();
   if (strings) *strings = e->st.nstrings();
   return GK_OK;
@@ -2129,35 +2449,29 @@ extern "C" int gk_debug_store_sizes(gk_engine* e, uint64_t* nodes, uint64_t* str
 extern "C" int gk_debug_stage_inputs(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n,
                                      gk_batch** out) {
   if (!e || !out || (n && !inputs)) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  try {
-    rebuild_constraints(e);
-    rebuild_regex(e);
-  } catch (const std::exception& ex) {
-    return fail(e, GK_EPARSE, ex.what());
-  }
+  ReadLock rl;
+  int rc = read_lock(e, rl, !e->host_only);
+  if (rc != GK_OK) return rc;
   std::vector<std::pair<const char*, size_t>> in;
   for (size_t i = 0; i < n; ++i) in.push_back({inputs[i], lens ? lens[i] : strlen(inputs[i])});
-  auto* b = new gk_batch();
+  auto b = std::make_unique<gk_batch>();
   b->eng = e;
-  reset_transient(e);
-  b->node_begin = (uint32_t)e->st.nodes().size();
-  int rc = flatten_inputs(e, in, b->cols);
-  if (rc != GK_OK) { delete b; return rc; }
-  b->node_end = (uint32_t)e->st.nodes().size();
+  b->node_begin = e->perm_nodes;
+  std::string err;
+  if (!flatten_reviews(e->st, e->smu, e->ns_cache, in, e->perm_nodes, b->arena, b->cols, err))
+    return fail(e, GK_EINVAL, err);
+  b->node_end = b->node_begin + (uint32_t)b->arena.size();
   b->nrev = (uint32_t)n;
   b->gen = e->gen;
   b->resources.assign(n, ResourceIds{e->st.s_empty, e->st.s_empty, e->st.s_empty, e->st.s_empty});
   b->node_count = b->node_end - b->node_begin;
-  if (e->host_only) { *out = b; return GK_OK; }
-  if (!ensure_device(e) || !sync_tables(e, false) || !up(b->d_revs, b->cols, false) ||
-      !b->d_nodes.upload(e->st.nodes().data(), (size_t)b->node_end * sizeof(Node), false)) {
+  if (e->host_only) { *out = b.release(); return GK_OK; }
+  if (!e->dev_ok || !sync_strings(e, nullptr) || !up(b->d_revs, b->cols, false) || !batch_upload(e, b.get())) {
     b->d_revs.free_();
     b->d_nodes.free_();
-    delete b;
     return fail(e, GK_EDEVICE, "upload failed");
   }
-  *out = b;
+  *out = b.release();
   return GK_OK;
 }
 
@@ -2171,14 +2485,19 @@ extern "C" int gk_debug_stage_inputs(gk_engine* e, const char* const* inputs, co
 // gk_clock_probe).  Diagnostics for box-to-box variance of kernel times.
 extern "C" int gk_debug_clock_mhz(gk_engine* e, double* mhz) {
   if (!e || !mhz) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  if (!ensure_device(e)) return fail(e, GK_EDEVICE, "no HIP device available");
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  if (!e->dev_ok) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  if (!ctx_device(e, lease.x)) return fail(e, GK_EDEVICE, "no HIP device available");
+  hipStream_t stream = lease.x->stream;
   unsigned long long* d = nullptr;
   unsigned long long h[3] = {0, 0, 0};
   if (hipMalloc(&d, sizeof h) != hipSuccess) return fail(e, GK_EDEVICE, "device allocation failed");
-  int lr = gk_launch_clock_probe(d, 1u << 22, e->stream);
-  bool ok = lr == 0 && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
-            hipStreamSynchronize(e->stream) == hipSuccess;
+  int lr = gk_launch_clock_probe(d, 1u << 22, stream);
+  bool ok = lr == 0 && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+            hipStreamSynchronize(stream) == hipSuccess;
   hipFree(d);
   if (!ok || h[1] == 0) return fail(e, GK_EDEVICE, "clock probe failed");
   *mhz = 100.0 * (double)h[0] / (double)h[1];
@@ -2187,9 +2506,23 @@ extern "C" int gk_debug_clock_mhz(gk_engine* e, double* mhz) {
 
 extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, size_t out_size) {
   if (!e || !b || !out || out_size != sizeof(DevArgs)) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  if (b->gen != e->gen || b->node_end > e->st.nodes().size() || b->node_end < e->perm_nodes)
-    return fail(e, GK_EINVAL, "batch is not the engine's latest staged batch");
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);
+  if (rc != GK_OK) return rc;
+  if (b->gen != e->gen || b->node_begin != e->perm_nodes)
+    return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
+  std::lock_guard<std::mutex> dg(e->dbg_mu);
+  // host copies: the permanent region followed by the batch's documents, and
+  // the string / number tables as of now (concurrent evaluations append to them)
+  e->dbg_nodes.assign(e->st.nodes().begin(), e->st.nodes().begin() + e->perm_nodes);
+  e->dbg_nodes.insert(e->dbg_nodes.end(), b->arena.begin(), b->arena.end());
+  {
+    std::lock_guard<std::mutex> g(e->smu);
+    e->dbg_strs = e->st.strings();
+    e->dbg_sflags = e->st.str_flags();
+    e->dbg_nums = e->st.numbers();
+    e->dbg_pool = e->st.pool();
+  }
   e->dbg_cons.clear();
   for (auto* c : e->corder) e->dbg_cons.push_back(c->spec);
   if (e->dbg_cons.empty()) e->dbg_cons.push_back(MatchSpec{});
@@ -2205,14 +2538,13 @@ extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, si
   e->dbg_dfa_words = e->dfa_words;
   if (e->dbg_dfa_keys.empty()) { e->dbg_dfa_keys.push_back(NO_ID); e->dbg_dfa_meta.push_back(2u << 30); }
   if (e->dbg_dfa_words.empty()) e->dbg_dfa_words.push_back(0);
-  e->dbg_pool = e->st.pool();
   e->dbg_pool.append(16, '\0');  // dword reads past the last string (devrt.h puts_)
   DevArgs a{};
-  a.nodes = e->st.nodes().data();
-  a.strs = e->st.strings().data();
+  a.nodes = e->dbg_nodes.data();
+  a.strs = e->dbg_strs.data();
   a.pool = (const uint8_t*)e->dbg_pool.data();
-  a.sflags = e->st.str_flags().data();
-  a.nums = e->st.numbers().data();
+  a.sflags = e->dbg_sflags.data();
+  a.nums = e->dbg_nums.data();
   a.code = e->bank.code.data();
   a.K = e->bank.consts.data();
   a.fmt = e->dbg_fmt.data();
@@ -2239,22 +2571,23 @@ extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint6
                                      const char* nss, const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns,
                                      int threads, uint64_t* hash, uint64_t* nodes, double* ms2) {
   if (!e) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  try {
-    rebuild_constraints(e);
-  } catch (const std::exception& ex) {
-    return fail(e, GK_EPARSE, ex.what());
-  }
-  reset_transient(e);
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);
+  if (rc != GK_OK) return rc;
   Page pg{objs, obj_offs, n, nss, ns_offs, n_ns, obj_ns};
   FlatResult fr;
   std::string err;
+  NodeArena arena;
   auto t0 = Clock::now();
   auto exit_ = e->excluded.find("audit");
   const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
-  if (!flatten_page(e->st, e->ns_cache, ex, pg, threads > 0 ? threads : default_threads(), fr, err))
+  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, pg, threads > 0 ? threads : default_threads(), e->perm_nodes, arena,
+                    fr, err))
     return fail(e, GK_EINVAL, err);
   double tot = ms_since(t0);
+  std::vector<Node> all(e->st.nodes().begin(), e->st.nodes().begin() + e->perm_nodes);
+  all.insert(all.end(), arena.begin(), arena.end());
+  std::lock_guard<std::mutex> sg(e->smu);
   uint64_t h = 0;
   for (size_t i = 0; i < fr.cols.size(); ++i) {
     const ReviewCol& c = fr.cols[i];
@@ -2263,13 +2596,13 @@ extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint6
       std::string_view v = e->st.str(sid);
       return fnv1a(v.data(), v.size());
     };
-    uint64_t x = doc_hash(e->st, c.root) * 31 + sh(c.group);
+    uint64_t x = doc_hash(e->st, all.data(), c.root) * 31 + sh(c.group);
     x = x * 31 + sh(c.kind);
     x = x * 31 + sh(c.ns);
     x = x * 31 + sh(c.nsname);
-    x = x * 31 + doc_hash(e->st, c.labels);
-    x = x * 31 + doc_hash(e->st, c.old_labels);
-    x = x * 31 + doc_hash(e->st, c.ns_labels);
+    x = x * 31 + doc_hash(e->st, all.data(), c.labels);
+    x = x * 31 + doc_hash(e->st, all.data(), c.old_labels);
+    x = x * 31 + doc_hash(e->st, all.data(), c.ns_labels);
     x = x * 31 + c.flags;
     const ResourceIds& r = fr.resources[i];
     x = x * 31 + sh(r.api_version);
@@ -2281,14 +2614,15 @@ extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint6
   if (hash) *hash = h;
   if (nodes) *nodes = fr.node_count;
   if (ms2) { ms2[0] = fr.ms_parse; ms2[1] = tot; }
-  reset_transient(e);
   return GK_OK;
 }
 
 extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   if (!e || !kind || !out) return GK_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  rebuild_modules(e);
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);
+  if (rc != GK_OK) return rc;
+  std::lock_guard<std::mutex> dg(e->dbg_mu);
   auto it = e->templates.find(kind);
   if (it == e->templates.end() || it->second.prog < 0) return GK_ENOTFOUND;
   const Program& p = e->progs[it->second.prog];

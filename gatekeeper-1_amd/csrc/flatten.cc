@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <thread>
+#include <mutex>
 #include <unordered_map>
 
 namespace gk {
@@ -322,87 +323,73 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
 
 }  // namespace
 
-bool flatten_page(Store& gst, const NsCache& ns_cache, const std::set<std::string>* excluded, const Page& pg,
-                  int threads, FlatResult& out, std::string& err) {
+// Phases 2 and 3 of every flattening: the parts' strings and numbers are
+// interned into the engine store (under `smu`: concurrent evaluations intern
+// into the one table), then each part's nodes are copied into `dst` -- node id
+// base + k lives at dst[k] -- with string / number ids and child indices
+// rewritten, and its columns relocated.
+static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, uint32_t base, NodeArena& dst,
+                        FlatResult& out, size_t n, std::string& err) {
   using Clock = std::chrono::steady_clock;
-  auto t0 = Clock::now();
-  const size_t n = pg.n;
-  int T = std::max(1, threads);
-  // at least ~2k objects per thread: below that the merge costs more than it saves
-  T = (int)std::min<size_t>((size_t)T, std::max<size_t>(1, n / 2048));
-  std::vector<Part> parts(T);
-  for (int t = 0; t < T; ++t) {
-    parts[t].lo = n * t / T;
-    parts[t].hi = n * (t + 1) / T;
-  }
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { run_part(parts[t], gst, ns_cache, excluded, pg); });
-    run_part(parts[0], gst, ns_cache, excluded, pg);
-    for (auto& x : th) x.join();
-  }
-  for (auto& p : parts)
-    if (!p.err.empty()) { err = p.err; return false; }
   auto t1 = Clock::now();
-  // phase 2: intern every part's strings and numbers into the engine store
+  const int T = (int)parts.size();
   const uint32_t nwell = Store().nstrings();  // well-known ids shared by every Store
   size_t extra = 0;
   for (auto& p : parts) extra += p.st.nstrings() - nwell;
   {
+    std::lock_guard<std::mutex> g(smu);
     std::vector<const Store*> src;
     for (auto& p : parts) src.push_back(&p.st);
     std::vector<std::vector<uint32_t>> maps;
     gst.intern_parts(src, nwell, maps, T);
     for (size_t k = 0; k < parts.size(); ++k) parts[k].smap.swap(maps[k]);
-  }
-  for (auto& p : parts) {
-    const Store& ls = p.st;
-    const auto& nums = ls.numbers();
-    p.nmap.resize(nums.size());
-    for (uint32_t k = 0; k < nums.size(); ++k) {
-      std::string_view v = ls.str(nums[k].text);
-      p.nmap[k] = gst.number(v.data(), v.size());
+    for (auto& p : parts) {
+      const Store& ls = p.st;
+      const auto& nums = ls.numbers();
+      p.nmap.resize(nums.size());
+      for (uint32_t k = 0; k < nums.size(); ++k) {
+        std::string_view v = ls.str(nums[k].text);
+        p.nmap[k] = gst.number(v.data(), v.size());
+      }
     }
   }
   auto t15 = Clock::now();
   if (getenv("GKGPU_FLATTEN_TRACE"))
-    fprintf(stderr, "flatten: parse %.1f ms, intern %.1f ms (%zu strings)\n",
-            std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t15 - t1).count(), extra);
-  // phase 3: relocate nodes and columns into the engine arena
-  uint64_t base = gst.nodes().size(), total = 0;
+    fprintf(stderr, "flatten: intern %.1f ms (%zu strings)\n", std::chrono::duration<double, std::milli>(t15 - t1).count(),
+            extra);
+  uint64_t total = 0;
   for (auto& p : parts) {
-    p.node_off = base + total;
+    p.node_off = total;  // position in dst
     total += p.st.nodes().size() - kFixedNodes;
   }
-  if (base + total >= NO_ID) { err = "node arena exceeds 2^32 nodes"; return false; }
-  auto tr0 = Clock::now();
-  gst.nodes().resize(base + total);
-  if (getenv("GKGPU_FLATTEN_TRACE"))
-    fprintf(stderr, "flatten: arena resize %.1f ms\n", std::chrono::duration<double, std::milli>(Clock::now() - tr0).count());
+  if ((uint64_t)base + total >= NO_ID) { err = "node arena exceeds 2^32 nodes"; return false; }
+  dst.resize(total);
   out.cols.resize(n);
   out.weight.resize(n);
   out.resources.resize(n);
   {
-    Node* dst = gst.nodes().data();
+    Node* dn = dst.data();
     auto relocate = [&](Part& p) {
       const auto& ln = p.st.nodes();
-      const uint32_t off = (uint32_t)p.node_off - kFixedNodes;
-      auto node = [&](uint32_t x) { return x == NO_ID ? NO_ID : x + off; };
+      // local node k >= kFixedNodes -> global base + node_off + k - kFixedNodes;
+      // the fixed nodes ({} null false true) are global 0..3 in every store
+      const uint32_t goff = base + (uint32_t)p.node_off - kFixedNodes;
+      Node* d = dn + p.node_off - kFixedNodes;  // d[k] = dst slot of local node k
+      auto node = [&](uint32_t x) { return x == NO_ID ? NO_ID : (x < kFixedNodes ? x : x + goff); };
       auto str = [&](uint32_t s) { return s == NO_ID ? NO_ID : p.smap[s]; };
       for (size_t k = kFixedNodes; k < ln.size(); ++k) {
         Node x = ln[k];
         if (x.type == NT_STR) x.val = p.smap[x.val];
         else if (x.type == NT_NUM) x.val = p.nmap[x.val];
-        else if ((x.type == NT_ARR || x.type == NT_OBJ) && x.n) x.first += off;
-        dst[k + off] = x;
+        else if ((x.type == NT_ARR || x.type == NT_OBJ) && x.n) x.first += goff;
+        d[k] = x;
       }
       // object member keys: rewrite in the copied arena (a child is copied
       // before or after its parent; keys are only meaningful under objects)
       for (size_t k = kFixedNodes; k < ln.size(); ++k) {
         const Node& x = ln[k];
         if (x.type != NT_OBJ) continue;
-        for (uint32_t c = 0; c < x.n; ++c) dst[x.first + off + c].key = p.smap[ln[x.first + c].key];
+        for (uint32_t c = 0; c < x.n; ++c) d[x.first + c].key = p.smap[ln[x.first + c].key];
       }
       for (size_t i = 0; i < p.cols.size(); ++i) {
         ReviewCol rc = p.cols[i];
@@ -430,9 +417,59 @@ bool flatten_page(Store& gst, const NsCache& ns_cache, const std::set<std::strin
   out.excluded = 0;
   for (auto& p : parts) out.excluded += p.excluded;
   out.node_count = total;
-  auto t2 = Clock::now();
-  out.ms_parse = std::chrono::duration<double, std::milli>(t1 - t0).count();
-  out.ms_merge = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  out.ms_merge = std::chrono::duration<double, std::milli>(Clock::now() - t1).count();
+  return true;
+}
+
+bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded,
+                  const Page& pg, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err) {
+  using Clock = std::chrono::steady_clock;
+  auto t0 = Clock::now();
+  const size_t n = pg.n;
+  int T = std::max(1, threads);
+  // at least ~2k objects per thread: below that the merge costs more than it saves
+  T = (int)std::min<size_t>((size_t)T, std::max<size_t>(1, n / 2048));
+  std::vector<Part> parts(T);
+  for (int t = 0; t < T; ++t) {
+    parts[t].lo = n * t / T;
+    parts[t].hi = n * (t + 1) / T;
+  }
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { run_part(parts[t], gst, ns_cache, excluded, pg); });
+    run_part(parts[0], gst, ns_cache, excluded, pg);
+    for (auto& x : th) x.join();
+  }
+  for (auto& p : parts)
+    if (!p.err.empty()) { err = p.err; return false; }
+  out.ms_parse = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+  if (getenv("GKGPU_FLATTEN_TRACE")) fprintf(stderr, "flatten: parse %.1f ms\n", out.ms_parse);
+  return merge_parts(gst, smu, parts, base, dst, out, n, err);
+}
+
+bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,
+                     const std::vector<std::pair<const char*, size_t>>& inputs, uint32_t base, NodeArena& dst,
+                     std::vector<ReviewCol>& cols, std::string& err) {
+  std::vector<Part> parts(1);
+  Part& p = parts[0];
+  p.lo = 0;
+  p.hi = inputs.size();
+  JDoc d;
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    JsonReader rd(inputs[i].first, inputs[i].second, &d);
+    int root = rd.parse();
+    if (root < 0) { err = "invalid input JSON: " + d.err; return false; }
+    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
+    uint32_t rn = rv >= 0 ? p.st.add_doc(d, rv) : NO_ID;
+    bool glob = false;
+    p.cols.push_back(review_columns(p.st, gst, ns_cache, rn, &glob));
+    p.nsglob.push_back(glob);
+    p.weight.push_back(0);
+    p.res.push_back(ResourceIds{p.st.s_empty, p.st.s_empty, p.st.s_empty, p.st.s_empty});
+  }
+  FlatResult out;
+  if (!merge_parts(gst, smu, parts, base, dst, out, inputs.size(), err)) return false;
+  cols.swap(out.cols);
   return true;
 }
 
@@ -442,7 +479,7 @@ namespace gk {
 
 // Content hash of a document (type, keys, string / number text, structure),
 // independent of node and string ids: compares flattenings across thread counts.
-uint64_t doc_hash(const Store& st, uint32_t node) {
+uint64_t doc_hash(const Store& st, const Node* nodes, uint32_t node) {
   if (node == NO_ID) return 0x9e3779b97f4a7c15ull;
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t x) { h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2); };
@@ -451,7 +488,7 @@ uint64_t doc_hash(const Store& st, uint32_t node) {
   while (!stack.empty()) {
     auto [k, obj_child] = stack.back();
     stack.pop_back();
-    const Node& x = st.nodes()[k];
+    const Node& x = nodes[k];
     mix(x.type);
     if (obj_child) mixs(x.key);
     if (x.type == NT_STR) mixs(x.val);

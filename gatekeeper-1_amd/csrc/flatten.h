@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <vector>
@@ -85,17 +86,26 @@ struct FlatResult {
   double ms_parse = 0, ms_merge = 0;
 };
 
-// Flattens a page into `st` (appending documents to its node arena) on
-// `threads` host threads.  Objects whose metadata.namespace is in
-// `excluded_ns` (Excluder.IsNamespaceExcluded(Audit, ns), manager.go:362-365)
-// get a column flagged RC_EXCLUDED and no document.  Returns false with `err`
-// on malformed JSON.
-bool flatten_page(Store& st, const NsCache& ns_cache, const std::set<std::string>* excluded_ns, const Page& page,
-                  int threads, FlatResult& out, std::string& err);
+// Flattens a page on `threads` host threads.  The review documents go to `dst`
+// (node id base + k at dst[k]; ids below base are the engine store's
+// permanent nodes); their strings and numbers are interned into `st` under
+// `smu`.  Objects whose metadata.namespace is in `excluded_ns`
+// (Excluder.IsNamespaceExcluded(Audit, ns), manager.go:362-365) get a column
+// flagged RC_EXCLUDED and no document.  Returns false with `err` on malformed
+// JSON.
+bool flatten_page(Store& st, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded_ns,
+                  const Page& page, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err);
+
+// Query inputs ({"review": ...} documents, Driver.Query's input) into `dst`
+// likewise, with their match columns.
+bool flatten_reviews(Store& st, std::mutex& smu, const NsCache& ns_cache,
+                     const std::vector<std::pair<const char*, size_t>>& inputs, uint32_t base, NodeArena& dst,
+                     std::vector<ReviewCol>& cols, std::string& err);
 
 int default_threads();
 
-// id-independent content hash of the document rooted at `node`
-uint64_t doc_hash(const Store& st, uint32_t node);
+// id-independent content hash of the document rooted at `node` (`nodes`: the
+// node array its ids index; strings and numbers of `st`)
+uint64_t doc_hash(const Store& st, const Node* nodes, uint32_t node);
 
 }  // namespace gk

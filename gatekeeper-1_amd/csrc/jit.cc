@@ -680,7 +680,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
     << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params) {\n"
     << g.body << "}\n"
     << "}  // namespace gk\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p) << ") " << name << "() {\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p) << ") " << name << "(gk::DevArgs) {\n"
     << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"
     << "    gk::" << name << "_pred(L, review, params);\n"
     << "  });\n"

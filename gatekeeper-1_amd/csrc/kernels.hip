@@ -85,19 +85,11 @@ __device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t par
   lane_fallback(L, FB_UNSUPPORTED);
 }
 
-__global__ void __launch_bounds__(256) audit_kernel() {
+__global__ void __launch_bounds__(256) audit_kernel(DevArgs) {
   audit_body([&](PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
     run_program(L, gk_args.prog_off[prog], review, params);
   });
 }
-
-// Format pass: one lane per output tuple whose message the audit kernels
-// deferred (devrt.h op_emit / flush_wave).  The arguments are heap-free values
-// (interned strings, slices, numbers, document nodes), so formatting reads only
-// the shared tables: the lane reference below is never dereferenced for them
-// (sview / coll_at touch a lane's buffers only for lane-heap values).  Lanes
-// write disjoint byte ranges [msg_off, msg_off + msg_len) reserved by the audit
-// kernel, consecutive tuples to consecutive ranges.
 
 // LDS-staged writer for one wavefront's message bytes
 struct LOut {
@@ -132,71 +124,202 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
+// Size + format passes over the tuples the predicate kernels wrote (devrt.h
+// emission): every tuple's output bytes are its message followed by its
+// details JSON, laid out in tuple order, so a tuple's byte offset is the
+// exclusive prefix sum of the byte counts before it.
+//   gk_size_kernel  — per tuple, its byte count (a deferred message is printed
+//                     on a counter from its argument words); per tile of FTILE
+//                     tuples, the tile's sum.  A deferred message that cannot be
+//                     printed (a verb / argument the GPU printer does not
+//                     reproduce) flags its review for the CPU fallback, as at
+//                     emission time.
+//   gk_scan_spine   — one block: exclusive prefix over the tile sums; the total
+//                     (bytes of the whole output) in counters[3].
+//   gk_format_kernel — per tile, a block-level prefix over its tuples gives each
+//                     tuple's offset; a wavefront's 64 consecutive tuples fill one
+//                     dense byte range, built in LDS and written back with
+//                     coalesced dword stores (byte stores for the two edge dwords,
+//                     which neighbouring wavefronts share).  The tuple is rewritten
+//                     with its final (msg_off, msg_len, det_len).
+// The tuple count is read on the device (counters[0]): the passes follow the
+// predicate kernels on the stream with no host round trip.
+
+__device__ __forceinline__ uint64_t ntuples() {
+  const uint64_t n = gk_args.counters[0];
+  return n < gk_args.out_cap ? n : gk_args.out_cap;
+}
+
+// a deferred tuple's printed message length; false = not printable here
+__device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint64_t i, uint32_t& len) {
+  const uint32_t fidx = v.msg_len & 0xffffffu, na = v.msg_len >> 24;
+  uint64_t a[FMT_MAXARGS];
+#pragma unroll
+  for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
+  if (size_plain(fidx, a, len)) return true;
+  Cnt cn{0, false};
+  if (!fmt_run(L, cn, fidx, [&](uint32_t j) { return a[j]; })) return false;
+  len = cn.n;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t det_bytes(const Viol& v) { return (v.pad & VF_DET_OBJ) ? 2u : v.det_len; }
+
+__global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
+  __shared__ unsigned long long wsum[4];
+  Lane L0;  // never dereferenced: deferred arguments are heap-free values
+  PLane& L = *(PLane*)&L0;
+  const uint64_t n = ntuples();
+  const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    unsigned long long s = 0;
+    for (uint32_t k = 0; k < FTILE; k += 256) {
+      const uint64_t i = t * FTILE + k + threadIdx.x;
+      if (i >= n) break;
+      const Viol v = gk_args.out[i];
+      uint32_t ml = v.msg_len;
+      if (v.pad & VF_DEFER) {
+        if (!size_deferred_msg(L, v, i, ml)) {
+          // the emission-time outcome: this review goes to CPU OPA
+          atomicOr(&gk_args.rflags[v.review], (uint32_t)RF_FALLBACK);
+          if (gk_args.rreason) atomicMax(&gk_args.rreason[v.review], (uint32_t)FB_PRINT);
+          atomicAdd(&gk_args.counters[2], 1ull);
+          ml = 0;
+        }
+      }
+      const uint32_t len = ml + det_bytes(v);
+      gk_args.lens[i] = len;
+      s += len;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) gk_args.part[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
+  __shared__ unsigned long long wtot[16];
+  const uint64_t n = ntuples();
+  const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long carry = 0;
+  for (uint64_t b = 0; b < ntile; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const unsigned long long x = i < ntile ? gk_args.part[i] : 0ull;
+    unsigned long long incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    unsigned long long before = 0, all = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < w) before += wtot[k];
+      all += wtot[k];
+    }
+    if (i < ntile) gk_args.part[i] = carry + before + incl - x;
+    carry += all;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gk_args.counters[3] = carry;
+}
+
 constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
 
-// A wavefront takes 64 consecutive tuples.  When their output bytes (messages
-// and details) form one dense range that fits in LDS — the usual case, since a
-// wave's tuples come from one audit-kernel reservation — the range is read
-// into LDS, the live lanes format their messages into it, and it is written
-// back with coalesced dword stores (byte stores for the two edge dwords, which
-// may hold a neighbouring wave's bytes).  Otherwise each lane formats straight
-// into HBM.
-__global__ void __launch_bounds__(256) gk_format_kernel() {
+__global__ void __launch_bounds__(256) gk_format_kernel(DevArgs) {
   __shared__ uint32_t stage[4][FSTAGE / 4];
-  const uint64_t n = gk_args.counters[0];
-  // an overflowed call left some reservations unwritten; the host retries it
-  if (n > gk_args.out_cap || gk_args.counters[1] > gk_args.bytes_cap) return;
-  Lane L0;  // never dereferenced: the arguments are heap-free values
+  __shared__ uint32_t wtot[4];
+  const uint64_t n = ntuples();
+  // an overflowed output buffer: the host grows it and runs the passes again
+  // (the tuples stay as the predicate kernels wrote them)
+  if (gk_args.counters[3] > gk_args.bytes_cap || gk_args.counters[0] > gk_args.out_cap ||
+      gk_args.counters[1] > gk_args.ebytes_cap)
+    return;
+  Lane L0;  // never dereferenced: deferred arguments are heap-free values
   PLane& L = *(PLane*)&L0;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* st = stage[wv];
   uint8_t* stb = (uint8_t*)st;
   uint32_t* gw = (uint32_t*)gk_args.bytes;
-  for (uint64_t base = ((uint64_t)blockIdx.x * 4 + wv) * 64; base < n; base += (uint64_t)gridDim.x * 256) {  // wave-uniform
-    uint64_t i = base + lane;
-    bool valid = i < n;
-    const uint64_t* w = gk_args.frec + i * FREC_WORDS;
-    uint64_t h = valid ? w[0] : 0;
-    Viol v{};
-    if (valid) v = gk_args.out[i];
-    uint64_t end = v.msg_off + v.msg_len + v.det_len;
-    bool live = valid && (h & FREC_LIVE) && v.msg_off + v.msg_len <= gk_args.bytes_cap;
-    if (!__any(live)) continue;
-    uint64_t lo = wave_min64(valid ? v.msg_off : ~0ull);
-    uint64_t hi = wave_max64(valid ? end : 0ull);
-    uint32_t tot = wave_sum(valid ? v.msg_len + v.det_len : 0u);
-    uint64_t lo4 = lo & ~(uint64_t)3, hi4 = (hi + 3) & ~(uint64_t)3;
-    if (tot == hi - lo && hi4 - lo4 <= FSTAGE && hi4 <= gk_args.bytes_cap) {
-      uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
-      // the range's bytes are read first unless this pass writes all of them:
-      // every tuple live with no details bytes from the audit kernel
-      // (FREC_DET_OBJ or none); the edge dwords are written bytewise anyway
-      const bool whole = __all(!valid || (live && ((h & FREC_DET_OBJ) || v.det_len == 0)));
-      if (!whole)
-        for (uint32_t k = lane; k < nw; k += 64) st[k] = gw[(lo4 >> 2) + k];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      if (live) {
-        LOut o{stb + (v.msg_off - lo4), 0};
-        fmt_run(L, o, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
-        if (h & FREC_DET_OBJ) { o.put('{'); o.put('}'); }
+  const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {  // block-uniform
+    uint64_t run = gk_args.part[t];
+    for (uint32_t k = 0; k < FTILE; k += 256) {
+      const uint64_t tb = t * FTILE + k;
+      if (tb >= n) break;  // block-uniform
+      const uint64_t i = tb + threadIdx.x;
+      const bool valid = i < n;
+      const uint32_t len = valid ? gk_args.lens[i] : 0u;
+      // block-level exclusive prefix of len
+      uint32_t incl = len;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t k = lane; k < nw; k += 64) {
-        uint64_t a = lo4 + 4 * (uint64_t)k;
-        if (a >= lo && a + 4 <= hi) {
-          gw[(lo4 >> 2) + k] = st[k];
-        } else {
-          for (uint32_t b = 0; b < 4; ++b)
-            if (a + b >= lo && a + b < hi) gk_args.bytes[a + b] = (char)stb[4 * k + b];
+      if (lane == 63) wtot[wv] = incl;
+      __syncthreads();
+      uint64_t wbase = run;
+      for (uint32_t q = 0; q < wv; ++q) wbase += wtot[q];
+      const uint64_t all = (uint64_t)wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      __syncthreads();
+      run += all;
+      const uint64_t dst = wbase + incl - len;
+      Viol v{};
+      if (valid) v = gk_args.out[i];
+      const bool defer = valid && (v.pad & VF_DEFER);
+      const uint32_t dl = valid ? det_bytes(v) : 0u;
+      const uint32_t ml = len - dl;
+      uint64_t a[FMT_MAXARGS];
+      const uint32_t na = defer ? (v.msg_len >> 24) : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
+      // the wave's range [lo, hi): consecutive tuples, consecutive bytes
+      const uint64_t lo = __shfl(dst, 0, 64);
+      const uint64_t hi = __shfl(dst + len, 63, 64);
+      const uint64_t lo4 = lo & ~(uint64_t)3, hi4 = (hi + 3) & ~(uint64_t)3;
+      auto body = [&](auto& o) {
+        if (defer) fmt_run(L, o, v.msg_len & 0xffffffu, [&](uint32_t j) { return a[j]; });
+        else puts_(o, gk_args.ebytes + v.msg_off, ml);
+        if (v.pad & VF_DET_OBJ) { o.put('{'); o.put('}'); }
+        else puts_(o, gk_args.ebytes + v.msg_off + (defer ? 0u : ml), dl);
+      };
+      if (hi > lo && hi4 - lo4 <= FSTAGE) {
+        const uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
+        if (valid && len) {
+          LOut o{stb + (dst - lo4), 0};
+          body(o);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t q = lane; q < nw; q += 64) {
+          const uint64_t ad = lo4 + 4 * (uint64_t)q;
+          if (ad >= lo && ad + 4 <= hi) {
+            gw[(lo4 >> 2) + q] = st[q];
+          } else {
+            for (uint32_t b = 0; b < 4; ++b)
+              if (ad + b >= lo && ad + b < hi) gk_args.bytes[ad + b] = (char)stb[4 * q + b];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (valid && len) {
+        GOut g{(uint8_t*)gk_args.bytes, dst, dst, 0, false};
+        body(g);
+        g.finish();
       }
-    } else if (live) {
-      GOut g{(uint8_t*)gk_args.bytes, v.msg_off, v.msg_off, 0, false};
-      fmt_run(L, g, (uint32_t)h & 0xffffffu, [&](uint32_t j) { return w[1 + j]; });
-      if (h & FREC_DET_OBJ) { g.put('{'); g.put('}'); }
-      g.finish();
+      if (valid) {
+        v.msg_off = dst;
+        v.msg_len = ml;
+        v.det_len = dl;
+        v.pad = 0;
+        gk_args.out[i] = v;
+      }
     }
   }
 }
@@ -204,11 +327,18 @@ __global__ void __launch_bounds__(256) gk_format_kernel() {
 }  // namespace gk
 
 // ------------------------------------------------------------------ host launch
-extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream) {
-  if (!a->frec) return 0;
-  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gk_args), a, sizeof(*a), 0, hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(2048), dim3(256), 0, stream);
+// the size, spine and format passes after the predicate kernels of a call
+// (grids sized for the output capacity; the passes read the tuple count on the
+// device).  ev (optional, 3 events): recorded after size, spine and format.
+extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev) {
+  const uint64_t tiles = (a->out_cap + gk::FTILE - 1) / gk::FTILE;
+  const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
+  hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
+  if (ev) hipEventRecord(ev[0], stream);
+  hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
+  if (ev) hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 0, stream, *a);
+  if (ev) hipEventRecord(ev[2], stream);
   return (int)hipGetLastError();
 }
 
@@ -217,9 +347,7 @@ extern "C" int gk_launch_audit(const gk::DevArgs* a, hipStream_t stream) {
   uint64_t threads = waves * 64;
   uint32_t blocks = (uint32_t)((threads + 255) / 256);
   if (blocks == 0) return 0;
-  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(gk_args), a, sizeof(*a), 0, hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gk::audit_kernel, dim3(blocks), dim3(256), 0, stream);
+  hipLaunchKernelGGL(gk::audit_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 

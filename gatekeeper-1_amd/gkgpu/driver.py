@@ -31,7 +31,7 @@ EXPORTS = [
     "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
-    "gk_results_export", "gk_results_samples_export",
+    "gk_results_export", "gk_results_samples_export", "gk_results_generation",
 ]
 
 
@@ -138,6 +138,8 @@ def load_library():
     lib.gk_results_constraint_total.argtypes = [vp, sz]
     lib.gk_results_constraint_total.restype = C.c_uint64
     lib.gk_results_timing.argtypes = [vp, C.POINTER(C.c_double)]
+    lib.gk_results_generation.argtypes = [vp]
+    lib.gk_results_generation.restype = C.c_uint64
     lib.gk_results_free.argtypes = [vp]
     pu64 = C.POINTER(C.c_uint64)
     lib.gk_batch_stats.argtypes = [vp, pu64, pu64, pu64, pu64]
@@ -221,6 +223,7 @@ class Results:
     n_fallbacks: int = 0
     vm_profile: List[int] = field(default_factory=list)  # GKGPU_PROFILE=1 diagnostics
     launches: List["Launch"] = field(default_factory=list)  # per kernel launch, in order
+    generation: int = 0        # engine state evaluated (gk_results_generation)
 
     def vm_stats(self):
         """per constraint: (sum VM steps, max lane steps, lanes run, sum of per-wave max steps)"""
@@ -329,7 +332,7 @@ def _collect_light(lib, h, with_status: bool = False) -> Results:
         ne, nf = C.c_uint64(), C.c_uint64()
         lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
         return Results([], status, [], totals, list(t), dt.value, db.value, ne.value, nf.value, _vm_profile(lib, h),
-                       _launches(lib, h))
+                       _launches(lib, h), lib.gk_results_generation(h))
     finally:
         lib.gk_results_free(h)
 
@@ -359,7 +362,7 @@ def _collect(lib, h, decode=True) -> Results:
         lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
         return Results(out, status, reason, totals, list(t), dt.value, db.value,
                        sum(1 for x in status if x & 1), sum(1 for x in status if x & 2), _vm_profile(lib, h),
-                       _launches(lib, h))
+                       _launches(lib, h), lib.gk_results_generation(h))
     finally:
         lib.gk_results_free(h)
 
@@ -646,6 +649,13 @@ class Driver:
         return Batch(self, out, len(o))
 
     # -- introspection
+    def debug_store_sizes(self):
+        """(nodes of the permanent region, interned strings) as the next evaluation sees them"""
+        n, st = C.c_uint64(), C.c_uint64()
+        self._lib.gk_debug_store_sizes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        self._check(self._lib.gk_debug_store_sizes(self._e, C.byref(n), C.byref(st)))
+        return n.value, st.value
+
     def debug_clock_mhz(self) -> float:
         """the shader clock (MHz) a spinning wavefront measures on this device
         (s_memtime over the 100 MHz s_memrealtime reference)"""

@@ -15,8 +15,18 @@
  * micro-batch use.  Ownership: every input buffer is borrowed for the
  * duration of the call only (the engine copies/flattens it); results are
  * engine-allocated and released with gk_results_free.  Every function
- * returns 0 on success or a GK_E* code; gk_last_error() holds the message.
- * Calls on one engine are serialized internally (mutations vs evaluation).
+ * returns 0 on success or a GK_E* code; gk_last_error() holds the message of
+ * the calling thread's last failure.
+ *
+ * Threading follows the local driver's RWMutex (drivers/local/local.go:62-68,
+ * 117, 303-304): evaluations (gk_query, gk_query_batch, gk_review_*,
+ * gk_batch_stage_*, gk_batch_eval*) run concurrently -- each on its own
+ * evaluation context (HIP stream, output buffers, per-launch kernel
+ * arguments) -- while mutations (gk_put_* / gk_delete_*, excluder changes)
+ * are exclusive: a mutation waits for the evaluations in flight and new
+ * evaluations wait for it, so every evaluation sees one engine state from
+ * start to end (gk_results_generation names it).  A staged batch belongs to
+ * the state it was staged in.
  */
 #ifndef GKGPU_H
 #define GKGPU_H
@@ -206,6 +216,10 @@ uint64_t gk_results_excluded(const gk_results* r);
 /* per-constraint violation totals (device-side counters), length = constraints */
 size_t gk_results_constraints(const gk_results* r);
 uint64_t gk_results_constraint_total(const gk_results* r, size_t constraint);
+/* the engine state the results were evaluated in: bumps on every mutation
+ * (module / data / excluder change), so concurrent callers can tell which
+ * state of the constraints and templates each evaluation saw */
+uint64_t gk_results_generation(const gk_results* r);
 /* timings of the call in milliseconds: [flatten, upload, kernel, download, decode] */
 int gk_results_timing(const gk_results* r, double* ms5);
 /* violation tuples (32 B each) and message/details bytes the kernel wrote */
@@ -213,11 +227,14 @@ int gk_results_device_counts(const gk_results* r, uint64_t* tuples, uint64_t* by
 /* The device-resident output of the call: dev_tuples gk_viol records and
  * dev_bytes message/details bytes (unordered: one reservation per wavefront).
  * Copied device-to-device into caller buffers on the engine's device (e.g.
- * tensors handed to an RCCL gather).  Valid until the engine's next
- * evaluation; GK_EINVAL after that. */
+ * tensors handed to an RCCL gather).  Valid until the evaluation context that
+ * produced the results runs another evaluation (for a single caller: the
+ * engine's next evaluation) or the engine state changes; GK_EINVAL after that. */
 typedef struct {
   uint32_t review, constraint;
-  uint16_t seq, rule;    /* emission order within (review, constraint); rule 0xffff = autoreject */
+  uint16_t seq, rule;    /* emission order key within (review, constraint): rows sort by it into the
+                            reference's evaluation order (consecutive for templates without fused
+                            rule bodies); rule 0xffff = autoreject */
   uint32_t msg_len;
   uint64_t msg_off;      /* message at [msg_off, +msg_len), details JSON right after it */
   uint32_t det_len, pad;

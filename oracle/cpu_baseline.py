@@ -61,9 +61,11 @@ def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int
     driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
     glib.gk_debug_store_sizes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     nn, ns = C.c_uint64(), C.c_uint64()
-    glib.gk_debug_store_sizes(driver._e, C.byref(nn), C.byref(ns))
+    driver._check(glib.gk_debug_store_sizes(driver._e, C.byref(nn), C.byref(ns)))
+    # node ids index the permanent region followed by the batch's documents
+    n_nodes = nn.value + batch.stats()[1]
     out = (C.c_uint64 * 5)()
     hi = batch.n if hi is None else hi
-    lib.gkcpu_referenced(buf, nn.value, ns.value, lo, hi, only, threads, out,
+    lib.gkcpu_referenced(buf, n_nodes, ns.value, lo, hi, only, threads, out,
                          C.cast(pc_hist, C.c_void_p) if pc_hist is not None else None)
     return {"nodes": out[0], "strings": out[1], "string_bytes": out[2], "violations": out[3], "flagged": out[4]}

@@ -35,15 +35,19 @@ using ::uint64_t;
 using ::uint8_t;
 }  // namespace __hip_internal
 #define __HIPCC_RTC__ 1
+#define GK_HOST 1
 #define GK_PRIV
 #define __device__
 #define __global__
 #define __host__
-#define __constant__
+// each worker thread evaluates with its own copy of the launch arguments,
+// whose output buffers are that thread's (OutBufs below)
+#define __constant__ thread_local
 #define __forceinline__ inline __attribute__((always_inline))
 #define __noinline__ __attribute__((noinline))
-// single-lane stand-ins: the wave-level paths (flush_wave, audit_body) are
-// compiled but never called here
+// single-lane stand-ins: the emission path's wave-level reservations see a
+// wave of one lane (devrt.h GK_HOST); audit_body / finish_lane are compiled
+// but never called here
 template <class T> static inline T __shfl_up(T v, int, int) { return v; }
 template <class T> static inline T __shfl(T v, int, int) { return v; }
 template <class T> static inline T __shfl_xor(T v, int, int) { return v; }
@@ -66,6 +70,11 @@ thread_local uint64_t* pc_hist = nullptr;  // executions per bytecode instructio
 #define GK_TOUCH_STR(s) (gkcpu_touch::str_bits[(uint32_t)(s) >> 6] |= 1ull << ((uint32_t)(s) & 63))
 #endif
 
+// the launch arguments devrt.h reads (the device reads its kernarg segment)
+#include "../gatekeeper-1_amd/csrc/common.h"
+extern "C" {
+__constant__ gk::DevArgs gk_args;
+}
 #include "../gatekeeper-1_amd/csrc/devrt.h"
 
 namespace gk {
@@ -145,13 +154,43 @@ struct Counts {
   uint64_t evals = 0, violations = 0, msg_bytes = 0, flagged = 0;
 };
 
+// A worker thread's output buffers: its copy of the launch arguments points
+// the emission path (devrt.h op_emit / emit_eager) at them.  One pair emits
+// at most EM_MAXIDX tuples (then it falls back), each staging at most BCAP
+// bytes, so the per-pair capacities never overflow.
+struct OutBufs {
+  std::vector<Viol> out;
+  std::vector<uint64_t> frec;
+  std::vector<char> ebytes;
+  unsigned long long counters[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t rflags[1] = {0};
+  void bind(const void* args) {
+    memcpy(&gk_args, args, sizeof(DevArgs));
+    out.resize(EM_MAXIDX + 1);
+    frec.resize((size_t)(EM_MAXIDX + 1) * FMT_MAXARGS);
+    ebytes.resize((size_t)(EM_MAXIDX + 1) * (BCAP + 64) + 16);
+    gk_args.out = out.data();
+    gk_args.out_cap = out.size();
+    gk_args.frec = frec.data();
+    gk_args.ebytes = ebytes.data();
+    gk_args.ebytes_cap = ebytes.size() - 16;
+    gk_args.counters = counters;
+    gk_args.rflags = rflags;
+    gk_args.rreason = nullptr;
+    gk_args.totals = nullptr;
+  }
+};
+
 // devrt.h audit_body for one (review position, constraint), then the message
-// bytes of every staged violation (the format pass's work)
+// bytes of every tuple it emitted (the size + format passes' work)
 static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t fcap) {
   Lane L;
   L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
-  L.nsz = 0;
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+  L.rv = 0;  // the thread's one-slot flag word
+  L.cn = c;
+  gk_args.counters[0] = 0;
+  gk_args.counters[1] = 0;
   const ReviewCol rc = gk_args.revs[rp];
   const MatchSpec m = gk_args.cons[c];
   ++k.evals;
@@ -160,7 +199,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
   } else {
     if ((m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) &&
         !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS))
-      stage_tuple(L, RULE_AUTOREJECT, "Namespace is not cached in OPA.", 31, "{}", 2, 0);
+      emit_eager(L, true, RULE_AUTOREJECT, "Namespace is not cached in OPA.", 31, nullptr, 2);
     int mr = match_constraint(m, rc);
     if (mr == -1) L.fail = RF_ERROR;
     else if (mr == -2) L.fail = RF_FALLBACK;
@@ -168,20 +207,22 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
     else if (mr == 1 && m.prog != NO_ID) {
       uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
       run_program(L, gk_args.prog_off[m.prog], mkv(V_NODE, rc.root), params);
-      if (L.nsz) size_deferred(L);
     }
   }
   if (L.fail) { ++k.flagged; return; }
-  for (uint32_t i = 0; i < L.en; ++i) {
-    uint32_t ml = L.em_mlen[i], dw = L.em_dlen[i], o = L.em_off[i];
-    if (dw & 0x8000u) {
-      const uint64_t* rec = (const uint64_t*)(L.B + o);
-      uint32_t h = (uint32_t)rec[0];
+  const uint64_t n = gk_args.counters[0];
+  for (uint64_t i = 0; i < n; ++i) {
+    const Viol& v = gk_args.out[i];
+    if (v.pad & VF_DEFER) {
+      const uint32_t fidx = v.msg_len & 0xffffffu, na = v.msg_len >> 24;
       Out out{fbuf, 0, fcap, false};
-      fmt_run(L, out, h & 0xffffffu, [&](uint32_t j) { return rec[1 + j]; });
+      if (!fmt_run(L, out, fidx, [&](uint32_t j) { return j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0ull; })) {
+        ++k.flagged;  // the size pass's outcome: the review goes to the CPU fallback
+        return;
+      }
       k.msg_bytes += out.n;
     } else {
-      k.msg_bytes += ml;
+      k.msg_bytes += v.msg_len;
     }
     ++k.violations;
   }
@@ -203,11 +244,14 @@ double gkcpu_sweep(const void* args, uint32_t lo, uint32_t hi, int threads, uint
   if (hi > gk_args.nrev) hi = gk_args.nrev;
   if (lo > hi) lo = hi;
   const uint32_t ncons = gk_args.ncons;
+  const void* shared_args = args;
   if (threads < 1) threads = 1;
   std::vector<gk::cpu::Counts> per(threads);
   std::atomic<uint32_t> next{lo};
   auto t0 = std::chrono::steady_clock::now();
   auto work = [&](int t) {
+    gk::cpu::OutBufs ob;
+    ob.bind(shared_args);
     std::vector<char> fbuf(1 << 16);
     gk::cpu::Counts& k = per[t];
     for (;;) {
@@ -251,6 +295,8 @@ int gkcpu_referenced(const void* args, uint64_t n_nodes, uint64_t n_strings, uin
   std::vector<gk_touch::cpu::Counts> per(threads);
   std::atomic<uint32_t> next{lo};
   auto work = [&](int t) {
+    gk_touch::cpu::OutBufs ob;
+    ob.bind(args);
     nb[t].assign(nwords, 0);
     sb[t].assign(swords, 0);
     gkcpu_touch::node_bits = nb[t].data();

@@ -12,7 +12,10 @@ R=${1:-r01}
 ROOT=$PWD
 OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
-export GKGPU_JIT_CACHE=$ROOT/.jitcache
+# template-kernel code objects: the tree's .jitcache plus new ones under gpurun_out/
+mkdir -p "$ROOT/gpurun_out/jitcache"
+cp -n "$ROOT"/.jitcache/*.co "$ROOT/gpurun_out/jitcache/" 2>/dev/null || true
+export GKGPU_JIT_CACHE=$ROOT/gpurun_out/jitcache
 cd /tmp && export TMPDIR=/tmp
 # GPU clocks around the run (box-to-box variance: compare only inside one call)
 rocm-smi --showclocks > "$OUT/clocks_before.txt" 2>&1 || true

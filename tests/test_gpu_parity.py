@@ -11,7 +11,7 @@ import pytest
 
 import gkgpu
 from gkgpu import workloads as W
-from gkgpu.client import Client, augmented_review
+from gkgpu.client import Client, augmented_review, constraint_path
 
 from parity import Report, compare, engine_for, oracle_for, oracle_review, run_objects
 
@@ -77,8 +77,9 @@ def test_config2_agilebank_pods():
     assert rep.violations > 5000
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
     kernels = {k for k, _, _ in res.launches}
-    assert "gk_format_kernel" in kernels, res.launches  # deferred messages formatted by the format pass
-    kernels.discard("gk_format_kernel")
+    # deferred messages sized and formatted by the size / format passes (kernels.hip)
+    assert {"gk_size_kernel", "gk_scan_spine", "gk_format_kernel"} <= kernels, res.launches
+    kernels -= {"gk_size_kernel", "gk_scan_spine", "gk_format_kernel"}
     if _BACKEND["jit"]:
         assert kernels and all(k.startswith("gk_t_") for k in kernels), res.launches
     else:
@@ -143,16 +144,24 @@ def test_config2_unique_service_selector_join_on_gpu():
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
 
 
-def test_unique_service_selector_inventory_changes():
-    """The inventory tree follows put/delete of synced objects between sweeps."""
+@pytest.mark.parametrize("compact", [False, True])
+def test_unique_service_selector_inventory_changes(monkeypatch, compact):
+    """The inventory tree follows put/delete of synced objects between sweeps.
+    compact: GKGPU_COMPACT_MIN=0 compacts the permanent node region (constraints,
+    namespaces, template constants and the inventory tree re-placed, templates
+    recompiled) whenever its garbage exceeds its live nodes -- here at every
+    rebuild -- and the results stay the oracle's."""
     from gkgpu.client import data_path
+    if compact:
+        monkeypatch.setenv("GKGPU_COMPACT_MIN", "0")
     ts, cs = W.config2()
     _, svcs, objs, nss = _pods_services_deployments(seed=45, n_pods=50, n_svc=80, n_dep=5)
     drv = Driver()
     engine_for(drv, ts, cs)
     od = oracle_for(ts, cs)
     reviews = [augmented_review(o, n) for o, n in zip(objs, nss)]
-    for step in range(3):
+    sizes = []
+    for step in range(5):
         if step == 1:
             for o in svcs[:40]:
                 drv.put_data(data_path(o), o)
@@ -161,8 +170,17 @@ def test_unique_service_selector_inventory_changes():
             for o in svcs[:20]:
                 drv.delete_data(data_path(o))
                 od.delete_data(data_path(o))
+        if step >= 3:
+            for o in svcs[20 + step:40 + step]:
+                drv.put_data(data_path(o), o)
+                od.put_data(data_path(o), json.dumps(o))
+            for c in cs:  # re-put: the old constraint documents become garbage
+                drv.put_data(constraint_path(c), c)
         rep = compare(od, reviews, drv.review_objects(objs, nss))
         _assert_clean(rep)
+        sizes.append(drv.debug_store_sizes()[0])
+    if compact:
+        assert sizes[-1] <= 2 * sizes[0] + 50000, sizes
 
 
 def test_unique_label_join_on_gpu():
@@ -226,16 +244,19 @@ def test_guard_program_routes_only_matching_reviews_to_cpu():
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts], guard=("K8sGuardedEncode",))
 
 
-def test_config2_in_kernel_formatting(monkeypatch):
-    """GKGPU_FORMAT_PASS=0: messages formatted inside the audit kernels (no format pass)."""
-    monkeypatch.setenv("GKGPU_FORMAT_PASS", "0")
+def test_config2_output_buffers_grow(monkeypatch):
+    """Output capacities far below the call's output (GKGPU_TEST_CAPS: tuples,
+    staged bytes, output bytes of a new evaluation context): the tuple /
+    staged-byte overflow re-runs the evaluation with grown buffers, the output
+    byte overflow re-runs only the size + format passes; results are unchanged."""
+    monkeypatch.setenv("GKGPU_TEST_CAPS", "64,256,1024")
     ts, cs = W.config2()
     pods, ns_of, ns_objs = W.gen_pods(600, seed=43, n_namespaces=50)
     nss = [ns_objs[n] for n in ns_of]
     rep, res = run_objects(Driver(), ts, cs, pods, nss)
     _assert_clean(rep)
     assert rep.violations > 1000
-    assert "gk_format_kernel" not in {k for k, _, _ in res.launches}
+    assert res.device_tuples > 64 and res.device_bytes > 1024
 
 
 def test_config2_agilebank_namespaces_regex():
