@@ -77,6 +77,7 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
   static char* pin[2] = {nullptr, nullptr};
   static hipStream_t st = nullptr;
   static hipEvent_t ev[2] = {nullptr, nullptr};
+  static bool pending[2] = {false, false};  // a copy out of pin[b] may still be in flight
   static int ok = -1;
   std::lock_guard<std::mutex> g(mu);
   if (ok < 0) {
@@ -98,7 +99,12 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
     const size_t len = std::min(chunk, n - off);
     const int b = (int)(k & 1);
     auto tw = std::chrono::steady_clock::now();
-    if (k >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) return false;
+    // the DMA of the chunk that last used this buffer (this call's, or a
+    // failed earlier call's) must have drained it before it is refilled
+    if (pending[b]) {
+      if (hipEventSynchronize(ev[b]) != hipSuccess) { hipStreamSynchronize(st); return false; }
+      pending[b] = false;
+    }
     auto tc = std::chrono::steady_clock::now();
     ms_wait += std::chrono::duration<double, std::milli>(tc - tw).count();
     char* dstp = pin[b];
@@ -112,10 +118,17 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
     part(0);
     for (auto& x : th) x.join();
     ms_copy += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
-    if (hipMemcpyAsync((char*)dst + off, dstp, len, hipMemcpyHostToDevice, st) != hipSuccess) return false;
-    if (hipEventRecord(ev[b], st) != hipSuccess) return false;
+    if (hipMemcpyAsync((char*)dst + off, dstp, len, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(ev[b], st) != hipSuccess) {
+      // earlier chunks may still be reading the pinned buffers: drain them
+      hipStreamSynchronize(st);
+      pending[0] = pending[1] = false;
+      return false;
+    }
+    pending[b] = true;
   }
   const bool ok_sync = hipStreamSynchronize(st) == hipSuccess;
+  if (ok_sync) pending[0] = pending[1] = false;
   if (trace)
     fprintf(stderr, "upload: %.1f MB in %.1f ms (host copies %.1f ms, DMA waits %.1f ms, %d threads)\n", n / 1e6,
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_all).count(), ms_copy, ms_wait, T);

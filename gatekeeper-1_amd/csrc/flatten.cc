@@ -180,7 +180,9 @@ uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const Ns
   if (s_kind == NO_ID) s_kind = st.s_empty;
   if (s_name == NO_ID) s_name = st.s_empty;
   if (s_objns == NO_ID) s_objns = st.s_empty;
-  // schema.ParseGroupVersion: "v" -> ("", v), "g/v" -> (g, v), more slashes -> ("", "")
+  // schema.ParseGroupVersion: "v" -> ("", v), "g/v" -> (g, v); more slashes
+  // fail to parse, and unstructured.GroupVersionKind() then returns an EMPTY
+  // GVK (unstructured.go:425-432): the review's kind.kind is "" as well
   uint32_t s_group = st.s_empty, s_version = st.s_empty;
   {
     std::string apiv(st.str(s_apiv));
@@ -189,6 +191,8 @@ uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const Ns
     else if (apiv.find('/', slash + 1) == std::string::npos) {
       s_group = st.intern(apiv.data(), slash);
       s_version = st.intern(apiv.data() + slash + 1, apiv.size() - slash - 1);
+    } else {
+      s_kind = st.s_empty;
     }
   }
   const bool has_name = s_name != st.s_empty, has_ns = !ns.name.empty();

@@ -79,13 +79,24 @@ class AuditWriter:
                 self.per_action[actions[c]] = self.per_action.get(actions[c], 0) + int(n)
 
     @staticmethod
-    def from_sweep(constraints, sweep, resource_of_review, limit: int = DEFAULT_LIMIT) -> "AuditWriter":
+    def from_sweep(constraints, sweep, resource_of_review, limit: int = DEFAULT_LIMIT, fallback=None) -> "AuditWriter":
         """status writer of one engine sweep (Batch.eval_audit);
-        resource_of_review(i) -> (kind, name, namespace)"""
+        resource_of_review(i) -> (kind, name, namespace).  Reviews the engine
+        flagged (sweep.flagged: error / CPU fallback) are answered by
+        `fallback(i)` -> [(constraint index, msg, enforcementAction)] in the
+        reference's per-review order, e.g. the embedded CPU OPA driver, and
+        merged in at their position in evaluation order; without a fallback a
+        sweep with flagged reviews raises (its status would silently miss
+        them).  A review whose Query errors returns [] (manager.go:376-381
+        skips it)."""
+        totals, rows = flagged_rows(sweep, fallback, 0)
         w = AuditWriter(constraints, limit)
-        w.set_totals(sweep.totals, sweep.actions)
+        w.set_totals(totals, sweep.actions)
         for s in sweep.samples:
-            w.add_sample(s.constraint, resource_of_review(s.review), s.msg, s.msg_len, s.enforcement_action)
+            rows.append((s.review, 0 if s.rule == 0xffff else 1, s.seq, s.constraint, s.msg, s.msg_len, s.enforcement_action))
+        rows.sort(key=lambda r: (r[3], r[0], r[1], r[2]))
+        for rv, _ar, _seq, c, head, ml, ea in rows:
+            w.add_sample(c, resource_of_review(rv), head, ml, ea)
         return w
 
     def add_results(self, results, resources: Sequence[Tuple[str, str, str]]):
@@ -129,6 +140,32 @@ class AuditWriter:
             for a, n in w.per_action.items():
                 m.per_action[a] = m.per_action.get(a, 0) + n
         return m
+
+
+class FlaggedReviews(RuntimeError):
+    """an engine sweep flagged reviews (error / CPU fallback) and no fallback
+    evaluator was given to answer them"""
+
+
+def flagged_rows(sweep, fallback, review_base: int):
+    """(totals including the flagged reviews' results, sample rows of those
+    results) -- rows (global review, autoreject last key 1, order, constraint,
+    message bytes, message length, enforcementAction)"""
+    totals = [int(x) for x in sweep.totals]
+    rows = []
+    flagged = list(getattr(sweep, "flagged", []) or [])
+    if not flagged:
+        return totals, rows
+    if fallback is None:
+        raise FlaggedReviews("%d reviews flagged error/fallback need the CPU driver (pass fallback=)" % len(flagged))
+    for rv in flagged:
+        for j, (c, msg, ea) in enumerate(fallback(rv)):
+            if c >= len(totals):
+                totals.extend([0] * (c + 1 - len(totals)))
+            totals[c] += 1
+            b = msg.encode("utf-8", "surrogateescape")
+            rows.append((int(review_base) + rv, 1, j, c, b[:MSG_SIZE], len(b), ea))
+    return totals, rows
 
 
 def resource_of(review_or_object: dict, is_review: bool = False) -> Tuple[str, str, str]:

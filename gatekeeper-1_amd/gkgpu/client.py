@@ -137,12 +137,27 @@ def constraint_path(constraint: dict) -> str:
 
 
 def group_version(api_version: str):
+    """schema.ParseGroupVersion (k8s.io/apimachinery schema/group_version.go):
+    "" and "/" -> ("", ""), "v" -> ("", v), "g/v" -> (g, v); more slashes are
+    an error, which unstructured.GroupVersionKind turns into an EMPTY GVK
+    (unstructured.go:425-432) -- kind included, see gvk_of"""
     if "/" not in api_version:
         return "", api_version
     parts = api_version.split("/")
     if len(parts) == 2:
         return parts[0], parts[1]
     return "", ""
+
+
+def gvk_of(obj: dict):
+    """obj.GroupVersionKind() (unstructured.go:425-432): (group, version, kind),
+    all empty when apiVersion does not parse"""
+    av = obj.get("apiVersion", "") if isinstance(obj.get("apiVersion"), str) else ""
+    kind = obj.get("kind", "") if isinstance(obj.get("kind"), str) else ""
+    if av.count("/") > 1:
+        return "", "", ""
+    g, v = group_version(av)
+    return g, v, kind
 
 
 def data_path(obj: dict) -> str:
@@ -160,8 +175,7 @@ def data_path(obj: dict) -> str:
 def augmented_review(obj: dict, ns: Optional[dict]) -> dict:
     """gkReview JSON for Review(AugmentedUnstructured{obj, ns}) (target.go:129-163):
     admission/v1beta1 AdmissionRequest field order, omitempty name/namespace."""
-    group, version = group_version(obj.get("apiVersion", "") if isinstance(obj.get("apiVersion"), str) else "")
-    kind = obj.get("kind", "") if isinstance(obj.get("kind"), str) else ""
+    group, version, kind = gvk_of(obj)
     md = obj.get("metadata") if isinstance(obj.get("metadata"), dict) else {}
     name = md.get("name", "") if isinstance(md.get("name"), str) else ""
     nsobj = ns if ns is not None else EMPTY_NAMESPACE

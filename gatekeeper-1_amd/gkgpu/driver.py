@@ -94,6 +94,12 @@ def load_library():
     if not os.path.exists(p):
         raise EngineUnavailable("libgkgpu.so not built (%s); run __graft_entry__.build()" % p)
     _one_hip_runtime()
+    # template-kernel code objects (jit.cc): the in-tree cache travels with the
+    # tree to the GPU box, so a fresh process there loads them instead of
+    # compiling every template with hipRTC again
+    tree_cache = os.path.join(os.path.dirname(os.path.dirname(_HERE)), ".jitcache")
+    if "GKGPU_JIT_CACHE" not in os.environ and os.path.isdir(tree_cache) and os.access(tree_cache, os.W_OK):
+        os.environ["GKGPU_JIT_CACHE"] = tree_cache
     lib = C.CDLL(p)
     vp = C.c_void_p
     sz = C.c_size_t
@@ -277,6 +283,10 @@ class AuditSweep:
     device_tuples: int
     device_bytes: int
     launches: List["Launch"]
+    # batch indices of the reviews flagged GK_REVIEW_ERROR / GK_REVIEW_FALLBACK:
+    # left out of totals and samples (the reference answers them on CPU OPA);
+    # AuditWriter.from_sweep / parallel.exchange_audit merge their results in
+    flagged: List[int] = field(default_factory=list)
 
 
 def _collect_audit(lib, h) -> AuditSweep:
@@ -306,8 +316,15 @@ def _collect_audit(lib, h) -> AuditSweep:
         lib.gk_results_device_counts(h, C.byref(dt), C.byref(db))
         ne, nf = C.c_uint64(), C.c_uint64()
         lib.gk_results_flag_counts(h, C.byref(ne), C.byref(nf))
+        flagged = []
+        if ne.value or nf.value:
+            import numpy as np
+            nr = lib.gk_results_reviews(h)
+            st = np.zeros(max(nr, 1), dtype=np.uint32)
+            lib.gk_results_copy_status(h, st.ctypes.data, None)
+            flagged = np.nonzero(st[:nr] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK))[0].tolist()
         return AuditSweep(totals, samples, actions, ne.value, nf.value, lib.gk_results_excluded(h), list(t), dt.value,
-                          db.value, _launches(lib, h))
+                          db.value, _launches(lib, h), flagged)
     finally:
         lib.gk_results_free(h)
 

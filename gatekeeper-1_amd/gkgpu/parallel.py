@@ -46,6 +46,15 @@ def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
     return start, min(n_total, start + per)
 
 
+def _global_rank(group):
+    """group rank -> the global rank torch.distributed.P2POp expects as its peer
+    (ranks are group-local everywhere else; identity for the default group)"""
+    import torch.distributed as dist
+    if group is None:
+        return lambda r: r
+    return lambda r: dist.get_global_rank(group, r)
+
+
 class DeviceOutput:
     """Reusable device buffers receiving one evaluation's raw output
     (Batch.eval(device_out=...)); grown on demand, kept across steps."""
@@ -100,6 +109,7 @@ class Gatherer:
         import torch.distributed as dist
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
+        peer = _global_rank(self.group)
         dev = tuples.device
         t = tuples
         if review_base:
@@ -125,16 +135,16 @@ class Gatherer:
                                        torch.empty(nb, dtype=torch.uint8, device=dev))
                 rt, rb = self._recv[key]
                 if nt:
-                    ops.append(dist.P2POp(dist.irecv, rt, r, self.group))
+                    ops.append(dist.P2POp(dist.irecv, rt, peer(r), self.group))
                 if nb:
-                    ops.append(dist.P2POp(dist.irecv, rb, r, self.group))
+                    ops.append(dist.P2POp(dist.irecv, rb, peer(r), self.group))
                 out.append((rt, rb))
         else:
             nt, nb = sizes[rank]
             if nt:
-                ops.append(dist.P2POp(dist.isend, t.contiguous(), self.dst, self.group))
+                ops.append(dist.P2POp(dist.isend, t.contiguous(), peer(self.dst), self.group))
             if nb:
-                ops.append(dist.P2POp(dist.isend, bytes_.contiguous(), self.dst, self.group))
+                ops.append(dist.P2POp(dist.isend, bytes_.contiguous(), peer(self.dst), self.group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
@@ -188,6 +198,7 @@ def gather_bytes(payload: bytes, dst: int = 0, device=None, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    peer = _global_rank(group)
     dev = device if device is not None else torch.device("cpu")
     n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
@@ -200,9 +211,9 @@ def gather_bytes(payload: bytes, dst: int = 0, device=None, group=None):
         for r in range(world):
             if r != rank and sizes[r]:
                 recv[r] = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
-                ops.append(dist.P2POp(dist.irecv, recv[r], r, group))
+                ops.append(dist.P2POp(dist.irecv, recv[r], peer(r), group))
     elif sizes[rank]:
-        ops.append(dist.P2POp(dist.isend, buf, dst, group))
+        ops.append(dist.P2POp(dist.isend, buf, peer(dst), group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -231,17 +242,25 @@ def merge_samples(rows, limit: int):
 
 
 def exchange_audit(sweep, review_base: int, resource_of_review, constraints, limit: int = 20, dst: int = 0,
-                   device=None, group=None):
+                   device=None, group=None, fallback=None):
     """The multi-rank audit exchange: totals all-reduce (int64) + samples
-    gathered to `dst`, merged into an AuditWriter there (None elsewhere)."""
+    gathered to `dst`, merged into an AuditWriter there (None elsewhere).
+    Reviews the rank's sweep flagged (error / CPU fallback) are answered by
+    `fallback(i)` -> [(constraint, msg, enforcementAction)] on that rank
+    before the exchange (AuditWriter.from_sweep); without one they raise."""
     import json
     import torch
     import torch.distributed as dist
-    from .audit import AuditWriter
+    from .audit import AuditWriter, flagged_rows
     dev = device if device is not None else torch.device("cpu")
-    tot = torch.tensor([int(x) for x in sweep.totals], dtype=torch.int64, device=dev)
+    totals, frows = flagged_rows(sweep, fallback, review_base)
+    tot = torch.tensor(totals, dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
-    payload = json.dumps(_sample_rows(sweep, review_base, resource_of_review)).encode()
+    rows = _sample_rows(sweep, review_base, resource_of_review)
+    for rv, ar, j, c, head, ml, ea in frows:
+        kind, name, ns = resource_of_review(rv - int(review_base))
+        rows.append([rv, c, ar, j, ml, head.decode("latin-1"), ea, kind, name, ns])
+    payload = json.dumps(rows).encode()
     parts = gather_bytes(payload, dst, dev, group)
     if parts is None:
         return None

@@ -79,3 +79,20 @@ def test_excluded_objects_carry_no_document(drv):
     finally:
         drv.excluder_clear()
     assert n_ex < n_all
+
+
+def test_unparsable_api_version_gives_an_empty_gvk():
+    """schema.ParseGroupVersion fails on more than one '/', and
+    unstructured.GroupVersionKind() then returns an EMPTY GVK
+    (k8s.io/apimachinery unstructured.go:425-432): review.kind is all "" --
+    kind included -- in the native flattener, in the Python envelope the
+    oracle is fed, and in HandleViolation's resource identity."""
+    from gkgpu.client import augmented_review
+    obj = {"apiVersion": "a/b/c", "kind": "Pod", "metadata": {"name": "p", "namespace": "n"}}
+    assert augmented_review(obj, None)["kind"] == {"group": "", "version": "", "kind": ""}
+    ok = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d", "namespace": "n"}}
+    assert augmented_review(ok, None)["kind"] == {"group": "apps", "version": "v1", "kind": "Deployment"}
+    d = gkgpu.Driver(host_only=True)
+    b = d.stage_objects([obj, ok], [None, None])
+    assert b.resource(0) == ("", "", "p", "n")
+    assert b.resource(1) == ("apps/v1", "Deployment", "d", "n")

@@ -187,3 +187,83 @@ def test_audit_exchange_equals_single_process_sweep(world, limit):
         p.join(60)
     assert status == "ok", same
     assert same and same_act and total > 100
+
+
+# -- flagged reviews (GK_REVIEW_ERROR / GK_REVIEW_FALLBACK): ADVICE r02.  The
+# engine leaves them out of totals and samples; the caller's CPU driver answers
+# them and the status writer merges them in at their place in evaluation order.
+
+def _flagged_sweep(per, lo, hi, ncons, actions, limit, flagged):
+    """_sweep_of with the reviews `flagged` (local indices) removed, as the
+    engine reports them"""
+    keep = [rows if (r - lo) not in flagged else [] for r, rows in enumerate(per[lo:hi], start=lo)]
+    full = list(per)
+    full[lo:hi] = keep
+    sw = _sweep_of(full, lo, hi, ncons, actions, limit)
+    sw.flagged = sorted(flagged)
+    return sw
+
+
+def test_from_sweep_merges_flagged_reviews():
+    from gkgpu.audit import AuditWriter, FlaggedReviews
+    per, cons, actions, res = _oracle_rows(120)
+    flagged = {0, 3, 17, 50, 119}
+    sweep = _flagged_sweep(per, 0, len(per), len(cons), actions, 5, flagged)
+    with pytest.raises(FlaggedReviews):
+        AuditWriter.from_sweep(cons, sweep, lambda i: res[i], 5)
+    fb = lambda i: [(c, msg, ea) for c, _ar, _seq, msg, ea in per[i]]  # noqa: E731  (the CPU driver)
+    got = AuditWriter.from_sweep(cons, sweep, lambda i: res[i], 5, fallback=fb)
+    want = AuditWriter(cons, 5)
+    for r, rows in enumerate(per):
+        for c, _ar, _seq, msg, ea in rows:
+            want.add(c, res[r], msg, ea)
+    assert got.statuses() == want.statuses()
+    assert got.per_action == want.per_action
+
+
+def _flagged_worker(rank, world, port, limit, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "gatekeeper-1_amd")]
+        from gkgpu.audit import AuditWriter
+        from gkgpu.parallel import exchange_audit
+        per, cons, actions, res = _oracle_rows()
+        lo, hi = shard_range(len(per), rank, world)
+        flagged = {i for i in range(hi - lo) if (i * 7 + rank) % 11 == 0}
+        sweep = _flagged_sweep(per, lo, hi, len(cons), actions, limit, flagged)
+        fb = lambda i: [(c, msg, ea) for c, _ar, _seq, msg, ea in per[lo + i]]  # noqa: E731
+        merged = exchange_audit(sweep, lo, lambda i: res[lo + i], cons, limit=limit, fallback=fb)
+        if rank == 0:
+            single = AuditWriter(cons, limit)
+            for r, rows in enumerate(per):
+                for c, _ar, _seq, msg, ea in rows:
+                    single.add(c, res[r], msg, ea)
+            q.put(("ok", merged.statuses() == single.statuses(), merged.per_action == single.per_action,
+                   sum(merged.totals.values())))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put(("err", traceback.format_exc(), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_audit_exchange_merges_flagged_reviews():
+    """each rank answers its flagged reviews through the fallback before the
+    exchange: the merged statuses equal one sweep's over all resources"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_flagged_worker, args=(r, world, port, 4, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    status, same, same_act, total = q.get(timeout=240)
+    for p in ps:
+        p.join(60)
+    assert status == "ok", same
+    assert same and same_act and total > 100
