@@ -244,6 +244,16 @@ def main():
         algo_bytes = None
     whole_store = nodes * 16 + str_bytes + col_bytes + dl.tuples * 32 + dl.bytes
     achieved = algo_bytes / (k_avg_ms / 1000.0) / 1e9 if algo_bytes else None
+    # Sweep-level roofline (SURVEY 8(d)'s own definition: every referenced byte
+    # counted ONCE per sweep, all constraints evaluated per resource): the union
+    # of the document values every constraint references + their distinct
+    # string bytes + the match id columns + 16 B per tuple of the whole sweep +
+    # 4 B per review, over the whole step (ms_per_step: every kernel, the
+    # format and sampling passes and the host work between them included)
+    sweep_ref = referenced_bytes(drv, batch, None, cons_ids, args.cpu_threads, every=True) if rank == 0 else None
+    sweep_bytes = None
+    if sweep_ref is not None:
+        sweep_bytes = 4 * sweep_ref["nodes"] + sweep_ref["string_bytes"] + 12 * nrev + 16 * last.device_tuples + 4 * nrev
     kernels = [{"kernel": ln.kernel, "avg_ms": sum(launch_ms[ln.kernel]) / len(launch_ms[ln.kernel]),
                 "constraints": ln.constraints, "tuples": ln.tuples, "bytes": ln.bytes} for ln in last.launches]
     # the message format pass (gk_format_kernel): per tuple it reads the 32-B
@@ -348,6 +358,11 @@ def main():
                 "kernel_ms_avg": k_avg_ms,
                 "kernel": dom,
                 "template": kinds_of.get(dom),
+                "sweep_algo_bytes": sweep_bytes,
+                "sweep_achieved": (sweep_bytes / (ms_per_step / 1000.0) / 1e9) if sweep_bytes else None,
+                "sweep_frac": (sweep_bytes / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS) if sweep_bytes else None,
+                "sweep_definition": "SURVEY 8(d) per sweep: 4 B x the union of document values all constraints reference "
+                                    "+ their distinct string bytes + 16 B x all tuples + 16 B x reviews, over ms_per_step",
             },
             "kernels": kernels,
             "format_pass": fmt_roof,
@@ -358,9 +373,19 @@ def main():
         dist.destroy_process_group()
 
 
-def referenced_bytes(drv, batch, kind, cons_ids, threads):
+def referenced_bytes(drv, batch, kind, cons_ids, threads, every=False):
     """SURVEY 8(d) reference accounting of the constraints of template `kind`
-    over the whole staged batch (oracle/cpuvm_touch.cc), or None"""
+    over the whole staged batch (oracle/cpuvm_touch.cc), or None; every=True:
+    all constraints at once (a value several constraints read counts once)"""
+    if every:
+        sys.path.insert(0, ROOT)
+        try:
+            from oracle import cpu_baseline as CB
+        except Exception:
+            return None
+        r = CB.referenced(drv, batch, -1, threads=threads if threads > 0 else min(16, os.cpu_count() or 1))
+        r["constraints"] = [n for _k, n in cons_ids]
+        return r
     if kind is None:
         return None
     kind = kind.replace(" (guard)", "")

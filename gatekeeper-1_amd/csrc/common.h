@@ -161,7 +161,16 @@ struct MatchSpec {
   uint32_t nssel_off;     // selector words
   uint32_t prog;          // program index of the template
   uint32_t params;        // node index of spec.parameters (or NO_ID => {})
+  // LDS staging (template kernels, devrt.h stage_wave): the node window
+  // [plo, plo + pn) holding the whole parameters subtree (pn = 0: not staged),
+  // and the offset of the constraint's regex stage record in `stage`
+  // (NO_ID: none) -- [n, then per DFA: pattern sid, word offset in dfa_c,
+  // bytes, nst | ncls << 16, start | sens << 16]
+  uint32_t plo, pn;
+  uint32_t stage_off;
+  uint32_t pad_;
 };
+static_assert(sizeof(MatchSpec) == 48, "MatchSpec layout");
 
 enum ReviewColFlags : uint32_t {
   RC_KIND_OK = 1,         // review.kind.{group,kind} are strings
@@ -267,6 +276,8 @@ struct DevArgs {
                               // of arrays: word j of tuple i at frec[j * out_cap + i]
   char* ebytes;               // bytes that existed at emission (eager messages, details JSON)
   uint64_t ebytes_cap;
+  const uint32_t* stage;      // per-constraint LDS stage records (MatchSpec.stage_off)
+  const uint32_t* dfa_c;      // byte-class-compressed DFAs the stage records point at
   uint32_t* lens;             // size pass: output bytes per tuple (message + details)
   unsigned long long* part;   // size pass: per tile of FTILE tuples, its bytes; then the
                               // exclusive prefix over tiles (spine)

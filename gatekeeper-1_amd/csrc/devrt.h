@@ -205,6 +205,81 @@ __device__ __forceinline__ uint64_t hget(const PLane& L, uint32_t w) { return L.
 __device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) { L.H[w] = v; }
 #endif
 
+// ------------------------------------------------------------------ LDS stage
+// Template kernels stage, per wavefront and at kernel entry, what every lane
+// of the wave reads again and again (the wave evaluates ONE constraint):
+//   GK_LDS_PARAMS  the constraint's parameters subtree (a node window of its
+//                  document, MatchSpec.plo/pn), read by the lookups the JIT
+//                  proves parameter-derived (jit.cc param_flow: vget_p,
+//                  op_iter_next_p) from LDS instead of the node store;
+//   GK_LDS_DFA     the byte-class-compressed DFAs of the regex patterns in
+//                  those parameters (MatchSpec.stage_off), walked by re_run
+//                  from LDS (two LDS reads per subject byte instead of a
+//                  dependent global load).
+// One area per wavefront of the 256-thread block (threadIdx.x >> 6).
+#ifndef GK_LDS_PARAMS
+#define GK_LDS_PARAMS 0
+#endif
+#ifndef GK_LDS_DFA
+#define GK_LDS_DFA 0
+#endif
+constexpr uint32_t LDS_PCAP = 64;          // parameter nodes per wave (1 KB)
+constexpr uint32_t LDS_DFA_BYTES = 1024;   // compressed DFA bytes per wave (engine.cc rebuild_stage)
+constexpr uint32_t LDS_DFA_MAX = 4;        // DFAs per wave
+#if GK_LDS_PARAMS
+__shared__ Node gk_lds_pnodes[4][LDS_PCAP];
+__device__ __forceinline__ Node pnode(uint32_t idx, uint32_t plo, uint32_t pn) {
+  GK_TOUCH_NODE(idx);
+  const uint32_t off = idx - plo;
+  if (off < pn) return gk_lds_pnodes[threadIdx.x >> 6][off];
+  return gk_args.nodes[idx];
+}
+#endif
+#if GK_LDS_DFA
+__shared__ uint32_t gk_lds_dfa[4][LDS_DFA_BYTES / 4];
+// per DFA: pattern sid, byte offset in the wave's area, nst | ncls << 16, start | sens << 16
+__shared__ uint32_t gk_lds_dfadir[4][1 + 4 * LDS_DFA_MAX];
+#endif
+
+// copies this wave's stage (all 64 lanes, wave-uniform m); the wave's own
+// lanes read it after the wave barrier
+__device__ __forceinline__ void stage_wave(const MatchSpec& m, uint32_t lane) {
+#if GK_LDS_PARAMS || GK_LDS_DFA
+  const uint32_t wv = threadIdx.x >> 6;
+#endif
+#if GK_LDS_PARAMS
+  const uint32_t pn = m.pn <= LDS_PCAP ? m.pn : 0;
+  for (uint32_t k = lane; k < pn; k += 64) gk_lds_pnodes[wv][k] = gk_args.nodes[m.plo + k];
+#endif
+#if GK_LDS_DFA
+  uint32_t nd = 0;
+  if (m.stage_off != NO_ID) {
+    const uint32_t* r = gk_args.stage + m.stage_off;
+    nd = r[0] < LDS_DFA_MAX ? r[0] : LDS_DFA_MAX;
+    uint32_t at = 0;
+    for (uint32_t i = 0; i < nd; ++i) {
+      const uint32_t* e = r + 1 + 5 * i;
+      const uint32_t words = (e[2] + 3) / 4;
+      if (at + words * 4 > LDS_DFA_BYTES) { nd = i; break; }
+      for (uint32_t k = lane; k < words; k += 64) gk_lds_dfa[wv][at / 4 + k] = gk_args.dfa_c[e[1] + k];
+      if (lane == 0) {
+        gk_lds_dfadir[wv][1 + 4 * i] = e[0];
+        gk_lds_dfadir[wv][2 + 4 * i] = at;
+        gk_lds_dfadir[wv][3 + 4 * i] = e[3];
+        gk_lds_dfadir[wv][4 + 4 * i] = e[4];
+      }
+      at += words * 4;
+    }
+  }
+  if (lane == 0) gk_lds_dfadir[wv][0] = nd;
+#endif
+#if GK_LDS_PARAMS || GK_LDS_DFA
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
 // a heap-resident value (must survive a loop's per-iteration heap reset when it
 // escapes to a register that outlives the iteration)
 __device__ __forceinline__ bool heap_val(uint64_t v) {
@@ -676,6 +751,26 @@ __device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
   return vget_slow(L, c, key);
 }
 
+#if GK_LDS_PARAMS
+// vget for a container the JIT proved parameter-derived (jit.cc param_flow):
+// the constraint's parameter nodes come from the wave's LDS stage
+__device__ __forceinline__ uint64_t vget_p(PLane& L, uint64_t c, uint64_t key, uint32_t plo, uint32_t pn) {
+  if (vtag(c) == V_NODE && vtag(key) == V_STR) {
+    const uint32_t ci = (uint32_t)vpay(c);
+    const Node n = pnode(ci, plo, pn);
+    if (!(n.flags & 1) && n.type == NT_OBJ) {
+      const uint32_t id = (uint32_t)vpay(key);
+      for (uint32_t i = 0; i < n.n; ++i) {
+        const Node ch = pnode(n.first + i, plo, pn);
+        if (ch.key == id) return nodeval_of(ch, n.first + i);
+      }
+      return mkv(V_UNDEF, 0);
+    }
+  }
+  return vget(L, c, key);
+}
+#endif
+
 // ------------------------------------------------------------------ printing
 // Output sinks of the printers below (each has put(c); puts_/put_* dispatch on it):
 //   Out  — the lane byte buffer (eagerly formatted strings, details JSON);
@@ -960,9 +1055,42 @@ __device__ int re_lookup(uint32_t sid) {
   }
   return -1;
 }
+#if GK_LDS_DFA
+// the walk over a byte-class-compressed DFA the wave staged (regex.cc
+// compress_regex_dfa layout); -3 when the pattern is not staged
+__device__ __forceinline__ int re_run_lds(const PLane& L, uint32_t sid, uint64_t val) {
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t nd = gk_lds_dfadir[wv][0];
+  for (uint32_t i = 0; i < nd; ++i) {
+    if (gk_lds_dfadir[wv][1 + 4 * i] != sid) continue;
+    const uint8_t* t = (const uint8_t*)gk_lds_dfa[wv] + gk_lds_dfadir[wv][2 + 4 * i];
+    const uint32_t nc = gk_lds_dfadir[wv][3 + 4 * i], ss = gk_lds_dfadir[wv][4 + 4 * i];
+    const uint32_t nst = nc & 0xffff, ncls = nc >> 16, sens = ss >> 16;
+    const uint8_t* acc = t + 256 + nst * ncls;
+    uint32_t s = ss & 0xffff;
+    SView v = sview(L, val);
+    for (uint32_t j = 0; j < v.n; ++j) {
+      const uint32_t c = (uint8_t)v.p[j];
+      if (c >= 0x80 && sens) return -2;
+      if (acc[s] & 1) return 1;
+      s = t[256 + s * ncls + t[c]];
+      if (s >= nst) return 0;
+    }
+    return (acc[s] & 3) ? 1 : 0;
+  }
+  return -3;
+}
+#endif
+
 // returns 1 match, 0 no match, -1 error (invalid pattern), -2 fallback
 __device__ int re_run(const PLane& L, uint64_t pat, uint64_t val) {
   if (vtag(pat) != V_STR) return -2;
+#if GK_LDS_DFA
+  {
+    const int r = re_run_lds(L, (uint32_t)vpay(pat), val);
+    if (r != -3) return r;
+  }
+#endif
   int e = re_lookup((uint32_t)vpay(pat));
   if (e < 0) return -2;
   uint32_t meta = gk_args.dfa_meta[e];
@@ -1140,34 +1268,15 @@ __device__ int match_constraint(const MatchSpec& m, const ReviewCol& rc) {
 // (rflags) drops them in every consumer, as it drops the rows of reviews
 // another constraint's lane flagged.
 
-// one slot per active lane with `want`, in lane order; one atomic per wave
+// Output reservations: a plain atomicAdd per emitting lane on the one
+// counter.  The address is wave-uniform, so the compiler's atomic optimizer
+// turns it into one atomic per wavefront (a scan over the active lanes, then a
+// broadcast of the base): consecutive slots for the lanes that emit at a site.
 __device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, bool want) {
-  const uint64_t m = gk_ballot(want);
-  if (!want) return 0;
-  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-  uint64_t base = 0;
-  if (gk_lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__builtin_popcountll(m));
-  base = __shfl(base, (int)leader, 64);
-  return base + gk_lanes_below(m);
+  return want ? (uint64_t)atomicAdd(ctr, 1ull) : 0;
 }
-
-// `n` bytes per active lane with `want` (n may differ per lane), in lane order
 __device__ __forceinline__ uint64_t wave_reserve_bytes(unsigned long long* ctr, bool want, uint32_t n) {
-  const uint64_t m = gk_ballot(want && n > 0);
-  if (!m) return 0;
-  uint64_t below = 0, tot = 0;
-  const uint32_t me = gk_lane_id();
-  for (uint64_t mm = m; mm; mm &= mm - 1) {
-    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-    const uint32_t v = (uint32_t)__shfl(n, (int)l, 64);
-    if (l < me) below += v;
-    tot += v;
-  }
-  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-  uint64_t base = 0;
-  if (me == leader) base = atomicAdd(ctr, (unsigned long long)tot);
-  base = __shfl(base, (int)leader, 64);
-  return base + below;
+  return (want && n) ? (uint64_t)atomicAdd(ctr, (unsigned long long)n) : 0;
 }
 
 // the tuple order key of the lane's next emission; false = over the limits
@@ -1178,9 +1287,13 @@ __device__ __forceinline__ bool next_seq(PLane& L, uint32_t& seq) {
   return true;
 }
 
-// an emission's bytes into the global staging buffer (slow path only)
-__device__ __forceinline__ void copy_out(char* dst, const char* src, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
+// an emission's bytes into the global staging buffer at `off` (slow path
+// only): source read a dword at a time, destination written in dwords (byte
+// stores only at the two ends, which neighbouring reservations share)
+__device__ __forceinline__ void copy_out(uint64_t off, const char* src, uint32_t n) {
+  GOut g{(uint8_t*)gk_args.ebytes, off, off, 0, false};
+  puts_(g, src, n);
+  g.finish();
 }
 
 __device__ __forceinline__ void slot_overflow(const PLane& L) { atomicOr(&gk_args.rflags[L.rv], (uint32_t)RF_OVERFLOW); }
@@ -1200,8 +1313,8 @@ __device__ __noinline__ void emit_eager(PLane& L, bool want, uint32_t rule, cons
   if (!want) return;
   L.en = L.en + 1u;
   if (slot >= gk_args.out_cap || eoff + eb > gk_args.ebytes_cap) { slot_overflow(L); return; }
-  copy_out(gk_args.ebytes + eoff, msg, mlen);
-  if (!detobj) copy_out(gk_args.ebytes + eoff + mlen, det, dlen);
+  copy_out(eoff, msg, mlen);
+  if (!detobj) copy_out(eoff + mlen, det, dlen);
   Viol v;
   v.review = L.rv;
   v.constraint = L.cn;
@@ -1733,6 +1846,28 @@ __device__ __forceinline__ bool op_iter_next(PLane& L, uint64_t coll, uint64_t& 
   return true;
 }
 
+#if GK_LDS_PARAMS
+// op_iter_next over a collection the JIT proved parameter-derived
+__device__ __forceinline__ bool op_iter_next_p(PLane& L, uint64_t coll, uint64_t& st, uint32_t y, uint64_t& k,
+                                               uint64_t& v, uint32_t plo, uint32_t pn) {
+  if (vtag(coll) != V_NODE) return op_iter_next(L, coll, st, y, k, v);
+  const uint32_t pos = (uint32_t)st;
+  const uint32_t d = y < MAXLOOP ? y : 0;
+  const uint32_t mh = (uint32_t)((st >> 32) & 0xffff), mb = (uint32_t)(st >> 48);
+  L.hp = mh > L.keepH[d] ? mh : L.keepH[d];
+  L.bp = mb > L.keepB[d] ? mb : L.keepB[d];
+  const uint32_t ci = (uint32_t)vpay(coll);
+  const Node n = pnode(ci, plo, pn);
+  if (pos >= n.n) return false;
+  const uint32_t c = n.first + pos;
+  const Node ch = pnode(c, plo, pn);
+  v = nodeval_of(ch, c);
+  k = n.type == NT_OBJ ? mkv(V_STR, ch.key) : mkint(pos);
+  st = (st & 0xffffffff00000000ull) | (pos + 1);
+  return true;
+}
+#endif
+
 __device__ __forceinline__ bool op_cmp(PLane& L, uint32_t kind, uint64_t x, uint64_t y, uint64_t& out) {
   if (vtag(x) == V_UNDEF || vtag(y) == V_UNDEF) { out = mkv(V_UNDEF, 0); return true; }
   int cr;
@@ -1920,8 +2055,8 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
   if (!ok) return false;
   L.en = L.en + 1u;
   if (slot >= gk_args.out_cap || eoff + eb > gk_args.ebytes_cap) { slot_overflow(L); return true; }
-  if (!defer) copy_out(gk_args.ebytes + eoff, ms.p, ms.n);
-  if (det) copy_out(gk_args.ebytes + eoff + (defer ? 0u : ms.n), det, dlen);
+  if (!defer) copy_out(eoff, ms.p, ms.n);
+  if (det) copy_out(eoff + (defer ? 0u : ms.n), det, dlen);
   Viol v;
   v.review = L.rv;
   v.constraint = L.cn;
@@ -2035,8 +2170,9 @@ __device__ __noinline__ void finish_lane(PLane& L, uint32_t lane, uint32_t c, bo
 // ------------------------------------------------------------------ kernel body
 // lane -> (review tile, constraint): a wave = 64 consecutive reviews x ONE
 // constraint of the launch's list, so every lane runs the same predicate and
-// the constraint's MatchSpec loads are wave-uniform.  `run(L, rc, m, r, c)`
-// evaluates the template predicate for a matched lane.
+// the constraint's MatchSpec loads are wave-uniform.  `run(L, review,
+// params, prog, plo, pn)` evaluates the template predicate for a matched lane
+// ([plo, plo + pn): the parameter nodes staged in LDS, template kernels).
 template <typename Run>
 __device__ __forceinline__ void audit_body(Run run) {
   uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2060,6 +2196,12 @@ __device__ __forceinline__ void audit_body(Run run) {
   L.rv = r;
   L.cn = c;
   const MatchSpec m = gk_args.cons[c];
+  stage_wave(m, lane);
+#if GK_LDS_PARAMS
+  const uint32_t plo = m.plo, pn = m.pn <= LDS_PCAP ? m.pn : 0;
+#else
+  const uint32_t plo = 0, pn = 0;
+#endif
   // autoreject_review (target_template_source.go:12-25)
   const bool autorej = live && !(rc.flags & RC_FALLBACK) && (m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) &&
                        rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) &&
@@ -2076,7 +2218,7 @@ __device__ __forceinline__ void audit_body(Run run) {
       else if (mr == 1 && (m.flags & MF_FALLBACK)) lane_fallback(L, FB_TEMPLATE);  // template served by CPU OPA
       else if (mr == 1 && m.prog != NO_ID) {
         uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
-        run(L, mkv(V_NODE, rc.root), params, m.prog, r, c);
+        run(L, mkv(V_NODE, rc.root), params, m.prog, plo, pn);
       }
     }
   }

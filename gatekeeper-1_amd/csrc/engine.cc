@@ -336,10 +336,15 @@ struct gk_engine {
   std::map<uint32_t, std::pair<uint32_t, uint32_t>> dfa_index;  // pattern sid -> (word offset, status)
   std::vector<uint32_t> dfa_words;
   std::vector<uint32_t> dfa_keys, dfa_meta;
+  // LDS stage (devrt.h stage_wave): byte-class-compressed DFAs (pattern sid ->
+  // [word offset in dfa_c, bytes, nst | ncls << 16, start | sens << 16]; empty:
+  // does not compress) and the per-constraint stage records
+  std::map<uint32_t, std::vector<uint32_t>> cdfa_index;
+  std::vector<uint32_t> dfa_c, stage;
   // device mirrors of the permanent tables (written under the exclusive lock,
   // except the append-only string / number tables: under smu, graveyard kept)
   gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
-      d_dfa_meta, d_dfa_words;
+      d_dfa_meta, d_dfa_words, d_stage, d_dfa_c;
   // gk_debug_host_args: host copies of the per-call tables (diagnostics / CPU baseline)
   std::vector<gk::MatchSpec> dbg_cons;
   std::vector<uint32_t> dbg_progoff, dbg_mwords, dbg_dfa_keys, dbg_dfa_meta, dbg_dfa_words, dbg_fmt;
@@ -889,6 +894,74 @@ static void rebuild_regex(gk_engine* e) {
   }
 }
 
+// ------------------------------------------------------------------ LDS stage plan
+// Per constraint (devrt.h stage_wave): the node window holding its whole
+// parameters subtree, and the compressed DFAs of the regex patterns among its
+// parameter strings (what re_match with a parameter pattern reads).
+static void rebuild_stage(gk_engine* e) {
+  e->stage.clear();
+  const bool any_regex = !e->dfa_index.empty();
+  for (auto* c : e->corder) {
+    MatchSpec& m = c->spec;
+    m.plo = 0;
+    m.pn = 0;
+    m.stage_off = NO_ID;
+    if (m.params == NO_ID) continue;
+    uint32_t lo = m.params, hi = m.params;
+    std::vector<uint32_t> strs, stack{m.params};
+    while (!stack.empty()) {
+      const uint32_t n = stack.back();
+      stack.pop_back();
+      lo = std::min(lo, n);
+      hi = std::max(hi, n);
+      const Node nd = e->st.nodes()[n];
+      if (nd.type == NT_STR) strs.push_back(nd.val);
+      if (nd.type == NT_ARR || nd.type == NT_OBJ)
+        for (uint32_t i = 0; i < nd.n; ++i) stack.push_back(nd.first + i);
+    }
+    m.plo = lo;
+    m.pn = hi - lo + 1;
+    if (!any_regex) continue;
+    std::vector<uint32_t> rec;
+    uint32_t bytes = 0;
+    std::set<uint32_t> seen;
+    for (uint32_t sid : strs) {
+      if (!seen.insert(sid).second) continue;
+      auto it = e->dfa_index.find(sid);
+      if (it == e->dfa_index.end() || it->second.second != RX_OK) continue;
+      auto ct = e->cdfa_index.find(sid);
+      if (ct == e->cdfa_index.end()) {
+        const size_t off = it->second.first, nst0 = e->dfa_words[off];
+        const size_t len = std::min(e->dfa_words.size() - off, 3 + nst0 * 129);
+        std::vector<uint32_t> dw(e->dfa_words.begin() + off, e->dfa_words.begin() + off + len);
+        std::vector<uint8_t> t;
+        uint32_t nst = 0, ncls = 0, start = 0, sens = 0;
+        std::vector<uint32_t> ent;
+        if (compress_regex_dfa(dw, 1024, t, nst, ncls, start, sens)) {
+          ent = {(uint32_t)e->dfa_c.size(), (uint32_t)t.size(), nst | (ncls << 16), start | (sens << 16)};
+          t.resize((t.size() + 3) & ~(size_t)3, 0);
+          for (size_t k = 0; k < t.size(); k += 4) {
+            uint32_t w;
+            memcpy(&w, t.data() + k, 4);
+            e->dfa_c.push_back(w);
+          }
+        }
+        ct = e->cdfa_index.emplace(sid, ent).first;
+      }
+      if (ct->second.empty()) continue;
+      const uint32_t nb = (ct->second[1] + 3) & ~3u;
+      if (bytes + nb > 1024 || rec.size() / 5 >= 4) continue;  // devrt.h LDS_DFA_BYTES / LDS_DFA_MAX
+      bytes += nb;
+      rec.push_back(sid);
+      rec.insert(rec.end(), ct->second.begin(), ct->second.end());
+    }
+    if (rec.empty()) continue;
+    m.stage_off = (uint32_t)e->stage.size();
+    e->stage.push_back((uint32_t)(rec.size() / 5));
+    e->stage.insert(e->stage.end(), rec.begin(), rec.end());
+  }
+}
+
 // ------------------------------------------------------------------ device sync + launch
 static bool ensure_device(gk_engine* e) {
   if (e->dev_ok) return true;
@@ -963,6 +1036,11 @@ static bool sync_tables(gk_engine* e) {
   ok &= up(e->d_dfa_keys, dk, false);
   ok &= up(e->d_dfa_meta, dm, false);
   ok &= up(e->d_dfa_words, dw, false);
+  std::vector<uint32_t> sg = e->stage, dc = e->dfa_c;
+  if (sg.empty()) sg.push_back(0);
+  if (dc.empty()) dc.push_back(0);
+  ok &= up(e->d_stage, sg, false);
+  ok &= up(e->d_dfa_c, dc, false);
   return ok;
 }
 
@@ -1000,6 +1078,7 @@ static int prepare_locked(gk_engine* e, bool device) {
     maybe_compact(e);
     rebuild_constraints(e);
     rebuild_regex(e);
+    rebuild_stage(e);
   } catch (const std::exception& ex) {
     return fail(e, GK_EPARSE, ex.what());
   }
@@ -1213,6 +1292,8 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.dfa_keys = (const uint32_t*)e->d_dfa_keys.p;
     a.dfa_meta = (const uint32_t*)e->d_dfa_meta.p;
     a.dfa_words = (const uint32_t*)e->d_dfa_words.p;
+    a.stage = (const uint32_t*)e->d_stage.p;
+    a.dfa_c = (const uint32_t*)e->d_dfa_c.p;
     a.ndfa = (uint32_t)std::max<size_t>(e->dfa_keys.size(), 1);
     a.ncode = (uint32_t)e->bank.code.size();
     a.ncons = ncons;
@@ -1439,7 +1520,8 @@ void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
   for (auto& x : e->ctxs) x->release_all();
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
-                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words})
+                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
+                  &e->d_stage, &e->d_dfa_c})
     b->free_();
   for (void* p : e->graveyard) hipFree(p);
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);

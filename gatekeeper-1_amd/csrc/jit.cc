@@ -262,6 +262,79 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
   return LF;
 }
 
+// Parameter-derived registers (devrt.h GK_LDS_PARAMS): which registers may
+// hold a node of the constraint's parameters subtree on entry to each
+// instruction (forward may-analysis).  Lookups and iterations over such a
+// register read the wave's LDS copy of the subtree (vget_p / op_iter_next_p);
+// those fall back to the node store for a node outside the staged window, so
+// the analysis only picks the cheaper path, it never decides a result.
+FmtFlow param_flow(const Program& p, const CodeBank& bank) {
+  const uint32_t b0 = p.code_off, n = p.code_len;
+  FmtFlow F;
+  F.nw = (p.nregs + 64) / 64;
+  F.in.assign(n, std::vector<uint64_t>(F.nw, 0));
+  F.reached.assign(n, 0);
+  auto has = [&](const std::vector<uint64_t>& s, uint32_t r) { return r < 64 * F.nw && ((s[r >> 6] >> (r & 63)) & 1); };
+  auto put = [&](std::vector<uint64_t>& s, uint32_t r, bool v) {
+    if (r >= 64 * F.nw) return;
+    if (v) s[r >> 6] |= 1ull << (r & 63);
+    else s[r >> 6] &= ~(1ull << (r & 63));
+  };
+  std::vector<uint32_t> work;
+  auto flow = [&](uint32_t to, const std::vector<uint64_t>& s) {
+    if (to < b0 || to >= b0 + n) return;
+    uint32_t k = to - b0;
+    bool ch = !F.reached[k];
+    F.reached[k] = 1;
+    for (uint32_t w = 0; w < F.nw; ++w) {
+      uint64_t nv = F.in[k][w] | s[w];
+      if (nv != F.in[k][w]) { F.in[k][w] = nv; ch = true; }
+    }
+    if (ch) work.push_back(k);
+  };
+  if (n) { F.reached[0] = 1; work.push_back(0); }
+  while (!work.empty()) {
+    uint32_t k = work.back();
+    work.pop_back();
+    const Ins& in = bank.code[b0 + k];
+    std::vector<uint64_t> s = F.in[k];
+    const uint32_t next = b0 + k + 1;
+    switch (in.op) {
+      case OP_END: case OP_FAIL_FALLBACK: continue;
+      case OP_JMP: flow(in.x, s); continue;
+      case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: flow(in.x, s); flow(next, s); continue;
+      case OP_ITER_NEXT: {
+        flow(in.x, s);
+        const bool pv = has(s, in.a);
+        if (in.b != 0xffff) put(s, in.b, false);
+        if (in.c != 0xffff) put(s, in.c, pv);
+        flow(next, s);
+        continue;
+      }
+      case OP_MEMO_GET: {
+        std::vector<uint64_t> t = s;
+        put(t, in.a, false);
+        flow(in.x, t);
+        flow(next, s);
+        continue;
+      }
+      case OP_LOADPARAM: put(s, in.a, true); break;
+      case OP_MOV: case OP_GET: case OP_GETK: put(s, in.a, has(s, in.b)); break;
+      case OP_YIELD: if (has(s, in.b)) put(s, in.a, true); break;
+      case OP_ITER_INIT: put(s, in.a, has(s, in.b)); put(s, in.a + 1u, false); break;
+      case OP_EMIT: case OP_MEMO_PUT: case OP_ORD: break;
+      default: put(s, in.a, false); break;
+    }
+    flow(next, s);
+  }
+  return F;
+}
+
+static bool lds_stage_on() {
+  const char* v = getenv("GKGPU_LDS_STAGE");  // A/B switch, default on
+  return !v || atoi(v) != 0;
+}
+
 // A literal re_match pattern's DFA (regex.cc layout; the semantics of re_run /
 // run_regex_dfa) as code: a switch over states with byte ranges as compares,
 // so matching loads only the subject's bytes.  "" when too large to inline.
@@ -342,6 +415,8 @@ std::string table_inline(const CodeBank& bank, const Store& st, uint32_t off, co
 struct Gen {
   std::string pre;   // helper functions (literal regex DFAs)
   std::string body;  // body of the predicate function
+  bool param_reads = false;  // lookups / iterations over parameter nodes (vget_p, op_iter_next_p)
+  bool param_regex = false;  // re_match with a computed (parameter) pattern (re_run -> re_run_lds)
 };
 
 // Body of the predicate function: one statement per bytecode instruction.
@@ -379,6 +454,8 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   if (!lm || atoi(lm) == 0) for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
   FmtFlow F = fmt_flow(p, bank);
   LookFlow LK = look_flow(p, bank, F);
+  FmtFlow PF = param_flow(p, bank);
+  const bool pstage = lds_stage_on();
   Gen g;
   // literal re_match patterns compiled to code
   std::vector<std::pair<uint64_t, std::string>> relits;  // (pattern value, function)
@@ -445,6 +522,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         const int have = kc >= 0 ? LK.find(k, in.b, (uint32_t)kc) : -1;
         if (have == (int)in.a) o << "/* " << a << " holds " << b << "[" << c << "] */";
         else if (have >= 0) o << a << " = " << R((uint32_t)have) << ";  // = vget(L, " << b << ", " << c << ")";
+        else if (pstage && PF.has(k, in.b)) { o << a << " = vget_p(L, " << b << ", " << c << ", plo, pn);"; g.param_reads = true; }
         else o << a << " = vget(L, " << b << ", " << c << ");";
         break;
       }
@@ -452,13 +530,22 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         const int have = LK.find(k, in.b, in.x);
         if (have == (int)in.a) o << "/* " << a << " holds " << b << "[K" << in.x << "] */";
         else if (have >= 0) o << a << " = " << R((uint32_t)have) << ";  // = vget(L, " << b << ", K" << in.x << ")";
-        else o << a << " = vget(L, " << b << ", " << lit(bank.consts[in.x]) << ");";
+        else if (pstage && PF.has(k, in.b)) {
+          o << a << " = vget_p(L, " << b << ", " << lit(bank.consts[in.x]) << ", plo, pn);";
+          g.param_reads = true;
+        } else o << a << " = vget(L, " << b << ", " << lit(bank.consts[in.x]) << ");";
         break;
       }
       case OP_ITER_INIT: o << "op_iter_init(L, " << a << ", " << R(in.a + 1) << ", " << b << ", " << y << ");"; break;
       case OP_ITER_NEXT:
-        o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next(L, " << a << ", " << R(in.a + 1)
-          << ", " << y << ", k_, v_)) goto " << x << ";";
+        if (pstage && PF.has(k, in.a)) {
+          o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next_p(L, " << a << ", " << R(in.a + 1)
+            << ", " << y << ", k_, v_, plo, pn)) goto " << x << ";";
+          g.param_reads = true;
+        } else {
+          o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next(L, " << a << ", " << R(in.a + 1)
+            << ", " << y << ", k_, v_)) goto " << x << ";";
+        }
         if (in.b != 0xffff) o << " " << b << " = k_;";
         if (in.c != 0xffff) o << " " << c << " = v_;";
         o << " }";
@@ -490,6 +577,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
             // canonify_cpu ran 4.48 -> 4.73 ms with it).
             const char* rm = getenv("GKGPU_RE_MEMO");
             const bool memo_re = (!rm || atoi(rm) != 0) && LK.konst(k, in.b) < 0;
+            if (LK.konst(k, in.b) < 0) g.param_regex = true;
             const std::string site = std::to_string(0x10000u + k) + "u";
             o << "{ uint64_t p_ = " << A0 << ", s_ = " << A1 << "; if (!is_strv(p_) || !is_strv(s_)) { lane_error(L); "
               << a << " = " << UND << "; }";
@@ -641,6 +729,24 @@ static bool lds_scalars() {
   return !v || atoi(v) != 0;
 }
 
+// LDS stage (devrt.h GK_LDS_PARAMS / GK_LDS_DFA): what the kernel's block may
+// add to the lane heap words and scalars and still fit the blocks per CU its
+// waves-per-EU asks for (160 KB per CU).  2-wave kernels (32 heap words, 73 KB)
+// take one of the two, 3-wave kernels (16 words, 41 KB) both.
+struct StagePlan { bool params = false, dfa = false; };
+static StagePlan stage_plan(const Program& p, const Gen& g) {
+  StagePlan sp;
+  if (!lds_stage_on()) return sp;
+  const char* w = getenv("GKGPU_JIT_WPE");
+  const int wpe = w ? atoi(w) : (small_program(p) ? 3 : 2);
+  const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
+  uint32_t used = (uint32_t)lds_heap_words(p) * 8u * 256u + (lds_scalars() ? 9u * 4u * 256u : 0u);
+  const uint32_t pbytes = 4u * 64u * 16u, dbytes = 4u * 1024u + 4u * 17u * 4u;  // devrt.h LDS_PCAP / LDS_DFA_*
+  if (g.param_regex && used + dbytes <= limit) { sp.dfa = true; used += dbytes; }
+  if (g.param_reads && used + pbytes <= limit) { sp.params = true; used += pbytes; }
+  return sp;
+}
+
 static std::string inline_hot_tag(const Program& p) {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
@@ -648,6 +754,7 @@ static std::string inline_hot_tag(const Program& p) {
   if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
   t += "d" + std::to_string(lds_heap_words(p));
   if (!lds_scalars()) t += "s0";
+  if (!lds_stage_on()) t += "p0";
   return t;
 }
 
@@ -674,15 +781,20 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words(p) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(p) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
+  const StagePlan sp = stage_plan(p, g);
+  if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
+  if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre
-    << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params) {\n"
+    << (sp.params ? "" : "#define vget_p(L, c, k, lo, n) vget(L, c, k)\n"
+                         "#define op_iter_next_p(L, c, st, y, k, v, lo, n) op_iter_next(L, c, st, y, k, v)\n")
+    << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params, uint32_t plo, uint32_t pn) {\n"
     << g.body << "}\n"
     << "}  // namespace gk\n"
     << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p) << ") " << name << "(gk::DevArgs) {\n"
-    << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t, uint32_t) {\n"
-    << "    gk::" << name << "_pred(L, review, params);\n"
+    << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t plo, uint32_t pn) {\n"
+    << "    gk::" << name << "_pred(L, review, params, plo, pn);\n"
     << "  });\n"
     << "}\n";
   return o.str();

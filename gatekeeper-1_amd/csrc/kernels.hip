@@ -86,7 +86,7 @@ __device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t par
 }
 
 __global__ void __launch_bounds__(256) audit_kernel(DevArgs) {
-  audit_body([&](PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t r, uint32_t c) {
+  audit_body([&](PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t, uint32_t) {
     run_program(L, gk_args.prog_off[prog], review, params);
   });
 }

@@ -561,3 +561,78 @@ extern "C" int gk_regex_test(const char* pattern, const char* text, size_t len) 
   if (st != gk::RX_OK) return -2;
   return gk::run_regex_dfa(w.data(), std::string(text, len));
 }
+
+namespace gk {
+
+// Byte-class compression of a DFA in compile_regex_dfa's layout, for the LDS
+// copy a wavefront stages (devrt.h re_run_lds): two bytes share a class when
+// every state sends them to the same state, so a row needs one entry per class
+// instead of 256.  Layout: [0, 256) class of each byte, then nst x ncls u8
+// transitions (255 = dead), then nst u8 accept flags (bit0 match already
+// found, bit1 accepting at end of text).  false when there are more than 254
+// states or the table exceeds max_bytes.
+bool compress_regex_dfa(const std::vector<uint32_t>& d, size_t max_bytes, std::vector<uint8_t>& out, uint32_t& nst,
+                        uint32_t& ncls, uint32_t& start, uint32_t& sens) {
+  if (d.size() < 3) return false;
+  nst = d[0];
+  start = d[1];
+  sens = d[2];
+  if (nst == 0 || nst > 254 || d.size() < 3 + (size_t)nst * 129) return false;
+  const uint32_t* st = d.data() + 3;
+  auto target = [&](uint32_t s, uint32_t c) -> uint32_t {
+    uint32_t w = st[s * 129 + 1 + (c >> 1)];
+    uint32_t t = (c & 1) ? (w >> 16) : (w & 0xffff);
+    return t >= nst ? 255u : t;
+  };
+  std::vector<uint8_t> cls(256);
+  std::vector<uint32_t> rep;  // a representative byte per class
+  for (uint32_t c = 0; c < 256; ++c) {
+    uint32_t k = 0;
+    for (; k < rep.size(); ++k) {
+      bool same = true;
+      for (uint32_t s = 0; s < nst && same; ++s) same = target(s, c) == target(s, rep[k]);
+      if (same) break;
+    }
+    if (k == rep.size()) rep.push_back(c);
+    cls[c] = (uint8_t)k;
+  }
+  ncls = (uint32_t)rep.size();
+  const size_t bytes = 256 + (size_t)nst * ncls + nst;
+  if (bytes > max_bytes) return false;
+  out.assign(bytes, 0);
+  for (uint32_t c = 0; c < 256; ++c) out[c] = cls[c];
+  for (uint32_t s = 0; s < nst; ++s) {
+    for (uint32_t k = 0; k < ncls; ++k) out[256 + s * ncls + k] = (uint8_t)target(s, rep[k]);
+    out[256 + (size_t)nst * ncls + s] = (uint8_t)(st[s * 129] & 3);
+  }
+  return true;
+}
+
+// host-side matcher over the compressed form (tests): the semantics of
+// run_regex_dfa / devrt.h re_run
+int run_regex_cdfa(const std::vector<uint8_t>& t, uint32_t nst, uint32_t ncls, uint32_t start, uint32_t sens,
+                   const std::string& text) {
+  uint32_t s = start;
+  for (unsigned char c : text) {
+    if (c >= 0x80 && sens) return -2;
+    if (t[256 + (size_t)nst * ncls + s] & 1) return 1;
+    s = t[256 + (size_t)s * ncls + t[c]];
+    if (s >= nst) return 0;
+  }
+  return (t[256 + (size_t)nst * ncls + s] & 3) ? 1 : 0;
+}
+
+}  // namespace gk
+
+// the byte-class-compressed form of the same DFA (tests: must agree with
+// gk_regex_test on every input); -3 when the DFA does not compress
+extern "C" int gk_regex_ctest(const char* pattern, const char* text, size_t len) {
+  std::vector<uint32_t> w;
+  int st = gk::compile_regex_dfa(pattern, w);
+  if (st == gk::RX_INVALID) return -1;
+  if (st != gk::RX_OK) return -2;
+  std::vector<uint8_t> t;
+  uint32_t nst, ncls, start, sens;
+  if (!gk::compress_regex_dfa(w, 1 << 20, t, nst, ncls, start, sens)) return -3;
+  return gk::run_regex_cdfa(t, nst, ncls, start, sens, std::string(text, len));
+}

@@ -17,4 +17,10 @@ int compile_regex_dfa(const std::string& pattern, std::vector<uint32_t>& out);
 // host-side matcher over the same DFA (tests / diagnostics)
 int run_regex_dfa(const uint32_t* dfa, const std::string& text);
 
+// byte-class-compressed copy of a DFA for LDS staging (layout in regex.cc)
+bool compress_regex_dfa(const std::vector<uint32_t>& dfa, size_t max_bytes, std::vector<uint8_t>& out, uint32_t& nst,
+                        uint32_t& ncls, uint32_t& start, uint32_t& sens);
+int run_regex_cdfa(const std::vector<uint8_t>& t, uint32_t nst, uint32_t ncls, uint32_t start, uint32_t sens,
+                   const std::string& text);
+
 }  // namespace gk

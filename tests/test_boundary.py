@@ -144,3 +144,32 @@ def test_dump_lists_modules():
     cl.add_template(W.REQUIRED_LABELS_BASIC)
     s = d.dump()
     assert "K8sRequiredLabels" in s
+
+
+def test_compressed_regex_dfa_agrees_with_the_full_table():
+    """regex.cc compress_regex_dfa (the byte-class form a wavefront stages in
+    LDS, devrt.h re_run_lds) decides every subject exactly as the full
+    129-word-per-state table does (run_regex_dfa / devrt.h re_run)."""
+    import ctypes
+    import random
+    lib = gkgpu.load_library()
+    full, comp = lib.gk_regex_test, lib.gk_regex_ctest
+    for f in (full, comp):
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    pats = ["^[a-z]+$", "^prod-[0-9]{2,4}$", "^(dev|staging|prod)$", "^[0-9]+$", "a|b|c", "^$", "x*y+",
+            "^[A-Za-z0-9_.-]{1,63}$", "team-[a-f0-9]+", "^https?://", "é+", "^v[0-9]+\\.[0-9]+(\\.[0-9]+)?$"]
+    rng = random.Random(3)
+    alphabet = b"abcxyz019-_.:/prodevstagingAZ\xc3\xa9 "
+    seen_match = 0
+    for p in pats:
+        subjects = [b"", b"prod", b"prod-12", b"staging", b"v1.2.3", b"https://x", b"\xc3\xa9\xc3\xa9", b"team-ab12"]
+        subjects += [bytes(rng.choice(alphabet) for _ in range(rng.randrange(0, 16))) for _ in range(300)]
+        for s in subjects:
+            a = full(p.encode(), s, len(s))
+            b = comp(p.encode(), s, len(s))
+            if b == -3:
+                continue  # does not compress: the device walks the full table
+            assert a == b, (p, s, a, b)
+            seen_match += a == 1
+    assert seen_match > 50

@@ -44,7 +44,26 @@ def test_lookup_cse_reuses_prologue_lookups_in_inlined_calls():
     assert reused >= 8, reused
     assert off.count("// = vget(") == 0
     # every lookup is either still a call or a copy
-    assert on.count("= vget(L,") == off.count("= vget(L,")
+    calls = lambda src: src.count("= vget(L,") + src.count("= vget_p(L,")  # noqa: E731
+    assert calls(on) == calls(off)
+
+
+def test_parameter_reads_come_from_the_wave_lds_stage():
+    """jit.cc param_flow: lookups and iterations over the constraint's
+    parameters read the wave's LDS copy of the subtree (devrt.h stage_wave,
+    vget_p / op_iter_next_p) when the kernel's LDS budget has room; a
+    re_match with a computed pattern also stages the compressed DFAs
+    (GK_LDS_DFA).  GKGPU_LDS_STAGE=0 turns both off."""
+    lim = _dump("K8sContainerLimits")
+    assert "#define GK_LDS_PARAMS 1" in lim
+    assert "= vget_p(L, " in lim
+    assert "#define GK_LDS_DFA 1" not in lim  # no computed re_match pattern
+    lab = _dump("K8sRequiredLabels")
+    assert "#define GK_LDS_DFA 1" in lab and "#define GK_LDS_PARAMS 1" in lab
+    assert "!op_iter_next_p(L, " in lab
+    off = _dump("K8sRequiredLabels", [("GKGPU_LDS_STAGE", "0")])
+    assert "GK_LDS_PARAMS" not in off and "GK_LDS_DFA" not in off
+    assert "= vget_p(L, " not in off and "!op_iter_next_p(L, " not in off
 
 
 def test_lazy_sprintf_argument_count_is_an_immediate():
