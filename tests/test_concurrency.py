@@ -73,7 +73,13 @@ def test_concurrent_queries_see_one_state_while_a_constraint_is_reput():
                 got = [collections.Counter(r) for r in engine_rows(res, len(batches[k]))]
                 assert not any(res.status), res.status
                 which = [s for s in ("A", "B") if got == want[s][k]]
-                assert which, "batch %d matches neither constraint set" % k
+                if not which:
+                    bad = [(i, dict(got[i]), dict(want["A"][k][i]), dict(want["B"][k][i]))
+                           for i in range(len(got)) if got[i] != want["A"][k][i] and got[i] != want["B"][k][i]]
+                    nA = sum(got[i] == want["A"][k][i] for i in range(len(got)))
+                    nB = sum(got[i] == want["B"][k][i] for i in range(len(got)))
+                    raise AssertionError("batch %d gen %d matches neither constraint set (rows like A %d, like B %d "
+                                         "of %d); reviews unlike both: %r" % (k, res.generation, nA, nB, len(got), bad[:2]))
                 with lock:
                     seen[which[0]] += 1
                     gens.setdefault(res.generation, set()).add(which[0])
