@@ -35,6 +35,13 @@ def parse():
                          "5 = admission-webhook micro-batch (256 AdmissionReviews per launch, p50/p99 latency)")
     ap.add_argument("--load", type=int, default=50, help="config 5: constraints loaded (policy_benchmark_test.go:268)")
     ap.add_argument("--batch", type=int, default=256, help="config 5: AdmissionReviews per launch")
+    ap.add_argument("--coalesce-us", type=int, default=0,
+                    help="config 5: instead of pre-assembled batches, --clients threads issue single-review "
+                         "Query calls at --rate requests/s (open loop) and the engine's micro-batch coalescer "
+                         "gathers them for this many microseconds (up to --batch per launch); latency includes "
+                         "the queueing")
+    ap.add_argument("--clients", type=int, default=64, help="config 5 coalesced: concurrent client threads")
+    ap.add_argument("--rate", type=float, default=20000.0, help="config 5 coalesced: offered requests/s (total)")
     ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="resources of the staged batch timed on the native CPU baseline (oracle/cpuvm.cc; "
@@ -494,7 +501,7 @@ def webhook_main(args):
     from gkgpu.webhook import handle_batch  # noqa: F401  (the per-request decision path tests use)
 
     templates, constraints = W.config5(args.load)
-    drv = gkgpu.Driver(device=local)
+    drv = gkgpu.Driver(device=local, coalesce_us=args.coalesce_us, coalesce_max=args.batch)
     cl = Client(drv)
     for t in templates:
         cl.add_template(t)
@@ -506,6 +513,8 @@ def webhook_main(args):
         drv.query_batch(batches[i % nb])
     if dist is not None:
         dist.barrier()
+    if args.coalesce_us:
+        return webhook_coalesced_main(args, drv, templates, constraints, batches, world, rank, dist)
     # Timed: the C-ABI call (parse, flatten, upload, kernels, download,
     # decode) and one bulk copy of every decoded row (message, details) plus
     # the per-review status words into this process (gk_results_export), as a
@@ -538,8 +547,11 @@ def webhook_main(args):
     n_cons = len(constraints)
     evals = args.steps * args.batch * n_cons * world
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = webhook_cpu_baseline(templates, constraints, batches[0][: min(args.batch, args.cpu_sample)])
+    if rank == 0 and world == 1 and args.cpu_sample != 0:
+        cpu = webhook_native_cpu_baseline(templates, constraints, batches, args.cpu_threads)
+        if args.oracle_sample > 0:
+            cpu["python_oracle"] = webhook_cpu_baseline(templates, constraints,
+                                                        batches[0][: min(args.batch, args.oracle_sample)])
     if rank == 0:
         out = {
             "metric": "resource x constraint evals/sec (1/2/4/8 GPU) + % HBM roofline; vs host-CPU OPA",
@@ -574,6 +586,133 @@ def webhook_main(args):
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def webhook_coalesced_main(args, drv, templates, constraints, batches, world, rank, dist):
+    inputs = [x for b in batches for x in b]
+    lat, elapsed, n, launches, served = webhook_coalesced(args, drv, inputs, len(constraints))
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    def pct(p):
+        return lat[min(len(lat) - 1, int(round(p / 100.0 * (len(lat) - 1))))]
+    n_cons = len(constraints)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample != 0:
+        cpu = webhook_native_cpu_baseline(templates, constraints, batches, args.cpu_threads)
+    if rank == 0:
+        out = {
+            "metric": "resource x constraint evals/sec (1/2/4/8 GPU) + % HBM roofline; vs host-CPU OPA",
+            "value": n * n_cons * world / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1000.0,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (PSP pods of policy_benchmark_test.go as UPDATE AdmissionReviews, seed 99)",
+            "config": {
+                "workload": "config5 coalesced: single-review Query calls from %d client threads at %.0f req/s "
+                            "offered (open loop), micro-batch coalescer window %d us / max %d, x %d PSP "
+                            "constraints (BASELINE configs[4])" % (args.clients, args.rate, args.coalesce_us,
+                                                                  args.batch, n_cons),
+                "requests": n,
+                "constraints": n_cons,
+                "offered_requests_per_s": args.rate,
+                "requests_per_s": n * world / elapsed,
+                "latency_ms": {"p50": pct(50), "p99": pct(99), "mean": sum(lat) / len(lat), "max": lat[-1]},
+                "latency_definition": "scheduled arrival -> the caller's rows back on the host (gk_query + "
+                                      "gk_results_export), queueing included",
+                "launches": launches,
+                "mean_requests_per_launch": served / max(1, launches),
+                "parallelism": "replicas%d (independent webhook replicas, no collective)" % world,
+            },
+            "roofline": None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def webhook_native_cpu_baseline(templates, constraints, batches, threads):
+    """oracle/cpuvm.cc (the engine's compiled bytecode + device runtime built
+    for the host, NOT OPA) on host threads over the same AdmissionReviews,
+    staged on the host: evals/s of the micro-batches' requests x constraints."""
+    import gkgpu
+    from gkgpu.client import Client
+    from oracle import cpu_baseline as CB
+    threads = threads or min(16, os.cpu_count() or 1)
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    inputs = [x for b in batches for x in b]
+    b = d.debug_stage_inputs(inputs)
+    secs, evals, viol, mbytes, flagged = CB.sweep(d, b, threads=threads)
+    b.free()
+    d.close()
+    return {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port",
+            "sample": "%d AdmissionReviews (the benchmark's %d micro-batches) x %d constraints; oracle/cpuvm.cc: the "
+                      "engine's compiled bytecode + device runtime on host threads, NOT OPA (Go/OPA not buildable "
+                      "offline)" % (len(inputs), len(batches), len(constraints)),
+            "seconds": secs, "violations": viol, "message_bytes": mbytes, "flagged_pairs": flagged,
+            "cpu_model": cpu_model()}
+
+
+def webhook_coalesced(args, drv, inputs, n_cons):
+    """Open-loop arrivals: `--clients` threads issue single-review
+    Query(violation) calls (the reference webhook's one Review per request,
+    pkg/webhook/policy.go:371-387) at `--rate` requests/s in total; the engine
+    coalesces concurrent calls (include/gkgpu.h coalesce_us).  A request's
+    latency runs from its scheduled arrival to its results back on the host,
+    so it includes the time spent queued behind a busy client or launch."""
+    import threading
+    viol = 'hooks["admission.k8s.gatekeeper.sh"].violation'
+    n = args.steps * args.batch  # requests
+    per = [n // args.clients + (1 if c < n % args.clients else 0) for c in range(args.clients)]
+    gap = args.clients / args.rate  # each client's inter-arrival time
+    lat = [[] for _ in range(args.clients)]
+    errs = []
+    start = [0.0]
+    go = threading.Barrier(args.clients + 1)
+    blobs = [b.encode() if isinstance(b, str) else b for b in inputs]
+
+    def client(c):
+        try:
+            go.wait()
+            t0 = start[0] + c * gap / args.clients
+            for k in range(per[c]):
+                due = t0 + k * gap
+                now = time.perf_counter()
+                if due > now:
+                    time.sleep(due - now)
+                drv.query_export(viol, blobs[(c + k * args.clients) % len(blobs)])
+                lat[c].append((time.perf_counter() - due) * 1000.0)
+        except Exception as ex:  # noqa: BLE001
+            errs.append(repr(ex))
+    th = [threading.Thread(target=client, args=(c,)) for c in range(args.clients)]
+    for t in th:
+        t.start()
+    b0, r0 = drv.coalesce_stats()
+    start[0] = time.perf_counter() + 0.05
+    go.wait()
+    for t in th:
+        t.join()
+    elapsed = time.perf_counter() - start[0]
+    if errs:
+        raise RuntimeError(errs[0])
+    b1, r1 = drv.coalesce_stats()
+    all_lat = sorted(x for l in lat for x in l)
+    return all_lat, elapsed, n, b1 - b0, r1 - r0
 
 
 def webhook_cpu_baseline(templates, constraints, inputs):

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
 #include <cstring>
 #include <map>
@@ -150,7 +151,14 @@ struct DBuf {
     nc = std::max<size_t>(nc, 4096);
     void* q = nullptr;
     if (hipMalloc(&q, nc) != hipSuccess) return false;
-    if (p && used) hipMemcpy(q, p, used, hipMemcpyDeviceToDevice);
+    // a device-to-device hipMemcpy does not wait for the copy on the host, and
+    // the evaluation contexts' streams are non-blocking (no implicit order with
+    // the null stream): finish it before any launch can read the new buffer
+    if (p && used &&
+        (hipMemcpy(q, p, used, hipMemcpyDeviceToDevice) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess)) {
+      hipFree(q);
+      return false;
+    }
     if (p) {
       if (graveyard) graveyard->push_back(p);
       else hipFree(p);
@@ -272,6 +280,33 @@ struct gk_batch {
   uint64_t dev_bytes = 0;
 };
 
+// Webhook micro-batch coalescer: concurrent single-review
+// gk_query calls -- the webhook's one Client.Review per admission request
+// (pkg/webhook/policy.go:371-387) -- are gathered into one launch of up to
+// `max_batch` reviews or whatever arrived within `window_us` of the first.
+// The first caller to find no batch collecting leads it: it waits for the
+// window (or a full batch), takes the queue, evaluates it as one
+// gk_query_batch and hands every caller its own results; callers that arrive
+// while it evaluates queue up for the next leader.
+struct CoalesceReq {
+  const char* input = nullptr;
+  size_t len = 0;
+  gk_results* out = nullptr;
+  int rc = GK_OK;
+  std::string err;
+  bool done = false;
+};
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable arrive;    // the collecting leader: a request arrived
+  std::condition_variable finished;  // followers: results handed out / a new leader is needed
+  std::vector<CoalesceReq*> queue;
+  bool collecting = false;
+  uint32_t window_us = 0;            // 0: off (every gk_query launches alone)
+  uint32_t max_batch = 256;
+  uint64_t batches = 0, requests = 0;
+};
+
 struct gk_engine {
   // drivers.Driver's locking (local.go:62-68, 117, 303-304): evaluations
   // (Query and the batch calls) share `rw`; mutations (Put/Delete of modules
@@ -285,6 +320,7 @@ struct gk_engine {
   std::mutex smu;
   std::mutex pool_mu;
   std::vector<std::unique_ptr<gk::EvalCtx>> ctxs;  // evaluation contexts (pool)
+  Coalescer co;
   std::vector<void*> graveyard;                     // superseded shared device tables
   uint64_t prepared_gen = 0;  // generation the compiled state and device tables were prepared for
   bool prepared_dev = false;
@@ -1499,6 +1535,10 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
       if (jv >= 0 && d.nodes[jv].type == NT_FALSE) e->jit_enabled = false;
       int hv = d.get(r, "host_only");
       if (hv >= 0 && d.nodes[hv].type == NT_TRUE) e->host_only = true;
+      int cv = d.get(r, "coalesce_us");
+      if (cv >= 0 && d.nodes[cv].type == NT_NUM) e->co.window_us = (uint32_t)std::min(1000000ll, std::max(0ll, atoll(d.str(d.nodes[cv]))));
+      int cm = d.get(r, "coalesce_max");
+      if (cm >= 0 && d.nodes[cm].type == NT_NUM) e->co.max_batch = (uint32_t)std::min(65536ll, std::max(1ll, atoll(d.str(d.nodes[cm]))));
       int mv = d.get(r, "max_violations");
       if (mv >= 0 && d.nodes[mv].type == NT_NUM) e->out_cap0 = std::max<size_t>(64, (size_t)atoll(d.str(d.nodes[mv])));
     }
@@ -1710,12 +1750,96 @@ static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, si
   return GK_OK;
 }
 
+// One caller's share of a coalesced launch: its rows (review index 0), status
+// and totals; the constraint table and timings of the launch.  The raw device
+// output stays with the launch (not exported per caller).
+static gk_results* split_results(const gk_results& all, uint32_t k) {
+  auto* r = new gk_results();
+  r->nrev = 1;
+  r->totals.assign(all.totals.size(), 0);
+  for (const auto& row : all.rows)
+    if (row.review == k) {
+      r->rows.push_back(row);
+      r->rows.back().review = 0;
+      if (row.constraint < r->totals.size()) ++r->totals[row.constraint];
+    }
+  if (!all.status.empty()) {
+    r->status.push_back(all.status[k]);
+    r->reason.push_back(all.reason.empty() ? 0 : all.reason[k]);
+  }
+  r->ckind = all.ckind;
+  r->cname = all.cname;
+  r->cea = all.cea;
+  r->cea_error = all.cea_error;
+  for (int i = 0; i < 5; ++i) r->ms[i] = all.ms[i];
+  r->gen = all.gen;
+  r->launches = all.launches;
+  return r;
+}
+
+static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_results** out) {
+  Coalescer& c = e->co;
+  CoalesceReq me;
+  me.input = input;
+  me.len = len;
+  std::unique_lock<std::mutex> lk(c.mu);
+  c.queue.push_back(&me);
+  if (c.collecting) c.arrive.notify_one();
+  while (!me.done) {
+    const bool queued = std::find(c.queue.begin(), c.queue.end(), &me) != c.queue.end();
+    if (!queued || c.collecting) {
+      c.finished.wait(lk);
+      continue;
+    }
+    // lead the next micro-batch: collect for the window (or until full)
+    c.collecting = true;
+    const auto deadline = Clock::now() + std::chrono::microseconds(c.window_us);
+    while (c.queue.size() < c.max_batch && c.arrive.wait_until(lk, deadline) != std::cv_status::timeout) {}
+    const size_t take = std::min<size_t>(c.queue.size(), c.max_batch);
+    std::vector<CoalesceReq*> batch(c.queue.begin(), c.queue.begin() + take);
+    c.queue.erase(c.queue.begin(), c.queue.begin() + take);
+    c.collecting = false;
+    ++c.batches;
+    c.requests += batch.size();
+    c.finished.notify_all();  // requests left in the queue elect the next leader
+    lk.unlock();
+    std::vector<std::pair<const char*, size_t>> in;
+    in.reserve(batch.size());
+    for (auto* q : batch) in.push_back({q->input, q->len});
+    gk_results* all = nullptr;
+    const int rc = eval_inputs(e, in, &all);
+    std::unique_ptr<gk_results> hold(all);
+    for (uint32_t k = 0; k < batch.size(); ++k) {
+      CoalesceReq* q = batch[k];
+      q->rc = rc;
+      if (rc == GK_OK) q->out = split_results(*all, k);
+      else q->err = tl_err;
+    }
+    lk.lock();
+    for (auto* q : batch) q->done = true;
+    c.finished.notify_all();
+  }
+  lk.unlock();
+  if (me.rc != GK_OK) return fail(e, me.rc, me.err);
+  *out = me.out;
+  return GK_OK;
+}
+
+int gk_coalesce_stats(gk_engine* e, uint64_t* batches, uint64_t* requests) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->co.mu);
+  if (batches) *batches = e->co.batches;
+  if (requests) *requests = e->co.requests;
+  return GK_OK;
+}
+
 int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len, gk_results** out) {
   if (!e || !path || !out) return GK_EINVAL;
   std::string p(path);
   std::string viol = std::string("hooks[\"") + TARGET + "\"].violation";
   std::string aud = std::string("hooks[\"") + TARGET + "\"].audit";
   if (p == viol) {
+    if (e->co.window_us) return coalesced_query(e, input_json ? input_json : "null", input_json ? len : 4, out);
     std::vector<std::pair<const char*, size_t>> in;
     in.push_back({input_json ? input_json : "null", input_json ? len : 4});
     return eval_inputs(e, in, out);
@@ -1766,6 +1890,108 @@ int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, 
   return eval_inputs(e, in, out);
 }
 
+// Divergence- and match-aware evaluation order of a page's reviews
+// (perm[k] = batch index of the k-th evaluated review).
+// Divergence-aware order: a wavefront evaluates 64 consecutive reviews, and
+// its lanes run as long as the largest document (e.g. the Pod with the most
+// containers).  Evaluating reviews in order of document size (node count)
+// puts similar documents in one wave; each column records the review's
+// index in the caller's batch, which every output carries (devrt.h
+// audit_body), so results are unchanged.
+//
+// Ahead of size, two match-affinity keys keep reviews that a constraint's
+// match stage rejects together, so those wavefronts exit after the match
+// instead of idling beside a few matching lanes: one bit per constraint
+// with a namespaces / excludedNamespaces list (membership of the review's
+// namespace), then the kind id.  Keys only reorder work; matching itself is
+// unchanged.
+// GKGPU_MATCH_ORDER (A/B switch): 0 = size keys only, 1 = signature first,
+// 2 (default) = kind, array elements, signature, nodes
+static void review_order(gk_engine* e, const std::vector<ReviewCol>& cols, const std::vector<uint32_t>& weight,
+                         size_t lo, size_t hi, std::vector<uint32_t>& perm) {
+  const size_t n = hi - lo;
+  const int mode = env_mode("GKGPU_MATCH_ORDER", 2, 2);
+  const bool match_order = mode != 0;
+  std::vector<uint32_t> sig(n, 0);  // indexed by batch index - lo
+  if (match_order && !e->constraints_dirty) {
+    const auto& W = e->mwords;
+    auto in_list = [&](uint32_t off, uint32_t id) {
+      if (off >= W.size()) return false;
+      uint32_t n = W[off];
+      for (uint32_t j = 0; j < n && off + 1 + j < W.size(); ++j) if (W[off + 1 + j] == id) return true;
+      return false;
+    };
+    // one signature per distinct namespace-name id (reviews share a few
+    // thousand namespaces), then a lookup per review
+    std::unordered_map<uint32_t, uint32_t> by_ns;
+    for (size_t i = lo; i < hi; ++i) {
+      uint32_t id = cols[i].nsname;
+      auto it = by_ns.find(id);
+      if (it == by_ns.end()) {
+        uint32_t s = 0, bit = 0;
+        for (auto* c : e->corder) {
+          if (bit >= 16) break;
+          const MatchSpec& m = c->spec;
+          if (!(m.flags & (MF_HAS_NAMESPACES | MF_HAS_EXCLUDED))) continue;
+          bool in = ((m.flags & MF_HAS_NAMESPACES) && in_list(m.ns_off, id)) ||
+                    ((m.flags & MF_HAS_EXCLUDED) && in_list(m.exns_off, id));
+          if (in) s |= 1u << bit;
+          ++bit;
+        }
+        it = by_ns.emplace(id, s).first;
+      }
+      sig[i - lo] = it->second;
+    }
+  }
+  perm.resize(n);
+  for (size_t i = 0; i < n; ++i) perm[i] = (uint32_t)(lo + i);
+  // the keys packed into one 60-bit integer per review (kind ids ranked, so
+  // their order is kept), then a stable LSD radix sort: the same permutation
+  // as the comparison sort below, which stays for more than 4096 kinds
+  std::vector<uint32_t> kind_ids;
+  kind_ids.reserve(64);
+  {
+    std::unordered_set<uint32_t> seen;
+    for (size_t i = lo; i < hi; ++i)
+      if (seen.insert(cols[i].kind).second) kind_ids.push_back(cols[i].kind);
+    std::sort(kind_ids.begin(), kind_ids.end());
+  }
+  if (kind_ids.size() <= 4096) {
+    std::unordered_map<uint32_t, uint64_t> krank;
+    for (size_t k = 0; k < kind_ids.size(); ++k) krank[kind_ids[k]] = k;
+    std::vector<uint64_t> key(n);
+    uint32_t last_kind = NO_ID;
+    uint64_t last_rank = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      if (cols[i].kind != last_kind) { last_kind = cols[i].kind; last_rank = krank[last_kind]; }
+      const uint64_t w = weight[i], sg = sig[i - lo] & 0xffffu;
+      if (mode == 2) key[i - lo] = (last_rank << 48) | ((w >> 20) << 36) | (sg << 20) | (w & 0xfffffu);
+      else key[i - lo] = (sg << 44) | ((match_order ? last_rank : 0) << 32) | w;
+    }
+    std::vector<uint32_t> tmp(perm.size());
+    std::vector<uint32_t> cnt(256);
+    for (int sh = 0; sh < 64; sh += 8) {
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (uint32_t x : perm) ++cnt[(key[x - lo] >> sh) & 0xff];
+      if (*std::max_element(cnt.begin(), cnt.end()) == perm.size()) continue;  // one bucket: order kept
+      uint32_t run = 0;
+      for (auto& c : cnt) { uint32_t v = c; c = run; run += v; }
+      for (uint32_t x : perm) tmp[cnt[(key[x - lo] >> sh) & 0xff]++] = x;
+      perm.swap(tmp);
+    }
+  } else std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+    if (mode == 2) {  // kind, array elements, namespace-list bits, nodes
+      if (cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
+      if ((weight[a] >> 20) != (weight[b] >> 20)) return (weight[a] >> 20) < (weight[b] >> 20);
+      if (sig[a - lo] != sig[b - lo]) return sig[a - lo] < sig[b - lo];
+      return weight[a] < weight[b];
+    }
+    if (sig[a - lo] != sig[b - lo]) return sig[a - lo] < sig[b - lo];
+    if (match_order && cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
+    return weight[a] < weight[b];
+  });
+}
+
 // Flattens one page of audit objects (flatten.cc, parallel host threads) and,
 // for staged batches, chooses the evaluation order.  `out` receives the
 // columns (in evaluation order; each carries its batch index in `orig` when
@@ -1773,116 +1999,30 @@ int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, 
 // number of reviews the process excluder skipped.
 static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size, NodeArena& arena,
                              std::vector<ReviewCol>& cols, std::vector<ResourceIds>* resources, uint64_t* excluded,
-                             double* ms_parse = nullptr) {
+                             double* ms_parse = nullptr, uint32_t* paths = nullptr) {
   FlatResult fr;
   std::string err;
   auto exit_ = e->excluded.find("audit");
   const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
-  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, page, default_threads(), e->perm_nodes, arena, fr, err))
+  // GKGPU_PATH_LAYOUT (A/B switch, default on): staged batches' documents in
+  // the path-grouped layout (flatten.h), ordered with the reviews
+  const bool path_layout = order_by_size && env_mode("GKGPU_PATH_LAYOUT", 1, 1) != 0;
+  std::vector<uint32_t> perm;
+  const OrderFn ord = [&](const FlatResult& f, size_t lo, size_t hi, std::vector<uint32_t>& p) {
+    review_order(e, f.cols, f.weight, lo, hi, p);
+  };
+  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, page, default_threads(), e->perm_nodes, arena, fr, err,
+                    path_layout ? &ord : nullptr, path_layout ? &perm : nullptr))
     return fail(e, GK_EINVAL, err);
   if (ms_parse) *ms_parse = fr.ms_parse;
+  if (paths) *paths = fr.paths;
   if (resources) resources->swap(fr.resources);
   if (excluded) *excluded = fr.excluded;
   cols.swap(fr.cols);
-  const std::vector<uint32_t>& weight = fr.weight;
   const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
   auto t_ord = Clock::now();
   if (order_by_size) {
-    // Divergence-aware order: a wavefront evaluates 64 consecutive reviews, and
-    // its lanes run as long as the largest document (e.g. the Pod with the most
-    // containers).  Evaluating reviews in order of document size (node count)
-    // puts similar documents in one wave; each column records the review's
-    // index in the caller's batch, which every output carries (devrt.h
-    // audit_body), so results are unchanged.
-    //
-    // Ahead of size, two match-affinity keys keep reviews that a constraint's
-    // match stage rejects together, so those wavefronts exit after the match
-    // instead of idling beside a few matching lanes: one bit per constraint
-    // with a namespaces / excludedNamespaces list (membership of the review's
-    // namespace), then the kind id.  Keys only reorder work; matching itself is
-    // unchanged.
-    // GKGPU_MATCH_ORDER (A/B switch): 0 = size keys only, 1 = signature first,
-    // 2 (default) = kind, array elements, signature, nodes
-    const int mode = env_mode("GKGPU_MATCH_ORDER", 2, 2);
-    const bool match_order = mode != 0;
-    std::vector<uint32_t> sig(cols.size(), 0);
-    if (match_order && !e->constraints_dirty) {
-      const auto& W = e->mwords;
-      auto in_list = [&](uint32_t off, uint32_t id) {
-        if (off >= W.size()) return false;
-        uint32_t n = W[off];
-        for (uint32_t j = 0; j < n && off + 1 + j < W.size(); ++j) if (W[off + 1 + j] == id) return true;
-        return false;
-      };
-      // one signature per distinct namespace-name id (reviews share a few
-      // thousand namespaces), then a lookup per review
-      std::unordered_map<uint32_t, uint32_t> by_ns;
-      for (size_t i = 0; i < cols.size(); ++i) {
-        uint32_t id = cols[i].nsname;
-        auto it = by_ns.find(id);
-        if (it == by_ns.end()) {
-          uint32_t s = 0, bit = 0;
-          for (auto* c : e->corder) {
-            if (bit >= 16) break;
-            const MatchSpec& m = c->spec;
-            if (!(m.flags & (MF_HAS_NAMESPACES | MF_HAS_EXCLUDED))) continue;
-            bool in = ((m.flags & MF_HAS_NAMESPACES) && in_list(m.ns_off, id)) ||
-                      ((m.flags & MF_HAS_EXCLUDED) && in_list(m.exns_off, id));
-            if (in) s |= 1u << bit;
-            ++bit;
-          }
-          it = by_ns.emplace(id, s).first;
-        }
-        sig[i] = it->second;
-      }
-    }
-    std::vector<uint32_t> perm(cols.size());
-    for (uint32_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    // the keys packed into one 60-bit integer per review (kind ids ranked, so
-    // their order is kept), then a stable LSD radix sort: the same permutation
-    // as the comparison sort below, which stays for more than 4096 kinds
-    std::vector<uint32_t> kind_ids;
-    kind_ids.reserve(64);
-    {
-      std::unordered_set<uint32_t> seen;
-      for (const auto& c : cols)
-        if (seen.insert(c.kind).second) kind_ids.push_back(c.kind);
-      std::sort(kind_ids.begin(), kind_ids.end());
-    }
-    if (kind_ids.size() <= 4096) {
-      std::unordered_map<uint32_t, uint64_t> krank;
-      for (size_t k = 0; k < kind_ids.size(); ++k) krank[kind_ids[k]] = k;
-      std::vector<uint64_t> key(cols.size());
-      uint32_t last_kind = NO_ID;
-      uint64_t last_rank = 0;
-      for (size_t i = 0; i < cols.size(); ++i) {
-        if (cols[i].kind != last_kind) { last_kind = cols[i].kind; last_rank = krank[last_kind]; }
-        const uint64_t w = weight[i], sg = sig[i] & 0xffffu;
-        if (mode == 2) key[i] = (last_rank << 48) | ((w >> 20) << 36) | (sg << 20) | (w & 0xfffffu);
-        else key[i] = (sg << 44) | ((match_order ? last_rank : 0) << 32) | w;
-      }
-      std::vector<uint32_t> tmp(perm.size());
-      std::vector<uint32_t> cnt(256);
-      for (int sh = 0; sh < 64; sh += 8) {
-        std::fill(cnt.begin(), cnt.end(), 0);
-        for (uint32_t x : perm) ++cnt[(key[x] >> sh) & 0xff];
-        if (*std::max_element(cnt.begin(), cnt.end()) == perm.size()) continue;  // one bucket: order kept
-        uint32_t run = 0;
-        for (auto& c : cnt) { uint32_t v = c; c = run; run += v; }
-        for (uint32_t x : perm) tmp[cnt[(key[x] >> sh) & 0xff]++] = x;
-        perm.swap(tmp);
-      }
-    } else std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
-      if (mode == 2) {  // kind, array elements, namespace-list bits, nodes
-        if (cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
-        if ((weight[a] >> 20) != (weight[b] >> 20)) return (weight[a] >> 20) < (weight[b] >> 20);
-        if (sig[a] != sig[b]) return sig[a] < sig[b];
-        return weight[a] < weight[b];
-      }
-      if (sig[a] != sig[b]) return sig[a] < sig[b];
-      if (match_order && cols[a].kind != cols[b].kind) return cols[a].kind < cols[b].kind;
-      return weight[a] < weight[b];
-    });
+    if (!path_layout) review_order(e, cols, fr.weight, 0, cols.size(), perm);
     std::vector<ReviewCol> sorted(cols.size());
     for (uint32_t i = 0; i < perm.size(); ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
     cols.swap(sorted);
@@ -1987,7 +2127,8 @@ int gk_review_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, siz
 static bool batch_upload(gk_engine* e, gk_batch* b) {
   const size_t perm = b->node_begin, docs = b->arena.size();
   if (!b->d_nodes.reserve((perm + docs + 1) * sizeof(Node))) return false;
-  if (perm && hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess)
+  if (perm && (hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess ||
+               hipStreamSynchronize(nullptr) != hipSuccess))  // (see DBuf::reserve)
     return false;
   const size_t bytes = docs * sizeof(Node);
   char* dst = (char*)b->d_nodes.p + perm * sizeof(Node);
@@ -2676,8 +2817,14 @@ extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint6
   auto t0 = Clock::now();
   auto exit_ = e->excluded.find("audit");
   const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
-  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, pg, threads > 0 ? threads : default_threads(), e->perm_nodes, arena,
-                    fr, err))
+  // threads < 0: the staged-batch form (path-grouped layout in evaluation order) on -threads threads
+  std::vector<uint32_t> perm;
+  const OrderFn ord = [&](const FlatResult& f, size_t lo, size_t hi, std::vector<uint32_t>& p) {
+    review_order(e, f.cols, f.weight, lo, hi, p);
+  };
+  const int nt = threads > 0 ? threads : threads < 0 ? -threads : default_threads();
+  if (!flatten_page(e->st, e->smu, e->ns_cache, ex, pg, nt, e->perm_nodes, arena, fr, err, threads < 0 ? &ord : nullptr,
+                    threads < 0 ? &perm : nullptr))
     return fail(e, GK_EINVAL, err);
   double tot = ms_since(t0);
   std::vector<Node> all(e->st.nodes().begin(), e->st.nodes().begin() + e->perm_nodes);

@@ -23,6 +23,9 @@ namespace gk {
 
 static const char* EMPTY_NS_JSON = "{\"metadata\":{\"creationTimestamp\":null},\"spec\":{},\"status\":{}}";
 static constexpr uint32_t kFixedNodes = 4;  // every Store starts with nodes {} null false true
+// path-grouped layout (flatten.h): local marker of a Namespace document's
+// nodes, whose runs every review of the namespace shares
+static constexpr uint8_t kShared = 0x80;
 
 int default_threads() {
   const char* v = getenv("GKGPU_THREADS");
@@ -229,6 +232,7 @@ uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const Ns
   // _unstable: {"namespace": <ns>} (the page's shared Namespace document)
   Node nsn = N[ns.root];
   nsn.key = st.s_namespace;
+  nsn.flags &= (uint8_t)~kShared;  // the review's own node; its members are the shared run
   N[uf] = nsn;
   // HandleViolation: apiVersion = group/version (version alone when group is "")
   res->api_version = s_group == st.s_empty ? s_version : s_apiv;
@@ -238,6 +242,39 @@ uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const Ns
   return root;
 }
 
+// ------------------------------------------------------------------ path-grouped layout (flatten.h)
+constexpr uint32_t kElem = 0xfffffffeu;   // path key of array elements
+constexpr uint32_t kMaxPaths = 1u << 16;  // per part; further distinct paths share their parent's region
+
+// A part's document paths: path 0 is the review root; path(child) =
+// (path(parent), member key id | kElem), key ids local to the part.  A path
+// names the region that holds the member runs of its instances.
+struct PathTab {
+  std::unordered_map<uint64_t, uint32_t> m;
+  std::vector<std::pair<uint32_t, uint32_t>> def;  // (parent, key)
+  static constexpr uint32_t C = 4096;
+  std::vector<uint64_t> ck;                         // direct-mapped cache of m
+  std::vector<uint32_t> cv;
+  PathTab() : def{{NO_ID, NO_ID}}, ck(C, ~0ull), cv(C, 0) {}
+  uint32_t child(uint32_t parent, uint32_t key) {
+    const uint64_t k = ((uint64_t)parent << 32) | key;
+    const uint32_t h = (uint32_t)((k * 0x9e3779b97f4a7c15ull) >> 52) & (C - 1);
+    if (ck[h] == k) return cv[h];
+    uint32_t id;
+    auto it = m.find(k);
+    if (it != m.end()) id = it->second;
+    else if (def.size() >= kMaxPaths) return parent;  // full: the table never changes again
+    else {
+      id = (uint32_t)def.size();
+      m.emplace(k, id);
+      def.push_back({parent, key});
+    }
+    ck[h] = k;
+    cv[h] = id;
+    return id;
+  }
+};
+
 struct Part {
   Store st;
   size_t lo = 0, hi = 0;
@@ -245,6 +282,12 @@ struct Part {
   std::vector<uint8_t> nsglob;       // per review: rc.ns_labels is a global node
   std::vector<uint32_t> weight;
   std::vector<ResourceIds> res;
+  std::vector<uint32_t> ns_roots;    // placed Namespace documents (their runs are shared by reviews)
+  // staged layout: the part's document paths and the nodes each path's
+  // region receives from the part, counted while each document is hot
+  bool count_paths = false;
+  PathTab paths;
+  std::vector<uint64_t> pcount;
   uint64_t excluded = 0;
   std::string err;
   // phase 2 maps (local id -> global id)
@@ -278,7 +321,40 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
       if (nm != NO_ID) { d->name = std::string(st.str(nm)); d->sid = nm; }
     }
     d->root = st.add_node(r);
+    p.ns_roots.push_back(d->root);
+    if (p.count_paths) {  // every review of the namespace shares these runs
+      std::vector<uint32_t> q{d->root};
+      for (size_t h = 0; h < q.size(); ++h) {
+        Node& x = st.nodes()[q[h]];
+        x.flags |= kShared;
+        if (x.type == NT_OBJ || x.type == NT_ARR)
+          for (uint32_t c = 0; c < x.n; ++c) q.push_back(x.first + c);
+      }
+    }
     return d;
+  };
+  // staged layout: the nodes each document path's region receives from a
+  // review, counted right after the review is built (its nodes are in cache)
+  std::vector<uint64_t> stack;
+  auto count_paths = [&](uint32_t root) {
+    const Node* ln = st.nodes().data();
+    stack.clear();
+    stack.push_back(root);
+    while (!stack.empty()) {
+      const uint64_t e = stack.back();
+      stack.pop_back();
+      const uint32_t path = (uint32_t)(e >> 32);
+      const Node& x = ln[(uint32_t)e];
+      if ((x.type != NT_OBJ && x.type != NT_ARR) || x.n == 0 || (ln[x.first].flags & kShared)) continue;
+      if (path >= p.pcount.size()) p.pcount.resize(path + 64, 0);
+      p.pcount[path] += x.n;
+      const bool obj = x.type == NT_OBJ;
+      for (uint32_t c = 0; c < x.n; ++c) {
+        const Node& y = ln[x.first + c];
+        if ((y.type == NT_OBJ || y.type == NT_ARR) && y.n)
+          stack.push_back((uint64_t)(x.first + c) | ((uint64_t)p.paths.child(path, obj ? y.key : kElem) << 32));
+      }
+    }
   };
   for (size_t i = p.lo; i < p.hi; ++i) {
     size_t n0 = st.nodes().size();
@@ -313,6 +389,7 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
     p.cols.push_back(review_columns(st, gst, ns_cache, root, &glob));
     p.nsglob.push_back(glob);
     p.res.push_back(rid);
+    if (p.count_paths) count_paths(root);
     // size key: array elements (what templates iterate: containers, ports,
     // volumes ...) first, then document nodes
     uint32_t elems = 0;
@@ -325,6 +402,231 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
   }
 }
 
+struct Remap {
+  const std::vector<uint32_t>& smap;
+  const std::vector<uint32_t>& nmap;
+  // a local node's scalar fields in global ids (key: by its parent's type)
+  Node operator()(Node y, bool obj_member) const {
+    if (obj_member) y.key = smap[y.key];
+    if (y.type == NT_STR) y.val = smap[y.val];
+    else if (y.type == NT_NUM) y.val = nmap[y.val];
+    y.flags &= (uint8_t)~kShared;
+    return y;
+  }
+};
+
+// Phase 3 of a staged page in the path-grouped layout (flatten.h).  Phase 2
+// (string / number interning) is done, and every part counted the nodes each
+// of its paths' regions receives (run_part).  Parts are ordered and placed
+// independently (the evaluation order is part-major: each part's reviews in
+// their own order, so a wavefront straddles two parts at most at the
+// boundaries), which keeps every pass over a part's arena on its own thread:
+//   1. columns with global string ids, then each part's evaluation order;
+//   2. the Namespace documents, placed once after the review roots;
+//   3. the parts' paths -> global paths; region g holds part 0's nodes at g,
+//      then part 1's, ...;
+//   4. per part, its reviews' nodes in its evaluation order at its cursors.
+static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst, FlatResult& out, size_t n,
+                         std::string& err, const OrderFn& order, std::vector<uint32_t>& perm,
+                         std::chrono::steady_clock::time_point t1) {
+  using Clock = std::chrono::steady_clock;
+  auto ms = [](Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const int T = (int)parts.size();
+  auto pfor = [&](const std::function<void(int)>& f) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(f, t);
+    f(0);
+    for (auto& x : th) x.join();
+  };
+  // 1.
+  out.cols.resize(n);
+  out.weight.resize(n);
+  out.resources.resize(n);
+  pfor([&](int t) {
+    Part& p = parts[t];
+    auto str = [&](uint32_t s) { return s == NO_ID ? NO_ID : p.smap[s]; };
+    for (size_t i = 0; i < p.cols.size(); ++i) {
+      ReviewCol rc = p.cols[i];
+      rc.group = str(rc.group);
+      rc.kind = str(rc.kind);
+      rc.ns = str(rc.ns);
+      rc.nsname = str(rc.nsname);
+      out.cols[p.lo + i] = rc;
+      out.weight[p.lo + i] = p.weight[i];
+      const ResourceIds& r = p.res[i];
+      out.resources[p.lo + i] = ResourceIds{str(r.api_version), str(r.kind), str(r.name), str(r.ns)};
+    }
+  });
+  auto t2 = Clock::now();
+  std::vector<std::vector<uint32_t>> porder(T);
+  std::vector<uint64_t> nlive_of(T, 0);
+  pfor([&](int t) {
+    Part& p = parts[t];
+    order(out, p.lo, p.hi, porder[t]);
+    for (uint32_t i : porder[t]) nlive_of[t] += out.cols[i].root != NO_ID;
+  });
+  perm.clear();
+  perm.reserve(n);
+  for (int t = 0; t < T; ++t) {
+    if (porder[t].size() != parts[t].hi - parts[t].lo) { err = "review order: bad permutation"; return false; }
+    perm.insert(perm.end(), porder[t].begin(), porder[t].end());
+  }
+  std::vector<uint64_t> root_at(T, 0);  // the part's first root position
+  uint64_t nlive = 0;
+  for (int t = 0; t < T; ++t) { root_at[t] = nlive; nlive += nlive_of[t]; }
+  auto t3 = Clock::now();
+  // 2.
+  std::vector<std::unordered_map<uint32_t, uint32_t>> nsmap(T);
+  uint64_t at_ns = nlive;
+  std::vector<std::pair<uint32_t, uint64_t>> q;  // (local id, position)
+  std::vector<Node> nsnodes;
+  for (int t = 0; t < T; ++t) {
+    Part& p = parts[t];
+    const Node* ln = p.st.nodes().data();
+    const Remap rm{p.smap, p.nmap};
+    for (uint32_t r : p.ns_roots) {
+      q.clear();
+      q.push_back({r, at_ns});
+      nsmap[t][r] = (uint32_t)(base + at_ns);
+      nsnodes.push_back(rm(ln[r], false));
+      ++at_ns;
+      for (size_t h = 0; h < q.size(); ++h) {
+        const auto [l, at] = q[h];
+        const Node& x = ln[l];
+        if ((x.type != NT_OBJ && x.type != NT_ARR) || x.n == 0) continue;
+        nsnodes[at - nlive].first = (uint32_t)(base + at_ns);
+        for (uint32_t c = 0; c < x.n; ++c) {
+          const uint32_t lc = x.first + c;
+          nsmap[t][lc] = (uint32_t)(base + at_ns);
+          nsnodes.push_back(rm(ln[lc], x.type == NT_OBJ));
+          q.push_back({lc, at_ns});
+          ++at_ns;
+        }
+      }
+    }
+  }
+  // 3. global paths (a part's paths are numbered parent first)
+  std::unordered_map<uint64_t, uint32_t> gm;
+  std::vector<std::vector<uint32_t>> g_of(T);
+  uint32_t G = 1;
+  for (int t = 0; t < T; ++t) {
+    const PathTab& pt = parts[t].paths;
+    g_of[t].assign(pt.def.size(), 0);
+    for (uint32_t l = 1; l < pt.def.size(); ++l) {
+      const uint32_t key = pt.def[l].second == kElem ? kElem : parts[t].smap[pt.def[l].second];
+      const uint64_t k = ((uint64_t)g_of[t][pt.def[l].first] << 32) | key;
+      auto it = gm.find(k);
+      if (it == gm.end()) it = gm.emplace(k, G++).first;
+      g_of[t][l] = it->second;
+    }
+  }
+  std::vector<std::vector<uint64_t>> pg(G, std::vector<uint64_t>(T, 0));  // nodes of part t at path g
+  for (int t = 0; t < T; ++t) {
+    const Part& p = parts[t];
+    for (uint32_t l = 0; l < p.pcount.size(); ++l)
+      if (p.pcount[l]) pg[g_of[t][l]][t] += p.pcount[l];
+  }
+  uint64_t total = at_ns;
+  for (uint32_t g = 0; g < G; ++g)
+    for (int t = 0; t < T; ++t) {
+      const uint64_t v = pg[g][t];
+      pg[g][t] = base + total;  // part t's first node in region g
+      total += v;
+    }
+  if ((uint64_t)base + total >= NO_ID) { err = "node arena exceeds 2^32 nodes"; return false; }
+  auto t4 = Clock::now();
+  dst.resize(total);
+  Node* dn = dst.data();
+  if (!nsnodes.empty()) memcpy(dn + nlive, nsnodes.data(), nsnodes.size() * sizeof(Node));
+  // 4.
+  std::vector<std::string> perr(T);
+  pfor([&](int t) {
+    Part& p = parts[t];
+    const Node* ln = p.st.nodes().data();
+    const Remap rm{p.smap, p.nmap};
+    std::vector<uint64_t> cur(p.paths.def.size(), 0), stack;
+    for (uint32_t l = 0; l < cur.size(); ++l) cur[l] = pg[g_of[t][l]][t];
+    uint64_t k = root_at[t];
+    for (uint32_t i : porder[t]) {
+      const size_t j = i - p.lo;
+      const ReviewCol& lc = p.cols[j];
+      if (lc.root == NO_ID) continue;
+      const uint32_t nroot = (uint32_t)(base + k);
+      dn[k] = rm(ln[lc.root], false);
+      dn[k].key = 0;
+      ++k;
+      uint32_t lb = NO_ID, old = NO_ID;
+      // depth first; stack entries: local id | path << 32, then the new id
+      stack.clear();
+      stack.push_back(lc.root);
+      stack.push_back(nroot);
+      while (!stack.empty()) {
+        const uint32_t nid = (uint32_t)stack.back();
+        stack.pop_back();
+        const uint64_t e = stack.back();
+        stack.pop_back();
+        const uint32_t path = (uint32_t)(e >> 32);
+        const Node& x = ln[(uint32_t)e];
+        if ((x.type != NT_OBJ && x.type != NT_ARR) || x.n == 0) continue;
+        if (ln[x.first].flags & kShared) {  // a Namespace document's members: placed once, shared
+          auto it = nsmap[t].find(x.first);
+          if (it == nsmap[t].end()) { perr[t] = "path layout: unplaced shared run"; return; }
+          dn[nid - base].first = it->second;
+          continue;
+        }
+        const bool obj = x.type == NT_OBJ;
+        const uint64_t start = cur[path];
+        cur[path] += x.n;
+        dn[nid - base].first = (uint32_t)start;
+        Node* out_run = dn + (start - base);
+        for (uint32_t c = 0; c < x.n; ++c) {
+          const uint32_t l = x.first + c;
+          const Node& y = ln[l];
+          out_run[c] = rm(y, obj);
+          if (l == lc.labels) lb = (uint32_t)(start + c);
+          if (l == lc.old_labels) old = (uint32_t)(start + c);
+          if ((y.type == NT_OBJ || y.type == NT_ARR) && y.n) {
+            stack.push_back((uint64_t)l | ((uint64_t)p.paths.child(path, obj ? y.key : kElem) << 32));
+            stack.push_back(start + c);
+          }
+        }
+      }
+      ReviewCol& rc = out.cols[i];
+      rc.root = nroot;
+      rc.labels = lc.labels == NO_ID ? NO_ID : lb;
+      rc.old_labels = lc.old_labels == NO_ID ? NO_ID : old;
+      if ((lc.labels != NO_ID && lb == NO_ID) || (lc.old_labels != NO_ID && old == NO_ID)) {
+        perr[t] = "path layout: a label node was not placed";
+        return;
+      }
+      if (!p.nsglob[j] && lc.ns_labels != NO_ID) {
+        auto it = nsmap[t].find(lc.ns_labels);
+        if (it == nsmap[t].end()) { perr[t] = "path layout: namespace labels outside the Namespace document"; return; }
+        rc.ns_labels = it->second;
+      }
+    }
+    // every cursor advanced by exactly the count run_part made
+    for (uint32_t l = 0; l < cur.size(); ++l)
+      if (cur[l] - pg[g_of[t][l]][t] != (l < p.pcount.size() ? p.pcount[l] : 0)) {
+        perr[t] = "path layout: region count mismatch";
+        return;
+      }
+  });
+  for (auto& e : perr)
+    if (!e.empty()) { err = e; return false; }
+  out.excluded = 0;
+  for (auto& p : parts) out.excluded += p.excluded;
+  out.node_count = total;
+  out.paths = G;
+  auto t5 = Clock::now();
+  out.ms_layout = ms(t3, t5);
+  out.ms_merge = ms(t1, t5);
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "flatten: intern+columns %.1f ms, order %.1f ms, path layout: regions %.1f + place %.1f ms (%u paths, %llu nodes)\n",
+            ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5), G, (unsigned long long)total);
+  return true;
+}
+
 }  // namespace
 
 // Phases 2 and 3 of every flattening: the parts' strings and numbers are
@@ -333,7 +635,8 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
 // base + k lives at dst[k] -- with string / number ids and child indices
 // rewritten, and its columns relocated.
 static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, uint32_t base, NodeArena& dst,
-                        FlatResult& out, size_t n, std::string& err) {
+                        FlatResult& out, size_t n, std::string& err, const OrderFn* order = nullptr,
+                        std::vector<uint32_t>* perm = nullptr) {
   using Clock = std::chrono::steady_clock;
   auto t1 = Clock::now();
   const int T = (int)parts.size();
@@ -361,6 +664,7 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
   if (getenv("GKGPU_FLATTEN_TRACE"))
     fprintf(stderr, "flatten: intern %.1f ms (%zu strings)\n", std::chrono::duration<double, std::milli>(t15 - t1).count(),
             extra);
+  if (order) return layout_parts(parts, base, dst, out, n, err, *order, *perm, t1);
   uint64_t total = 0;
   for (auto& p : parts) {
     p.node_off = total;  // position in dst
@@ -426,7 +730,8 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
 }
 
 bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded,
-                  const Page& pg, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err) {
+                  const Page& pg, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err,
+                  const OrderFn* order, std::vector<uint32_t>* perm) {
   using Clock = std::chrono::steady_clock;
   auto t0 = Clock::now();
   const size_t n = pg.n;
@@ -437,6 +742,7 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
   for (int t = 0; t < T; ++t) {
     parts[t].lo = n * t / T;
     parts[t].hi = n * (t + 1) / T;
+    parts[t].count_paths = order != nullptr;
   }
   {
     std::vector<std::thread> th;
@@ -448,7 +754,8 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
     if (!p.err.empty()) { err = p.err; return false; }
   out.ms_parse = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   if (getenv("GKGPU_FLATTEN_TRACE")) fprintf(stderr, "flatten: parse %.1f ms\n", out.ms_parse);
-  return merge_parts(gst, smu, parts, base, dst, out, n, err);
+  if (order && !perm) { err = "flatten_page: order without perm"; return false; }
+  return merge_parts(gst, smu, parts, base, dst, out, n, err, order, perm);
 }
 
 bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,

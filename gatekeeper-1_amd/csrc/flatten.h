@@ -8,6 +8,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -83,8 +84,15 @@ struct FlatResult {
   std::vector<ResourceIds> resources; // per review (batch order)
   uint64_t excluded = 0;              // reviews skipped by the process excluder
   uint64_t node_count = 0;
-  double ms_parse = 0, ms_merge = 0;
+  uint32_t paths = 0;                 // path-grouped layout: document paths (regions) laid out
+  double ms_parse = 0, ms_merge = 0, ms_layout = 0;
 };
+
+// Evaluation order of the reviews [lo, hi) of a flattened page, computed from
+// its columns (string ids global, node ids not yet final) and size keys:
+// perm[k] = the batch index of the review of the range evaluated k-th.  Given
+// to flatten_page, it selects the path-grouped node layout below.
+using OrderFn = std::function<void(const FlatResult&, size_t lo, size_t hi, std::vector<uint32_t>& perm)>;
 
 // Flattens a page on `threads` host threads.  The review documents go to `dst`
 // (node id base + k at dst[k]; ids below base are the engine store's
@@ -93,8 +101,22 @@ struct FlatResult {
 // (Excluder.IsNamespaceExcluded(Audit, ns), manager.go:362-365) get a column
 // flagged RC_EXCLUDED and no document.  Returns false with `err` on malformed
 // JSON.
+//
+// Without `order`, each document's nodes are contiguous (BFS per document, in
+// batch order).  With `order` (staged batches), the nodes are laid out
+// **path-grouped** in evaluation order (`perm`: part-major, each host
+// thread's range of the page in the order `order` gives it):
+//   [review roots, in evaluation order]
+//   [Namespace documents (shared by the reviews of a namespace)]
+//   [one region per document path P (root.object.spec.containers[*] ...):
+//    the member runs of every instance of P, in evaluation order]
+// An object's (array's) members stay one contiguous run in document order, so
+// every consumer of the node store reads it unchanged; what changes is that
+// the wavefront's 64 consecutive reviews find their nodes at one path next to
+// each other (a column of node runs per path) instead of in 64 documents.
 bool flatten_page(Store& st, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded_ns,
-                  const Page& page, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err);
+                  const Page& page, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err,
+                  const OrderFn* order = nullptr, std::vector<uint32_t>* perm = nullptr);
 
 // Query inputs ({"review": ...} documents, Driver.Query's input) into `dst`
 // likewise, with their match columns.

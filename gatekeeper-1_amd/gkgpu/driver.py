@@ -31,7 +31,7 @@ EXPORTS = [
     "gk_review_page", "gk_batch_stage_page", "gk_batch_timing", "gk_batch_excluded", "gk_batch_resource",
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
-    "gk_results_export", "gk_results_samples_export", "gk_results_generation",
+    "gk_results_export", "gk_results_samples_export", "gk_results_generation", "gk_coalesce_stats",
 ]
 
 
@@ -122,6 +122,7 @@ def load_library():
     lib.gk_dump.argtypes = [vp, C.POINTER(vp)]
     lib.gk_free_string.argtypes = [vp]
     lib.gk_query_batch.argtypes = [vp, ppc, psz, sz, C.POINTER(vp)]
+    lib.gk_coalesce_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.gk_review_objects.argtypes = [vp, ppc, psz, ppc, psz, sz, C.POINTER(vp)]
     lib.gk_batch_stage_objects.argtypes = [vp, ppc, psz, ppc, psz, sz, C.POINTER(vp)]
     lib.gk_batch_eval.argtypes = [vp, vp, C.c_int, C.POINTER(vp)]
@@ -473,14 +474,21 @@ class Batch:
 class Driver:
     """drivers.Driver over libgkgpu (interface.go:21-39)."""
 
-    def __init__(self, device: int = 0, jit: bool = True, host_only: bool = False):
+    def __init__(self, device: int = 0, jit: bool = True, host_only: bool = False, coalesce_us: int = 0,
+                 coalesce_max: int = 256):
         """jit=False pins every template to the bytecode VM kernel (A/B parity);
-        host_only=True stages batches on the host only (CPU baseline, tests)."""
+        host_only=True stages batches on the host only (CPU baseline, tests);
+        coalesce_us > 0 gathers concurrent query(violation) calls into one
+        launch of up to coalesce_max reviews (the webhook micro-batch
+        coalescer, include/gkgpu.h)."""
         self._lib = load_library()
         e = C.c_void_p()
         opts = {"device": device, "jit": jit}
         if host_only:
             opts["host_only"] = True
+        if coalesce_us:
+            opts["coalesce_us"] = int(coalesce_us)
+            opts["coalesce_max"] = int(coalesce_max)
         rc = self._lib.gk_engine_create(_b(json.dumps(opts)), C.byref(e))
         if rc != 0:
             raise EngineUnavailable("gk_engine_create failed (%d)" % rc)
@@ -554,6 +562,12 @@ class Driver:
         self._check(self._lib.gk_query(self._e, _b(path), js, len(js), C.byref(out)))
         return _collect(self._lib, out)
 
+    def coalesce_stats(self):
+        """(launches, gk_query calls served) of the micro-batch coalescer"""
+        b, r = C.c_uint64(), C.c_uint64()
+        self._check(self._lib.gk_coalesce_stats(self._e, C.byref(b), C.byref(r)))
+        return b.value, r.value
+
     # -- Driver.Dump (interface.go:38)
     def dump(self) -> str:
         p = C.c_void_p()
@@ -589,6 +603,25 @@ class Driver:
             st = (C.c_uint32 * max(1, nr))()
             self._lib.gk_results_copy_status(h, st, None)
             return buf.raw[:need.value], st[:nr]
+        finally:
+            self._lib.gk_results_free(h)
+
+    def query_export(self, path: str, input_json):
+        """Driver.Query of one input (bytes / str JSON), its rows copied out in
+        one gk_results_export call: (blob, status word).  With the coalescer
+        on, concurrent calls share launches."""
+        js = input_json if isinstance(input_json, bytes) else _b(input_json)
+        out = C.c_void_p()
+        self._check(self._lib.gk_query(self._e, _b(path), js, len(js), C.byref(out)))
+        h = out
+        try:
+            need = C.c_size_t()
+            self._lib.gk_results_export(h, None, 0, C.byref(need))
+            buf = C.create_string_buffer(max(1, need.value))
+            self._check(self._lib.gk_results_export(h, buf, need.value, C.byref(need)))
+            st = (C.c_uint32 * 1)()
+            self._lib.gk_results_copy_status(h, st, None)
+            return buf.raw[:need.value], st[0]
         finally:
             self._lib.gk_results_free(h)
 

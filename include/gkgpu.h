@@ -56,7 +56,13 @@ typedef struct gk_engine gk_engine;
 typedef struct gk_results gk_results;
 typedef struct gk_batch gk_batch;
 
-/* opts_json: {"device": 0, "max_violations": N} (may be NULL) */
+/* opts_json (may be NULL): {"device": 0, "max_violations": N,
+ *   "coalesce_us": W, "coalesce_max": M}
+ * coalesce_us > 0 turns on the webhook micro-batch coalescer:
+ * concurrent gk_query(violation) calls -- one per admission request in the
+ * reference, pkg/webhook/policy.go:371-387 -- are evaluated together in one
+ * launch of up to M (default 256) reviews, or whatever arrived within W
+ * microseconds of the first; each caller still gets its own gk_results. */
 int gk_engine_create(const char* opts_json, gk_engine** out);
 void gk_engine_destroy(gk_engine* e);
 const char* gk_last_error(gk_engine* e);
@@ -95,6 +101,8 @@ void gk_free_string(char* s);
 /* ---- batch extensions ----------------------------------------------------- */
 /* n independent Query(violation, inputs[i]) calls in one launch (webhook micro-batch) */
 int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n, gk_results** out);
+/* the coalescer's launches and the gk_query calls they served (diagnostics) */
+int gk_coalesce_stats(gk_engine* e, uint64_t* batches, uint64_t* requests);
 /* audit discovery mode: Review(AugmentedUnstructured{objs[i], ns(objs[i])}) for
  * every object (pkg/audit/manager.go:361-389, pkg/target/target.go:129-163).
  * ns_json[i] is the JSON of the object's corev1.Namespace (NULL / len 0 for

@@ -1,0 +1,93 @@
+"""The webhook micro-batch coalescer (include/gkgpu.h coalesce_us):
+concurrent single-review Query(violation) calls -- one per admission request in
+the reference (pkg/webhook/policy.go:371-387, Client.Review -> Driver.Query,
+vendor/.../frameworks/constraint/pkg/client/client.go:763-800) -- are evaluated
+together in one launch, and every caller gets exactly its own review's results.
+
+ctypes releases the GIL for the duration of each C call, so these Python
+threads really are concurrent callers of gk_query."""
+import collections
+import json
+import threading
+
+import pytest
+
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+
+from parity import engine_rows, oracle_for, oracle_review
+
+VIOLATION = 'hooks["admission.k8s.gatekeeper.sh"].violation'
+
+
+def _driver(**kw):
+    d = gkgpu.Driver(**kw)
+    cl = Client(d)
+    ts, cs = W.config2()
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    return d, ts, cs
+
+
+def _race(n, call):
+    out, errs = [None] * n, []
+    go = threading.Barrier(n)
+
+    def run(i):
+        try:
+            go.wait()
+            out[i] = call(i)
+        except Exception as ex:  # noqa: BLE001
+            out[i] = ex
+    th = [threading.Thread(target=run, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    return out, errs
+
+
+def test_coalesced_callers_all_get_the_launch_error_without_a_device():
+    """Host-only container: the coalesced launch fails (no HIP device); every
+    caller of the launch gets the failure with its message, none hangs, and
+    the launches served fewer launches than calls."""
+    if gkgpu.Driver.device_available():
+        pytest.skip("a HIP device is visible: the GPU test covers the coalescer")
+    d, _, _ = _driver(coalesce_us=20000, coalesce_max=64)
+    pods, ns_of, ns_objs = W.gen_pods(24, seed=3, n_namespaces=4)
+    inputs = [json.dumps({"review": augmented_review(p, ns_objs[n])}) for p, n in zip(pods, ns_of)]
+    out, _ = _race(len(inputs), lambda i: d.query(VIOLATION, inputs[i]))
+    assert all(isinstance(o, RuntimeError) for o in out), out
+    assert all("device" in str(o).lower() for o in out), out[0]
+    launches, served = d.coalesce_stats()
+    assert served == len(inputs)
+    assert launches < len(inputs)
+
+
+@pytest.mark.gpu
+def test_coalesced_queries_equal_the_oracle():
+    """64 concurrent Query(violation) calls with the coalescer on: every result
+    set equals the oracle's for that caller's own review, and the calls were
+    served by fewer launches than calls."""
+    if not gkgpu.Driver.device_available():
+        pytest.fail("no HIP device visible")
+    d, ts, cs = _driver(coalesce_us=5000, coalesce_max=256)
+    pods, ns_of, ns_objs = W.gen_pods(64, seed=17, n_namespaces=8)
+    reviews = [augmented_review(p, ns_objs[n]) for p, n in zip(pods, ns_of)]
+    inputs = [json.dumps({"review": rv}) for rv in reviews]
+    d.query(VIOLATION, inputs[0])  # compile the template kernels first
+    od = oracle_for(ts, cs)
+    want = [collections.Counter(oracle_review(od, rv)) for rv in reviews]
+    out, _ = _race(len(inputs), lambda i: d.query(VIOLATION, inputs[i]))
+    for i, res in enumerate(out):
+        assert not isinstance(res, Exception), res
+        assert not any(res.status), res.status
+        assert all(r.review == 0 for r in res.results)
+        got = collections.Counter(engine_rows(res, 1)[0])
+        assert got == want[i], (i, got, want[i])
+    launches, served = d.coalesce_stats()
+    assert served == len(inputs) + 1
+    assert launches < served

@@ -30,6 +30,47 @@ def test_flatten_same_content_at_every_thread_count(drv):
     assert len(hashes) == 1
 
 
+def test_path_layout_keeps_every_document(drv):
+    """The staged-batch form (flatten.h path-grouped layout: review roots, the
+    Namespace documents, then one region of member runs per document path, in
+    evaluation order) holds the same documents, columns and node count as the
+    per-document layout, at every thread count."""
+    objs, nss = W.gen_pods_json(9000, seed=42, n_namespaces=50)
+    pg = Page.from_lists(objs, nss)
+    # (every part parses its own copy of a Namespace document: node counts
+    # depend on the thread count, the same in both layouts)
+    for t in (1, 3, 8):
+        assert drv.debug_flatten(pg, t)[:2] == drv.debug_flatten(pg, -t)[:2]
+    assert len({drv.debug_flatten(pg, -t)[0] for t in (1, 2, 8)}) == 1
+    objs, nss = W.gen_config4_json(6000, seed=99)
+    pg = Page.from_lists(objs, nss)
+    assert drv.debug_flatten(pg, 2)[:2] == drv.debug_flatten(pg, -2)[:2]
+
+
+def test_path_layout_evaluates_like_the_document_layout(monkeypatch):
+    """The engine's programs on the host runtime (oracle/cpuvm.cc) give the same
+    violations and message bytes over a batch staged in the path-grouped layout
+    as over the same batch staged per document (GKGPU_PATH_LAYOUT=0)."""
+    from oracle import cpu_baseline
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    ts, cs = W.config2()
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    objs, nss = W.gen_pods_json(12000, seed=5, n_namespaces=40)
+    pg = Page.from_lists(objs, nss)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GKGPU_PATH_LAYOUT", mode)
+        b = d.stage_page(pg)
+        out[mode] = cpu_baseline.sweep(d, b, threads=4)[1:]
+        b.free()
+    assert out["0"] == out["1"]
+    assert out["1"][1] > 10000 and out["1"][3] == 0
+
+
 def test_flatten_mixed_kinds_cluster_scoped_and_escapes(drv):
     objs, nss = W.gen_config4_json(6000, seed=1234)
     objs.append('{"apiVersion":"v1","kind":"ConfigMap","metadata":{"name":"esc\\u00e9\\n\\"q\\"","namespace":"c4-ns-0001"},'

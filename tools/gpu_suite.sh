@@ -2,7 +2,7 @@
 # GPU check: selected "first" tests (verbose, allowed to fail: their log is kept),
 # then the whole -m gpu suite without them, then optionally the profile sequence
 # of profiles/run_profile.sh.
-#   bash tools/gpu_suite.sh <tag> <profile-tag|-> [first test node ids...]
+#   bash tools/gpu_suite.sh <tag> <profile-tag|bench|-> [first test node ids...]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; PROF=$2; shift 2
@@ -24,4 +24,7 @@ rc=$?
 tail -3 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ]; then echo PYTEST_FAIL $rc; grep -E "FAILED|Error" "$OUT/pytest_gpu.log" | head -20; exit 1; fi
 echo PYTEST_OK
-if [ "$PROF" != "-" ]; then bash profiles/run_profile.sh "$PROF"; fi
+if [ "$PROF" = "bench" ]; then
+  timeout -k 10 400 python -u bench.py --steps 10 --warmup 2 --cpu-sample 200000 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo BENCH_FAIL; tail "$OUT/bench.err"; exit 1; }
+  echo BENCH_OK
+elif [ "$PROF" != "-" ]; then bash profiles/run_profile.sh "$PROF"; fi
