@@ -64,10 +64,22 @@ def _configs():
               "config3: 10 allowedRegex label/annotation constraints over Deployments + Services (BASELINE configs[2])"),
         "4": (W.config4, lambda n, start: W.gen_config4_json(n, seed=1234, start=start), 1_250_000,
               "config4: mixed kinds x 50 randomized constraints, 1.25M resources per GPU = 10M over 8 (BASELINE configs[3])"),
+        "6": (W.config6, lambda n, start: W.gen_config6_json(n, start=start), 20_000,
+              "config6: config 2's agilebank policies + demo/basic unique-label over synced Services and labelled "
+              "Deployments, the same objects in data.inventory (the joins of VERDICT r02 next #6)"),
     }
 
 
-CONFIGS = ("2", "3", "4", "5")
+def _inventory(config, gen, n):
+    """config 6: the objects the audit reviews are also the synced inventory"""
+    if config != "6":
+        return []
+    from gkgpu import workloads as W
+    objs, _ = gen(n, 0)
+    return W.inventory_paths(objs)
+
+
+CONFIGS = ("2", "3", "4", "5", "6")
 
 
 def spawn(args):
@@ -127,6 +139,8 @@ def main():
         cl.add_template(t)
     for c in constraints:
         cl.add_constraint(c)
+    for path, obj in _inventory(args.config, cfg_gen, args.pods * world):
+        drv.put_data(path, obj)
     n_cons = len(constraints)
     kinds = [t["spec"]["crd"]["spec"]["names"]["kind"] for t in templates]
     kinds_of = {}  # kernel name -> template kind

@@ -72,6 +72,7 @@ enum Tag : uint32_t {
   V_LIST = 9,                                      // LIST: heap list (set/array/object); kind in bits 56..59
   V_SLICE = 10,                                    // SLICE: string id:32 | start:14 | len:14
   V_FMT = 11,                                      // FMT: deferred sprintf (template kernels only): fidx:24 <<32 | args (bit31: node, else heap list offset)
+  V_GSTR = 12,                                     // GSTR: string in the evaluation's memo-string arena (off:40 << 20 | len:20)
 };
 enum ListKind : uint32_t { LK_SET = 1, LK_ARR = 2, LK_OBJ = 3 };
 
@@ -233,6 +234,7 @@ struct SampleRec {
 static_assert(sizeof(SampleRec) == 276, "SampleRec layout");
 constexpr uint32_t MEMO_SLOTS = 16;  // memoized function call sites per template (per lane)
 constexpr uint32_t GMEMO_ENTRIES = 1u << 15;  // cross-lane memo table of a template launch (32 B entries)
+constexpr uint64_t MSTR_BYTES = 16ull << 20;  // memo-string arena of an evaluation (V_GSTR)
 
 // ------------------------------------------------------------------ launch
 // Kernel arguments of one audit launch (passed by value; shared by the bytecode
@@ -272,6 +274,11 @@ struct DevArgs {
   unsigned long long* prof;   // optional: per constraint [sum steps, max lane steps, lanes run, sum wave-max steps]
   uint64_t* gmemo;            // template kernels: cross-lane memo of pure function calls (4 words per entry)
   uint32_t gmemo_mask;        // entries - 1 (power of two)
+  uint32_t nperm;             // node ids below this are the permanent region (constraints, inventory):
+                              // memo keys (devrt.h gm_key)
+  char* mstr;                 // memo-string arena of the evaluation (V_GSTR bytes; null: off)
+  unsigned long long* mstr_top;  // its bump cursor (bytes used)
+  uint64_t mstr_cap;
   uint64_t* frec;             // per output tuple, a deferred message's argument words, structure
                               // of arrays: word j of tuple i at frec[j * out_cap + i]
   char* ebytes;               // bytes that existed at emission (eager messages, details JSON)

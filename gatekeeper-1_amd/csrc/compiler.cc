@@ -33,6 +33,13 @@ constexpr uint16_t NOREG = 0xffff;
 
 struct Env {
   std::map<std::string, int> vars;
+  // lazy arrays (Comp::lazy_def): a local bound to array comprehensions (in
+  // order) that is never materialized; its element iterations run them
+  struct LazyPart {
+    TermP compr;
+    std::vector<std::string> locals;  // names its body binds (unbound at the definition)
+  };
+  std::map<std::string, std::vector<LazyPart>> lazy;
   Env* parent = nullptr;
   const Module* mod = nullptr;
   int lookup(const std::string& v) const {
@@ -41,6 +48,14 @@ struct Env {
       if (it != e->vars.end()) return it->second;
     }
     return -1;
+  }
+  const std::vector<LazyPart>* lazy_lookup(const std::string& v) const {
+    for (const Env* e = this; e; e = e->parent) {
+      if (e->vars.count(v)) return nullptr;
+      auto it = e->lazy.find(v);
+      if (it != e->lazy.end()) return &it->second;
+    }
+    return nullptr;
   }
 };
 
@@ -377,6 +392,7 @@ class Comp {
 
   // ---------------------------------------------------------------- bodies
   void body_k(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    if (i < body.size() && lazy_def(body, i, env)) { body_k(body, i + 1, env, fail, succ); return; }
     if (guard_) { guarded_body_k(body, i, env, fail, succ); return; }
     if (i == body.size()) { succ(fail); return; }
     expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
@@ -413,6 +429,181 @@ class Comp {
       if (prog_.fallback_reason.empty()) prog_.fallback_reason = ex.what();
       ++prog_.fallback_sites;
       emit(OP_FAIL_FALLBACK, 0, 0, 0, 0, FB_TEMPLATE);
+    }
+  }
+
+  // ---------------------------------------------------------------- lazy arrays
+  // An array comprehension bound to a local that the rest of the body only
+  // iterates -- `x[_]`, directly or through array.concat / aliases -- is not
+  // materialized: each iteration runs the comprehension's body as a generator
+  // (in order, so elements come in array order, duplicates kept).  This is
+  // how demo/basic's K8sUniqueLabel scans data.inventory
+  // (k8suniquelabel_template.yaml:49-52: cluster_objs / ns_objs /
+  // array.concat / all_objs[_]) without holding the whole inventory in the
+  // lane heap.  The comprehension is pure, so evaluating it at its use (with
+  // the definition's bindings, which stay bound) gives the same elements.
+  static bool is_wild(const TermP& t) { return t && t->k == T_VAR && t->s.rfind("$_", 0) == 0; }
+  static bool is_var(const TermP& t, const std::string& x) { return t && t->k == T_VAR && t->s == x; }
+  static bool concat_call(const ExprP& e) {
+    if (e->kind != Expr::TERM || e->negated || !e->withs.empty()) return false;
+    const TermP& t = e->terms[0];
+    return t->k == T_CALL && t->op == std::vector<std::string>{"array", "concat"} && t->items.size() == 3 &&
+           t->items[0]->k == T_VAR && t->items[1]->k == T_VAR && t->items[2]->k == T_VAR;
+  }
+  static bool alias_expr(const ExprP& e, std::string* dst, std::string* src) {
+    if ((e->kind != Expr::ASSIGN && e->kind != Expr::UNIFY) || e->negated || !e->withs.empty() || e->terms.size() != 2)
+      return false;
+    if (e->terms[0]->k != T_VAR || e->terms[1]->k != T_VAR) return false;
+    *dst = e->terms[0]->s;
+    *src = e->terms[1]->s;
+    return true;
+  }
+  // every occurrence of x inside t is `x[<wildcard>]...`
+  static bool lazy_term_ok(const TermP& t, const std::string& x) {
+    if (!t) return true;
+    switch (t->k) {
+      case T_SCALAR: return true;
+      case T_VAR: return t->s != x;
+      case T_REF:
+        if (is_var(t->head, x)) {
+          if (t->items.empty() || !is_wild(t->items[0])) return false;
+        } else if (!lazy_term_ok(t->head, x)) {
+          return false;
+        }
+        for (auto& i : t->items) if (!lazy_term_ok(i, x)) return false;
+        return true;
+      case T_ARRCOMPR: case T_SETCOMPR: case T_OBJCOMPR:
+        if (!lazy_term_ok(t->key, x) || !lazy_term_ok(t->value, x)) return false;
+        for (auto& e : t->body) if (!lazy_expr_ok(e, x)) return false;
+        return true;
+      default:
+        for (auto& i : t->items) if (!lazy_term_ok(i, x)) return false;
+        return true;
+    }
+  }
+  static bool lazy_expr_ok(const ExprP& e, const std::string& x) {
+    for (auto& t : e->terms) if (!lazy_term_ok(t, x)) return false;
+    for (auto& w : e->withs) if (!lazy_term_ok(w.target, x) || !lazy_term_ok(w.value, x)) return false;
+    return true;
+  }
+  // x (defined by body[i]) may stay lazy: every later use iterates it, or
+  // feeds an array.concat / alias whose result may stay lazy
+  bool lazy_ok(const std::vector<ExprP>& body, size_t i, const std::string& x, int depth = 0) {
+    if (depth > 8) return false;
+    bool used = false;
+    for (size_t j = i + 1; j < body.size(); ++j) {
+      const ExprP& e = body[j];
+      std::string dst, src;
+      if (concat_call(e) && (is_var(e->terms[0]->items[0], x) || is_var(e->terms[0]->items[1], x))) {
+        if (is_var(e->terms[0]->items[2], x) || !lazy_ok(body, j, e->terms[0]->items[2]->s, depth + 1)) return false;
+        used = true;
+        continue;
+      }
+      if (alias_expr(e, &dst, &src) && src == x) {
+        if (dst == x || !lazy_ok(body, j, dst, depth + 1)) return false;
+        used = true;
+        continue;
+      }
+      if (!lazy_expr_ok(e, x)) return false;
+      used = used || !lazy_term_ok_unused(e, x);
+    }
+    return used;
+  }
+  static bool lazy_term_ok_unused(const ExprP& e, const std::string& x) {
+    // true when x does not occur in e at all (also inside comprehension bodies)
+    struct F {
+      static bool occ(const TermP& t, const std::string& x) {
+        if (!t) return false;
+        if (t->k == T_VAR) return t->s == x;
+        if (occ(t->head, x) || occ(t->key, x) || occ(t->value, x)) return true;
+        for (auto& i : t->items) if (occ(i, x)) return true;
+        for (auto& b : t->body)
+          for (auto& u : b->terms) if (occ(u, x)) return true;
+        return false;
+      }
+    };
+    for (auto& t : e->terms) if (F::occ(t, x)) return false;
+    return true;
+  }
+  bool lazy_def(const std::vector<ExprP>& body, size_t i, Env* env) {
+    if (!lazy_on()) return false;
+    const ExprP& e = body[i];
+    std::string dst, src;
+    if ((e->kind == Expr::ASSIGN || e->kind == Expr::UNIFY) && !e->negated && e->withs.empty() && e->terms.size() == 2 &&
+        e->terms[0]->k == T_VAR && e->terms[1]->k == T_ARRCOMPR && unbound(env, e->terms[0])) {
+      const std::string& x = e->terms[0]->s;
+      if (!lazy_ok(body, i, x)) return false;
+      Env::LazyPart part{e->terms[1], {}};
+      compr_locals(e->terms[1], env, part.locals);
+      env->lazy[x] = {part};
+      return true;
+    }
+    if (concat_call(e)) {
+      const TermP& c = e->terms[0];
+      const auto* a = env->lazy_lookup(c->items[0]->s);
+      const auto* b = env->lazy_lookup(c->items[1]->s);
+      if (!a || !b || !unbound(env, c->items[2]) || !lazy_ok(body, i, c->items[2]->s)) return false;
+      std::vector<Env::LazyPart> l = *a;
+      l.insert(l.end(), b->begin(), b->end());
+      env->lazy[c->items[2]->s] = l;
+      return true;
+    }
+    if (alias_expr(e, &dst, &src)) {
+      const auto* a = env->lazy_lookup(src);
+      if (!a || env->lookup(dst) >= 0 || !lazy_ok(body, i, dst)) return false;
+      env->lazy[dst] = *a;
+      return true;
+    }
+    return false;
+  }
+  static bool lazy_on() {
+    const char* v = getenv("GKGPU_LAZY_ARRAYS");  // A/B switch, default on
+    return !v || atoi(v) != 0;
+  }
+  // names a comprehension's body binds itself (not bound in env)
+  void compr_locals(const TermP& t, Env* env, std::vector<std::string>& out) {
+    std::function<void(const TermP&)> rec = [&](const TermP& u) {
+      if (!u) return;
+      if (u->k == T_VAR) {
+        if (u->s != "input" && u->s != "data" && env->lookup(u->s) < 0 && !is_global(env, u->s)) out.push_back(u->s);
+        return;
+      }
+      rec(u->head);
+      rec(u->key);
+      rec(u->value);
+      for (auto& i : u->items) rec(i);
+      for (auto& b : u->body)
+        for (auto& v : b->terms) rec(v);
+    };
+    for (auto& b : t->body)
+      for (auto& v : b->terms) rec(v);
+    rec(t->key);
+  }
+  // `x[_]...` over a lazy array: each comprehension's solutions in turn
+  void lazy_iter(const std::vector<Env::LazyPart>& list, const TermP& ref, Env* env, int fail, const K& k) {
+    const auto& path = ref->items;
+    NoFuse nf(this);  // array order is observable
+    for (auto& part : list)
+      for (auto& v : part.locals)
+        if (env->lookup(v) >= 0) throw Unsupported("lazy array: comprehension local " + v + " bound at its use");
+    for (size_t c = 0; c < list.size(); ++c) {
+      const TermP& C = list[c].compr;
+      const bool last = c + 1 == list.size();
+      const int Lnext = last ? fail : label();
+      Env inner;
+      inner.parent = env;
+      inner.mod = env->mod;
+      body_k(C->body, 0, &inner, Lnext, [&](int f) {
+        term(C->key, &inner, f, [&](int vr, int f2) {
+          const int idx = loadk(tag_val(V_INT, 0));  // the index wildcard is never read
+          bind(env, path[0]->s, idx);
+          walk(vr, path, 1, env, f2, k);
+          unbind(env, path[0]->s);
+          emit_jmp(OP_JMP, 0, f2);
+        });
+      });
+      if (last) emit_jmp(OP_JMP, 0, fail);
+      else place(Lnext);
     }
   }
 
@@ -630,6 +821,11 @@ class Comp {
     if (head->k != T_VAR) throw Unsupported("ref head");
     int r = env->lookup(head->s);
     if (r >= 0) { walk(r, path, 0, env, fail, k); return; }
+    if (const auto* lz = env->lazy_lookup(head->s)) {
+      if (path.empty() || !is_wild(path[0])) throw Unsupported("lazy array use");
+      lazy_iter(*lz, t, env, fail, k);
+      return;
+    }
     if (head->s == "input") {
       if (path.empty()) throw Unsupported("whole input document");
       const TermP& p0 = path[0];

@@ -120,7 +120,10 @@ __device__ __forceinline__ uint64_t mkhstr(uint32_t off, uint32_t len) { return 
 __device__ __forceinline__ uint64_t mkslice(uint32_t sid, uint32_t st, uint32_t len) {
   return mkv(V_SLICE, ((uint64_t)sid << 28) | ((uint64_t)st << 14) | len);
 }
-__device__ __forceinline__ bool is_strv(uint64_t v) { uint32_t t = vtag(v); return t == V_STR || t == V_HSTR || t == V_SLICE; }
+__device__ __forceinline__ bool is_strv(uint64_t v) {
+  uint32_t t = vtag(v);
+  return t == V_STR || t == V_HSTR || t == V_SLICE || t == V_GSTR;
+}
 __device__ __forceinline__ bool is_numv(uint64_t v) { uint32_t t = vtag(v); return t == V_NUM || t == V_INT || t == V_BFN; }
 
 // GK_LDS_SCALARS (template kernels, jit.cc): the lane's hot scalars (heap and
@@ -333,6 +336,7 @@ __device__ __forceinline__ SView sview(const PLane& L, uint64_t v) {
   uint32_t t = vtag(v);
   if (t == V_STR) { GK_TOUCH_STR((uint32_t)vpay(v)); const StrEnt& s = gk_args.strs[(uint32_t)vpay(v)]; return SView{(const char*)gk_args.pool + s.off, s.len}; }
   if (t == V_HSTR) { uint64_t p = vpay(v); return SView{L.B + (uint32_t)(p >> 16), (uint32_t)(p & 0xffff)}; }
+  if (t == V_GSTR) { uint64_t p = vpay(v); return SView{gk_args.mstr + (p >> 20), (uint32_t)(p & 0xfffff)}; }
   if (t == V_SLICE) {
     uint64_t p = vpay(v);
     GK_TOUCH_STR((uint32_t)(p >> 28));
@@ -477,7 +481,7 @@ __device__ __forceinline__ int tclass(uint64_t v) {
     case V_NULL: return 1;
     case V_BOOL: return 2;
     case V_NUM: case V_INT: case V_BFN: return 3;
-    case V_STR: case V_HSTR: case V_SLICE: return 4;
+    case V_STR: case V_HSTR: case V_SLICE: case V_GSTR: return 4;
     case V_NODE: GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
     case V_LIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
   }
@@ -674,7 +678,7 @@ __device__ __noinline__ uint64_t vget_slow(PLane& L, uint64_t c, uint64_t key) {
         for (uint32_t i = 0; i < n.n; ++i) if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
         return mkv(V_UNDEF, 0);
       }
-      if (kt == V_HSTR || kt == V_SLICE) {
+      if (kt == V_HSTR || kt == V_SLICE || kt == V_GSTR) {
         SView kv = sview(L, key);
         for (uint32_t i = 0; i < n.n; ++i) {
           const StrEnt& s = gk_args.strs[gk_args.nodes[n.first + i].key];
@@ -925,7 +929,7 @@ template <class O> __device__ int put_scalar(PLane& L, O& o, uint64_t v, bool js
     case V_NUM: put_sid(o, gk_args.nums[(uint32_t)vpay(v)].text); return 1;
     case V_INT: put_intv(o, v); return 1;
     case V_BFN: return -1;
-    case V_STR: case V_HSTR: case V_SLICE:
+    case V_STR: case V_HSTR: case V_SLICE: case V_GSTR:
       return (json ? put_json_str(o, sview(L, v)) : put_quoted(o, sview(L, v))) ? 1 : -1;
     case V_FMT: return -1;  // forced before any printing (jit.cc)
     default: return 0;
@@ -996,7 +1000,7 @@ template <class O> __device__ __forceinline__ bool put_json(PLane& L, O& o, uint
 // Go fmt conversion of one sprintf argument (topdown/strings.go:355-367)
 template <class O> __device__ bool put_fmt_arg(PLane& L, O& o, uint64_t v, uint32_t verb) {
   uint32_t t = vtag(v);
-  if (t == V_STR || t == V_HSTR || t == V_SLICE) {
+  if (t == V_STR || t == V_HSTR || t == V_SLICE || t == V_GSTR) {
     SView s = sview(L, v);
     if (verb == 'd') { put_cstr(o, "%!d(string="); puts_(o, s.p, s.n); put(o, ')'); return true; }
     puts_(o, s.p, s.n);
@@ -1456,6 +1460,7 @@ __device__ GK_HOT uint64_t bi_substring(PLane& L, uint64_t a0, uint64_t a1, uint
   uint32_t len = end - (uint32_t)st;
   if (vtag(a0) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a0), (uint32_t)st, len);
   if (vtag(a0) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + (uint32_t)st, len);
+  if (vtag(a0) == V_GSTR) return mkv(V_GSTR, (((vpay(a0) >> 20) + (uint64_t)st) << 20) | len);
   if (vtag(a0) == V_SLICE) {
     uint64_t p = vpay(a0);
     return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + (uint32_t)st, len);
@@ -1471,6 +1476,7 @@ __device__ uint64_t str_sub(PLane& L, uint64_t a0, SView s, uint32_t st, uint32_
   if (len == 0) return mkv(V_STR, 0);
   if (vtag(a0) == V_STR && s.n < 0x3fff) return mkslice((uint32_t)vpay(a0), st, len);
   if (vtag(a0) == V_HSTR) return mkhstr((uint32_t)(s.p - L.B) + st, len);
+  if (vtag(a0) == V_GSTR) return mkv(V_GSTR, (((vpay(a0) >> 20) + (uint64_t)st) << 20) | len);
   if (vtag(a0) == V_SLICE) {
     uint64_t p = vpay(a0);
     return mkslice((uint32_t)(p >> 28), (uint32_t)((p >> 14) & 0x3fff) + st, len);
@@ -1991,9 +1997,31 @@ __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t
   return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull));
 }
 __device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
-// keys are scalars: a document node is met by one lane only and would just
-// evict shared entries
-__device__ __forceinline__ bool gm_key(uint64_t v) { return vtag(v) != V_NODE && memo_stable(v); }
+// keys are scalars and permanent nodes (constraint parameters, data.inventory
+// objects: every lane of the launch meets the same ones, e.g. the Services a
+// unique-selector join scans); a review document's node is met by one lane
+// only and would just evict shared entries
+__device__ __forceinline__ bool gm_key(uint64_t v) {
+  return vtag(v) == V_NODE ? (uint32_t)vpay(v) < gk_args.nperm : memo_stable(v);
+}
+// a memo value: heap-free as it is, or a lane-buffer string copied into the
+// evaluation's memo-string arena (V_GSTR); 0 = not memoizable.  Each string
+// gets cache lines of its own (128-B aligned), written and fenced before the
+// memo entry that names it is stored: a reader on another CU learns the
+// offset only from that entry, so its L1 cannot hold an older copy of the
+// line (offsets are never reused within an evaluation; L1 is invalidated at
+// every launch).
+__device__ __noinline__ uint64_t gm_value_slow(const PLane& L, uint64_t v) {
+  if (vtag(v) != V_HSTR || !gk_args.mstr) return 0;
+  const SView s = sview(L, v);
+  if (s.n > 0xfffff) return 0;
+  const unsigned long long need = ((unsigned long long)s.n + 127) & ~127ull;
+  const unsigned long long at = atomicAdd(gk_args.mstr_top, need ? need : 128ull);
+  if (at + s.n > gk_args.mstr_cap) return 0;
+  for (uint32_t i = 0; i < s.n; ++i) gk_args.mstr[at + i] = s.p[i];
+  __threadfence();
+  return mkv(V_GSTR, ((uint64_t)at << 20) | s.n);
+}
 
 __device__ __forceinline__ bool gm_get(uint32_t site, uint64_t k0, uint64_t k1, uint64_t& out) {
   if (!gk_args.gmemo || !gm_key(k0) || !gm_key(k1)) return false;
@@ -2009,7 +2037,8 @@ __device__ __forceinline__ bool gm_get(uint32_t site, uint64_t k0, uint64_t k1, 
 }
 
 __device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k0, uint64_t k1, uint64_t v) {
-  if (L.fail || !gk_args.gmemo || !gm_key(k0) || !gm_key(k1) || !memo_stable(v)) return;
+  if (L.fail || !gk_args.gmemo || !gm_key(k0) || !gm_key(k1)) return;
+  if (!memo_stable(v) && (v = gm_value_slow(L, v)) == 0) return;
   uint64_t h = gm_hash(site, k0, k1);
   uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
   if (gk_args.gmemo[4 * i + 3] != 0) i ^= 1;

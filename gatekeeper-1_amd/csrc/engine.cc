@@ -220,6 +220,7 @@ struct EvalCtx {
   std::mutex busy;  // held by the evaluation using it (and by a raw-output copy of its results)
   hipStream_t stream = nullptr;
   std::vector<hipEvent_t> events;
+  DBuf d_mstr, d_mtop;  // memo-string arena + its cursor (V_GSTR)
   DBuf d_nodes, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist, d_gmemo,
       d_frec, d_hist, d_cut, d_ftot, d_cand, d_ncand, d_cerr, d_ebytes, d_lens, d_part;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20, ebytes_cap = 16u << 20, cand_cap = 1 << 14;
@@ -229,7 +230,7 @@ struct EvalCtx {
   NodeArena arena;           // host documents of the current query (node id perm_nodes + k)
   void release_all() {
     for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
-                    &d_clist, &d_gmemo, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
+                    &d_clist, &d_gmemo, &d_mstr, &d_mtop, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
                     &d_part})
       b->free_();
     for (hipEvent_t x : events) hipEventDestroy(x);
@@ -1230,7 +1231,9 @@ static bool ctx_nodes(gk_engine* e, EvalCtx* x, const NodeArena& arena) {
 // when it is the context's own buffer), `nodes` the documents, `tp` the string
 // tables as of this call.  Shared lock held.
 static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, const std::vector<ReviewCol>& cols,
-                              DBuf* revbuf, bool decode, gk_results* res, const void* nodes, uint64_t n_excluded = 0) {
+                              DBuf* revbuf, bool decode, gk_results* res, const void* nodes, uint64_t n_excluded = 0,
+                              uint32_t nperm = NO_ID) {
+  if (nperm == NO_ID) nperm = e->perm_nodes;  // a query's documents follow the engine's permanent region
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
   res->nrev = nrev;
@@ -1314,6 +1317,15 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     if (hist) hipMemsetAsync(x->d_pchist.p, 0, ncode * 4, x->stream);
     a.pchist = hist ? (unsigned int*)x->d_pchist.p : nullptr;
     a.nodes = (const Node*)nodes;
+    a.nperm = nperm;
+    // memo-string arena (devrt.h gm_value_slow): one per evaluation, read by
+    // the format pass after every template launch
+    if (env_mode("GKGPU_GMEMO", 1, 1) != 0 && x->d_mstr.reserve(MSTR_BYTES) && x->d_mtop.reserve(8)) {
+      hipMemsetAsync(x->d_mtop.p, 0, 8, x->stream);
+      a.mstr = (char*)x->d_mstr.p;
+      a.mstr_top = (unsigned long long*)x->d_mtop.p;
+      a.mstr_cap = MSTR_BYTES;
+    }
     a.strs = tp.strs;
     a.pool = tp.pool;
     a.sflags = tp.sflags;
@@ -2240,7 +2252,8 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   TablePtrs tp;
   if (!ctx_device(e, lease.x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto res = std::make_unique<gk_results>();
-  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, decode != 0, res.get(), b->d_nodes.p, b->excluded);
+  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, decode != 0, res.get(), b->d_nodes.p, b->excluded,
+                          b->node_begin);
   if (rc != GK_OK) return rc;
   *out = res.release();
   return GK_OK;
@@ -2264,7 +2277,7 @@ int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** 
   if (!ctx_device(e, x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto resp = std::make_unique<gk_results>();
   gk_results* res = resp.get();
-  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded);
+  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded, b->node_begin);
   if (rc != GK_OK) return rc;
   res->audited = true;
   const uint32_t ncons = (uint32_t)e->corder.size(), nrev = b->nrev;

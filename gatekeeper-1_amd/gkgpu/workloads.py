@@ -646,6 +646,51 @@ def gen_config3_json(n, seed=7, start=0, n_namespaces=200):
     return objs, nss
 
 
+# -- config 6 (VERDICT r02 "next" #6): config 2 with its data.inventory joins
+# exercised -- Services and labelled Deployments synced into the inventory and
+# reviewed by the audit, unique-service-selector (agilebank) and a
+# unique-label constraint (demo/basic) over them
+def config6():
+    templates, constraints = config2()
+    templates = templates + [UNIQUE_LABEL]
+    constraints = constraints + [constraint(
+        "K8sUniqueLabel", "deployment-app-label-unique",
+        match={"kinds": [{"apiGroups": ["apps"], "kinds": ["Deployment"]}]}, parameters={"label": "app"})]
+    return templates, constraints
+
+
+def gen_config6_json(n, seed=11, start=0, n_namespaces=100, n_selectors=None):
+    """n objects, half Services (spec.selector {app, tier?}) and half
+    Deployments (metadata.labels.app), over n_namespaces namespaces; selector
+    and label values repeat (n_selectors distinct, default n // 4), so the
+    joins find duplicates.  JSON text, with each object's Namespace."""
+    k = n_selectors or max(1, n // 4)
+    names = ["j-ns-%03d" % i for i in range(n_namespaces)]
+    ns_json = {nm: dumps(namespace_obj(nm)) for nm in names}
+    r = random.Random(seed * 7919 + start)
+    rb = r.getrandbits
+    objs, nss = [], []
+    for i in range(start, start + n):
+        ns = names[rb(16) % len(names)]
+        app = "app-%d" % (rb(30) % k)
+        if i % 2 == 0:
+            sel = '{"app":"%s"}' % app if rb(2) else '{"app":"%s","tier":"%s"}' % (app, ("web", "db")[rb(1)])
+            objs.append('{"apiVersion":"v1","kind":"Service","metadata":{"name":"svc-%08d","namespace":"%s"},'
+                        '"spec":{"selector":%s,"ports":[{"port":80}]}}' % (i, ns, sel))
+        else:
+            objs.append('{"apiVersion":"apps/v1","kind":"Deployment","metadata":{"name":"dep-%08d","namespace":"%s",'
+                        '"labels":{"app":"%s"}},"spec":{"replicas":1}}' % (i, ns, app))
+        nss.append(ns_json[ns])
+    return objs, nss
+
+
+def inventory_paths(objs_json):
+    """(data path, object JSON) of synced objects (client.data_path:
+    K8sValidationTarget.ProcessData, pkg/target/target.go:62-76)"""
+    from .client import data_path
+    return [(data_path(json.loads(js)), js) for js in objs_json]
+
+
 # -- config 4: 50 constraints cloned from the subset templates, randomized match
 _C4_KINDS = [("", "Pod"), ("apps", "Deployment"), ("", "Service"), ("", "ConfigMap"), ("", "Namespace")]
 

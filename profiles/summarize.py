@@ -51,7 +51,8 @@ def traffic(d, bench):
     for k in fetch:
         if k.endswith("gk_format_kernel"):
             kt[k] = "gk_format_kernel"
-    out = {"pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
+    cfg = bench["config"].get("workload", "config2").split(":")[0].replace("config", "") or "2"
+    out = {"config": cfg, "pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
            "note": "FETCH_SIZE x2 (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE, median per dispatch",
            "hbm_bytes_per_launch": {}, "fetch_bytes_x2": {}, "write_bytes": {}}
     for k, kind in kt.items():
@@ -73,15 +74,19 @@ def main():
     bench = bench_line(os.path.join(d, "bench.json"))
     tb = bench_line(os.path.join(d, "bench_trace.json"))
     kt = bench["config"]["kernel_templates"]
-    hdr = ("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0\n"
-           "# (config2, %d pods, %d constraints); bench HIP-event avg of the dominant kernel %s: %.3f ms\n"
-           % (tb["config"]["resources_per_gpu"], tb["config"]["constraints"], tb["roofline"]["kernel"],
-              tb["roofline"]["kernel_ms_avg"]))
+    cfg = bench["config"].get("workload", "config2").split(":")[0]
+    hdr = ("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0%s\n"
+           "# (%s, %d resources, %d constraints); bench HIP-event avg of the dominant kernel %s: %.3f ms\n"
+           % ("" if cfg == "config2" else " --config " + cfg[6:], cfg, tb["config"]["resources_per_gpu"],
+              tb["config"]["constraints"], tb["roofline"]["kernel"], tb["roofline"]["kernel_ms_avg"]))
     for k, kind in kt.items():
         hdr += "# %s = %s\n" % (k, kind)
     open(os.path.join(HERE, "%s_kernel_stats.txt" % rnd), "w").write(hdr + txt)
     out = traffic(d, bench)
-    for name in ("%s_traffic.json" % rnd, "traffic_latest.json"):
+    names = ["%s_traffic.json" % rnd]
+    if out["config"] == "2":  # bench.py's default line reads this one
+        names.append("traffic_latest.json")
+    for name in names:
         json.dump(out, open(os.path.join(HERE, name), "w"), indent=1)
     open(os.path.join(HERE, "%s_bench.json" % rnd), "w").write(json.dumps(bench) + "\n")
     print(hdr + txt)

@@ -81,6 +81,11 @@ def test_coalesced_queries_equal_the_oracle():
     d.query(VIOLATION, inputs[0])  # compile the template kernels first
     od = oracle_for(ts, cs)
     want = [collections.Counter(oracle_review(od, rv)) for rv in reviews]
+    # the same inputs as one explicit micro-batch (no coalescer): the reference point
+    d2, _, _ = _driver()
+    batch = engine_rows(d2.query_batch(inputs), len(inputs))
+    bad = [i for i in range(len(inputs)) if collections.Counter(batch[i]) != want[i]]
+    assert not bad, ("query_batch differs from the oracle", bad[:5], collections.Counter(batch[bad[0]]), want[bad[0]])
     out, _ = _race(len(inputs), lambda i: d.query(VIOLATION, inputs[i]))
     for i, res in enumerate(out):
         assert not isinstance(res, Exception), res

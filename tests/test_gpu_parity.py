@@ -183,19 +183,22 @@ def test_unique_service_selector_inventory_changes(monkeypatch, compact):
         assert sizes[-1] <= 2 * sizes[0] + 50000, sizes
 
 
-def test_unique_label_join_on_gpu():
+def test_unique_label_join_on_gpu(monkeypatch):
     """demo/basic's K8sUniqueLabel (data.inventory over both scopes,
     array.concat, negated helper calls) over Namespaces synced as inventory:
-    results equal the oracle's.  The template materialises every inventory
-    object in lane-heap arrays, so beyond a few dozen objects the lanes go to
-    the CPU fallback (FB_HEAP) -- still bit-exact for the rest."""
+    results equal the oracle's.  Its inventory arrays are iterated lazily
+    (compiler.cc lazy arrays), so no lane falls back at any inventory size;
+    with the lazy path switched off (GKGPU_LAZY_ARRAYS=0) the lane heap holds
+    them and beyond a few dozen objects the lanes go to the CPU fallback
+    (FB_HEAP) -- still bit-exact for the rest."""
     import random
     from gkgpu.client import data_path
     ts = [W.UNIQUE_LABEL]
     cs = [W.constraint("K8sUniqueLabel", "ns-gk-label-unique",
                        match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
                        parameters={"label": "gatekeeper"})]
-    for n, want_fb in ((12, False), (60, True)):
+    for n, lazy, want_fb in ((12, "1", False), (60, "1", False), (400, "1", False), (60, "0", True)):
+        monkeypatch.setenv("GKGPU_LAZY_ARRAYS", lazy)
         rng = random.Random(n)
         nss = []
         for i in range(n):

@@ -141,10 +141,9 @@ def test_unique_label_counts_match_oracle():
     cs = [W.constraint("K8sUniqueLabel", "ns-gk-label-unique",
                        match={"kinds": [{"apiGroups": [""], "kinds": ["Namespace"]}]},
                        parameters={"label": "gatekeeper"})]
-    # the template materialises every inventory object in two lane-heap arrays
-    # and their concatenation: small inventories fit the 128-word lane heap
-    # (larger ones go to the CPU fallback, FB_HEAP)
-    nss = _namespaces(12)
+    # the template's inventory arrays and their concatenation are iterated
+    # lazily (compiler.cc lazy arrays): no lane-heap limit on the inventory
+    nss = _namespaces(150)
     extra = [(data_path(o), o) for o in nss]
     d = gkgpu.Driver(host_only=True)
     cl = Client(d)
@@ -161,3 +160,31 @@ def test_unique_label_counts_match_oracle():
     assert flagged == 0
     assert want >= 2
     assert viol == want
+
+
+def test_config6_joins_without_lane_heap_fallback():
+    """bench.py --config 6: agilebank's five constraints
+    plus a unique-label constraint over synced Services and labelled
+    Deployments that are also the reviewed objects.  unique-label's
+    inventory arrays (cluster_objs / ns_objs / all_objs) are iterated lazily
+    (compiler.cc lazy arrays), so no review falls back on the lane heap, and
+    the host runtime's violation count equals the oracle's."""
+    import json
+    ts, cs = W.config6()
+    objs, nss = W.gen_config6_json(160)
+    inv = W.inventory_paths(objs)
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    for p, o in inv:
+        d.put_data(p, o)
+    b = d.stage_objects(objs, nss)
+    _, evals, viol, _, flagged = cpu_baseline.sweep(d, b, threads=2)
+    od = oracle_for(ts, cs, [(p, json.loads(o)) for p, o in inv])
+    want = _oracle_count(od, [json.loads(o) for o in objs], [json.loads(n) for n in nss])
+    assert flagged == 0
+    assert evals == len(objs) * len(cs)
+    assert viol == want and want > 50
