@@ -1993,10 +1993,20 @@ __device__ __forceinline__ uint64_t gm_mix(uint64_t x) {
   x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull; x ^= x >> 27; x *= 0x94d049bb133111ebull; x ^= x >> 31;
   return x;
 }
+// Two 64-bit multiplies for the slot hash and one for the check (the
+// splitmix-style pair per word cost ~150 VALU instructions per probe): the
+// check is a bijection of h ^ v, so any torn or foreign (key, value) pair
+// that differs from the reader's reads as a miss.  A real key is never 0
+// (every tagged value but undefined is non-zero), so empty entries never match.
 __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
-  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull));
+  uint64_t h = (k0 ^ ((uint64_t)(site + 1) << 44)) * 0x9e3779b97f4a7c15ull;
+  h ^= h >> 29;
+  h += k1 * 0xbf58476d1ce4e5b9ull;
+  return h ^ (h >> 32);
 }
-__device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
+__device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) {
+  return (h ^ v) * 0x94d049bb133111ebull + 0x632be59bd9b4e019ull;
+}
 // keys are scalars and permanent nodes (constraint parameters, data.inventory
 // objects: every lane of the launch meets the same ones, e.g. the Services a
 // unique-selector join scans); a review document's node is met by one lane

@@ -227,6 +227,7 @@ struct EvalCtx {
   uint64_t eval_epoch = 0;   // bumps on every evaluation (output buffers reused)
   uint64_t perm_gen = 0;     // engine generation whose permanent nodes d_nodes holds below perm_nodes
   uint32_t perm_nodes = 0;
+  void* perm_buf = nullptr;  // the d_nodes buffer that copy went to
   NodeArena arena;           // host documents of the current query (node id perm_nodes + k)
   void release_all() {
     for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
@@ -303,10 +304,16 @@ struct Coalescer {
   std::condition_variable finished;  // followers: results handed out / a new leader is needed
   std::vector<CoalesceReq*> queue;
   bool collecting = false;
+  uint32_t inflight = 0;             // coalesced launches being evaluated
   uint32_t window_us = 0;            // 0: off (every gk_query launches alone)
   uint32_t max_batch = 256;
   uint64_t batches = 0, requests = 0;
 };
+// Under load a leader keeps collecting past its window while kMaxInflight
+// launches are still being evaluated (the batch grows instead of a second
+// small launch queueing behind them), for at most kWindowCap windows.
+constexpr uint32_t kMaxInflight = 2;
+constexpr uint32_t kWindowCap = 16;
 
 struct gk_engine {
   // drivers.Driver's locking (local.go:62-68, 117, 303-304): evaluations
@@ -1213,11 +1220,14 @@ static bool ctx_device(gk_engine* e, EvalCtx* x) {
 static bool ctx_nodes(gk_engine* e, EvalCtx* x, const NodeArena& arena) {
   const size_t perm = e->perm_nodes;
   if (!x->d_nodes.reserve((perm + arena.size() + 1) * sizeof(Node))) return false;
-  if (x->perm_gen != e->prepared_gen || x->perm_nodes != perm) {
+  // a grown buffer starts empty (DBuf::reserve keeps only uploaded bytes): the
+  // permanent region is copied again into it
+  if (x->perm_gen != e->prepared_gen || x->perm_nodes != perm || x->perm_buf != x->d_nodes.p) {
     if (perm && hipMemcpyAsync(x->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice, x->stream) != hipSuccess)
       return false;
     x->perm_gen = e->prepared_gen;
     x->perm_nodes = (uint32_t)perm;
+    x->perm_buf = x->d_nodes.p;
   }
   if (arena.size() &&
       hipMemcpyAsync((char*)x->d_nodes.p + perm * sizeof(Node), arena.data(), arena.size() * sizeof(Node),
@@ -1317,10 +1327,12 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     if (hist) hipMemsetAsync(x->d_pchist.p, 0, ncode * 4, x->stream);
     a.pchist = hist ? (unsigned int*)x->d_pchist.p : nullptr;
     a.nodes = (const Node*)nodes;
-    a.nperm = nperm;
+    // memo keys on permanent nodes (devrt.h gm_key); GKGPU_MEMO_NODES=0: scalars only (A/B)
+    a.nperm = env_mode("GKGPU_MEMO_NODES", 1, 1) ? nperm : 0;
     // memo-string arena (devrt.h gm_value_slow): one per evaluation, read by
-    // the format pass after every template launch
-    if (env_mode("GKGPU_GMEMO", 1, 1) != 0 && x->d_mstr.reserve(MSTR_BYTES) && x->d_mtop.reserve(8)) {
+    // the format pass after every template launch (GKGPU_MEMO_STRINGS=0: off, A/B)
+    if (env_mode("GKGPU_GMEMO", 1, 1) != 0 && env_mode("GKGPU_MEMO_STRINGS", 1, 1) != 0 &&
+        x->d_mstr.reserve(MSTR_BYTES) && x->d_mtop.reserve(8)) {
       hipMemsetAsync(x->d_mtop.p, 0, 8, x->stream);
       a.mstr = (char*)x->d_mstr.p;
       a.mstr_top = (unsigned long long*)x->d_mtop.p;
@@ -1803,14 +1815,26 @@ static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_resul
       c.finished.wait(lk);
       continue;
     }
-    // lead the next micro-batch: collect for the window (or until full)
+    // lead the next micro-batch: collect for the window (or until full);
+    // past it, keep collecting while kMaxInflight launches are evaluating
     c.collecting = true;
-    const auto deadline = Clock::now() + std::chrono::microseconds(c.window_us);
-    while (c.queue.size() < c.max_batch && c.arrive.wait_until(lk, deadline) != std::cv_status::timeout) {}
+    const auto t0 = Clock::now();
+    const auto deadline = t0 + std::chrono::microseconds(c.window_us);
+    const auto cap = t0 + std::chrono::microseconds((uint64_t)c.window_us * kWindowCap);
+    for (;;) {
+      if (c.queue.size() >= c.max_batch) break;
+      const bool busy = c.inflight >= kMaxInflight;
+      if (c.arrive.wait_until(lk, busy ? cap : deadline) == std::cv_status::timeout) {
+        if (!busy || Clock::now() >= cap) break;
+      } else if (!busy && Clock::now() >= deadline) {
+        break;
+      }
+    }
     const size_t take = std::min<size_t>(c.queue.size(), c.max_batch);
     std::vector<CoalesceReq*> batch(c.queue.begin(), c.queue.begin() + take);
     c.queue.erase(c.queue.begin(), c.queue.begin() + take);
     c.collecting = false;
+    ++c.inflight;
     ++c.batches;
     c.requests += batch.size();
     c.finished.notify_all();  // requests left in the queue elect the next leader
@@ -1829,6 +1853,8 @@ static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_resul
     }
     lk.lock();
     for (auto* q : batch) q->done = true;
+    --c.inflight;
+    c.arrive.notify_all();  // a leader waiting on the in-flight launches
     c.finished.notify_all();
   }
   lk.unlock();

@@ -71,28 +71,54 @@ def test_coalesced_callers_all_get_the_launch_error_without_a_device():
 def test_coalesced_queries_equal_the_oracle():
     """64 concurrent Query(violation) calls with the coalescer on: every result
     set equals the oracle's for that caller's own review, and the calls were
-    served by fewer launches than calls."""
+    served by fewer launches than calls.  Also, as references: the same inputs
+    as one explicit gk_query_batch, sequential coalesced calls (batches of
+    one), and concurrent calls with coalesce_max 1 (concurrent single-review
+    launches)."""
     if not gkgpu.Driver.device_available():
         pytest.fail("no HIP device visible")
-    d, ts, cs = _driver(coalesce_us=5000, coalesce_max=256)
     pods, ns_of, ns_objs = W.gen_pods(64, seed=17, n_namespaces=8)
     reviews = [augmented_review(p, ns_objs[n]) for p, n in zip(pods, ns_of)]
     inputs = [json.dumps({"review": rv}) for rv in reviews]
-    d.query(VIOLATION, inputs[0])  # compile the template kernels first
+    ts, cs = W.config2()
     od = oracle_for(ts, cs)
     want = [collections.Counter(oracle_review(od, rv)) for rv in reviews]
-    # the same inputs as one explicit micro-batch (no coalescer): the reference point
+
+    def check(tag, results):
+        bad = []
+        for i, res in enumerate(results):
+            if isinstance(res, Exception):
+                bad.append((i, repr(res)))
+                continue
+            got = collections.Counter(engine_rows(res, 1)[0]) if all(r.review == 0 for r in res.results) else None
+            if any(res.status) or got != want[i]:
+                bad.append((i, len(res.results), sum(want[i].values()), list(res.status)))
+        return "%s: %d of %d differ %r" % (tag, len(bad), len(results), bad[:4]) if bad else None
+
     d2, _, _ = _driver()
     batch = engine_rows(d2.query_batch(inputs), len(inputs))
-    bad = [i for i in range(len(inputs)) if collections.Counter(batch[i]) != want[i]]
-    assert not bad, ("query_batch differs from the oracle", bad[:5], collections.Counter(batch[bad[0]]), want[bad[0]])
+    errs = []
+    b = [i for i in range(len(inputs)) if collections.Counter(batch[i]) != want[i]]
+    if b:
+        errs.append("query_batch: %d differ %r" % (len(b), b[:4]))
+    d, _, _ = _driver(coalesce_us=5000, coalesce_max=256)
+    errs.append(check("sequential coalesced", [d.query(VIOLATION, x) for x in inputs[:8]]))
+    warm = engine_rows(d.query_batch(inputs), len(inputs))  # the same engine, after the calls above
+    b = [i for i in range(len(inputs)) if collections.Counter(warm[i]) != want[i]]
+    if b:
+        errs.append("query_batch on the coalescing engine: %d differ %r" % (len(b), b[:4]))
+    d1, _, _ = _driver(coalesce_us=5000, coalesce_max=1)
+    out1, _ = _race(len(inputs), lambda i: d1.query(VIOLATION, inputs[i]))
+    errs.append(check("concurrent, max 1", out1))
     out, _ = _race(len(inputs), lambda i: d.query(VIOLATION, inputs[i]))
-    for i, res in enumerate(out):
-        assert not isinstance(res, Exception), res
-        assert not any(res.status), res.status
-        assert all(r.review == 0 for r in res.results)
-        got = collections.Counter(engine_rows(res, 1)[0])
-        assert got == want[i], (i, got, want[i])
     launches, served = d.coalesce_stats()
-    assert served == len(inputs) + 1
+    if any(isinstance(o, Exception) or any(o.status) or collections.Counter(engine_rows(o, 1)[0]) != want[i]
+           for i, o in enumerate(out)):
+        tot_got = sum(len(o.results) for o in out if not isinstance(o, Exception))
+        errs.append("coalesced rows %d vs oracle %d; review 0 got %r" % (
+            tot_got, sum(sum(w.values()) for w in want), sorted(engine_rows(out[0], 1)[0])[:6]))
+    errs.append(check("concurrent coalesced (%d launches for %d calls)" % (launches, served), out))
+    errs = [e for e in errs if e]
+    assert not errs, errs
+    assert served == len(inputs) + 8, (launches, served)
     assert launches < served
