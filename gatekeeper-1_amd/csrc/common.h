@@ -301,6 +301,6 @@ constexpr uint32_t FMT_MAXARGS = 6;
 // message's details (unless VF_DET_OBJ) are at ebytes[msg_off, +det_len)
 constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2;
 // the size / format passes work in tiles of FTILE consecutive tuples
-constexpr uint32_t FTILE = 4096;
+constexpr uint32_t FTILE = 256;  // one block pass: a small output still spreads over many blocks
 
 }  // namespace gk

@@ -1998,6 +1998,15 @@ __device__ __forceinline__ uint64_t gm_mix(uint64_t x) {
 // check is a bijection of h ^ v, so any torn or foreign (key, value) pair
 // that differs from the reader's reads as a miss.  A real key is never 0
 // (every tagged value but undefined is non-zero), so empty entries never match.
+#ifndef GK_GM_HASH_OLD
+#define GK_GM_HASH_OLD 0
+#endif
+#if GK_GM_HASH_OLD  // diagnostics (GKGPU_JIT_PRE="GK_GM_HASH_OLD=1"): the round-2 mixers
+__device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
+  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull));
+}
+__device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
+#else
 __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
   uint64_t h = (k0 ^ ((uint64_t)(site + 1) << 44)) * 0x9e3779b97f4a7c15ull;
   h ^= h >> 29;
@@ -2007,6 +2016,7 @@ __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t
 __device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) {
   return (h ^ v) * 0x94d049bb133111ebull + 0x632be59bd9b4e019ull;
 }
+#endif
 // keys are scalars and permanent nodes (constraint parameters, data.inventory
 // objects: every lane of the launch meets the same ones, e.g. the Services a
 // unique-selector join scans); a review document's node is met by one lane

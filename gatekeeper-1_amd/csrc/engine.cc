@@ -1242,7 +1242,7 @@ static bool ctx_nodes(gk_engine* e, EvalCtx* x, const NodeArena& arena) {
 // tables as of this call.  Shared lock held.
 static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, const std::vector<ReviewCol>& cols,
                               DBuf* revbuf, bool decode, gk_results* res, const void* nodes, uint64_t n_excluded = 0,
-                              uint32_t nperm = NO_ID) {
+                              uint32_t nperm = NO_ID, bool audit = false) {
   if (nperm == NO_ID) nperm = e->perm_nodes;  // a query's documents follow the engine's permanent region
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
@@ -1485,6 +1485,15 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     bool flagged = false;
     for (uint32_t r = 0; r < nrev && !flagged; ++r) flagged = res->status[r] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
     if (!decode && !flagged && !ea_err) { res->ms[3] = ms_since(t1); mark_excluded(); return GK_OK; }
+    if (audit && !ea_err) {
+      // the audit sampling passes recount the totals on the device without the
+      // flagged reviews (gk_sample_*): no tuple download (14M tuples = 450 MB
+      // at config 4) just to recount them here
+      for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
+      res->ms[3] = ms_since(t1);
+      mark_excluded();
+      return GK_OK;
+    }
     std::vector<Viol> vs(counters[0]);
     std::string bytes;
     if (counters[0]) d2h(x, vs.data(), x->d_out.p, counters[0] * sizeof(Viol));
@@ -2303,7 +2312,7 @@ int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** 
   if (!ctx_device(e, x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto resp = std::make_unique<gk_results>();
   gk_results* res = resp.get();
-  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded, b->node_begin);
+  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded, b->node_begin, true);
   if (rc != GK_OK) return rc;
   res->audited = true;
   const uint32_t ncons = (uint32_t)e->corder.size(), nrev = b->nrev;

@@ -165,10 +165,16 @@ __device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint6
 
 __device__ __forceinline__ uint32_t det_bytes(const Viol& v) { return (v.pad & VF_DET_OBJ) ? 2u : v.det_len; }
 
+// The lane the size / format passes hand to the printers.  Deferred arguments
+// are heap-free values, so nothing reads it; a failing print only sets its
+// fail word, which nobody reads either (the print's own result decides).  A
+// module global instead of a local object: a local Lane put ~6 KB of private
+// segment on every lane, and the dispatch paid for it (~1 ms fixed per call).
+__device__ Lane gk_pass_lane;
+
 __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
   __shared__ unsigned long long wsum[4];
-  Lane L0;  // never dereferenced: deferred arguments are heap-free values
-  PLane& L = *(PLane*)&L0;
+  PLane& L = *(PLane*)&gk_pass_lane;
   const uint64_t n = ntuples();
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
@@ -231,7 +237,7 @@ __global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
 
 constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
 
-__global__ void __launch_bounds__(256) gk_format_kernel(DevArgs) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(DevArgs) {
   __shared__ uint32_t stage[4][FSTAGE / 4];
   __shared__ uint32_t wtot[4];
   const uint64_t n = ntuples();
@@ -240,8 +246,7 @@ __global__ void __launch_bounds__(256) gk_format_kernel(DevArgs) {
   if (gk_args.counters[3] > gk_args.bytes_cap || gk_args.counters[0] > gk_args.out_cap ||
       gk_args.counters[1] > gk_args.ebytes_cap)
     return;
-  Lane L0;  // never dereferenced: deferred arguments are heap-free values
-  PLane& L = *(PLane*)&L0;
+  PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* st = stage[wv];
   uint8_t* stb = (uint8_t*)st;

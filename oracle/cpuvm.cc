@@ -55,6 +55,7 @@ template <class T, class U> static inline T atomicAdd(T* p, U v) { T o = *p; *p 
 template <class T, class U> static inline T atomicOr(T* p, U v) { T o = *p; *p = (T)(o | v); return o; }
 template <class T, class U> static inline T atomicMax(T* p, U v) { T o = *p; if ((T)v > o) *p = (T)v; return o; }
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+static inline void __threadfence() {}  // the host build has no memo arena (gk_args.mstr is null)
 struct CpuDim3 { uint32_t x = 0, y = 0, z = 0; };
 static CpuDim3 blockIdx, threadIdx, blockDim{64, 1, 1}, gridDim{1, 1, 1};
 

@@ -1,13 +1,18 @@
 #!/bin/bash
-# GPU diagnostic: bench before and after the GPU test suite in one call.
+# A/B of the template-kernel switches on config 2 at 1M Pods (tools/probe_repeat.py:
+# per-launch kernel ms over 12 sweeps of one staged batch), one process per setting.
+#   bash tools/gpu_ab.sh <tag> "<setting>" ["<setting>" ...]   (setting: "" or "VAR=val VAR2=val")
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-export GKGPU_JIT_CACHE=$PWD/.jitcache
-b() { timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/ab_$1.json 2>gpurun_out/ab_$1.err && python3 -c "
-import json; d=json.load(open('gpurun_out/ab_$1.json')); print('$1', round(d['ms_per_step'],2), [(k['kernel'][-6:], round(k['avg_ms'],2)) for k in d['kernels']])"; }
-b A || exit 1
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-echo PYTEST_OK
-b B || exit 1
-rocm-smi --showclocks --showtemp --showpower 2>&1 | tail -20 > gpurun_out/smi.txt
-b C
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT" gpurun_out/jitcache
+cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
+export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+i=0
+for s in "$@"; do
+  i=$((i+1))
+  echo "== [$i] ${s:-default}" | tee -a "$OUT/ab.log"
+  env $s timeout -k 10 300 python3 -u tools/probe_repeat.py 1000000 >> "$OUT/ab.log" 2>&1 || { echo "AB_FAIL [$i]"; tail -5 "$OUT/ab.log"; exit 1; }
+  grep "step 11" "$OUT/ab.log" | tail -1
+done

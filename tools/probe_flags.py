@@ -27,15 +27,21 @@ b = d.stage_page(Page.from_lists(objs, nss))
 for k in range(3):  # repeated sweeps of one staged batch (bench.py's steps)
     a = b.eval_audit(limit=20)
     print("sweep %d: errors %d fallbacks %d" % (k, a.n_errors, a.n_fallbacks), flush=True)
-r = b.eval(decode=False, light=True, with_status=True)
+import ctypes as C  # noqa: E402
+import json  # noqa: E402
 import numpy as np  # noqa: E402
-st = np.asarray(r.status)
-fl = np.nonzero(st & 3)[0]
-print("config %s n %d flagged %d errors %d fallbacks %d" % (cfg, n, len(fl), r.n_errors, r.n_fallbacks), flush=True)
+lib = d._lib
+out = C.c_void_p()
+d._check(lib.gk_batch_eval(d._e, b._h, 0, C.byref(out)))
+nr = lib.gk_results_reviews(out)
+st = np.zeros(max(nr, 1), dtype=np.uint32)
+rs = np.zeros(max(nr, 1), dtype=np.uint32)
+lib.gk_results_copy_status(out, st.ctypes.data, rs.ctypes.data)
+lib.gk_results_free(out)
+fl = np.nonzero(st[:nr] & 3)[0]
+print("config %s n %d flagged %d (error %d, fallback %d)" % (cfg, n, len(fl), int((st & 1).astype(bool).sum()),
+                                                             int((st & 2).astype(bool).sum())), flush=True)
 if len(fl):
-    res = d.review_objects([objs[i] for i in fl[:200]], [nss[i] for i in fl[:200]])
-    print("reasons", collections.Counter(res.reason), "status", collections.Counter(res.status))
-    import json
-    kinds = collections.Counter(json.loads(objs[i])["kind"] for i in fl)
-    print("kinds", kinds)
-    print("example", objs[fl[0]][:600])
+    print("reasons", collections.Counter(rs[fl].tolist()), "status", collections.Counter(st[fl].tolist()))
+    print("kinds", collections.Counter(json.loads(objs[i])["kind"] for i in fl))
+    print("example", objs[fl[0]][:800])
