@@ -16,3 +16,5 @@ timeout -k 10 300 python -u bench.py --config 5 --steps 500 --warmup 20 --cpu-sa
 python3 -c "import json; d=json.load(open('$OUT/c5_batch.json')); c=d['config']; print('c5', c['latency_ms'], c['kernel_ms_last_launch'])"
 timeout -k 10 300 python3 -u tools/probe_repeat.py 1000000 > "$OUT/repeat.log" 2>&1 || { echo REPEAT_FAIL; tail -3 "$OUT/repeat.log"; exit 1; }
 grep "step 11" "$OUT/repeat.log"
+timeout -k 10 400 python -u bench.py --config 6 --steps 5 --warmup 1 > "$OUT/c6.json" 2> "$OUT/c6.err" || { echo C6_FAIL; tail "$OUT/c6.err"; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/c6.json')); c=d['config']; print('c6', d['value'], d['ms_per_step'], c['fallback_reviews'], c['error_reviews'], [(k['kernel'], round(k['avg_ms'],3)) for k in d['kernels']])"
