@@ -1051,3 +1051,22 @@ def _check_emission_order(t, c, fuse):
         assert got[i] == want, (i, got[i], want)
         multi += len(want) > 1
     assert multi > 100
+
+
+@pytest.mark.gpu
+def test_config6_joins_on_gpu_equal_the_oracle():
+    """bench.py --config 6 at 400 objects: agilebank's five constraints plus
+    demo/basic unique-label over synced Services and labelled Deployments that
+    are also the reviewed objects; every review's results equal the oracle's
+    and no review falls back (lazy inventory arrays, memoized per-object join
+    keys on the device)."""
+    ts, cs = W.config6()
+    objs_js, nss_js = W.gen_config6_json(300)
+    objs = [json.loads(o) for o in objs_js]
+    nss = [json.loads(n) for n in nss_js]
+    extra = [(p, json.loads(o)) for p, o in W.inventory_paths(objs_js)]
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, nss, extra_data=extra)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.fallback == 0 and rep.errors == 0, rep
+    assert rep.violations > 60, rep
