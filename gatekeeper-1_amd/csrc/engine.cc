@@ -2071,7 +2071,15 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
   if (order_by_size) {
     if (!path_layout) review_order(e, cols, fr.weight, 0, cols.size(), perm);
     std::vector<ReviewCol> sorted(cols.size());
-    for (uint32_t i = 0; i < perm.size(); ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
+    const size_t n = perm.size();
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 65536));
+    auto gather = [&](int t) {
+      for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(gather, t);
+    gather(0);
+    for (auto& x : th) x.join();
     cols.swap(sorted);
     if (trace) fprintf(stderr, "flatten: review order %.1f ms\n", ms_since(t_ord));
   }

@@ -350,9 +350,13 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
       p.pcount[path] += x.n;
       const bool obj = x.type == NT_OBJ;
       for (uint32_t c = 0; c < x.n; ++c) {
-        const Node& y = ln[x.first + c];
-        if ((y.type == NT_OBJ || y.type == NT_ARR) && y.n)
-          stack.push_back((uint64_t)(x.first + c) | ((uint64_t)p.paths.child(path, obj ? y.key : kElem) << 32));
+        Node& y = st.nodes()[x.first + c];
+        if ((y.type == NT_OBJ || y.type == NT_ARR) && y.n) {
+          // the child's path, kept in its (unused) value field for the layout
+          // pass (Remap clears it)
+          y.val = p.paths.child(path, obj ? y.key : kElem);
+          stack.push_back((uint64_t)(x.first + c) | ((uint64_t)y.val << 32));
+        }
       }
     }
   };
@@ -410,6 +414,7 @@ struct Remap {
     if (obj_member) y.key = smap[y.key];
     if (y.type == NT_STR) y.val = smap[y.val];
     else if (y.type == NT_NUM) y.val = nmap[y.val];
+    else if (y.type == NT_OBJ || y.type == NT_ARR) y.val = 0;  // the layout's path id (count_paths)
     y.flags &= (uint8_t)~kShared;
     return y;
   }
@@ -586,7 +591,7 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
           if (l == lc.labels) lb = (uint32_t)(start + c);
           if (l == lc.old_labels) old = (uint32_t)(start + c);
           if ((y.type == NT_OBJ || y.type == NT_ARR) && y.n) {
-            stack.push_back((uint64_t)l | ((uint64_t)p.paths.child(path, obj ? y.key : kElem) << 32));
+            stack.push_back((uint64_t)l | ((uint64_t)y.val << 32));  // its path (count_paths)
             stack.push_back(start + c);
           }
         }
