@@ -107,6 +107,13 @@ enum Op : uint16_t {
   OP_MEMO_PUT,     // memo slot y := (R[b], R[c]) -> R[a] when arguments and value are heap-free
   OP_ORD,          // y: emission order key of fused rule bodies (compiler.cc rule_group):
                    //    y < 2^31: key = base + y; else base += y & 0x7fffffff, key = base
+  // inventory joins (compiler.cc join_site, devrt.h op_jprobe): an iteration
+  // over data.inventory leaves whose key equals R[b] through the constraint's
+  // join index, or a jump to the plain scan when there is none
+  OP_JPROBE,       // a(iter base: a=range, a+1=pos), b(probe value), x=scan path, y=loop depth | site << 8
+  OP_JNEXT,        // a(iter base), b(leaf dst), x=exit, y=loop depth : next candidate leaf
+  OP_JVAR,         // a(dst), b(iter base), y=selector : the current leaf's key at path variable y
+  OP_KEYOUT,       // a : key pass (gk_key_kernel) -- the leaf's join key hash
   OP_COUNT_
 };
 
@@ -288,7 +295,23 @@ struct DevArgs {
   uint32_t* lens;             // size pass: output bytes per tuple (message + details)
   unsigned long long* part;   // size pass: per tile of FTILE tuples, its bytes; then the
                               // exclusive prefix over tiles (spine)
+  // inventory join indexes (engine.cc build_joins; null: every join site scans)
+  const uint32_t* jdir;       // per (constraint, site): [hash offset, entries, ready, pad] (JMAX_SITES sites)
+  const uint64_t* jhash;      // key hashes, sorted within each index
+  const uint32_t* jord;       // per hash entry: word offset of its leaf row in jleaf (leaf order within a hash)
+  const uint64_t* jleaf;      // leaf rows: [leaf value, key at each path variable...]
+  // key pass (gk_key_kernel): leaf i = jleaf[jrow0 + i * jstride], key hash -> jkeys[i]
+  uint64_t* jkeys;
+  uint64_t jparams;           // the constraint's parameters value
+  uint32_t jpc, jstride;
+  uint64_t jrow0;
 };
+// join sites per template program (compiler.cc join_site)
+constexpr uint32_t JMAX_SITES = 4;
+// gk_key_kernel results besides a hash (a string key's hash has bit 63 set)
+constexpr uint64_t KH_NONE = 0;       // key undefined or composite: the leaf is in no bucket
+constexpr uint64_t KH_FAIL = 1;       // the key program failed (error / fallback): no index, scan
+constexpr uint64_t KH_NUM = 2, KH_NULL = 3, KH_FALSE = 4, KH_TRUE = 5;
 // A deferred message's sprintf takes at most FMT_MAXARGS arguments (the
 // argument words a tuple carries in frec)
 constexpr uint32_t FMT_MAXARGS = 6;

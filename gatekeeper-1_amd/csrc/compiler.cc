@@ -40,7 +40,19 @@ struct Env {
     std::vector<std::string> locals;  // names its body binds (unbound at the definition)
   };
   std::map<std::string, std::vector<LazyPart>> lazy;
+  // parameter-derived locals (`label := input.parameters.label`): the value as a
+  // term over input.parameters, so a join's key program can recompute it
+  std::map<std::string, TermP> pdef;
   Env* parent = nullptr;
+  const TermP* pdef_lookup(const std::string& v) const {
+    for (const Env* e = this; e; e = e->parent) {
+      if (e->vars.count(v)) {
+        auto it = e->pdef.find(v);
+        return it == e->pdef.end() ? nullptr : &it->second;
+      }
+    }
+    return nullptr;
+  }
   const Module* mod = nullptr;
   int lookup(const std::string& v) const {
     for (const Env* e = this; e; e = e->parent) {
@@ -265,6 +277,7 @@ class Comp {
     for (auto& in : code_) {
       switch (in.op) {
         case OP_JMP: case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT: case OP_MEMO_GET:
+        case OP_JPROBE: case OP_JNEXT:
           if (labels_[in.x] < 0) throw std::runtime_error("unplaced label");
           in.x = prog_.code_off + (uint32_t)labels_[in.x];
           break;
@@ -395,6 +408,8 @@ class Comp {
     if (i < body.size() && lazy_def(body, i, env)) { body_k(body, i + 1, env, fail, succ); return; }
     if (guard_) { guarded_body_k(body, i, env, fail, succ); return; }
     if (i == body.size()) { succ(fail); return; }
+    if (join_site(body, i, env, fail, succ)) return;
+    if (lazy_inline(body, i, env, fail, succ)) return;
     expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
   }
 
@@ -607,6 +622,497 @@ class Comp {
     }
   }
 
+  // ---------------------------------------------------------------- inventory joins
+  // The cross-resource templates (k8suniqueserviceselector_template.yaml:40-44,
+  // k8suniquelabel_template.yaml:49-52) iterate every synced object and keep
+  // the ones whose key equals the review's:
+  //     other := data.inventory.namespace[ns][_][_][name]      (body[i])
+  //     ... other_selector := flatten_selector(other) ...      (the key slice)
+  //     input_selector == other_selector                       (body[j])
+  // A scan is O(inventory) per review.  join_site compiles such an iteration
+  // as a probe of a hash index -- the engine's key pass (kernels.hip
+  // gk_key_kernel) runs the key slice once per leaf and keeps (key hash, leaf)
+  // sorted per constraint -- so each review visits only the leaves in its
+  // key's bucket, in iteration order.  Every body literal after body[i] still
+  // runs for those leaves (the equality included: a hash collision finds
+  // nothing), and the plain scan is compiled beside the probe for lanes without
+  // an index (none built, a key pass that failed, a composite probe value).
+  // The probe skips the literals between body[i] and body[j] for leaves outside
+  // the bucket, so join_site requires those to be error-free (err_free_expr):
+  // skipping an undefined literal changes nothing, skipping an error would.
+  static bool joins_on() {
+    const char* v = getenv("GKGPU_JOINS");  // A/B switch, default on
+    return !v || atoi(v) != 0;
+  }
+  struct JoinPlan {
+    std::string x;                       // the leaf variable
+    std::vector<JoinSite::Sel> path;
+    std::vector<std::string> pvars;      // names of the variable selectors (in order)
+    TermP a;                             // the probe side (a variable bound before body[i], or a constant)
+    TermP key;                           // the key side (a term over x and slice outputs)
+    std::vector<ExprP> slice;            // literals of (i, j) that derive the key
+    std::vector<std::string> params;     // parameter-derived locals the key reads
+  };
+
+  // value of a parameter-derived term as a term over input.parameters
+  TermP param_def(const Env* env, const TermP& t) {
+    if (t->k == T_SCALAR) return t;
+    if (t->k == T_VAR) {
+      if (is_global(env, t->s)) return nullptr;
+      const TermP* d = env->pdef_lookup(t->s);
+      return d ? *d : nullptr;
+    }
+    if (t->k == T_REF && t->head && t->head->k == T_VAR && t->head->s == "input" && env->lookup("input") < 0 &&
+        !t->items.empty() && t->items[0]->k == T_SCALAR && t->items[0]->s == "parameters") {
+      auto c = std::make_shared<Term>(*t);
+      for (auto& it : c->items) {
+        if (it->k == T_SCALAR) continue;
+        TermP d = it->k == T_VAR ? param_def(env, it) : nullptr;
+        if (!d || d->k != T_SCALAR) return nullptr;
+        it = d;
+      }
+      return c;
+    }
+    return nullptr;
+  }
+
+  static void occ_vars(const TermP& t, std::set<std::string>& out) {
+    if (!t) return;
+    if (t->k == T_VAR) { out.insert(t->s); return; }
+    occ_vars(t->head, out);
+    occ_vars(t->key, out);
+    occ_vars(t->value, out);
+    for (auto& i : t->items) occ_vars(i, out);
+    for (auto& b : t->body)
+      for (auto& u : b->terms) occ_vars(u, out);
+  }
+  static std::set<std::string> expr_vars(const ExprP& e) {
+    std::set<std::string> s;
+    for (auto& t : e->terms) occ_vars(t, s);
+    return s;
+  }
+  // variables a literal binds (given the ones bound before it), or false when
+  // it is not a single-valued definition (a generator, a negation, a test)
+  bool defines(const ExprP& e, const std::set<std::string>& bound, const Env* env, std::string* out) {
+    if (e->negated || !e->withs.empty()) return false;
+    auto iter_free = [&](const TermP& t) {
+      // no ref selector is an unbound variable (which would iterate)
+      std::function<bool(const TermP&)> ok = [&](const TermP& u) -> bool {
+        if (!u) return true;
+        if (u->k == T_ARRCOMPR || u->k == T_SETCOMPR || u->k == T_OBJCOMPR) return true;  // collected, not iterated
+        if (u->k == T_REF)
+          for (auto& s : u->items)
+            if (s->k == T_VAR && !bound.count(s->s) && env->lookup(s->s) < 0 && !is_global(env, s->s)) return false;
+        if (!ok(u->head)) return false;
+        for (auto& s : u->items) if (!ok(s)) return false;
+        return true;
+      };
+      return ok(t);
+    };
+    if ((e->kind == Expr::ASSIGN || e->kind == Expr::UNIFY) && e->terms.size() == 2 && e->terms[0]->k == T_VAR &&
+        !bound.count(e->terms[0]->s) && env->lookup(e->terms[0]->s) < 0 && !is_global(env, e->terms[0]->s)) {
+      if (!iter_free(e->terms[1])) return false;
+      *out = e->terms[0]->s;
+      return true;
+    }
+    if (e->kind == Expr::TERM && e->terms[0]->k == T_CALL && !e->terms[0]->items.empty()) {
+      const TermP& o = e->terms[0]->items.back();
+      if (o->k != T_VAR || o->s.rfind("$l", 0) != 0 || bound.count(o->s)) return false;
+      for (size_t q = 0; q + 1 < e->terms[0]->items.size(); ++q) if (!iter_free(e->terms[0]->items[q])) return false;
+      *out = o->s;
+      return true;
+    }
+    return false;
+  }
+
+  // user functions a call resolves to (module-local name or data.<pkg>.<name>)
+  std::vector<std::shared_ptr<Rule>> fn_rules(const Module* mod, const std::vector<std::string>& op) {
+    if (op.size() == 1 && mod) return mods_.rules(mod->pkg, op[0]);
+    if (op.size() >= 2 && op[0] == "data") {
+      std::vector<std::string> pkg(op.begin() + 1, op.end() - 1);
+      return mods_.rules(pkg, op.back());
+    }
+    return {};
+  }
+  // the term never reads `input` (also through the functions it calls)
+  bool input_free(const TermP& t, const Module* mod, int depth) {
+    if (!t) return true;
+    if (t->k == T_VAR) return t->s != "input";
+    if (t->k == T_CALL) {
+      auto rules = fn_rules(mod, t->op);
+      if (!rules.empty()) {
+        if (depth > 6) return false;
+        for (auto& r : rules) {
+          for (auto& e : cbody(r, {}))
+            for (auto& u : e->terms) if (!input_free(u, r->mod, depth + 1)) return false;
+          if (!input_free(r->value, r->mod, depth + 1)) return false;
+        }
+      }
+    }
+    if (!input_free(t->head, mod, depth) || !input_free(t->key, mod, depth) || !input_free(t->value, mod, depth))
+      return false;
+    for (auto& i : t->items) if (!input_free(i, mod, depth)) return false;
+    for (auto& b : t->body)
+      for (auto& u : b->terms) if (!input_free(u, mod, depth)) return false;
+    return true;
+  }
+
+  // ---- error-freedom (conservative): the literal cannot raise an evaluation
+  // error (only succeed or be undefined).  Comparisons and lookups never err;
+  // sprintf over an array literal does not; a user function does not when its
+  // bodies do not and no two of them can yield different values (a single
+  // body, one constant value, or bodies that test one path against the same
+  // constant with == and != -- make_apiversion's shape).
+  bool err_free_term(const TermP& t, const Module* mod, int depth) {
+    if (!t) return true;
+    switch (t->k) {
+      case T_SCALAR: case T_VAR: return true;
+      case T_REF:
+        if (!t->head || t->head->k != T_VAR) return false;
+        if (mod && t->head->s != "input" && t->head->s != "data" && !mods_.rules(mod->pkg, t->head->s).empty()) return false;
+        if (t->head->s == "data" && (t->items.empty() || t->items[0]->k != T_SCALAR || t->items[0]->s != "inventory")) return false;
+        for (auto& i : t->items) if (!err_free_term(i, mod, depth)) return false;
+        return true;
+      case T_ARRAY: case T_SET:
+        for (auto& i : t->items) if (!err_free_term(i, mod, depth)) return false;
+        return true;
+      case T_OBJECT:
+        for (size_t q = 0; q < t->items.size(); q += 2)
+          if (t->items[q]->k != T_SCALAR || !err_free_term(t->items[q + 1], mod, depth)) return false;
+        return true;
+      case T_CALL: return err_free_call(t, mod, depth);
+      default: return false;
+    }
+  }
+  bool err_free_call(const TermP& t, const Module* mod, int depth) {
+    static const std::set<std::string> cmp = {"equal", "neq", "lt", "lte", "gt", "gte"};
+    size_t nargs = t->items.size();
+    if (!t->items.empty() && t->items.back()->k == T_VAR && t->items.back()->s.rfind("$l", 0) == 0) --nargs;
+    for (size_t q = 0; q < nargs; ++q) if (!err_free_term(t->items[q], mod, depth)) return false;
+    if (t->op.size() == 1 && cmp.count(t->op[0])) return true;
+    if (t->op == std::vector<std::string>{"sprintf"})
+      return nargs == 2 && t->items[0]->k == T_SCALAR && t->items[0]->stype == S_STR && t->items[1]->k == T_ARRAY;
+    auto rules = fn_rules(mod, t->op);
+    if (rules.empty() || depth > 6) return false;
+    return fn_err_free(rules, depth + 1);
+  }
+  bool err_free_expr(const ExprP& e, const Module* mod, int depth) {
+    if (!e->withs.empty()) return false;
+    if (e->kind == Expr::SOME) return true;
+    for (auto& t : e->terms) if (!err_free_term(t, mod, depth)) return false;
+    return true;
+  }
+  bool fn_err_free(const std::vector<std::shared_ptr<Rule>>& rules, int depth) {
+    for (auto& r : rules) {
+      if (r->kind != Rule::FUNC || r->is_else || r->is_default) return false;
+      for (auto& e : cbody(r, {})) if (!err_free_expr(e, r->mod, depth)) return false;
+      if (!err_free_term(r->value, r->mod, depth)) return false;
+    }
+    if (rules.size() == 1) return true;
+    bool same_const = true;
+    for (auto& r : rules) same_const = same_const && r->value && is_const(r->value) && same_term(r->value, rules[0]->value);
+    if (same_const) return true;
+    for (size_t p = 0; p < rules.size(); ++p)
+      for (size_t q = p + 1; q < rules.size(); ++q)
+        if (!exclusive(rules[p], rules[q])) return false;
+    return true;
+  }
+  // canonical text of a body-local term: function arguments by position,
+  // single-assignment locals by their definition, constant-key refs
+  bool canon(const TermP& t, const std::shared_ptr<Rule>& r, const std::vector<ExprP>& body, int depth, std::string* out) {
+    if (depth > 8) return false;
+    if (t->k == T_SCALAR) { *out = std::to_string(t->stype) + ":" + t->s; return true; }
+    if (t->k == T_VAR) {
+      for (size_t a = 0; a < r->args.size(); ++a)
+        if (r->args[a]->k == T_VAR && r->args[a]->s == t->s) { *out = "$arg" + std::to_string(a); return true; }
+      for (auto& e : body)
+        if ((e->kind == Expr::ASSIGN || e->kind == Expr::UNIFY) && !e->negated && e->terms.size() == 2 &&
+            e->terms[0]->k == T_VAR && e->terms[0]->s == t->s)
+          return canon(e->terms[1], r, body, depth + 1, out);
+      return false;
+    }
+    if (t->k == T_REF && t->head && t->head->k == T_VAR) {
+      std::string h;
+      if (!canon(t->head, r, body, depth + 1, &h)) return false;
+      for (auto& i : t->items) {
+        if (i->k != T_SCALAR) return false;
+        h += "[" + std::to_string(i->stype) + ":" + i->s + "]";
+      }
+      *out = h;
+      return true;
+    }
+    return false;
+  }
+  bool exclusive(const std::shared_ptr<Rule>& r1, const std::shared_ptr<Rule>& r2) {
+    struct Test { std::string path, c; bool eq; };
+    auto tests = [&](const std::shared_ptr<Rule>& r) {
+      std::vector<Test> out;
+      const auto& body = cbody(r, {});
+      for (auto& e : body) {
+        if (e->negated || e->kind != Expr::TERM || e->terms[0]->k != T_CALL) continue;
+        const TermP& c = e->terms[0];
+        if (c->op.size() != 1 || (c->op[0] != "equal" && c->op[0] != "neq") || c->items.size() != 2) continue;
+        const TermP *p = &c->items[0], *k = &c->items[1];
+        if ((*p)->k == T_SCALAR) std::swap(p, k);
+        if ((*k)->k != T_SCALAR) continue;
+        std::string ps;
+        if (!canon(*p, r, body, 0, &ps)) continue;
+        out.push_back({ps, std::to_string((*k)->stype) + ":" + (*k)->s, c->op[0] == "equal"});
+      }
+      return out;
+    };
+    for (auto& a : tests(r1))
+      for (auto& b : tests(r2))
+        if (a.path == b.path && a.c == b.c && a.eq != b.eq) return true;
+    return false;
+  }
+
+  bool plan_join(const std::vector<ExprP>& body, size_t i, Env* env, JoinPlan& P) {
+    const ExprP& e = body[i];
+    if ((e->kind != Expr::ASSIGN && e->kind != Expr::UNIFY) || e->negated || !e->withs.empty() || e->terms.size() != 2)
+      return false;
+    const TermP& xv = e->terms[0];
+    const TermP& ref = e->terms[1];
+    if (xv->k != T_VAR || !unbound(env, xv) || env->lazy_lookup(xv->s)) return false;
+    if (ref->k != T_REF || !ref->head || ref->head->k != T_VAR || ref->head->s != "data" || env->lookup("data") >= 0)
+      return false;
+    if (ref->items.empty() || ref->items[0]->k != T_SCALAR || ref->items[0]->s != "inventory") return false;
+    if (bank_.inventory_node == 0xffffffffu) return false;
+    P = JoinPlan{};
+    P.x = xv->s;
+    std::set<std::string> bound;  // bound by body[i..j)
+    bound.insert(P.x);
+    for (size_t q = 1; q < ref->items.size(); ++q) {
+      const TermP& s = ref->items[q];
+      JoinSite::Sel sel;
+      if (s->k == T_SCALAR && s->stype == S_STR) {
+        sel.sid = st_.intern(s->s);
+      } else if (s->k == T_VAR && unbound(env, s) && !bound.count(s->s)) {
+        sel.var = true;
+        P.pvars.push_back(s->s);
+        bound.insert(s->s);
+      } else {
+        return false;
+      }
+      P.path.push_back(sel);
+    }
+    if (P.pvars.empty()) return false;
+    std::vector<std::set<std::string>> defs(body.size());
+    for (size_t j = i + 1; j < body.size(); ++j) {
+      const ExprP& ej = body[j];
+      // the key equality: `A == K` / `A = K` with A bound before body[i]
+      TermP l, r;
+      if (!ej->negated && ej->withs.empty()) {
+        if (ej->kind == Expr::TERM && ej->terms[0]->k == T_CALL && ej->terms[0]->op == std::vector<std::string>{"equal"} &&
+            ej->terms[0]->items.size() == 2) {
+          l = ej->terms[0]->items[0];
+          r = ej->terms[0]->items[1];
+        } else if (ej->kind == Expr::UNIFY && ej->terms.size() == 2) {
+          l = ej->terms[0];
+          r = ej->terms[1];
+        }
+      }
+      auto outer = [&](const TermP& t) {
+        return (t->k == T_VAR && !bound.count(t->s) && env->lookup(t->s) >= 0) || (t->k == T_SCALAR);
+      };
+      auto over_x = [&](const TermP& t) {
+        std::set<std::string> vs;
+        occ_vars(t, vs);
+        bool dep = false;  // reads the leaf (directly or through a local derived from it)
+        for (auto& v : vs) {
+          if (bound.count(v)) { dep = true; continue; }
+          if (is_global(env, v)) continue;
+          if (env->lookup(v) >= 0 && env->pdef_lookup(v)) continue;
+          return false;
+        }
+        return dep;
+      };
+      if (l && r) {
+        if (outer(r) && !outer(l)) std::swap(l, r);
+        if (outer(l) && !outer(r) && over_x(r)) {
+          P.a = l;
+          P.key = r;
+          // the key slice: definitions the key depends on, back to body[i]
+          std::set<std::string> need;
+          occ_vars(P.key, need);
+          std::vector<bool> in_slice(j, false);
+          for (size_t m = j; m-- > i + 1;) {
+            std::string d;
+            bool hit = false;
+            for (auto& v : defs[m]) if (need.count(v)) hit = true;
+            if (!hit) continue;
+            std::set<std::string> pre;  // bound before body[m]
+            pre.insert(P.x);
+            for (auto& v : P.pvars) pre.insert(v);
+            for (size_t q = i + 1; q < m; ++q) pre.insert(defs[q].begin(), defs[q].end());
+            if (!defines(body[m], pre, env, &d)) return false;
+            in_slice[m] = true;
+            for (auto& v : expr_vars(body[m])) need.insert(v);
+          }
+          for (size_t m = i + 1; m < j; ++m) {
+            if (in_slice[m]) { P.slice.push_back(body[m]); continue; }
+            if (!err_free_expr(body[m], env->mod, 0)) return false;  // skipped for leaves outside the bucket
+          }
+          // what the slice and key read besides the leaf: their own outputs,
+          // globals (functions) and parameter-derived locals; never input or
+          // the path variables (the key pass binds the leaf only)
+          std::set<std::string> own;
+          for (size_t m = i + 1; m < j; ++m) if (in_slice[m]) own.insert(defs[m].begin(), defs[m].end());
+          for (auto& v : need) {
+            if (v == P.x || own.count(v)) continue;
+            if (is_global(env, v)) return false;  // input, data, rule references
+            if (std::find(P.pvars.begin(), P.pvars.end(), v) != P.pvars.end()) return false;
+            if (env->lookup(v) >= 0 && env->pdef_lookup(v)) { P.params.push_back(v); continue; }
+            return false;
+          }
+          for (auto& s : P.slice)
+            for (auto& t : s->terms) if (!input_free(t, env->mod, 0)) return false;
+          if (!input_free(P.key, env->mod, 0)) return false;
+          return true;
+        }
+      }
+      // not the equality: what it binds (for later literals)
+      std::string d;
+      std::set<std::string> pre = bound;
+      if (defines(ej, pre, env, &d)) { defs[j].insert(d); bound.insert(d); continue; }
+      // any other literal must be a test over bound values (a generator or a
+      // binding this planner does not follow ends the search)
+      std::set<std::string> vs = expr_vars(ej);
+      if (!ej->negated)
+        for (auto& v : vs)
+          if (!bound.count(v) && env->lookup(v) < 0 && !is_global(env, v)) return false;
+    }
+    return false;
+  }
+
+  // the key program of a join: input.review is the leaf; the slice, then the key
+  JoinSite compile_key(const JoinPlan& P, const Env* env) {
+    Comp sub(st_, mods_, bank_, false);
+    Env kenv;
+    kenv.mod = env->mod;
+    sub.bind(&kenv, P.x, sub.input_root(true));
+    const int Lend = sub.label();
+    // the parameter-derived locals (each undefined parameter: no key), then
+    // the slice and the key
+    std::function<void(size_t, int)> params = [&](size_t q, int f) {
+      if (q == P.params.size()) {
+        sub.body_k(P.slice, 0, &kenv, f, [&](int f2) {
+          sub.term(P.key, &kenv, f2, [&](int r, int) { sub.emit(OP_KEYOUT, (uint16_t)r); });
+        });
+        return;
+      }
+      const TermP* d = env->pdef_lookup(P.params[q]);
+      if (!d) throw Unsupported("join key parameter");
+      sub.term(*d, &kenv, f, [&, q](int r, int f2) {
+        sub.bind(&kenv, P.params[q], r);
+        params(q + 1, f2);
+      });
+    };
+    params(0, Lend);
+    sub.place(Lend);
+    sub.emit(OP_END);
+    Program kp = sub.finish();
+    JoinSite js;
+    js.path = P.path;
+    js.nvars = (uint32_t)P.pvars.size();
+    js.key_off = kp.code_off;
+    js.key_len = kp.code_len;
+    js.key_nregs = kp.nregs;
+    if (js.key_nregs > 192) throw Unsupported("join key program registers");
+    js.desc = "data.inventory";
+    for (size_t q = 0; q < P.path.size(); ++q) js.desc += P.path[q].var ? "[_]" : "." + std::string(st_.str(P.path[q].sid));
+    return js;
+  }
+
+  bool join_site(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    if (!joins_on() || guard_ || prog_.joins.size() >= JMAX_SITES) return false;
+    JoinPlan P;
+    if (!plan_join(body, i, env, P)) return false;
+    JoinSite js;
+    try {
+      js = compile_key(P, env);
+    } catch (const Unsupported&) {
+      return false;  // the scan remains
+    }
+    const uint32_t site = (uint32_t)prog_.joins.size();
+    prog_.joins.push_back(js);
+    NoFuse nf(this);
+    const int save = reg_top_;
+    int av;
+    if (P.a->k == T_SCALAR) av = loadk(scalar_val(P.a));
+    else av = env->lookup(P.a->s);
+    if (loop_base_.size() >= 15) throw Unsupported("loop nesting too deep");
+    const int it = alloc(2);
+    const int leaf = alloc();
+    const int vb = alloc((int)P.pvars.size());
+    const int Lscan = label();
+    emit(OP_JPROBE, (uint16_t)it, (uint16_t)av, 0, (uint32_t)Lscan, ((uint32_t)loop_base_.size() + 1) | (site << 8));
+    loop_base_.push_back(reg_top_);
+    loop_var_lo_.push_back(it + 2);
+    const int Ln = label();
+    place(Ln);
+    emit(OP_JNEXT, (uint16_t)it, (uint16_t)leaf, 0, (uint32_t)fail, (uint32_t)depth());
+    for (size_t q = 0; q < P.pvars.size(); ++q) emit(OP_JVAR, (uint16_t)(vb + q), (uint16_t)it, 0, 0, (uint32_t)q);
+    bind(env, P.x, leaf);
+    for (size_t q = 0; q < P.pvars.size(); ++q) bind(env, P.pvars[q], vb + (int)q);
+    body_k(body, i + 1, env, Ln, succ);
+    for (auto& v : P.pvars) unbind(env, v);
+    unbind(env, P.x);
+    emit_jmp(OP_JMP, 0, Ln);
+    close_loop();
+    // no index for this lane: the iteration as written
+    place(Lscan);
+    reg_top_ = save;
+    expr(body[i], env, fail, [&, i, env](int f) { body_k(body, i + 1, env, f, succ); });
+    return true;
+  }
+
+  // `v = L[_]` over a lazy array L (lazy_def): each comprehension's body,
+  // then `v = <its element>`, then the rest of this body, compiled in line --
+  // the same solutions in the same order as lazy_iter, but a join inside a
+  // comprehension (unique-label's `o = data.inventory.namespace[_][_][_][_]`)
+  // now sees the key equality that follows the element's use.  Only when a
+  // part has a join site.
+  bool lazy_inline(const std::vector<ExprP>& body, size_t i, Env* env, int fail, const KE& succ) {
+    if (!joins_on() || guard_) return false;
+    const ExprP& e = body[i];
+    if ((e->kind != Expr::ASSIGN && e->kind != Expr::UNIFY) || e->negated || !e->withs.empty() || e->terms.size() != 2)
+      return false;
+    const TermP& v = e->terms[0];
+    const TermP& r = e->terms[1];
+    if (v->k != T_VAR || !unbound(env, v) || r->k != T_REF || !r->head || r->head->k != T_VAR || r->items.size() != 1 ||
+        !is_wild(r->items[0]))
+      return false;
+    const auto* lz = env->lazy_lookup(r->head->s);
+    if (!lz) return false;
+    std::vector<std::vector<ExprP>> bodies;
+    bool any = false;
+    for (auto& part : *lz) {
+      for (auto& l : part.locals) if (env->lookup(l) >= 0) return false;
+      std::vector<ExprP> b = part.compr->body;
+      auto el = std::make_shared<Expr>();
+      el->kind = Expr::UNIFY;
+      el->terms = {v, part.compr->key};
+      b.push_back(el);
+      b.insert(b.end(), body.begin() + i + 1, body.end());
+      for (size_t q = 0; q < part.compr->body.size() && !any; ++q) {
+        JoinPlan P;
+        any = plan_join(b, q, env, P);
+      }
+      bodies.push_back(std::move(b));
+    }
+    if (!any) return false;
+    NoFuse nf(this);  // array order is observable
+    for (size_t c = 0; c < bodies.size(); ++c) {
+      const bool last = c + 1 == bodies.size();
+      const int Lnext = last ? fail : label();
+      body_k(bodies[c], 0, env, Lnext, succ);
+      if (last) emit_jmp(OP_JMP, 0, fail);
+      else place(Lnext);
+    }
+    return true;
+  }
+
   void expr(const ExprP& e, Env* env, int fail, const KE& k) {
     if (!e->withs.empty()) throw Unsupported("with modifier in template");
     if (e->kind == Expr::SOME) { k(fail); return; }
@@ -647,7 +1153,7 @@ class Comp {
 
   // ---------------------------------------------------------------- unify
   void bind(Env* env, const std::string& v, int r) { env->vars[v] = r; }
-  void unbind(Env* env, const std::string& v) { env->vars.erase(v); }
+  void unbind(Env* env, const std::string& v) { env->vars.erase(v); env->pdef.erase(v); }
 
   bool pattern_has_unbound(const Env* env, const TermP& t) {
     std::vector<std::string> vs;
@@ -667,6 +1173,7 @@ class Comp {
           return;
         }
         bind(env, a->s, r);
+        if (TermP d = param_def(env, b)) env->pdef[a->s] = d;
         k(f);
         unbind(env, a->s);
       });

@@ -26,6 +26,23 @@ struct Unsupported : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// An inventory join site (compiler.cc join_site): `X := data.inventory<path>`
+// whose body later requires `A == key(X)` with A bound before the iteration.
+// The engine enumerates the path's leaves in iteration order, runs `key` (a
+// program of the body literals that derive the key from the leaf; input.review
+// is the leaf) on the device per leaf, and keeps (key hash, leaf) sorted per
+// constraint: OP_JPROBE iterates only the leaves in A's bucket.
+struct JoinSite {
+  struct Sel {
+    bool var = false;   // an unbound variable (iterated); else a constant string key
+    uint32_t sid = 0;   // the key's string id
+  };
+  std::vector<Sel> path;  // selectors after `data.inventory`
+  uint32_t nvars = 0;     // variable selectors (leaf row: leaf value, then their keys)
+  uint32_t key_off = 0, key_len = 0, key_nregs = 0;  // the key program in the code bank
+  std::string desc;       // diagnostics
+};
+
 struct Program {
   uint32_t code_off = 0;   // offset into the global code array
   uint32_t code_len = 0;
@@ -38,6 +55,7 @@ struct Program {
   // compiled to OP_FAIL_FALLBACK, and the first one's reason
   uint32_t fallback_sites = 0;
   std::string fallback_reason;
+  std::vector<JoinSite> joins;  // inventory join sites (site index = OP_JPROBE y >> 8)
 };
 
 // All modules known to the driver, indexed by package path.

@@ -1852,6 +1852,72 @@ __device__ __forceinline__ bool op_iter_next(PLane& L, uint64_t coll, uint64_t& 
   return true;
 }
 
+// ------------------------------------------------------------------ inventory joins
+// A join key's bucket: equal Rego values (ast.Compare == 0) get equal hashes.
+// Strings hash their bytes (whatever the representation); every number falls
+// in one bucket (1 == 1.0); composite values get none (KH_NONE: a composite
+// key never equals a scalar probe, and a composite probe takes the scan path).
+__device__ __forceinline__ uint64_t key_hash(const PLane& L, uint64_t v) {
+  const uint32_t t = vtag(v);
+  if (is_strv(v)) {
+    const SView s = sview(L, v);
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t i = 0; i < s.n; ++i) { h ^= (uint8_t)s.p[i]; h *= 1099511628211ull; }
+    return h | (1ull << 63);
+  }
+  if (t == V_NUM || t == V_INT || t == V_BFN) return KH_NUM;
+  if (t == V_NULL) return KH_NULL;
+  if (t == V_BOOL) return vpay(v) ? KH_TRUE : KH_FALSE;
+  return KH_NONE;
+}
+
+// opens a probe of the lane's constraint's index `site` (y >> 8) for R[b]:
+// it = [lo, hi) of the matching hash entries; false when there is no index or
+// the probe value has no bucket (the caller runs the plain scan instead)
+__device__ __forceinline__ bool op_jprobe(PLane& L, uint64_t& it, uint64_t& st, uint64_t key, uint32_t y) {
+  uint32_t d = (y & 0xff) < MAXLOOP ? (y & 0xff) : 0;
+  L.keepH[d] = 0;
+  L.keepB[d] = 0;
+  st = ((uint64_t)L.hp << 32) | ((uint64_t)L.bp << 48);
+  const uint32_t site = y >> 8;
+  if (!gk_args.jdir || site >= JMAX_SITES) return false;
+  const uint32_t* dir = gk_args.jdir + ((uint64_t)L.cn * JMAX_SITES + site) * 4;
+  if (!dir[2]) return false;
+  const uint64_t h = key_hash(L, key);
+  if (h == KH_NONE) return false;
+  uint32_t lo = dir[0], hi = dir[0] + dir[1];
+  // lower bound of h
+  uint32_t a = lo, b = hi;
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if (gk_args.jhash[m] < h) a = m + 1; else b = m;
+  }
+  uint32_t e = a;
+  while (e < hi && gk_args.jhash[e] == h) ++e;
+  it = (uint64_t)a | ((uint64_t)e << 32);
+  return true;
+}
+
+// next candidate leaf of a probe (per-iteration heap reclamation as op_iter_next)
+__device__ __forceinline__ bool op_jnext(PLane& L, uint64_t it, uint64_t& st, uint32_t y, uint64_t& leaf) {
+  const uint32_t pos = (uint32_t)st;
+  const uint32_t d = y < MAXLOOP ? y : 0;
+  const uint32_t mh = (uint32_t)((st >> 32) & 0xffff), mb = (uint32_t)(st >> 48);
+  L.hp = mh > L.keepH[d] ? mh : L.keepH[d];
+  L.bp = mb > L.keepB[d] ? mb : L.keepB[d];
+  const uint32_t p = (uint32_t)it + pos;
+  if (p >= (uint32_t)(it >> 32)) return false;
+  leaf = gk_args.jleaf[gk_args.jord[p]];
+  st = (st & 0xffffffff00000000ull) | (pos + 1);
+  return true;
+}
+
+// the current candidate's key at path variable j
+__device__ __forceinline__ uint64_t op_jvar(uint64_t it, uint64_t st, uint32_t j) {
+  const uint32_t p = (uint32_t)it + (uint32_t)st - 1;
+  return gk_args.jleaf[(uint64_t)gk_args.jord[p] + 1 + j];
+}
+
 #if GK_LDS_PARAMS
 // op_iter_next over a collection the JIT proved parameter-derived
 __device__ __forceinline__ bool op_iter_next_p(PLane& L, uint64_t coll, uint64_t& st, uint32_t y, uint64_t& k,

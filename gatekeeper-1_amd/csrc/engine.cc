@@ -31,6 +31,7 @@
 namespace gk {
 }
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
+extern "C" int gk_launch_keys(const gk::DevArgs* args, hipStream_t stream);
 extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev);
 extern "C" size_t gk_devargs_size();
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
@@ -399,6 +400,14 @@ struct gk_engine {
   std::string dbg_pool;
   uint32_t dev_nodes_ok = 0;       // leading permanent nodes whose d_nodes copy matches the host arena
   size_t out_cap0 = 1 << 20;       // initial tuple capacity of a new context (opts max_violations)
+  // inventory join indexes (build_joins; under the exclusive lock)
+  std::vector<uint32_t> jdir;
+  std::vector<uint64_t> jhash, jleaf;
+  std::vector<uint32_t> jord;
+  gk::DBuf d_jdir, d_jhash, d_jord, d_jleaf, d_jkeys;
+  bool joins_built = false;         // the device indexes match the current state
+  uint64_t join_indexes = 0, join_entries = 0, join_unindexed = 0, join_leaves = 0;
+  double join_ms = 0;
 };
 
 namespace gk {
@@ -534,25 +543,37 @@ static void rebuild_modules(gk_engine* e) {
         }
         te.guard = true;
       }
-      // structural validation of the bytecode before it can reach the device
-      for (uint32_t k = 0; k < p.code_len; ++k) {
-        const Ins& in = e->bank.code[p.code_off + k];
-        auto reg_ok = [&](uint16_t r) { return r < p.nregs || r == 0xffff; };
-        if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
-        const bool no_regs = in.op == OP_END || in.op == OP_JMP || in.op == OP_FAIL_FALLBACK || in.op == OP_ORD;
-        if (!no_regs && (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))))
-          throw std::runtime_error("internal: register out of range");
-        if (in.op == OP_ITER_INIT && in.a + 1u >= p.nregs) throw std::runtime_error("internal: iterator registers");
-        if (in.op == OP_CALL && in.b + (uint32_t)in.c > p.nregs) throw std::runtime_error("internal: call args");
-        bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE ||
-                   in.op == OP_ITER_NEXT || in.op == OP_MEMO_GET;
-        if ((in.op == OP_MEMO_GET || in.op == OP_MEMO_PUT) && in.y >= MEMO_SLOTS) throw std::runtime_error("internal: memo slot");
-        if (jmp && (in.x < p.code_off || in.x >= p.code_off + p.code_len)) throw std::runtime_error("internal: jump target");
-        if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x >= e->bank.consts.size()) throw std::runtime_error("internal: constant index");
-        if (in.op == OP_SPRINTF && in.x >= e->bank.fmt.size()) throw std::runtime_error("internal: format index");
-        if (in.op == OP_TABLE && (in.x >= e->bank.consts.size() || in.x + 1 + 2 * e->bank.consts[in.x] > e->bank.consts.size()))
-          throw std::runtime_error("internal: table bounds");
-      }
+      // structural validation of the bytecode before it can reach the device:
+      // the template program, then each join site's key program
+      auto validate = [&](uint32_t off, uint32_t len, uint32_t nregs, bool key) {
+        for (uint32_t k = 0; k < len; ++k) {
+          const Ins& in = e->bank.code[off + k];
+          auto reg_ok = [&](uint16_t r) { return r < nregs || r == 0xffff; };
+          if (in.op >= OP_COUNT_) throw std::runtime_error("internal: bad opcode");
+          const bool no_regs = in.op == OP_END || in.op == OP_JMP || in.op == OP_FAIL_FALLBACK || in.op == OP_ORD;
+          if (!no_regs && (!reg_ok(in.a) || !reg_ok(in.b) || (in.op != OP_EMIT && !reg_ok(in.c))))
+            throw std::runtime_error("internal: register out of range");
+          if (in.op == OP_ITER_INIT && in.a + 1u >= nregs) throw std::runtime_error("internal: iterator registers");
+          if (in.op == OP_CALL && in.b + (uint32_t)in.c > nregs) throw std::runtime_error("internal: call args");
+          bool jmp = in.op == OP_JMP || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE ||
+                     in.op == OP_ITER_NEXT || in.op == OP_MEMO_GET || in.op == OP_JPROBE || in.op == OP_JNEXT;
+          if ((in.op == OP_JPROBE && in.a + 1u >= nregs) || (in.op == OP_JVAR && in.b + 1u >= nregs))
+            throw std::runtime_error("internal: join iterator registers");
+          if (in.op == OP_JPROBE && (key || (in.y >> 8) >= p.joins.size())) throw std::runtime_error("internal: join site");
+          if (!key && in.op == OP_KEYOUT)
+            throw std::runtime_error("internal: key output in a template program");
+          if (key && (in.op == OP_EMIT || in.op == OP_JNEXT || in.op == OP_JVAR))
+            throw std::runtime_error("internal: emission in a join key program");
+          if ((in.op == OP_MEMO_GET || in.op == OP_MEMO_PUT) && in.y >= MEMO_SLOTS) throw std::runtime_error("internal: memo slot");
+          if (jmp && (in.x < off || in.x >= off + len)) throw std::runtime_error("internal: jump target");
+          if ((in.op == OP_LOADK || in.op == OP_GETK) && in.x >= e->bank.consts.size()) throw std::runtime_error("internal: constant index");
+          if (in.op == OP_SPRINTF && in.x >= e->bank.fmt.size()) throw std::runtime_error("internal: format index");
+          if (in.op == OP_TABLE && (in.x >= e->bank.consts.size() || in.x + 1 + 2 * e->bank.consts[in.x] > e->bank.consts.size()))
+            throw std::runtime_error("internal: table bounds");
+        }
+      };
+      validate(p.code_off, p.code_len, p.nregs, false);
+      for (auto& js : p.joins) validate(js.key_off, js.key_len, js.key_nregs, true);
       te.prog = (int)e->progs.size();
       te.supported = !te.guard;
       e->uses_inventory |= p.uses_inventory;
@@ -1088,6 +1109,176 @@ static bool sync_tables(gk_engine* e) {
   return ok;
 }
 
+// ------------------------------------------------------------------ inventory join indexes
+// The value a lane sees for node `idx` (devrt.h nodeval), on the host.
+static uint64_t host_nodeval(const Store& st, uint32_t idx) {
+  const Node& n = st.nodes()[idx];
+  switch (n.type) {
+    case NT_NULL: return tag_val(V_NULL, 0);
+    case NT_FALSE: return tag_val(V_BOOL, 0);
+    case NT_TRUE: return tag_val(V_BOOL, 1);
+    case NT_NUM: return tag_val(V_NUM, n.val);
+    case NT_STR: return tag_val(V_STR, n.val);
+    case NT_ARR: case NT_OBJ: return tag_val(V_NODE, idx);
+  }
+  return tag_val(V_UNDEF, 0);
+}
+
+// The solutions of `data.inventory<path>` in the order the device's
+// iteration (op_iter_next / vget over the node store) produces them: rows of
+// [leaf value, key at each variable selector].
+static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite::Sel>& path, size_t q,
+                        std::vector<uint64_t>& keys, std::vector<uint64_t>& rows) {
+  if (q == path.size()) {
+    rows.push_back(v);
+    rows.insert(rows.end(), keys.begin(), keys.end());
+    return;
+  }
+  if ((v >> 60) != V_NODE) return;  // a scalar has no members
+  const uint32_t idx = (uint32_t)(v & 0x0fffffffffffffffull);
+  const Node n = st.nodes()[idx];
+  if (path[q].var) {
+    for (uint32_t c = 0; c < n.n; ++c) {
+      const uint32_t ci = n.first + c;
+      keys.push_back(n.type == NT_OBJ ? tag_val(V_STR, st.nodes()[ci].key) : tag_val(V_INT, c));
+      enum_leaves(st, host_nodeval(st, ci), path, q + 1, keys, rows);
+      keys.pop_back();
+    }
+    return;
+  }
+  if (n.type != NT_OBJ) return;  // a string key selects nothing in an array
+  for (uint32_t c = 0; c < n.n; ++c)
+    if (st.nodes()[n.first + c].key == path[q].sid) {
+      enum_leaves(st, host_nodeval(st, n.first + c), path, q + 1, keys, rows);
+      return;
+    }
+}
+
+// Per (constraint, join site): the site's leaves are enumerated once per
+// template, the key pass (kernels.hip gk_key_kernel) computes every leaf's key
+// bucket on the device under the constraint's parameters, and the (hash, leaf
+// row) pairs are sorted by hash, leaves in iteration order within a hash.  A
+// key pass with a failed lane leaves the site unindexed (jdir ready = 0): its
+// lanes take the plain scan, which reports that failure where the reference
+// would.  Rebuilt whenever the engine is prepared (any mutation), under the
+// exclusive lock, after sync_tables.
+static bool build_joins(gk_engine* e) {
+  const auto t0 = std::chrono::steady_clock::now();
+  Store& st = e->st;
+  const size_t ncons = std::max<size_t>(e->corder.size(), 1);
+  e->jdir.assign(ncons * JMAX_SITES * 4, 0);
+  e->jhash.clear();
+  e->jord.clear();
+  e->jleaf.clear();
+  e->join_indexes = e->join_entries = e->join_unindexed = e->join_leaves = 0;
+  bool any = false;
+  for (auto& p : e->progs) any = any || !p.joins.empty();
+  bool ok = true;
+  if (any && e->inv_node != NO_ID) {
+    // leaves of every (template, site)
+    std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint32_t>> rows;  // -> (row0, leaves)
+    for (uint32_t pi = 0; pi < e->progs.size(); ++pi)
+      for (uint32_t s = 0; s < e->progs[pi].joins.size(); ++s) {
+        const JoinSite& js = e->progs[pi].joins[s];
+        const uint64_t row0 = e->jleaf.size();
+        std::vector<uint64_t> keys;
+        enum_leaves(st, tag_val(V_NODE, e->inv_node), js.path, 0, keys, e->jleaf);
+        rows[{pi, s}] = {row0, (uint32_t)((e->jleaf.size() - row0) / (1 + js.nvars))};
+      }
+    std::vector<uint64_t> jl = e->jleaf;
+    if (jl.empty()) jl.push_back(0);
+    ok = ok && up(e->d_jleaf, jl, false);
+    TablePtrs tp;
+    ok = ok && sync_strings(e, &tp);
+    std::vector<uint64_t> keys;
+    for (uint32_t ci = 0; ok && ci < e->corder.size(); ++ci) {
+      const MatchSpec& m = e->corder[ci]->spec;
+      if (m.prog == NO_ID || (m.flags & MF_FALLBACK) || m.prog >= e->progs.size()) continue;
+      const Program& p = e->progs[m.prog];
+      for (uint32_t s = 0; ok && s < p.joins.size() && s < JMAX_SITES; ++s) {
+        const JoinSite& js = p.joins[s];
+        const auto rw = rows[{m.prog, s}];
+        uint32_t* dir = &e->jdir[((size_t)ci * JMAX_SITES + s) * 4];
+        dir[0] = (uint32_t)e->jhash.size();
+        dir[1] = 0;
+        dir[2] = 0;
+        const uint32_t stride = 1 + js.nvars;
+        keys.assign(rw.second, KH_NONE);
+        if (rw.second) {
+          ok = ok && e->d_jkeys.reserve((size_t)rw.second * 8);
+          if (!ok) break;
+          DevArgs a{};
+          a.nodes = (const Node*)e->d_nodes.p;
+          a.strs = tp.strs;
+          a.pool = tp.pool;
+          a.sflags = tp.sflags;
+          a.nums = tp.nums;
+          a.code = (const Ins*)e->d_code.p;
+          a.K = (const uint64_t*)e->d_K.p;
+          a.fmt = (const uint32_t*)e->d_fmt.p;
+          a.cons = (const MatchSpec*)e->d_cons.p;
+          a.mwords = (const uint32_t*)e->d_mwords.p;
+          a.prog_off = (const uint32_t*)e->d_progoff.p;
+          a.dfa_keys = (const uint32_t*)e->d_dfa_keys.p;
+          a.dfa_meta = (const uint32_t*)e->d_dfa_meta.p;
+          a.dfa_words = (const uint32_t*)e->d_dfa_words.p;
+          a.stage = (const uint32_t*)e->d_stage.p;
+          a.dfa_c = (const uint32_t*)e->d_dfa_c.p;
+          a.ndfa = (uint32_t)std::max<size_t>(e->dfa_keys.size(), 1);
+          a.ncode = (uint32_t)e->bank.code.size();
+          a.ncons = (uint32_t)e->corder.size();
+          a.nrev = rw.second;
+          a.jleaf = (const uint64_t*)e->d_jleaf.p;
+          a.jkeys = (uint64_t*)e->d_jkeys.p;
+          a.jparams = m.params == NO_ID ? tag_val(V_NODE, 0) : host_nodeval(st, m.params);
+          a.jpc = js.key_off;
+          a.jstride = stride;
+          a.jrow0 = rw.first;
+          ok = gk_launch_keys(&a, nullptr) == 0 && hipStreamSynchronize(nullptr) == hipSuccess &&
+               hipMemcpy(keys.data(), e->d_jkeys.p, (size_t)rw.second * 8, hipMemcpyDeviceToHost) == hipSuccess;
+          if (!ok) break;
+        }
+        e->join_leaves += rw.second;
+        bool failed = false;
+        std::vector<std::pair<uint64_t, uint32_t>> ent;
+        for (uint32_t i = 0; i < rw.second; ++i) {
+          if (keys[i] == KH_FAIL) { failed = true; break; }
+          if (keys[i] != KH_NONE) ent.push_back({keys[i], (uint32_t)(rw.first + (uint64_t)i * stride)});
+        }
+        if (failed) { ++e->join_unindexed; continue; }
+        std::stable_sort(ent.begin(), ent.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (auto& en : ent) { e->jhash.push_back(en.first); e->jord.push_back(en.second); }
+        dir[1] = (uint32_t)ent.size();
+        dir[2] = 1;
+        ++e->join_indexes;
+        e->join_entries += ent.size();
+      }
+    }
+  }
+  std::vector<uint64_t> jh = e->jhash;
+  std::vector<uint32_t> jo = e->jord;
+  if (jh.empty()) jh.push_back(0);
+  if (jo.empty()) jo.push_back(0);
+  if (e->jleaf.empty()) { std::vector<uint64_t> z{0}; ok = ok && up(e->d_jleaf, z, false); }
+  ok = ok && up(e->d_jdir, e->jdir, false) && up(e->d_jhash, jh, false) && up(e->d_jord, jo, false);
+  e->joins_built = ok && any;
+  e->join_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (getenv("GKGPU_JOIN_TRACE"))
+    fprintf(stderr, "joins: %llu indexes, %llu entries, %llu unindexed, %llu leaves, %.2f ms\n",
+            (unsigned long long)e->join_indexes, (unsigned long long)e->join_entries,
+            (unsigned long long)e->join_unindexed, (unsigned long long)e->join_leaves, e->join_ms);
+  return ok;
+}
+
+// The join index pointers a launch passes (null: every site scans).
+static void set_join_args(const gk_engine* e, DevArgs& a) {
+  if (!e->joins_built) return;
+  a.jdir = (const uint32_t*)e->d_jdir.p;
+  a.jhash = (const uint64_t*)e->d_jhash.p;
+  a.jord = (const uint32_t*)e->d_jord.p;
+  a.jleaf = (const uint64_t*)e->d_jleaf.p;
+}
+
 // Compiles (hipRTC, in parallel) every template kernel not yet built; with a
 // device, loads the code objects.  A template whose kernel fails to compile
 // stays on the bytecode VM kernel (same semantics, slower).
@@ -1129,6 +1320,7 @@ static int prepare_locked(gk_engine* e, bool device) {
   if (device && ensure_device(e)) {
     ensure_jit(e, true);
     if (!sync_tables(e)) return fail(e, GK_EDEVICE, "device upload failed");
+    if (!build_joins(e)) return fail(e, GK_EDEVICE, "inventory join index build failed");
   }
   e->prepared_gen = e->gen;
   // the device side was brought up to date, or there is no device to use
@@ -1372,6 +1564,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.ebytes_cap = x->ebytes_cap;
     a.lens = (uint32_t*)x->d_lens.p;
     a.part = (unsigned long long*)x->d_part.p;
+    set_join_args(e, a);
     while (x->events.size() < plan.size() + 4) {
       hipEvent_t ev1;
       if (hipEventCreate(&ev1) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
@@ -2703,6 +2896,41 @@ int gk_template_status(gk_engine* e, const char* kind, const char** reason) {
   return it->second.supported ? 1 : 0;
 }
 
+int gk_template_joins(gk_engine* e, const char* kind, const char** sites) {
+  if (!e || !kind) return GK_EINVAL;
+  WriteLock g(e);  // compiles on demand
+  try {
+    rebuild_modules(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  auto it = e->templates.find(kind);
+  if (it == e->templates.end()) return GK_ENOTFOUND;
+  it->second.detail.clear();
+  int n = 0;
+  if (it->second.prog >= 0)
+    for (auto& js : e->progs[it->second.prog].joins) {
+      it->second.detail += (n ? ";" : "") + js.desc;
+      ++n;
+    }
+  if (sites) *sites = it->second.detail.c_str();
+  return n;
+}
+
+int gk_join_stats(gk_engine* e, uint64_t* indexes, uint64_t* entries, uint64_t* unindexed, uint64_t* leaves,
+                  double* build_ms) {
+  if (!e) return GK_EINVAL;
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  if (indexes) *indexes = e->join_indexes;
+  if (entries) *entries = e->join_entries;
+  if (unindexed) *unindexed = e->join_unindexed;
+  if (leaves) *leaves = e->join_leaves;
+  if (build_ms) *build_ms = e->join_ms;
+  return GK_OK;
+}
+
 size_t gk_constraint_count(gk_engine* e) {
   if (!e) return 0;
   ReadLock rl;
@@ -2927,7 +3155,7 @@ extern "C" int gk_debug_disasm(gk_engine* e, const char* kind, char** out) {
   static const char* names[] = {"END", "JMP", "JUNDEF", "JFALSE", "JTRUE", "LOADK", "LOADREV", "LOADPARAM", "MOV",
                                 "GET", "GETK", "ITER_INIT", "ITER_NEXT", "CMP", "ARITH", "LIST_NEW", "LIST_ADD",
                                 "OBJ_PUT", "YIELD", "CALL", "SPRINTF", "EMIT", "LEN_EQ", "FAIL_FALLBACK", "TABLE",
-                                "MEMO_GET", "MEMO_PUT", "ORD"};
+                                "MEMO_GET", "MEMO_PUT", "ORD", "JPROBE", "JNEXT", "JVAR", "KEYOUT"};
   static_assert(sizeof(names) / sizeof(names[0]) == OP_COUNT_, "opcode names");
   std::string s = "nregs=" + std::to_string(p.nregs) + " len=" + std::to_string(p.code_len) + "\n";
   for (uint32_t i = 0; i < p.code_len; ++i) {

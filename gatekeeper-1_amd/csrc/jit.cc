@@ -49,7 +49,9 @@ std::vector<uint32_t> fmt_reads(const Ins& in) {
   auto add = [&](uint32_t r) { if (r != 0xffff) rs.push_back(r); };
   switch (in.op) {
     case OP_GET: case OP_CMP: case OP_ARITH: case OP_MEMO_GET: add(in.b); add(in.c); break;
-    case OP_GETK: case OP_ITER_INIT: case OP_SPRINTF: case OP_LEN_EQ: case OP_TABLE: case OP_EMIT: add(in.b); break;
+    case OP_GETK: case OP_ITER_INIT: case OP_SPRINTF: case OP_LEN_EQ: case OP_TABLE: case OP_EMIT: case OP_JPROBE:
+      add(in.b);
+      break;
     case OP_LIST_ADD: add(in.a); add(in.b); break;
     case OP_OBJ_PUT: add(in.a); add(in.b); add(in.c); break;
     case OP_CALL: for (uint32_t i = 0; i < in.c; ++i) add(in.b + i); break;
@@ -111,6 +113,17 @@ FmtFlow fmt_flow(const Program& p, const CodeBank& bank) {
         flow(in.x, s);
         if (in.b != 0xffff) put(s, in.b, false);
         if (in.c != 0xffff) put(s, in.c, false);
+        flow(next, s);
+        continue;
+      case OP_JPROBE:
+        put(s, in.a, false);
+        put(s, in.a + 1u, false);
+        flow(in.x, s);
+        flow(next, s);
+        continue;
+      case OP_JNEXT:
+        flow(in.x, s);
+        put(s, in.b, false);
         flow(next, s);
         continue;
       case OP_MEMO_GET: {
@@ -230,6 +243,19 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         flow(next, s);
         continue;
       }
+      case OP_JPROBE:
+        kill(s, in.a);
+        kill(s, in.a + 1u);
+        flow(in.x, s);
+        flow(next, s);
+        continue;
+      case OP_JNEXT:
+        // like OP_ITER_NEXT: the previous iteration's heap is reclaimed here
+        s.facts.clear();
+        flow(in.x, s);
+        kill(s, in.b);
+        flow(next, s);
+        continue;
       case OP_MEMO_GET: {
         State t = s;
         kill(t, in.a);
@@ -311,6 +337,17 @@ FmtFlow param_flow(const Program& p, const CodeBank& bank) {
         flow(next, s);
         continue;
       }
+      case OP_JPROBE:
+        put(s, in.a, false);
+        put(s, in.a + 1u, false);
+        flow(in.x, s);
+        flow(next, s);
+        continue;
+      case OP_JNEXT:
+        flow(in.x, s);
+        put(s, in.b, false);
+        flow(next, s);
+        continue;
       case OP_MEMO_GET: {
         std::vector<uint64_t> t = s;
         put(t, in.a, false);
@@ -433,6 +470,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
     const Ins& in = bank.code[pc];
     switch (in.op) {
       case OP_JMP: case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT: case OP_MEMO_GET:
+      case OP_JPROBE: case OP_JNEXT:
         labels.insert(in.x);
         break;
       default: break;
@@ -652,6 +690,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       }
       case OP_FAIL_FALLBACK: o << "lane_fallback(L, " << y << "); return;"; break;
       case OP_ORD: o << "op_ord(L, " << y << ");"; break;
+      case OP_JPROBE:
+        o << "if (!op_jprobe(L, " << a << ", " << R(in.a + 1) << ", " << b << ", " << y << ")) goto " << x << ";";
+        break;
+      case OP_JNEXT:
+        o << "{ uint64_t v_ = " << UND << "; if (!op_jnext(L, " << a << ", " << R(in.a + 1) << ", " << y << ", v_)) goto "
+          << x << "; " << b << " = v_; }";
+        break;
+      case OP_JVAR: o << a << " = op_jvar(" << b << ", " << R(in.b + 1) << ", " << y << ");"; break;
       default: o << "lane_fallback(L, FB_UNSUPPORTED); return;"; break;
     }
     o << "\n";

@@ -79,6 +79,15 @@ __device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t par
       }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
       case OP_ORD: op_ord(L, in.y); break;
+      case OP_JPROBE: if (!op_jprobe(L, R[in.a], R[in.a + 1], R[in.b], in.y)) pc = in.x; break;
+      case OP_JNEXT: {
+        uint64_t v = UND;
+        if (!op_jnext(L, R[in.a], R[in.a + 1], in.y, v)) { pc = in.x; break; }
+        R[in.b] = v;
+        break;
+      }
+      case OP_JVAR: R[in.a] = op_jvar(R[in.b], R[in.b + 1], in.y); break;
+      case OP_KEYOUT: if (gk_args.jkeys) gk_args.jkeys[L.rv] = key_hash(L, R[in.a]); return;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
@@ -89,6 +98,26 @@ __global__ void __launch_bounds__(256) audit_kernel(DevArgs) {
   audit_body([&](PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t, uint32_t) {
     run_program(L, gk_args.prog_off[prog], review, params);
   });
+}
+
+// Key pass of an inventory join (engine.cc build_joins): one lane per leaf of
+// the site's data.inventory iteration runs the site's key program (the body
+// literals that derive the join key from the leaf, compiler.cc join_site) with
+// the leaf as its input document and the constraint's parameters, and writes
+// the key's bucket hash (OP_KEYOUT; KH_NONE when the key is undefined,
+// KH_FAIL when the program errs or needs the CPU).
+__global__ void __launch_bounds__(256) gk_key_kernel(DevArgs) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= gk_args.nrev) return;
+  Lane L0;
+  PLane& L = *(PLane*)&L0;
+  L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+  for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+  L.rv = (uint32_t)i;
+  L.cn = 0;
+  gk_args.jkeys[i] = KH_NONE;
+  run_program(L, gk_args.jpc, gk_args.jleaf[gk_args.jrow0 + i * gk_args.jstride], gk_args.jparams);
+  if (L.fail) gk_args.jkeys[i] = KH_FAIL;
 }
 
 // LDS-staged writer for one wavefront's message bytes
@@ -344,6 +373,13 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   if (ev) hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[2], stream);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gk_launch_keys(const gk::DevArgs* a, hipStream_t stream) {
+  const uint32_t blocks = (uint32_t)(((uint64_t)a->nrev + 255) / 256);
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(gk::gk_key_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ EXPORTS = [
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
     "gk_results_export", "gk_results_samples_export", "gk_results_generation", "gk_coalesce_stats",
+    "gk_template_joins", "gk_join_stats",
 ]
 
 
@@ -157,6 +158,10 @@ def load_library():
     lib.gk_results_launches.restype = sz
     lib.gk_results_launch.argtypes = [vp, sz, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint32), pu64, pu64]
     lib.gk_template_backend.argtypes = [vp, cp, C.POINTER(C.c_int), C.POINTER(cp)]
+    lib.gk_template_joins.argtypes = [vp, cp, C.POINTER(cp)]
+    lib.gk_template_joins.restype = C.c_int
+    u64p = C.POINTER(C.c_uint64)
+    lib.gk_join_stats.argtypes = [vp, u64p, u64p, u64p, u64p, C.POINTER(C.c_double)]
     lib.gk_results_copy_device_output.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_uint64)]
     lib.gk_results_vm_profile.argtypes = [vp, C.c_void_p, sz]
     lib.gk_results_vm_profile.restype = sz
@@ -731,6 +736,25 @@ class Driver:
         b, d = C.c_int(), C.c_char_p()
         self._check(self._lib.gk_template_backend(self._e, _b(kind), C.byref(b), C.byref(d)))
         return b.value, (d.value or b"").decode("utf-8", "replace")
+
+    def template_joins(self, kind: str):
+        """the template's inventory join sites (compiler.cc join_site): a list of
+        data.inventory paths whose iteration probes a per-constraint hash index"""
+        d = C.c_char_p()
+        n = self._lib.gk_template_joins(self._e, _b(kind), C.byref(d))
+        if n < 0:
+            self._check(n)
+        s = (d.value or b"").decode("utf-8", "replace")
+        return s.split(";") if n else []
+
+    def join_stats(self) -> dict:
+        """the join indexes of the current state (built on the device when the
+        engine is prepared): indexes, entries, unindexed sites, leaves, build ms"""
+        v = [C.c_uint64() for _ in range(4)]
+        ms = C.c_double()
+        self._check(self._lib.gk_join_stats(self._e, *[C.byref(x) for x in v], C.byref(ms)))
+        return {"indexes": v[0].value, "entries": v[1].value, "unindexed": v[2].value, "leaves": v[3].value,
+                "build_ms": ms.value}
 
     def template_status(self, kind: str):
         r = C.c_char_p()

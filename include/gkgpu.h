@@ -272,6 +272,17 @@ int gk_template_status(gk_engine* e, const char* kind, const char** reason);
  * flagged GK_REVIEW_FALLBACK (detail = reason), 0 = CPU fallback for every
  * matched review (detail = reason).  Compiles on demand. */
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail);
+/* inventory join sites of a template (compiler.cc join_site): iterations of
+ * data.inventory whose body filters on `A == key(leaf)` run as probes of a
+ * per-constraint hash index built on the device (the reference scans:
+ * k8suniqueserviceselector_template.yaml:40-44, k8suniquelabel_template.yaml:49-52).
+ * Returns the number of sites (sites = their paths, ';'-separated) or < 0. */
+int gk_template_joins(gk_engine* e, const char* kind, const char** sites);
+/* the indexes of the last prepared state: (constraint, site) indexes built,
+ * their entries, sites left to the scan (a key pass that failed), leaves keyed,
+ * and the build time (key passes + sort + upload).  Prepares the device state. */
+int gk_join_stats(gk_engine* e, uint64_t* indexes, uint64_t* entries, uint64_t* unindexed, uint64_t* leaves,
+                  double* build_ms);
 size_t gk_constraint_count(gk_engine* e);
 int gk_constraint_info(gk_engine* e, size_t i, const char** kind, const char** name);
 

@@ -145,6 +145,16 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
       }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
       case OP_ORD: op_ord(L, in.y); break;
+      // inventory joins: the checker has no join index (jdir null), so every
+      // probe takes the plain scan the compiler emits beside it
+      case OP_JPROBE: if (!op_jprobe(L, R[in.a], R[in.a + 1], R[in.b], in.y)) pc = in.x; break;
+      case OP_JNEXT: {
+        uint64_t v = UND;
+        if (!op_jnext(L, R[in.a], R[in.a + 1], in.y, v)) { pc = in.x; break; }
+        R[in.b] = v;
+        break;
+      }
+      case OP_JVAR: R[in.a] = op_jvar(R[in.b], R[in.b + 1], in.y); break;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
