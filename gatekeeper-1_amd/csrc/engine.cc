@@ -394,6 +394,7 @@ struct gk_engine {
   std::vector<gk::MatchSpec> dbg_cons;
   std::vector<uint32_t> dbg_progoff, dbg_mwords, dbg_dfa_keys, dbg_dfa_meta, dbg_dfa_words, dbg_fmt;
   std::vector<gk::Node> dbg_nodes;
+  std::vector<uint64_t> dbg_jleaf, dbg_jsite;
   std::vector<gk::StrEnt> dbg_strs;
   std::vector<uint8_t> dbg_sflags;
   std::vector<gk::NumEnt> dbg_nums;
@@ -404,6 +405,7 @@ struct gk_engine {
   std::vector<uint32_t> jdir;
   std::vector<uint64_t> jhash, jleaf;
   std::vector<uint32_t> jord;
+  std::vector<uint64_t> jsite;      // plan_joins: 7 words per (constraint, site) key pass
   gk::DBuf d_jdir, d_jhash, d_jord, d_jleaf, d_jkeys;
   bool joins_built = false;         // the device indexes match the current state
   uint64_t join_indexes = 0, join_entries = 0, join_unindexed = 0, join_leaves = 0;
@@ -1162,47 +1164,64 @@ static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite:
 // lanes take the plain scan, which reports that failure where the reference
 // would.  Rebuilt whenever the engine is prepared (any mutation), under the
 // exclusive lock, after sync_tables.
+// The join plan of the current state (host data work, every prepare): the
+// leaf rows of every (template, site) and one key-pass record per
+// (constraint, site): [constraint, site, key program pc, row stride, first row
+// word, leaves, parameters value].
+static void plan_joins(gk_engine* e) {
+  e->jleaf.clear();
+  e->jsite.clear();
+  bool any = false;
+  for (auto& p : e->progs) any = any || !p.joins.empty();
+  if (!any || e->inv_node == NO_ID) return;
+  Store& st = e->st;
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint32_t>> rows;  // -> (row0, leaves)
+  for (uint32_t pi = 0; pi < e->progs.size(); ++pi)
+    for (uint32_t s = 0; s < e->progs[pi].joins.size(); ++s) {
+      const JoinSite& js = e->progs[pi].joins[s];
+      const uint64_t row0 = e->jleaf.size();
+      std::vector<uint64_t> keys;
+      enum_leaves(st, tag_val(V_NODE, e->inv_node), js.path, 0, keys, e->jleaf);
+      rows[{pi, s}] = {row0, (uint32_t)((e->jleaf.size() - row0) / (1 + js.nvars))};
+    }
+  for (uint32_t ci = 0; ci < e->corder.size(); ++ci) {
+    const MatchSpec& m = e->corder[ci]->spec;
+    if (m.prog == NO_ID || (m.flags & MF_FALLBACK) || m.prog >= e->progs.size()) continue;
+    const Program& p = e->progs[m.prog];
+    for (uint32_t s = 0; s < p.joins.size() && s < JMAX_SITES; ++s) {
+      const auto rw = rows[{m.prog, s}];
+      const uint64_t params = m.params == NO_ID ? tag_val(V_NODE, 0) : host_nodeval(st, m.params);
+      e->jsite.insert(e->jsite.end(), {ci, s, p.joins[s].key_off, 1u + p.joins[s].nvars, rw.first, rw.second, params});
+    }
+  }
+}
+
 static bool build_joins(gk_engine* e) {
   const auto t0 = std::chrono::steady_clock::now();
-  Store& st = e->st;
   const size_t ncons = std::max<size_t>(e->corder.size(), 1);
   e->jdir.assign(ncons * JMAX_SITES * 4, 0);
   e->jhash.clear();
   e->jord.clear();
-  e->jleaf.clear();
   e->join_indexes = e->join_entries = e->join_unindexed = e->join_leaves = 0;
-  bool any = false;
-  for (auto& p : e->progs) any = any || !p.joins.empty();
+  const bool any = !e->jsite.empty();
   bool ok = true;
-  if (any && e->inv_node != NO_ID) {
-    // leaves of every (template, site)
-    std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint32_t>> rows;  // -> (row0, leaves)
-    for (uint32_t pi = 0; pi < e->progs.size(); ++pi)
-      for (uint32_t s = 0; s < e->progs[pi].joins.size(); ++s) {
-        const JoinSite& js = e->progs[pi].joins[s];
-        const uint64_t row0 = e->jleaf.size();
-        std::vector<uint64_t> keys;
-        enum_leaves(st, tag_val(V_NODE, e->inv_node), js.path, 0, keys, e->jleaf);
-        rows[{pi, s}] = {row0, (uint32_t)((e->jleaf.size() - row0) / (1 + js.nvars))};
-      }
+  if (any) {
     std::vector<uint64_t> jl = e->jleaf;
     if (jl.empty()) jl.push_back(0);
     ok = ok && up(e->d_jleaf, jl, false);
     TablePtrs tp;
     ok = ok && sync_strings(e, &tp);
     std::vector<uint64_t> keys;
-    for (uint32_t ci = 0; ok && ci < e->corder.size(); ++ci) {
-      const MatchSpec& m = e->corder[ci]->spec;
-      if (m.prog == NO_ID || (m.flags & MF_FALLBACK) || m.prog >= e->progs.size()) continue;
-      const Program& p = e->progs[m.prog];
-      for (uint32_t s = 0; ok && s < p.joins.size() && s < JMAX_SITES; ++s) {
-        const JoinSite& js = p.joins[s];
-        const auto rw = rows[{m.prog, s}];
+    for (size_t q = 0; ok && q < e->jsite.size(); q += 7) {
+      const uint64_t* sr = &e->jsite[q];
+      const uint32_t ci = (uint32_t)sr[0], s = (uint32_t)sr[1];
+      const std::pair<uint64_t, uint32_t> rw{sr[4], (uint32_t)sr[5]};
+      {
         uint32_t* dir = &e->jdir[((size_t)ci * JMAX_SITES + s) * 4];
         dir[0] = (uint32_t)e->jhash.size();
         dir[1] = 0;
         dir[2] = 0;
-        const uint32_t stride = 1 + js.nvars;
+        const uint32_t stride = (uint32_t)sr[3];
         keys.assign(rw.second, KH_NONE);
         if (rw.second) {
           ok = ok && e->d_jkeys.reserve((size_t)rw.second * 8);
@@ -1230,8 +1249,8 @@ static bool build_joins(gk_engine* e) {
           a.nrev = rw.second;
           a.jleaf = (const uint64_t*)e->d_jleaf.p;
           a.jkeys = (uint64_t*)e->d_jkeys.p;
-          a.jparams = m.params == NO_ID ? tag_val(V_NODE, 0) : host_nodeval(st, m.params);
-          a.jpc = js.key_off;
+          a.jparams = sr[6];
+          a.jpc = (uint32_t)sr[2];
           a.jstride = stride;
           a.jrow0 = rw.first;
           ok = gk_launch_keys(&a, nullptr) == 0 && hipStreamSynchronize(nullptr) == hipSuccess &&
@@ -1314,6 +1333,7 @@ static int prepare_locked(gk_engine* e, bool device) {
     rebuild_constraints(e);
     rebuild_regex(e);
     rebuild_stage(e);
+    plan_joins(e);
   } catch (const std::exception& ex) {
     return fail(e, GK_EPARSE, ex.what());
   }
@@ -3024,6 +3044,16 @@ extern "C" int gk_debug_clock_mhz(gk_engine* e, double* mhz) {
   return GK_OK;
 }
 
+// The key-pass records of the join plan as of the last gk_debug_host_args
+// (7 words per (constraint, site): engine.cc plan_joins); for the CPU checker.
+extern "C" int gk_debug_join_plan(gk_engine* e, const uint64_t** sites, uint64_t* nsites) {
+  if (!e || !sites || !nsites) return GK_EINVAL;
+  std::lock_guard<std::mutex> dg(e->dbg_mu);
+  *sites = e->dbg_jsite.empty() ? nullptr : e->dbg_jsite.data();
+  *nsites = e->dbg_jsite.size() / 7;
+  return GK_OK;
+}
+
 extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, size_t out_size) {
   if (!e || !b || !out || out_size != sizeof(DevArgs)) return GK_EINVAL;
   ReadLock rl;
@@ -3059,7 +3089,12 @@ extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, si
   if (e->dbg_dfa_keys.empty()) { e->dbg_dfa_keys.push_back(NO_ID); e->dbg_dfa_meta.push_back(2u << 30); }
   if (e->dbg_dfa_words.empty()) e->dbg_dfa_words.push_back(0);
   e->dbg_pool.append(16, '\0');  // dword reads past the last string (devrt.h puts_)
+  e->dbg_jleaf = e->jleaf;
+  e->dbg_jsite = e->jsite;
   DevArgs a{};
+  // the join plan's leaf rows (the CPU checker builds its own indexes from
+  // them: oracle/cpuvm.cc gkcpu_build_joins; without, every site scans)
+  a.jleaf = e->dbg_jleaf.empty() ? nullptr : e->dbg_jleaf.data();
   a.nodes = e->dbg_nodes.data();
   a.strs = e->dbg_strs.data();
   a.pool = (const uint8_t*)e->dbg_pool.data();

@@ -26,26 +26,44 @@ def load():
         lib.gkcpu_devargs_size.restype = C.c_size_t
         lib.gkcpu_sweep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]
         lib.gkcpu_sweep.restype = C.c_double
+        lib.gkcpu_build_joins.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
+        lib.gkcpu_build_joins.restype = C.c_int
         _LIB = lib
     return _LIB
 
 
-def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1):
-    """(seconds, evals, violations, message bytes, flagged pairs) of reviews
-    [lo, hi) of `batch` x every constraint, on `threads` host threads"""
+def _host_args(driver, batch, joins: bool, threads: int):
+    """the batch's host launch arguments; joins: with the checker's own join
+    indexes built from the engine's join plan (cpuvm.cc gkcpu_build_joins),
+    else every join site scans"""
     lib = load()
     glib = driver._lib
     n = lib.gkcpu_devargs_size()
     buf = (C.c_uint8 * n)()
     glib.gk_debug_host_args.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
     driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
+    if joins:
+        glib.gk_debug_join_plan.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+        sites, ns = C.c_void_p(), C.c_uint64()
+        driver._check(glib.gk_debug_join_plan(driver._e, C.byref(sites), C.byref(ns)))
+        if ns.value:
+            lib.gkcpu_build_joins(buf, sites, ns.value, max(1, threads))
+    return buf
+
+
+def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1, joins: bool = True):
+    """(seconds, evals, violations, message bytes, flagged pairs) of reviews
+    [lo, hi) of `batch` x every constraint, on `threads` host threads (the
+    join indexes' build not timed)"""
+    lib = load()
+    buf = _host_args(driver, batch, joins, threads)
     out = (C.c_uint64 * 4)()
     hi = batch.n if hi is None else hi
     s = lib.gkcpu_sweep(buf, lo, hi, threads, out)
     return s, out[0], out[1], out[2], out[3]
 
 
-def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1, pc_hist=None):
+def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1, pc_hist=None, joins: bool = True):
     """SURVEY 8(d) reference accounting of reviews [lo, hi) x constraint `only`
     (all when < 0): dict(nodes, strings, string_bytes, violations, flagged);
     pc_hist: a ctypes uint64 array of the code size receiving per-instruction
@@ -55,10 +73,7 @@ def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int
     lib.gkcpu_referenced.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
                                      C.POINTER(C.c_uint64), C.c_void_p]
     lib.gkcpu_referenced.restype = C.c_int
-    n = lib.gkcpu_devargs_size()
-    buf = (C.c_uint8 * n)()
-    glib.gk_debug_host_args.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
-    driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
+    buf = _host_args(driver, batch, joins, threads)
     glib.gk_debug_store_sizes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     nn, ns = C.c_uint64(), C.c_uint64()
     driver._check(glib.gk_debug_store_sizes(driver._e, C.byref(nn), C.byref(ns)))

@@ -16,6 +16,7 @@
 //
 // Per pair it follows devrt.h audit_body (autoreject, matching_constraints,
 // template program) and kernels.hip run_program (the bytecode VM loop).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -145,8 +146,8 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
       }
       case OP_FAIL_FALLBACK: lane_fallback(L, in.y); return;
       case OP_ORD: op_ord(L, in.y); break;
-      // inventory joins: the checker has no join index (jdir null), so every
-      // probe takes the plain scan the compiler emits beside it
+      // inventory joins: with gkcpu_build_joins' indexes the probe, else
+      // (jdir null) the plain scan the compiler emits beside it
       case OP_JPROBE: if (!op_jprobe(L, R[in.a], R[in.a + 1], R[in.b], in.y)) pc = in.x; break;
       case OP_JNEXT: {
         uint64_t v = UND;
@@ -155,6 +156,7 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
         break;
       }
       case OP_JVAR: R[in.a] = op_jvar(R[in.b], R[in.b + 1], in.y); break;
+      case OP_KEYOUT: if (gk_args.jkeys) gk_args.jkeys[L.rv] = key_hash(L, R[in.a]); return;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
@@ -243,9 +245,83 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
 }  // namespace gk
 
 #ifndef GKCPU_TOUCH
+namespace gk {
+namespace cpu {
+// the checker's own join indexes (gkcpu_build_joins), same layout as the
+// engine's device indexes (engine.cc build_joins)
+static std::vector<uint32_t> j_dir, j_ord;
+static std::vector<uint64_t> j_hash;
+}  // namespace cpu
+}  // namespace gk
+
 extern "C" {
 
 size_t gkcpu_devargs_size() { return sizeof(gk::DevArgs); }
+
+// Builds the join indexes of the engine's join plan on the host -- the key
+// programs run by this interpreter per leaf, (hash, leaf row) sorted per
+// (constraint, site) -- and points `args` (gk_debug_host_args, whose jleaf
+// holds the plan's leaf rows) at them, so the checker's sweeps probe as the
+// device does.  sites: gk_debug_join_plan's records.  Returns the number of
+// (constraint, site) pairs left unindexed (a failed key program).
+int gkcpu_build_joins(void* args, const uint64_t* sites, uint64_t nsites, int threads) {
+  using namespace gk;
+  DevArgs& A = *(DevArgs*)args;
+  A.jdir = nullptr;
+  A.jhash = nullptr;
+  A.jord = nullptr;
+  if (!nsites || !A.jleaf) return 0;
+  cpu::j_dir.assign((size_t)(A.ncons ? A.ncons : 1) * JMAX_SITES * 4, 0);
+  cpu::j_hash.clear();
+  cpu::j_ord.clear();
+  if (threads < 1) threads = 1;
+  int unindexed = 0;
+  for (uint64_t q = 0; q < nsites; ++q) {
+    const uint64_t* sr = sites + 7 * q;
+    const uint32_t ci = (uint32_t)sr[0], site = (uint32_t)sr[1], pc = (uint32_t)sr[2], stride = (uint32_t)sr[3];
+    const uint64_t row0 = sr[4], n = sr[5], params = sr[6];
+    std::vector<uint64_t> keys(n, KH_NONE);
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+      memcpy(&gk_args, args, sizeof(DevArgs));
+      gk_args.jkeys = keys.data();
+      gk_args.jdir = nullptr;
+      for (;;) {
+        const uint64_t i = next.fetch_add(1);
+        if (i >= n) break;
+        Lane L;
+        L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
+        for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+        L.rv = (uint32_t)i;
+        L.cn = 0;
+        cpu::run_program(L, pc, A.jleaf[row0 + i * stride], params);
+        if (L.fail) keys[i] = KH_FAIL;
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    uint32_t* dir = &cpu::j_dir[((size_t)ci * JMAX_SITES + site) * 4];
+    dir[0] = (uint32_t)cpu::j_hash.size();
+    std::vector<std::pair<uint64_t, uint32_t>> ent;
+    bool failed = false;
+    for (uint64_t i = 0; i < n && !failed; ++i) {
+      if (keys[i] == KH_FAIL) failed = true;
+      else if (keys[i] != KH_NONE) ent.push_back({keys[i], (uint32_t)(row0 + i * stride)});
+    }
+    if (failed) { ++unindexed; continue; }
+    std::stable_sort(ent.begin(), ent.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (auto& e : ent) { cpu::j_hash.push_back(e.first); cpu::j_ord.push_back(e.second); }
+    dir[1] = (uint32_t)ent.size();
+    dir[2] = 1;
+  }
+  if (cpu::j_hash.empty()) { cpu::j_hash.push_back(0); cpu::j_ord.push_back(0); }
+  A.jdir = cpu::j_dir.data();
+  A.jhash = cpu::j_hash.data();
+  A.jord = cpu::j_ord.data();
+  return unindexed;
+}
 
 // Evaluates reviews [lo, hi) of the staged batch described by `args` (host
 // pointers, gk_debug_host_args) against every constraint on `threads` threads.

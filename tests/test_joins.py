@@ -126,6 +126,41 @@ def _ns(objs):
     return [{"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": o["metadata"]["namespace"]}} for o in objs]
 
 
+def _oracle_count(od, objs, nss):
+    from parity import oracle_review
+    n = 0
+    for o, ns in zip(objs, nss):
+        r = oracle_review(od, augmented_review(o, ns))
+        assert r != "ERROR"
+        n += len(r)
+    return n
+
+
+def test_checker_probe_equals_scan_and_oracle():
+    """The probe code the compiler emits, run by the CPU checker with its own
+    host-built indexes (oracle/cpuvm.cc gkcpu_build_joins), against the scan
+    beside it and the oracle: tag values of every JSON type, and config 6."""
+    from oracle import cpu_baseline
+    vals = ["a", "b", 7, 7.0, True, None, {"x": 1}, "a", 3, False]
+    objs = _labelled(120, 5, value=lambda r, i: vals[r.randint(0, len(vals) - 1)])
+    cs = [W.constraint("K8sJoinLabelParam", "c", parameters={"label": "app"})]
+    extra = [(data_path(o), o) for o in objs]
+    d = _driver([LABEL_PARAM], cs, extra, host_only=True)
+    b = d.stage_objects(objs, _ns(objs))
+    probe = cpu_baseline.sweep(d, b, threads=2)[1:]
+    scan = cpu_baseline.sweep(d, b, threads=2, joins=False)[1:]
+    assert probe == scan and probe[3] == 0, (probe, scan)
+    assert probe[1] == _oracle_count(oracle_for([LABEL_PARAM], cs, extra), objs, _ns(objs)) > 100
+    ts, cs = W.config6()
+    objs_js, nss_js = W.gen_config6_json(1200)
+    inv = [(p, json.loads(o)) for p, o in W.inventory_paths(objs_js)]
+    d = _driver(ts, cs, inv, host_only=True)
+    b = d.stage_objects(objs_js, nss_js)
+    probe = cpu_baseline.sweep(d, b, threads=4)
+    scan = cpu_baseline.sweep(d, b, threads=4, joins=False)
+    assert probe[1:] == scan[1:] and probe[4] == 0 and probe[2] > 500, (probe, scan)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("jit", [True, False])
 def test_join_index_matches_oracle_with_edge_keys(jit):
