@@ -300,7 +300,8 @@ struct DevArgs {
   const uint64_t* jhash;      // key hashes, sorted within each index
   const uint32_t* jord;       // per hash entry: word offset of its leaf row in jleaf (leaf order within a hash)
   const uint64_t* jleaf;      // leaf rows: [leaf value, key at each path variable...]
-  // key pass (gk_key_kernel): leaf i = jleaf[jrow0 + i * jstride], key hash -> jkeys[i]
+  // key pass (gk_key_kernel): leaf i = jleaf[jrow0 + i * jstride], its key
+  // hashes -> jkeys[i * JKEYS_MAX ..] (KH_NONE-padded)
   uint64_t* jkeys;
   uint64_t jparams;           // the constraint's parameters value
   uint32_t jpc, jstride;
@@ -308,6 +309,9 @@ struct DevArgs {
 };
 // join sites per template program (compiler.cc join_site)
 constexpr uint32_t JMAX_SITES = 4;
+// keys one leaf may have (a key over a generator, `other.spec.rules[_].host`);
+// a leaf with more leaves its site unindexed
+constexpr uint32_t JKEYS_MAX = 8;
 // gk_key_kernel results besides a hash (a string key's hash has bit 63 set)
 constexpr uint64_t KH_NONE = 0;       // key undefined or composite: the leaf is in no bucket
 constexpr uint64_t KH_FAIL = 1;       // the key program failed (error / fallback): no index, scan

@@ -9,6 +9,7 @@
 // complete rules, comprehensions, negation) compile their inner body with a
 // fresh "done" label and continue after it.
 #include "compiler.h"
+#include "regex.h"
 
 #include <functional>
 #include <map>
@@ -644,6 +645,7 @@ class Comp {
     const char* v = getenv("GKGPU_JOINS");  // A/B switch, default on
     return !v || atoi(v) != 0;
   }
+  const std::vector<std::string>* str_vars_ = nullptr;  // err_free_call: variables known to hold strings
   struct JoinPlan {
     std::string x;                       // the leaf variable
     std::vector<JoinSite::Sel> path;
@@ -702,7 +704,9 @@ class Comp {
         if (u->k == T_ARRCOMPR || u->k == T_SETCOMPR || u->k == T_OBJCOMPR) return true;  // collected, not iterated
         if (u->k == T_REF)
           for (auto& s : u->items)
-            if (s->k == T_VAR && !bound.count(s->s) && env->lookup(s->s) < 0 && !is_global(env, s->s)) return false;
+            if (s->k == T_VAR && !bound.count(s->s) && env->lookup(s->s) < 0 && !is_global(env, s->s) &&
+                s->s.rfind("$_", 0) != 0)
+              return false;
         if (!ok(u->head)) return false;
         for (auto& s : u->items) if (!ok(s)) return false;
         return true;
@@ -792,6 +796,16 @@ class Comp {
     if (t->op.size() == 1 && cmp.count(t->op[0])) return true;
     if (t->op == std::vector<std::string>{"sprintf"})
       return nargs == 2 && t->items[0]->k == T_SCALAR && t->items[0]->stype == S_STR && t->items[1]->k == T_ARRAY;
+    if (t->op == std::vector<std::string>{"re_match"} || t->op == std::vector<std::string>{"regex", "match"}) {
+      // a valid literal pattern over a string: no error (regex.go:89-102
+      // errs on a bad pattern or a non-string operand)
+      if (nargs != 2 || t->items[0]->k != T_SCALAR || t->items[0]->stype != S_STR) return false;
+      std::vector<uint32_t> dfa;
+      if (compile_regex_dfa(t->items[0]->s, dfa) != RX_OK) return false;
+      const TermP& a = t->items[1];
+      if (a->k == T_SCALAR) return a->stype == S_STR;
+      return a->k == T_VAR && str_vars_ && std::find(str_vars_->begin(), str_vars_->end(), a->s) != str_vars_->end();
+    }
     auto rules = fn_rules(mod, t->op);
     if (rules.empty() || depth > 6) return false;
     return fn_err_free(rules, depth + 1);
@@ -923,6 +937,7 @@ class Comp {
           if (bound.count(v)) { dep = true; continue; }
           if (is_global(env, v)) continue;
           if (env->lookup(v) >= 0 && env->pdef_lookup(v)) continue;
+          if (v.rfind("$_", 0) == 0 && env->lookup(v) < 0) continue;  // a wildcard: several key values
           return false;
         }
         return dep;
@@ -949,17 +964,19 @@ class Comp {
             in_slice[m] = true;
             for (auto& v : expr_vars(body[m])) need.insert(v);
           }
+          str_vars_ = &P.pvars;  // object keys: strings (engine.cc plan_joins checks the tree)
           for (size_t m = i + 1; m < j; ++m) {
             if (in_slice[m]) { P.slice.push_back(body[m]); continue; }
-            if (!err_free_expr(body[m], env->mod, 0)) return false;  // skipped for leaves outside the bucket
+            if (!err_free_expr(body[m], env->mod, 0)) { str_vars_ = nullptr; return false; }  // skipped outside the bucket
           }
+          str_vars_ = nullptr;
           // what the slice and key read besides the leaf: their own outputs,
           // globals (functions) and parameter-derived locals; never input or
           // the path variables (the key pass binds the leaf only)
           std::set<std::string> own;
           for (size_t m = i + 1; m < j; ++m) if (in_slice[m]) own.insert(defs[m].begin(), defs[m].end());
           for (auto& v : need) {
-            if (v == P.x || own.count(v)) continue;
+            if (v == P.x || own.count(v) || v.rfind("$_", 0) == 0) continue;
             if (is_global(env, v)) return false;  // input, data, rule references
             if (std::find(P.pvars.begin(), P.pvars.end(), v) != P.pvars.end()) return false;
             if (env->lookup(v) >= 0 && env->pdef_lookup(v)) { P.params.push_back(v); continue; }
@@ -997,7 +1014,11 @@ class Comp {
     std::function<void(size_t, int)> params = [&](size_t q, int f) {
       if (q == P.params.size()) {
         sub.body_k(P.slice, 0, &kenv, f, [&](int f2) {
-          sub.term(P.key, &kenv, f2, [&](int r, int) { sub.emit(OP_KEYOUT, (uint16_t)r); });
+          // every value of the key (a generator in it yields several), then the next
+          sub.term(P.key, &kenv, f2, [&](int r, int f3) {
+            sub.emit(OP_KEYOUT, (uint16_t)r);
+            sub.emit_jmp(OP_JMP, 0, f3);
+          });
         });
         return;
       }

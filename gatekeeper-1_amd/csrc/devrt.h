@@ -1871,6 +1871,16 @@ __device__ __forceinline__ uint64_t key_hash(const PLane& L, uint64_t v) {
   return KH_NONE;
 }
 
+// key pass: the leaf's next key value (the lane's emission counter counts
+// them; a value past JKEYS_MAX fails the lane, and with it the index)
+__device__ __forceinline__ void op_keyout(PLane& L, uint64_t v) {
+  if (!gk_args.jkeys) return;
+  const uint32_t j = L.en;
+  if (j >= JKEYS_MAX) { lane_fallback(L, FB_HEAP); return; }
+  L.en = j + 1;
+  gk_args.jkeys[(uint64_t)L.rv * JKEYS_MAX + j] = key_hash(L, v);
+}
+
 // opens a probe of the lane's constraint's index `site` (y >> 8) for R[b]:
 // it = [lo, hi) of the matching hash entries; false when there is no index or
 // the probe value has no bucket (the caller runs the plain scan instead)

@@ -405,7 +405,7 @@ struct gk_engine {
   std::vector<uint32_t> jdir;
   std::vector<uint64_t> jhash, jleaf;
   std::vector<uint32_t> jord;
-  std::vector<uint64_t> jsite;      // plan_joins: 7 words per (constraint, site) key pass
+  std::vector<uint64_t> jsite;      // plan_joins: 8 words per (constraint, site) key pass
   gk::DBuf d_jdir, d_jhash, d_jord, d_jleaf, d_jkeys;
   bool joins_built = false;         // the device indexes match the current state
   uint64_t join_indexes = 0, join_entries = 0, join_unindexed = 0, join_leaves = 0;
@@ -1130,7 +1130,7 @@ static uint64_t host_nodeval(const Store& st, uint32_t idx) {
 // iteration (op_iter_next / vget over the node store) produces them: rows of
 // [leaf value, key at each variable selector].
 static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite::Sel>& path, size_t q,
-                        std::vector<uint64_t>& keys, std::vector<uint64_t>& rows) {
+                        std::vector<uint64_t>& keys, std::vector<uint64_t>& rows, bool* arr_var) {
   if (q == path.size()) {
     rows.push_back(v);
     rows.insert(rows.end(), keys.begin(), keys.end());
@@ -1140,10 +1140,11 @@ static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite:
   const uint32_t idx = (uint32_t)(v & 0x0fffffffffffffffull);
   const Node n = st.nodes()[idx];
   if (path[q].var) {
+    if (n.type != NT_OBJ && n.n) *arr_var = true;  // a path variable bound to an index, not a string
     for (uint32_t c = 0; c < n.n; ++c) {
       const uint32_t ci = n.first + c;
       keys.push_back(n.type == NT_OBJ ? tag_val(V_STR, st.nodes()[ci].key) : tag_val(V_INT, c));
-      enum_leaves(st, host_nodeval(st, ci), path, q + 1, keys, rows);
+      enum_leaves(st, host_nodeval(st, ci), path, q + 1, keys, rows, arr_var);
       keys.pop_back();
     }
     return;
@@ -1151,7 +1152,7 @@ static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite:
   if (n.type != NT_OBJ) return;  // a string key selects nothing in an array
   for (uint32_t c = 0; c < n.n; ++c)
     if (st.nodes()[n.first + c].key == path[q].sid) {
-      enum_leaves(st, host_nodeval(st, n.first + c), path, q + 1, keys, rows);
+      enum_leaves(st, host_nodeval(st, n.first + c), path, q + 1, keys, rows, arr_var);
       return;
     }
 }
@@ -1167,7 +1168,9 @@ static void enum_leaves(const Store& st, uint64_t v, const std::vector<JoinSite:
 // The join plan of the current state (host data work, every prepare): the
 // leaf rows of every (template, site) and one key-pass record per
 // (constraint, site): [constraint, site, key program pc, row stride, first row
-// word, leaves, parameters value].
+// word, leaves, parameters value, flags].  flags 1: a path variable iterates
+// an array somewhere in the tree -- the planner assumed path variables are
+// object keys (strings: compiler.cc err_free_call), so the site scans.
 static void plan_joins(gk_engine* e) {
   e->jleaf.clear();
   e->jsite.clear();
@@ -1176,13 +1179,16 @@ static void plan_joins(gk_engine* e) {
   if (!any || e->inv_node == NO_ID) return;
   Store& st = e->st;
   std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint32_t>> rows;  // -> (row0, leaves)
+  std::map<std::pair<uint32_t, uint32_t>, bool> arr;
   for (uint32_t pi = 0; pi < e->progs.size(); ++pi)
     for (uint32_t s = 0; s < e->progs[pi].joins.size(); ++s) {
       const JoinSite& js = e->progs[pi].joins[s];
       const uint64_t row0 = e->jleaf.size();
       std::vector<uint64_t> keys;
-      enum_leaves(st, tag_val(V_NODE, e->inv_node), js.path, 0, keys, e->jleaf);
+      bool arr_var = false;
+      enum_leaves(st, tag_val(V_NODE, e->inv_node), js.path, 0, keys, e->jleaf, &arr_var);
       rows[{pi, s}] = {row0, (uint32_t)((e->jleaf.size() - row0) / (1 + js.nvars))};
+      arr[{pi, s}] = arr_var;
     }
   for (uint32_t ci = 0; ci < e->corder.size(); ++ci) {
     const MatchSpec& m = e->corder[ci]->spec;
@@ -1191,7 +1197,8 @@ static void plan_joins(gk_engine* e) {
     for (uint32_t s = 0; s < p.joins.size() && s < JMAX_SITES; ++s) {
       const auto rw = rows[{m.prog, s}];
       const uint64_t params = m.params == NO_ID ? tag_val(V_NODE, 0) : host_nodeval(st, m.params);
-      e->jsite.insert(e->jsite.end(), {ci, s, p.joins[s].key_off, 1u + p.joins[s].nvars, rw.first, rw.second, params});
+      e->jsite.insert(e->jsite.end(),
+                      {ci, s, p.joins[s].key_off, 1u + p.joins[s].nvars, rw.first, rw.second, params, arr[{m.prog, s}] ? 1u : 0u});
     }
   }
 }
@@ -1212,7 +1219,7 @@ static bool build_joins(gk_engine* e) {
     TablePtrs tp;
     ok = ok && sync_strings(e, &tp);
     std::vector<uint64_t> keys;
-    for (size_t q = 0; ok && q < e->jsite.size(); q += 7) {
+    for (size_t q = 0; ok && q < e->jsite.size(); q += 8) {
       const uint64_t* sr = &e->jsite[q];
       const uint32_t ci = (uint32_t)sr[0], s = (uint32_t)sr[1];
       const std::pair<uint64_t, uint32_t> rw{sr[4], (uint32_t)sr[5]};
@@ -1222,9 +1229,10 @@ static bool build_joins(gk_engine* e) {
         dir[1] = 0;
         dir[2] = 0;
         const uint32_t stride = (uint32_t)sr[3];
-        keys.assign(rw.second, KH_NONE);
+        if (sr[7] & 1) { ++e->join_unindexed; continue; }
+        keys.assign((size_t)rw.second * JKEYS_MAX, KH_NONE);
         if (rw.second) {
-          ok = ok && e->d_jkeys.reserve((size_t)rw.second * 8);
+          ok = ok && e->d_jkeys.reserve((size_t)rw.second * JKEYS_MAX * 8);
           if (!ok) break;
           DevArgs a{};
           a.nodes = (const Node*)e->d_nodes.p;
@@ -1254,15 +1262,22 @@ static bool build_joins(gk_engine* e) {
           a.jstride = stride;
           a.jrow0 = rw.first;
           ok = gk_launch_keys(&a, nullptr) == 0 && hipStreamSynchronize(nullptr) == hipSuccess &&
-               hipMemcpy(keys.data(), e->d_jkeys.p, (size_t)rw.second * 8, hipMemcpyDeviceToHost) == hipSuccess;
+               hipMemcpy(keys.data(), e->d_jkeys.p, keys.size() * 8, hipMemcpyDeviceToHost) == hipSuccess;
           if (!ok) break;
         }
         e->join_leaves += rw.second;
         bool failed = false;
         std::vector<std::pair<uint64_t, uint32_t>> ent;
-        for (uint32_t i = 0; i < rw.second; ++i) {
-          if (keys[i] == KH_FAIL) { failed = true; break; }
-          if (keys[i] != KH_NONE) ent.push_back({keys[i], (uint32_t)(rw.first + (uint64_t)i * stride)});
+        for (uint32_t i = 0; i < rw.second && !failed; ++i) {
+          const uint64_t* k = &keys[(size_t)i * JKEYS_MAX];
+          if (k[0] == KH_FAIL) { failed = true; break; }
+          // a leaf once per distinct hash of its key values (the probe's body
+          // iterates them itself)
+          for (uint32_t j = 0; j < JKEYS_MAX && k[j] != KH_NONE; ++j) {
+            bool dup = false;
+            for (uint32_t h = 0; h < j; ++h) dup = dup || k[h] == k[j];
+            if (!dup) ent.push_back({k[j], (uint32_t)(rw.first + (uint64_t)i * stride)});
+          }
         }
         if (failed) { ++e->join_unindexed; continue; }
         std::stable_sort(ent.begin(), ent.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
@@ -3045,12 +3060,12 @@ extern "C" int gk_debug_clock_mhz(gk_engine* e, double* mhz) {
 }
 
 // The key-pass records of the join plan as of the last gk_debug_host_args
-// (7 words per (constraint, site): engine.cc plan_joins); for the CPU checker.
+// (8 words per (constraint, site): engine.cc plan_joins); for the CPU checker.
 extern "C" int gk_debug_join_plan(gk_engine* e, const uint64_t** sites, uint64_t* nsites) {
   if (!e || !sites || !nsites) return GK_EINVAL;
   std::lock_guard<std::mutex> dg(e->dbg_mu);
   *sites = e->dbg_jsite.empty() ? nullptr : e->dbg_jsite.data();
-  *nsites = e->dbg_jsite.size() / 7;
+  *nsites = e->dbg_jsite.size() / 8;
   return GK_OK;
 }
 

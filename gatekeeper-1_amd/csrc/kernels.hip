@@ -87,7 +87,7 @@ __device__ void run_program(PLane& L, uint32_t pc, uint64_t review, uint64_t par
         break;
       }
       case OP_JVAR: R[in.a] = op_jvar(R[in.b], R[in.b + 1], in.y); break;
-      case OP_KEYOUT: if (gk_args.jkeys) gk_args.jkeys[L.rv] = key_hash(L, R[in.a]); return;
+      case OP_KEYOUT: op_keyout(L, R[in.a]); break;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
@@ -104,8 +104,9 @@ __global__ void __launch_bounds__(256) audit_kernel(DevArgs) {
 // the site's data.inventory iteration runs the site's key program (the body
 // literals that derive the join key from the leaf, compiler.cc join_site) with
 // the leaf as its input document and the constraint's parameters, and writes
-// the key's bucket hash (OP_KEYOUT; KH_NONE when the key is undefined,
-// KH_FAIL when the program errs or needs the CPU).
+// the bucket hash of each of the key's values (OP_KEYOUT; KH_NONE-padded, none
+// when the key is undefined; KH_FAIL first when the program errs, needs the
+// CPU or yields more than JKEYS_MAX values).
 __global__ void __launch_bounds__(256) gk_key_kernel(DevArgs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= gk_args.nrev) return;
@@ -115,9 +116,9 @@ __global__ void __launch_bounds__(256) gk_key_kernel(DevArgs) {
   for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
   L.rv = (uint32_t)i;
   L.cn = 0;
-  gk_args.jkeys[i] = KH_NONE;
+  for (uint32_t j = 0; j < JKEYS_MAX; ++j) gk_args.jkeys[i * JKEYS_MAX + j] = KH_NONE;
   run_program(L, gk_args.jpc, gk_args.jleaf[gk_args.jrow0 + i * gk_args.jstride], gk_args.jparams);
-  if (L.fail) gk_args.jkeys[i] = KH_FAIL;
+  if (L.fail) gk_args.jkeys[i * JKEYS_MAX] = KH_FAIL;
 }
 
 // LDS-staged writer for one wavefront's message bytes

@@ -322,6 +322,49 @@ violation[{"msg": msg}] {
 }
 """)
 
+# demo/agilebank/dryrun/k8suniqueingresshost_template.yaml: the third
+# data.inventory join of the reference (a multi-valued key: every rule host)
+UNIQUE_INGRESS_HOST = _tmpl("K8sUniqueIngressHost", """package k8suniqueingresshost
+
+identical(obj, review) {
+	obj.metadata.namespace == review.object.metadata.namespace
+	obj.metadata.name == review.object.metadata.name
+}
+
+violation[{"msg": msg}] {
+	input.review.kind.kind == "Ingress"
+	re_match("^(extensions|networking.k8s.io)$", input.review.kind.group)
+	host := input.review.object.spec.rules[_].host
+	other := data.inventory.namespace[ns][otherapiversion]["Ingress"][name]
+	re_match("^(extensions|networking.k8s.io)/.+$", otherapiversion)
+	other.spec.rules[_].host == host
+	not identical(other, input.review)
+	msg := sprintf("ingress host conflicts with an existing ingress <%v>", [host])
+}
+""")
+
+
+def gen_ingresses(n, seed=5, n_namespaces=20, n_hosts=None):
+    """n Ingresses (extensions/v1beta1 and networking.k8s.io/v1beta1, one in
+    eight under another group) with 1-3 rule hosts each drawn from n_hosts
+    names (default n // 2, so hosts collide), over n_namespaces namespaces.
+    (objects, their Namespaces)"""
+    k = n_hosts or max(1, n // 2)
+    r = random.Random(seed)
+    names = ["ing-ns-%02d" % i for i in range(n_namespaces)]
+    objs, nss = [], []
+    for i in range(n):
+        ns = names[r.randrange(n_namespaces)]
+        av = ("extensions/v1beta1", "networking.k8s.io/v1beta1", "example.com/v1")[2 if i % 8 == 7 else i % 2]
+        rules = [{"host": "h%d.example.com" % r.randrange(k)} for _ in range(1 + r.randrange(3))]
+        if i % 11 == 0:
+            rules.append({"http": {"paths": []}})  # a rule without a host
+        objs.append({"apiVersion": av, "kind": "Ingress", "metadata": {"name": "ing-%05d" % i, "namespace": ns},
+                     "spec": {"rules": rules}})
+        nss.append(namespace_obj(ns))
+    return objs, nss
+
+
 ALLOWED_LABEL_REGEX = _tmpl("K8sAllowedLabelRegex", """package k8sallowedlabelregex
 
 violation[{"msg": msg, "details": {"label": key}}] {

@@ -156,7 +156,7 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
         break;
       }
       case OP_JVAR: R[in.a] = op_jvar(R[in.b], R[in.b + 1], in.y); break;
-      case OP_KEYOUT: if (gk_args.jkeys) gk_args.jkeys[L.rv] = key_hash(L, R[in.a]); return;
+      case OP_KEYOUT: op_keyout(L, R[in.a]); break;
       default: lane_fallback(L, FB_UNSUPPORTED); return;
     }
   }
@@ -277,10 +277,11 @@ int gkcpu_build_joins(void* args, const uint64_t* sites, uint64_t nsites, int th
   if (threads < 1) threads = 1;
   int unindexed = 0;
   for (uint64_t q = 0; q < nsites; ++q) {
-    const uint64_t* sr = sites + 7 * q;
+    const uint64_t* sr = sites + 8 * q;
     const uint32_t ci = (uint32_t)sr[0], site = (uint32_t)sr[1], pc = (uint32_t)sr[2], stride = (uint32_t)sr[3];
     const uint64_t row0 = sr[4], n = sr[5], params = sr[6];
-    std::vector<uint64_t> keys(n, KH_NONE);
+    if (sr[7] & 1) { ++unindexed; continue; }  // a path variable over an array: the site scans
+    std::vector<uint64_t> keys(n * JKEYS_MAX, KH_NONE);
     std::atomic<uint64_t> next{0};
     auto work = [&]() {
       memcpy(&gk_args, args, sizeof(DevArgs));
@@ -295,7 +296,7 @@ int gkcpu_build_joins(void* args, const uint64_t* sites, uint64_t nsites, int th
         L.rv = (uint32_t)i;
         L.cn = 0;
         cpu::run_program(L, pc, A.jleaf[row0 + i * stride], params);
-        if (L.fail) keys[i] = KH_FAIL;
+        if (L.fail) keys[i * JKEYS_MAX] = KH_FAIL;
       }
     };
     std::vector<std::thread> th;
@@ -307,8 +308,13 @@ int gkcpu_build_joins(void* args, const uint64_t* sites, uint64_t nsites, int th
     std::vector<std::pair<uint64_t, uint32_t>> ent;
     bool failed = false;
     for (uint64_t i = 0; i < n && !failed; ++i) {
-      if (keys[i] == KH_FAIL) failed = true;
-      else if (keys[i] != KH_NONE) ent.push_back({keys[i], (uint32_t)(row0 + i * stride)});
+      const uint64_t* k = &keys[i * JKEYS_MAX];
+      if (k[0] == KH_FAIL) { failed = true; break; }
+      for (uint32_t j = 0; j < JKEYS_MAX && k[j] != KH_NONE; ++j) {
+        bool dup = false;
+        for (uint32_t h = 0; h < j; ++h) dup = dup || k[h] == k[j];
+        if (!dup) ent.push_back({k[j], (uint32_t)(row0 + i * stride)});
+      }
     }
     if (failed) { ++unindexed; continue; }
     std::stable_sort(ent.begin(), ent.end(), [](const auto& x, const auto& y) { return x.first < y.first; });

@@ -45,6 +45,10 @@ def test_join_sites_of_the_cross_resource_templates():
                                                   "data.inventory.namespace[_][_][_][_]"]
     for k in ("K8sRequiredLabels", "K8sAllowedRepos", "K8sContainerLimits", "K8sRequiredProbes"):
         assert d.template_joins(k) == []
+    # agilebank's dry-run unique-ingress-host: every rule host is a key value,
+    # re_match over the apiVersion path variable is skipped outside the bucket
+    d = _driver([W.UNIQUE_INGRESS_HOST], [W.constraint("K8sUniqueIngressHost", "u")], host_only=True)
+    assert d.template_joins("K8sUniqueIngressHost") == ["data.inventory.namespace[_][_].Ingress[_]"]
 
 
 def test_join_switch_off(monkeypatch):
@@ -159,6 +163,46 @@ def test_checker_probe_equals_scan_and_oracle():
     probe = cpu_baseline.sweep(d, b, threads=4)
     scan = cpu_baseline.sweep(d, b, threads=4, joins=False)
     assert probe[1:] == scan[1:] and probe[4] == 0 and probe[2] > 500, (probe, scan)
+
+
+def test_checker_multi_valued_keys_and_array_levels():
+    """unique-ingress-host (1-3 hosts per Ingress, colliding; a rule without a
+    host; an apiVersion outside the regex): checker probe = scan = oracle.
+    Then an array synced where a path variable iterates (its key would be an
+    index, not a string, and re_match would fail): the site is left to the
+    scan, which fails those reviews exactly as before."""
+    from oracle import cpu_baseline
+    objs, nss = W.gen_ingresses(300)
+    cs = [W.constraint("K8sUniqueIngressHost", "uih")]
+    extra = [(data_path(o), o) for o in objs]
+    d = _driver([W.UNIQUE_INGRESS_HOST], cs, extra, host_only=True)
+    b = d.stage_objects(objs, nss)
+    probe = cpu_baseline.sweep(d, b, threads=4)[1:]
+    scan = cpu_baseline.sweep(d, b, threads=4, joins=False)[1:]
+    assert probe == scan and probe[3] == 0, (probe, scan)
+    assert probe[1] == _oracle_count(oracle_for([W.UNIQUE_INGRESS_HOST], cs, extra), objs, nss) > 300
+    b.free()
+    d.put_data("/external/admission.k8s.gatekeeper.sh/namespace/ing-ns-00", [{"x": 1}])
+    b = d.stage_objects(objs, nss)
+    probe = cpu_baseline.sweep(d, b, threads=4)[1:]
+    scan = cpu_baseline.sweep(d, b, threads=4, joins=False)[1:]
+    assert probe == scan, (probe, scan)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+def test_unique_ingress_host_join_on_gpu(jit):
+    """the multi-valued join on the device (both back ends) equals the oracle;
+    one index, entries for every distinct host of every Ingress"""
+    objs, nss = W.gen_ingresses(400, seed=8)
+    cs = [W.constraint("K8sUniqueIngressHost", "uih")]
+    extra = [(data_path(o), o) for o in objs]
+    drv = gkgpu.Driver(jit=jit)
+    rep, res = run_objects(drv, [W.UNIQUE_INGRESS_HOST], cs, objs, nss, extra_data=extra)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.fallback == 0 and rep.errors == 0 and rep.violations > 300, rep
+    st = drv.join_stats()
+    assert st["indexes"] == 1 and st["unindexed"] == 0 and st["entries"] > len(objs), st
 
 
 @pytest.mark.gpu
