@@ -1070,3 +1070,43 @@ def test_config6_joins_on_gpu_equal_the_oracle():
     assert not rep.mismatches, rep.mismatches[:3]
     assert rep.fallback == 0 and rep.errors == 0, rep
     assert rep.violations > 60, rep
+
+
+def _heavy_pods(n, seed=3, cap=400):
+    """Pods whose container count is heavy-tailed (Pareto, alpha 0.9, capped):
+    most have one or two containers, a few dozen have hundreds"""
+    import random
+    rng = random.Random(seed)
+    pool = [W._container(rng, "c%d" % i) for i in range(512)]
+    objs, nss = [], []
+    for i in range(n):
+        k = min(cap, int(rng.paretovariate(0.9)))
+        conts = []
+        for j in range(k):
+            c = dict(pool[rng.randrange(len(pool))])
+            c["name"] = "c%d" % j
+            conts.append(c)
+        objs.append({"apiVersion": "v1", "kind": "Pod",
+                     "metadata": {"name": "p%d" % i, "namespace": "team-1", "labels": {"app": "a"}},
+                     "spec": {"containers": conts}})
+        nss.append(W.namespace_obj("team-1", {"env": "dev"}))
+    return objs, nss
+
+
+def test_heavy_tailed_pods_fall_back_only_past_the_lane_limits():
+    """the lane limits (heap words, byte buffer, 256
+    emissions per lane) send a review to the CPU fallback.  On a heavy-tailed
+    Pod distribution (1-400 containers) every review the engine keeps equals
+    the oracle's, and only Pods with many containers fall back (reported)."""
+    ts, cs = W.config2()
+    objs, nss = _heavy_pods(1200)
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, nss)
+    assert not rep.mismatches, rep.mismatches[:3]
+    sizes = [len(o["spec"]["containers"]) for o in objs]
+    fb = [sizes[i] for i in range(len(objs)) if res.status[i] & 2]
+    floor = 64 if _BACKEND["jit"] else 8
+    print("heavy-tailed pods: %d of %d fall back (container counts %s); %d > 100 containers" %
+          (len(fb), len(objs), sorted(fb)[:12], sum(1 for s in sizes if s > 100)))
+    assert all(s >= floor for s in fb), sorted(fb)
+    assert rep.compared >= len(objs) - len(fb) - rep.errors
