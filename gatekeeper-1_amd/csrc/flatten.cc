@@ -545,7 +545,7 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
   if (!nsnodes.empty()) memcpy(dn + nlive, nsnodes.data(), nsnodes.size() * sizeof(Node));
   // 4.
   std::vector<std::string> perr(T);
-  pfor([&](int t) {
+  auto place_part = [&](int t) {
     Part& p = parts[t];
     const Node* ln = p.st.nodes().data();
     const Remap rm{p.smap, p.nmap};
@@ -616,7 +616,13 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
         perr[t] = "path layout: region count mismatch";
         return;
       }
-  });
+  };
+  if (getenv("GKGPU_PLACE_TWICE")) {  // diagnostics: the placement once more into touched memory
+    auto ta = Clock::now();
+    pfor(place_part);
+    fprintf(stderr, "flatten: place (first touch) %.1f ms\n", ms(ta, Clock::now()));
+  }
+  pfor(place_part);
   for (auto& e : perr)
     if (!e.empty()) { err = e; return false; }
   out.excluded = 0;
