@@ -354,6 +354,10 @@ struct gk_engine {
     hipFunction_t fn = nullptr;
   };
   std::vector<Jit> jits;
+  // GKGPU_FUSED=1 (A/B): one kernel for every template program (jit.cc
+  // jit_fused_source); its launch takes every constraint the per-template
+  // kernels would
+  Jit fused;
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
   bool host_only = false;    // opts {"host_only": true}: stage on the host only (CPU baseline / tests); no evaluation
   std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
@@ -501,6 +505,8 @@ static void rebuild_modules(gk_engine* e) {
   e->progs.clear();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   e->jits.clear();
+  if (e->fused.mod) hipModuleUnload(e->fused.mod);
+  e->fused = gk_engine::Jit{};
   e->templates.clear();
   // drop the transient region before appending new permanent constant nodes
   reset_transient(e);
@@ -591,6 +597,12 @@ static void rebuild_modules(gk_engine* e) {
       if (te.reason.empty()) te.reason = ex.what();
     }
     e->templates[kind] = te;
+  }
+  if (env_mode("GKGPU_FUSED", 0, 1) && e->progs.size() >= 2) {
+    std::vector<const Program*> ps;
+    std::vector<uint32_t> ids;
+    for (uint32_t i = 0; i < e->progs.size(); ++i) { ps.push_back(&e->progs[i]); ids.push_back(i); }
+    e->fused.src = jit_fused_source(ps, ids, e->bank, e->st, &e->fused.name);
   }
   e->perm_nodes = (uint32_t)e->st.nodes().size();
   e->module_nodes = e->st.nodes().size() - n_before;
@@ -1323,9 +1335,15 @@ static void ensure_jit(gk_engine* e, bool load) {
     if (j.state != 0) continue;
     th.emplace_back([&j] { j.state = jit_compile(j.src, j.code, j.log) ? 1 : -1; });
   }
+  if (!e->fused.src.empty() && e->fused.state == 0)
+    th.emplace_back([e] { e->fused.state = jit_compile(e->fused.src, e->fused.code, e->fused.log) ? 1 : -1; });
   for (auto& t : th) t.join();
   if (!load) return;
-  for (auto& j : e->jits) {
+  std::vector<gk_engine::Jit*> all;
+  for (auto& j : e->jits) all.push_back(&j);
+  if (!e->fused.src.empty()) all.push_back(&e->fused);
+  for (auto* jp : all) {
+    auto& j = *jp;
     if (j.state != 1 || j.fn) continue;
     if (hipModuleLoadData(&j.mod, j.code.data()) != hipSuccess ||
         hipModuleGetFunction(&j.fn, j.mod, j.name.c_str()) != hipSuccess) {
@@ -1524,12 +1542,19 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
   std::vector<Step> plan;
   {
     std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
+    const bool fused = e->fused.fn != nullptr;
+    std::vector<uint32_t> fused_cons;
     for (uint32_t c = 0; c < ncons; ++c) {
       uint32_t p = e->corder[c]->spec.prog;
-      bool jit = p != NO_ID && p < e->jits.size() && e->jits[p].fn;
+      bool jit = p != NO_ID && p < e->jits.size() && (e->jits[p].fn || fused);
+      if (jit && fused) { fused_cons.push_back(c); continue; }
       groups[jit ? p : e->progs.size()].push_back(c);
     }
     std::vector<uint32_t> clist;
+    if (!fused_cons.empty()) {
+      plan.push_back({e->fused.fn, e->fused.name, 0, (uint32_t)fused_cons.size()});
+      clist = fused_cons;
+    }
     for (size_t g = 0; g < groups.size(); ++g) {
       if (groups[g].empty()) continue;
       bool vm = g == e->progs.size();
