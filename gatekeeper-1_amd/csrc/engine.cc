@@ -191,6 +191,7 @@ struct TemplateEnt {
   bool guard = false;      // outside the subset; prog is its guard program
   std::string reason;
   std::string detail;      // gk_template_backend text
+  std::string joins;       // gk_template_joins text
   int prog = -1;
 };
 
@@ -2966,14 +2967,14 @@ int gk_template_joins(gk_engine* e, const char* kind, const char** sites) {
   }
   auto it = e->templates.find(kind);
   if (it == e->templates.end()) return GK_ENOTFOUND;
-  it->second.detail.clear();
+  it->second.joins.clear();
   int n = 0;
   if (it->second.prog >= 0)
     for (auto& js : e->progs[it->second.prog].joins) {
-      it->second.detail += (n ? ";" : "") + js.desc;
+      it->second.joins += (n ? ";" : "") + js.desc;
       ++n;
     }
-  if (sites) *sites = it->second.detail.c_str();
+  if (sites) *sites = it->second.joins.c_str();
   return n;
 }
 
