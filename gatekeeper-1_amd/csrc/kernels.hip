@@ -204,6 +204,10 @@ __device__ Lane gk_pass_lane;
 
 __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
   __shared__ unsigned long long wsum[4];
+  // an overflowed evaluation is re-run whole by the host: an emission that
+  // found its slot but not its staged bytes left that slot unwritten, so the
+  // tuples must not be read (the format pass returns here too)
+  if (gk_args.counters[0] > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;
   PLane& L = *(PLane*)&gk_pass_lane;
   const uint64_t n = ntuples();
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
