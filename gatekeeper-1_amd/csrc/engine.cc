@@ -2263,6 +2263,9 @@ static void review_order(gk_engine* e, const std::vector<ReviewCol>& cols, const
       if (seen.insert(cols[i].kind).second) kind_ids.push_back(cols[i].kind);
     std::sort(kind_ids.begin(), kind_ids.end());
   }
+  // GKGPU_ORDER_DESC=1 (A/B): within a kind, the largest documents first
+  // (their wavefronts run longest; launched last they leave a tail)
+  const bool desc = env_mode("GKGPU_ORDER_DESC", 0, 1) != 0;
   if (kind_ids.size() <= 4096) {
     std::unordered_map<uint32_t, uint64_t> krank;
     for (size_t k = 0; k < kind_ids.size(); ++k) krank[kind_ids[k]] = k;
@@ -2271,7 +2274,7 @@ static void review_order(gk_engine* e, const std::vector<ReviewCol>& cols, const
     uint64_t last_rank = 0;
     for (size_t i = lo; i < hi; ++i) {
       if (cols[i].kind != last_kind) { last_kind = cols[i].kind; last_rank = krank[last_kind]; }
-      const uint64_t w = weight[i], sg = sig[i - lo] & 0xffffu;
+      const uint64_t w = desc ? (uint64_t)(0xffffffffu - weight[i]) : weight[i], sg = sig[i - lo] & 0xffffu;
       if (mode == 2) key[i - lo] = (last_rank << 48) | ((w >> 20) << 36) | (sg << 20) | (w & 0xfffffu);
       else key[i - lo] = (sg << 44) | ((match_order ? last_rank : 0) << 32) | w;
     }
