@@ -12,7 +12,6 @@
 //                       wavefront (wave prefix sum); messages are formatted on
 //                       the GPU (Go fmt / ast.Term.String rules).
 #include <algorithm>
-#include <cstdlib>
 
 #include "devrt.h"
 
@@ -127,28 +126,6 @@ struct LOut {
   uint8_t* p;
   uint32_t pos;
   __device__ __forceinline__ void put(char c) { p[pos++] = (uint8_t)c; }
-  __device__ __forceinline__ void finish() {}
-};
-// The same with one LDS store per four bytes (GKGPU_FMT_WORDS=1, A/B): bytes
-// gather in a register and go out as aligned dwords; the partial dwords at
-// the two ends, which the neighbouring lanes' ranges share, as bytes.
-struct LOutW {
-  uint8_t* base;
-  uint32_t start, pos, acc;
-  __device__ __forceinline__ void word(uint32_t w) {
-    if (w >= start) *(uint32_t*)(base + w) = acc;
-    else for (uint32_t i = start - w; i < 4; ++i) base[w + i] = (uint8_t)(acc >> (8 * i));
-  }
-  __device__ __forceinline__ void put(char c) {
-    acc |= (uint32_t)(uint8_t)c << ((pos & 3) * 8);
-    if ((++pos & 3) == 0) { word(pos - 4); acc = 0; }
-  }
-  __device__ __forceinline__ void finish() {
-    if (pos & 3) {
-      const uint32_t w = pos & ~3u, lo = w > start ? w : start;
-      for (uint32_t i = lo; i < pos; ++i) base[i] = (uint8_t)(acc >> (8 * (i - w)));
-    }
-  }
 };
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
@@ -294,7 +271,6 @@ __global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
 
 constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
 
-template <bool WORDS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(DevArgs) {
   __shared__ uint32_t stage[4][FSTAGE / 4];
   __shared__ uint32_t wtot[4];
@@ -355,14 +331,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       if (hi > lo && hi4 - lo4 <= FSTAGE) {
         const uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
         if (valid && len) {
-          if (WORDS) {
-            LOutW o{stb, (uint32_t)(dst - lo4), (uint32_t)(dst - lo4), 0u};
-            body(o);
-            o.finish();
-          } else {
-            LOut o{stb + (dst - lo4), 0};
-            body(o);
-          }
+          LOut o{stb + (dst - lo4), 0};
+          body(o);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -406,9 +376,7 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
-  static const bool words = getenv("GKGPU_FMT_WORDS") && atoi(getenv("GKGPU_FMT_WORDS")) != 0;
-  if (words) hipLaunchKernelGGL(gk::gk_format_kernel<true>, dim3(blocks), dim3(256), 0, stream, *a);
-  else hipLaunchKernelGGL(gk::gk_format_kernel<false>, dim3(blocks), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[2], stream);
   return (int)hipGetLastError();
 }
