@@ -767,10 +767,79 @@ class Comp {
   // bodies do not and no two of them can yield different values (a single
   // body, one constant value, or bodies that test one path against the same
   // constant with == and != -- make_apiversion's shape).
+  // value kinds the analysis can prove, for builtins that err on others: 1 a
+  // collection (count), 2 a set (set difference).  Locals resolve through
+  // their definitions in ctx_body_; a complete rule through its one body.
+  const std::vector<ExprP>* ctx_body_ = nullptr;
+  int coll_kind(const TermP& t, const Module* mod, int depth) {
+    if (!t || depth > 8) return 0;
+    switch (t->k) {
+      case T_SETCOMPR: case T_SET: return 2;
+      case T_ARRCOMPR: case T_ARRAY: case T_OBJCOMPR: case T_OBJECT: return 1;
+      case T_VAR: {
+        if (ctx_body_)
+          for (auto& e : *ctx_body_) {
+            if (e->negated) continue;
+            if ((e->kind == Expr::ASSIGN || e->kind == Expr::UNIFY) && e->terms.size() == 2 && e->terms[0]->k == T_VAR &&
+                e->terms[0]->s == t->s)
+              return coll_kind(e->terms[1], mod, depth + 1);
+            if (e->kind == Expr::TERM && e->terms[0]->k == T_CALL && e->terms[0]->items.size() == 3 &&
+                e->terms[0]->items[2]->k == T_VAR && e->terms[0]->items[2]->s == t->s &&
+                e->terms[0]->op == std::vector<std::string>{"minus"})
+              return coll_kind(e->terms[0]->items[0], mod, depth + 1) == 2 &&
+                             coll_kind(e->terms[0]->items[1], mod, depth + 1) == 2
+                         ? 2
+                         : 0;
+          }
+        if (mod) {
+          auto rs = mods_.rules(mod->pkg, t->s);
+          if (rs.size() == 1 && rs[0]->kind == Rule::COMPLETE && !rs[0]->is_default && !rs[0]->is_else) {
+            const auto* save = ctx_body_;
+            ctx_body_ = &cbody(rs[0], {});
+            const int k = coll_kind(rs[0]->value, rs[0]->mod, depth + 1);
+            ctx_body_ = save;
+            return k;
+          }
+        }
+        return 0;
+      }
+      default: return 0;
+    }
+  }
+  // a rule referenced as a value cannot err: error-free bodies, and a complete
+  // rule cannot conflict (one body, or one constant value)
+  bool rule_err_free(const std::vector<std::shared_ptr<Rule>>& rules, int depth) {
+    if (depth > 6) return false;
+    bool same_const = true;
+    for (auto& r : rules) {
+      if (r->is_else || (r->kind != Rule::COMPLETE && r->kind != Rule::PSET)) return false;
+      const auto* save = ctx_body_;
+      ctx_body_ = &cbody(r, {});
+      bool ok = true;
+      for (auto& e : *ctx_body_) ok = ok && err_free_expr(e, r->mod, depth + 1);
+      ok = ok && err_free_term(r->kind == Rule::PSET ? r->key : r->value, r->mod, depth + 1);
+      ctx_body_ = save;
+      if (!ok) return false;
+      same_const = same_const && r->value && is_const(r->value) && same_term(r->value, rules[0]->value);
+    }
+    return rules[0]->kind == Rule::PSET || rules.size() == 1 || same_const;
+  }
   bool err_free_term(const TermP& t, const Module* mod, int depth) {
     if (!t) return true;
     switch (t->k) {
-      case T_SCALAR: case T_VAR: return true;
+      case T_SCALAR: return true;
+      case T_VAR: {
+        if (mod && t->s != "input" && t->s != "data") {
+          auto rs = mods_.rules(mod->pkg, t->s);
+          if (!rs.empty()) return rule_err_free(rs, depth);
+        }
+        return true;
+      }
+      case T_SETCOMPR: case T_ARRCOMPR: {
+        if (!err_free_term(t->key, mod, depth)) return false;
+        for (auto& e : t->body) if (!err_free_expr(e, mod, depth)) return false;
+        return true;
+      }
       case T_REF:
         if (!t->head || t->head->k != T_VAR) return false;
         if (mod && t->head->s != "input" && t->head->s != "data" && !mods_.rules(mod->pkg, t->head->s).empty()) return false;
@@ -794,6 +863,9 @@ class Comp {
     if (!t->items.empty() && t->items.back()->k == T_VAR && t->items.back()->s.rfind("$l", 0) == 0) --nargs;
     for (size_t q = 0; q < nargs; ++q) if (!err_free_term(t->items[q], mod, depth)) return false;
     if (t->op.size() == 1 && cmp.count(t->op[0])) return true;
+    if (t->op == std::vector<std::string>{"count"}) return nargs == 1 && coll_kind(t->items[0], mod, 0) >= 1;
+    if (t->op == std::vector<std::string>{"minus"})
+      return nargs == 2 && coll_kind(t->items[0], mod, 0) == 2 && coll_kind(t->items[1], mod, 0) == 2;
     if (t->op == std::vector<std::string>{"sprintf"})
       return nargs == 2 && t->items[0]->k == T_SCALAR && t->items[0]->stype == S_STR && t->items[1]->k == T_ARRAY;
     if (t->op == std::vector<std::string>{"re_match"} || t->op == std::vector<std::string>{"regex", "match"}) {
@@ -819,8 +891,13 @@ class Comp {
   bool fn_err_free(const std::vector<std::shared_ptr<Rule>>& rules, int depth) {
     for (auto& r : rules) {
       if (r->kind != Rule::FUNC || r->is_else || r->is_default) return false;
-      for (auto& e : cbody(r, {})) if (!err_free_expr(e, r->mod, depth)) return false;
-      if (!err_free_term(r->value, r->mod, depth)) return false;
+      const auto* save = ctx_body_;
+      ctx_body_ = &cbody(r, {});
+      bool ok = true;
+      for (auto& e : *ctx_body_) ok = ok && err_free_expr(e, r->mod, depth);
+      ok = ok && err_free_term(r->value, r->mod, depth);
+      ctx_body_ = save;
+      if (!ok) return false;
     }
     if (rules.size() == 1) return true;
     bool same_const = true;
@@ -1932,7 +2009,12 @@ class Comp {
           uint16_t k1 = nargs == 2 ? (uint16_t)regs[1] : NOREG;
           if (slot >= 0) emit(OP_MEMO_GET, (uint16_t)out, (uint16_t)regs[0], k1, (uint32_t)Lhit, (uint32_t)slot);
           if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
-          for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out);
+          // every body yields one constant and none can err: the first
+          // solution is the value (OPA would go on through the other bodies
+          // and solutions only to find the same value; GKGPU_FN_EARLY=0, A/B)
+          const int Ldone = early_exit_ok(rules) ? label() : -1;
+          for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out, Ldone);
+          if (Ldone >= 0) place(Ldone);
           --inline_depth_;
           if (slot >= 0) emit(OP_MEMO_PUT, (uint16_t)out, (uint16_t)regs[0], k1, pure_func(rules) ? 1u : 0u, (uint32_t)slot);
           place(Lhit);
@@ -2102,7 +2184,20 @@ class Comp {
     return (int)off;
   }
 
-  void inline_func(const std::shared_ptr<Rule>& r, const std::vector<int>& args, int out, bool stmt) {
+  bool early_exit_ok(const std::vector<std::shared_ptr<Rule>>& rules) {
+    static const bool on = !getenv("GKGPU_FN_EARLY") || atoi(getenv("GKGPU_FN_EARLY")) != 0;
+    if (!on || rules.empty()) return false;
+    for (auto& r : rules)
+      if (!r->value || !is_const(r->value) || !same_term(r->value, rules[0]->value)) {
+        if (getenv("GKGPU_FN_TRACE")) fprintf(stderr, "fn %s: value not one constant\n", rules[0]->name.c_str());
+        return false;
+      }
+    const bool ok = fn_err_free(rules, 0);
+    if (getenv("GKGPU_FN_TRACE")) fprintf(stderr, "fn %s: early exit %s\n", rules[0]->name.c_str(), ok ? "yes" : "no");
+    return ok;
+  }
+
+  void inline_func(const std::shared_ptr<Rule>& r, const std::vector<int>& args, int out, bool stmt, int done = -1) {
     if (r->is_else) throw Unsupported("else in function");
     int save = reg_top_;
     int Lend = label();
@@ -2113,7 +2208,7 @@ class Comp {
         term(r->value, &fenv, f2, [&](int v, int f3) {
           if (stmt) emit_jmp(OP_JFALSE, v, f3);
           emit(OP_YIELD, (uint16_t)out, (uint16_t)v, 0, 0, escape_range(out));
-          emit_jmp(OP_JMP, 0, f3);
+          emit_jmp(OP_JMP, 0, done >= 0 ? done : f3);
         });
       });
     });
