@@ -2011,7 +2011,7 @@ class Comp {
           if (++inline_depth_ > 64) throw Unsupported("recursion / inline depth");
           // every body yields one constant and none can err: the first
           // solution is the value (OPA would go on through the other bodies
-          // and solutions only to find the same value; GKGPU_FN_EARLY=0, A/B)
+          // and solutions only to find the same value; GKGPU_FN_EARLY=1, A/B)
           const int Ldone = early_exit_ok(rules) ? label() : -1;
           for (auto& r : rules) inline_func(r, regs, out, stmt && !has_out, Ldone);
           if (Ldone >= 0) place(Ldone);
@@ -2185,7 +2185,7 @@ class Comp {
   }
 
   bool early_exit_ok(const std::vector<std::shared_ptr<Rule>>& rules) {
-    static const bool on = !getenv("GKGPU_FN_EARLY") || atoi(getenv("GKGPU_FN_EARLY")) != 0;
+    static const bool on = getenv("GKGPU_FN_EARLY") && atoi(getenv("GKGPU_FN_EARLY")) != 0;  // A/B, off until measured
     if (!on || rules.empty()) return false;
     for (auto& r : rules)
       if (!r->value || !is_const(r->value) || !same_term(r->value, rules[0]->value)) {

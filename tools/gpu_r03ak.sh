@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the early exit of constant-valued, error-free functions
-# (GKGPU_FN_EARLY=0 off), configs 2 and 4, alternating, then parity tests.
+(GKGPU_FN_EARLY=1 on), configs 2 and 4, alternating, then parity tests.
 #   bash tools/gpu_r03ak.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -23,7 +23,7 @@ for rep in 1 2; do
   run c2_off_$rep 2 GKGPU_FN_EARLY=0 && run c2_on_$rep 2 GKGPU_FN_EARLY=1 && \
   run c4_off_$rep 4 GKGPU_FN_EARLY=0 && run c4_on_$rep 4 GKGPU_FN_EARLY=1 || exit 1
 done
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_joins.py -m gpu -v --timeout 300 \
+GKGPU_FN_EARLY=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_joins.py -m gpu -v --timeout 300 \
   --timeout-method thread -k "config2 or config4 or config6 or probes or limits or unique or join or scale or heavy or emission" > "$OUT/pytest.log" 2>&1
 rc=$?
 tail -2 "$OUT/pytest.log"
