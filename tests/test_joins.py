@@ -13,6 +13,7 @@ and against the scan path (GKGPU_JOINS=0) at a few thousand objects.
 """
 import collections
 import json
+import os
 
 import pytest
 
@@ -22,6 +23,8 @@ from gkgpu.client import Client, data_path
 
 from parity import compare, engine_rows, oracle_for, run_objects
 from gkgpu.client import augmented_review
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _driver(ts, cs, extra=(), **kw):
@@ -301,3 +304,50 @@ def test_config6_probe_equals_scan_at_scale(monkeypatch):
     assert n > 1000
     for i in range(len(objs)):
         assert rows["1"][i] == rows["0"][i], (i, rows["1"][i][:3], rows["0"][i][:3])
+
+
+def test_function_early_exit_keeps_results():
+    """GKGPU_FN_EARLY=1 (compiler.cc early_exit_ok): a function whose bodies
+    all yield one constant and cannot err stops at its first solution --
+    probe_is_missing / missing / identical in the agilebank templates.  The
+    CPU checker's counts with it equal the oracle's on config 2 Pods and on
+    config 6 (a subprocess: the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import json, sys
+sys.path[:0] = [%r, %r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+from oracle import cpu_baseline
+from parity import oracle_for, oracle_review
+def drv(ts, cs, extra=()):
+    d = gkgpu.Driver(host_only=True); cl = Client(d)
+    for t in ts: cl.add_template(t)
+    for c in cs: cl.add_constraint(c)
+    for p, o in extra: d.put_data(p, o)
+    return d
+ts, cs = W.config2()
+pods, ns_of, ns_objs = W.gen_pods(400, seed=9, n_namespaces=20)
+nss = [ns_objs[n] for n in ns_of]
+d = drv(ts, cs)
+got = cpu_baseline.sweep(d, d.stage_objects(pods, nss), threads=2)
+od = oracle_for(ts, cs)
+want = sum(len(oracle_review(od, augmented_review(p, n))) for p, n in zip(pods, nss))
+ts6, cs6 = W.config6()
+objs, onss = W.gen_config6_json(200)
+inv = [(p, json.loads(o)) for p, o in W.inventory_paths(objs)]
+d6 = drv(ts6, cs6, inv)
+got6 = cpu_baseline.sweep(d6, d6.stage_objects(objs, onss), threads=2)
+od6 = oracle_for(ts6, cs6, inv)
+want6 = sum(len(oracle_review(od6, augmented_review(json.loads(o), json.loads(n)))) for o, n in zip(objs, onss))
+print(json.dumps([got[2], got[4], want, got6[2], got6[4], want6]))
+''' % (os.path.join(ROOT, "gatekeeper-1_amd"), ROOT, os.path.join(ROOT, "tests"))
+    env = dict(os.environ, GKGPU_FN_EARLY="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    v, fl, want, v6, fl6, want6 = json.loads(out.stdout.strip().splitlines()[-1])
+    assert fl == 0 and fl6 == 0
+    assert v == want > 100 and v6 == want6 > 20, (v, want, v6, want6)
