@@ -771,33 +771,54 @@ class Comp {
   // collection (count), 2 a set (set difference).  Locals resolve through
   // their definitions in ctx_body_; a complete rule through its one body.
   const std::vector<ExprP>* ctx_body_ = nullptr;
+  const std::vector<TermP>* ctx_args_ = nullptr;  // the function's arguments (fn_err_free)
+  static bool expr_mentions(const ExprP& e, const std::string& v) {
+    std::vector<std::string> vs;
+    for (auto& u : e->terms) term_vars(u, vs);
+    return std::find(vs.begin(), vs.end(), v) != vs.end();
+  }
   int coll_kind(const TermP& t, const Module* mod, int depth) {
     if (!t || depth > 8) return 0;
     switch (t->k) {
       case T_SETCOMPR: case T_SET: return 2;
       case T_ARRCOMPR: case T_ARRAY: case T_OBJCOMPR: case T_OBJECT: return 1;
       case T_VAR: {
+        // an argument is whatever the caller passes (and shadows a rule name)
+        if (ctx_args_) {
+          std::vector<std::string> vs;
+          for (auto& a : *ctx_args_) term_vars(a, vs);
+          if (std::find(vs.begin(), vs.end(), t->s) != vs.end()) return 0;
+        }
+        // the variable's definition: `v := term`, or `v = term` / the output
+        // of a set difference when nothing before it mentions v (otherwise the
+        // unification is a test on a value bound elsewhere)
         if (ctx_body_)
           for (auto& e : *ctx_body_) {
-            if (e->negated) continue;
-            if ((e->kind == Expr::ASSIGN || e->kind == Expr::UNIFY) && e->terms.size() == 2 && e->terms[0]->k == T_VAR &&
-                e->terms[0]->s == t->s)
-              return coll_kind(e->terms[1], mod, depth + 1);
-            if (e->kind == Expr::TERM && e->terms[0]->k == T_CALL && e->terms[0]->items.size() == 3 &&
-                e->terms[0]->items[2]->k == T_VAR && e->terms[0]->items[2]->s == t->s &&
-                e->terms[0]->op == std::vector<std::string>{"minus"})
-              return coll_kind(e->terms[0]->items[0], mod, depth + 1) == 2 &&
-                             coll_kind(e->terms[0]->items[1], mod, depth + 1) == 2
-                         ? 2
-                         : 0;
+            if (!e->negated) {
+              if (e->kind == Expr::ASSIGN && e->terms.size() == 2 && e->terms[0]->k == T_VAR && e->terms[0]->s == t->s)
+                return coll_kind(e->terms[1], mod, depth + 1);
+              if (e->kind == Expr::UNIFY && e->terms.size() == 2 && e->terms[0]->k == T_VAR && e->terms[0]->s == t->s)
+                return coll_kind(e->terms[1], mod, depth + 1);
+              if (e->kind == Expr::TERM && e->terms[0]->k == T_CALL && e->terms[0]->items.size() == 3 &&
+                  e->terms[0]->items[2]->k == T_VAR && e->terms[0]->items[2]->s == t->s &&
+                  e->terms[0]->op == std::vector<std::string>{"minus"})
+                return coll_kind(e->terms[0]->items[0], mod, depth + 1) == 2 &&
+                               coll_kind(e->terms[0]->items[1], mod, depth + 1) == 2
+                           ? 2
+                           : 0;
+            }
+            if (expr_mentions(e, t->s)) return 0;  // bound (or used) before any definition
           }
         if (mod) {
           auto rs = mods_.rules(mod->pkg, t->s);
           if (rs.size() == 1 && rs[0]->kind == Rule::COMPLETE && !rs[0]->is_default && !rs[0]->is_else) {
             const auto* save = ctx_body_;
+            const auto* save_a = ctx_args_;
             ctx_body_ = &cbody(rs[0], {});
+            ctx_args_ = nullptr;
             const int k = coll_kind(rs[0]->value, rs[0]->mod, depth + 1);
             ctx_body_ = save;
+            ctx_args_ = save_a;
             return k;
           }
         }
@@ -814,11 +835,14 @@ class Comp {
     for (auto& r : rules) {
       if (r->is_else || (r->kind != Rule::COMPLETE && r->kind != Rule::PSET)) return false;
       const auto* save = ctx_body_;
+      const auto* save_a = ctx_args_;
       ctx_body_ = &cbody(r, {});
+      ctx_args_ = nullptr;
       bool ok = true;
       for (auto& e : *ctx_body_) ok = ok && err_free_expr(e, r->mod, depth + 1);
       ok = ok && err_free_term(r->kind == Rule::PSET ? r->key : r->value, r->mod, depth + 1);
       ctx_body_ = save;
+      ctx_args_ = save_a;
       if (!ok) return false;
       same_const = same_const && r->value && is_const(r->value) && same_term(r->value, rules[0]->value);
     }
@@ -892,11 +916,14 @@ class Comp {
     for (auto& r : rules) {
       if (r->kind != Rule::FUNC || r->is_else || r->is_default) return false;
       const auto* save = ctx_body_;
+      const auto* save_a = ctx_args_;
       ctx_body_ = &cbody(r, {});
+      ctx_args_ = &r->args;
       bool ok = true;
       for (auto& e : *ctx_body_) ok = ok && err_free_expr(e, r->mod, depth);
       ok = ok && err_free_term(r->value, r->mod, depth);
       ctx_body_ = save;
+      ctx_args_ = save_a;
       if (!ok) return false;
     }
     if (rules.size() == 1) return true;

@@ -1872,13 +1872,17 @@ __device__ __forceinline__ uint64_t key_hash(const PLane& L, uint64_t v) {
 }
 
 // key pass: the leaf's next key value (the lane's emission counter counts
-// them; a value past JKEYS_MAX fails the lane, and with it the index)
+// them; a value past JKEYS_MAX fails the lane, and with it the index). A
+// composite key value has no bucket and takes no slot: KH_NONE pads the unused
+// slots, and the host stops reading a leaf's keys at the first one.
 __device__ __forceinline__ void op_keyout(PLane& L, uint64_t v) {
   if (!gk_args.jkeys) return;
+  const uint64_t h = key_hash(L, v);
+  if (h == KH_NONE) return;
   const uint32_t j = L.en;
   if (j >= JKEYS_MAX) { lane_fallback(L, FB_HEAP); return; }
   L.en = j + 1;
-  gk_args.jkeys[(uint64_t)L.rv * JKEYS_MAX + j] = key_hash(L, v);
+  gk_args.jkeys[(uint64_t)L.rv * JKEYS_MAX + j] = h;
 }
 
 // opens a probe of the lane's constraint's index `site` (y >> 8) for R[b]:

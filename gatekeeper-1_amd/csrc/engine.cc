@@ -2120,6 +2120,20 @@ static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_resul
       if (rc == GK_OK) q->out = split_results(*all, k);
       else q->err = tl_err;
     }
+    // A failed launch (one input that is not JSON, a device or arena failure)
+    // must not fail unrelated callers: each request of the batch is evaluated
+    // again on its own, so every caller gets the result an uncoalesced
+    // gk_query would have given it.
+    if (rc != GK_OK && batch.size() > 1) {
+      for (auto* q : batch) {
+        std::vector<std::pair<const char*, size_t>> one{{q->input, q->len}};
+        gk_results* r1 = nullptr;
+        q->rc = eval_inputs(e, one, &r1);
+        q->out = q->rc == GK_OK ? r1 : nullptr;
+        q->err = q->rc == GK_OK ? std::string() : tl_err;
+        if (q->rc != GK_OK) delete r1;
+      }
+    }
     lk.lock();
     for (auto* q : batch) q->done = true;
     --c.inflight;

@@ -247,15 +247,28 @@ def exchange_audit(sweep, review_base: int, resource_of_review, constraints, lim
     gathered to `dst`, merged into an AuditWriter there (None elsewhere).
     Reviews the rank's sweep flagged (error / CPU fallback) are answered by
     `fallback(i)` -> [(constraint, msg, enforcementAction)] on that rank
-    before the exchange (AuditWriter.from_sweep); without one they raise."""
+    before the exchange (AuditWriter.from_sweep); without one they raise --
+    on every rank together: the all-reduce carries one more word, the number
+    of ranks that could not answer their flagged reviews, so no rank is left
+    waiting in a collective its peers never enter."""
     import json
     import torch
     import torch.distributed as dist
-    from .audit import AuditWriter, flagged_rows
+    from .audit import AuditWriter, FlaggedReviews, flagged_rows
     dev = device if device is not None else torch.device("cpu")
-    totals, frows = flagged_rows(sweep, fallback, review_base)
-    tot = torch.tensor(totals, dtype=torch.int64, device=dev)
+    err = None
+    try:
+        totals, frows = flagged_rows(sweep, fallback, review_base)
+    except FlaggedReviews as ex:
+        err, totals, frows = ex, [int(x) for x in sweep.totals], []
+    n = max(len(constraints), len(totals))
+    tot = torch.tensor(totals + [0] * (n - len(totals)) + [1 if err is not None else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
+    failed = int(tot[-1].item())
+    if failed:
+        raise err if err is not None else FlaggedReviews(
+            "%d peer rank(s) hold flagged reviews without a fallback evaluator" % failed)
+    tot = tot[:-1]
     rows = _sample_rows(sweep, review_base, resource_of_review)
     for rv, ar, j, c, head, ml, ea in frows:
         kind, name, ns = resource_of_review(rv - int(review_base))

@@ -68,6 +68,33 @@ def test_coalesced_callers_all_get_the_launch_error_without_a_device():
 
 
 @pytest.mark.gpu
+def test_one_bad_input_fails_only_its_own_caller():
+    """On the device: 32 concurrent coalesced callers, one of them with an
+    input that is not JSON.  That caller gets an error; every other caller
+    gets exactly the oracle's results for its own review."""
+    if not gkgpu.Driver.device_available():
+        pytest.fail("no HIP device visible")
+    pods, ns_of, ns_objs = W.gen_pods(32, seed=23, n_namespaces=6)
+    reviews = [augmented_review(p, ns_objs[n]) for p, n in zip(pods, ns_of)]
+    inputs = [json.dumps({"review": rv}) for rv in reviews]
+    bad = 9
+    inputs[bad] = '{"review": {"object": '
+    ts, cs = W.config2()
+    od = oracle_for(ts, cs)
+    d, _, _ = _driver(coalesce_us=20000, coalesce_max=64)
+    out, _ = _race(len(inputs), lambda i: d.query(VIOLATION, inputs[i]))
+    assert isinstance(out[bad], RuntimeError), out[bad]
+    for i, o in enumerate(out):
+        if i == bad:
+            continue
+        assert not isinstance(o, Exception), (i, o)
+        assert not any(o.status), (i, list(o.status))
+        assert collections.Counter(engine_rows(o, 1)[0]) == collections.Counter(oracle_review(od, reviews[i])), i
+    launches, served = d.coalesce_stats()
+    assert served == len(inputs) and launches < served
+
+
+@pytest.mark.gpu
 def test_coalesced_queries_equal_the_oracle():
     """64 concurrent Query(violation) calls with the coalescer on: every result
     set equals the oracle's for that caller's own review, and the calls were

@@ -192,6 +192,46 @@ def test_checker_multi_valued_keys_and_array_levels():
     assert probe == scan, (probe, scan)
 
 
+def _ingresses_with_composite_hosts(n, seed):
+    """gen_ingresses plus, on every fifth Ingress, a rule whose host is an
+    object or array placed before the string hosts: the composite key value has
+    no bucket and must not hide the string keys after it (devrt.h op_keyout)."""
+    objs, nss = W.gen_ingresses(n, seed=seed)
+    for i, o in enumerate(objs):
+        if i % 5 == 0:
+            o["spec"]["rules"].insert(0, {"host": {"x": i % 3}} if i % 2 else {"host": ["a", i % 4]})
+    return objs, nss
+
+
+def test_checker_composite_key_before_scalar_keys():
+    """a leaf whose first key value is composite keeps its later string keys in
+    the index: checker probe = scan = oracle, and nothing falls back"""
+    from oracle import cpu_baseline
+    objs, nss = _ingresses_with_composite_hosts(200, 12)
+    cs = [W.constraint("K8sUniqueIngressHost", "uih")]
+    extra = [(data_path(o), o) for o in objs]
+    d = _driver([W.UNIQUE_INGRESS_HOST], cs, extra, host_only=True)
+    b = d.stage_objects(objs, nss)
+    probe = cpu_baseline.sweep(d, b, threads=4)[1:]
+    scan = cpu_baseline.sweep(d, b, threads=4, joins=False)[1:]
+    assert probe == scan and probe[3] == 0, (probe, scan)
+    assert probe[1] == _oracle_count(oracle_for([W.UNIQUE_INGRESS_HOST], cs, extra), objs, nss) > 150
+
+
+@pytest.mark.gpu
+def test_composite_key_before_scalar_keys_on_gpu():
+    """the same Ingresses on the device: rows equal the oracle's, the index is built"""
+    objs, nss = _ingresses_with_composite_hosts(300, 13)
+    cs = [W.constraint("K8sUniqueIngressHost", "uih")]
+    extra = [(data_path(o), o) for o in objs]
+    drv = gkgpu.Driver()
+    rep, res = run_objects(drv, [W.UNIQUE_INGRESS_HOST], cs, objs, nss, extra_data=extra)
+    assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.fallback == 0 and rep.errors == 0 and rep.violations > 200, rep
+    st = drv.join_stats()
+    assert st["indexes"] == 1 and st["unindexed"] == 0, st
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("jit", [True, False])
 def test_unique_ingress_host_join_on_gpu(jit):

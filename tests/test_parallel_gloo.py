@@ -267,3 +267,47 @@ def test_audit_exchange_merges_flagged_reviews():
         p.join(60)
     assert status == "ok", same
     assert same and same_act and total > 100
+
+
+def _one_flagged_worker(rank, world, port, q):
+    """only rank 1 holds flagged reviews and nobody passes a fallback: every
+    rank must raise FlaggedReviews (none may wait in a collective)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "gatekeeper-1_amd")]
+        from gkgpu.audit import FlaggedReviews
+        from gkgpu.parallel import exchange_audit
+        per, cons, actions, res = _oracle_rows(60)
+        lo, hi = shard_range(len(per), rank, world)
+        flagged = {2, 5} if rank == 1 else set()
+        sweep = _flagged_sweep(per, lo, hi, len(cons), actions, 4, flagged)
+        try:
+            exchange_audit(sweep, lo, lambda i: res[lo + i], cons, limit=4)
+            q.put((rank, "returned"))
+        except FlaggedReviews as ex:
+            q.put((rank, "raised: " + str(ex)))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "err " + traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_audit_exchange_flagged_on_one_rank_raises_everywhere():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_one_flagged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert got[1].startswith("raised: 2 reviews flagged"), got
+    assert got[0].startswith("raised: 1 peer rank"), got
