@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="resources of the staged batch timed on the native CPU baseline (oracle/cpuvm.cc; "
                          "-1 = all of them, 0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cpu count))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every core this process may run on: the CPU affinity set, "
+                         "capped by a cgroup CPU quota when one is set)")
     ap.add_argument("--oracle-sample", type=int, default=0,
                     help="resources also timed on the Python oracle (1 core; 0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -414,7 +416,7 @@ def referenced_bytes(drv, batch, kind, cons_ids, threads, every=False):
             from oracle import cpu_baseline as CB
         except Exception:
             return None
-        r = CB.referenced(drv, batch, -1, threads=threads if threads > 0 else min(16, os.cpu_count() or 1))
+        r = CB.referenced(drv, batch, -1, threads=threads if threads > 0 else host_cpus()["lease"])
         r["constraints"] = [n for _k, n in cons_ids]
         return r
     if kind is None:
@@ -426,7 +428,7 @@ def referenced_bytes(drv, batch, kind, cons_ids, threads, every=False):
     except Exception:
         return None
     if threads <= 0:
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpus()["lease"]
     tot = {"nodes": 0, "strings": 0, "string_bytes": 0, "violations": 0, "flagged": 0, "constraints": []}
     for c, (k, name) in enumerate(cons_ids):
         if k != kind:
@@ -449,6 +451,29 @@ def device_info(dev):
         return None
 
 
+def host_cpus():
+    """the host cores this process is leased: nproc (os.cpu_count), the CPU
+    affinity set, and a cgroup CPU quota (v2 cpu.max or v1 cfs quota/period)
+    if one is set; `lease` = the affinity set, capped by the quota"""
+    import math
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    lease = min(aff, max(1, math.ceil(quota))) if quota else aff
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "lease": lease}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -468,10 +493,11 @@ def native_cpu_baseline(drv, batch, n_cpu, threads, gpu_sweep):
     reference's per-Review topdown + JSON round trips."""
     sys.path.insert(0, ROOT)
     from oracle import cpu_baseline as CB
+    hc = host_cpus()
     if threads <= 0:
-        threads = min(16, os.cpu_count() or 1)
+        threads = hc["lease"]
     secs, evals, viol, mbytes, flagged = CB.sweep(drv, batch, 0, n_cpu, threads)
-    out = {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port",
+    out = {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port", "host_cpus": hc,
            "sample": "%d resources x %d constraints of the same staged batch (%s); oracle/cpuvm.cc: the engine's "
                      "compiled bytecode + device runtime on host threads, NOT OPA (Go/OPA not buildable offline)"
                      % (n_cpu, len(gpu_sweep.totals), "all" if n_cpu == batch.n else "prefix"),
@@ -672,7 +698,8 @@ def webhook_native_cpu_baseline(templates, constraints, batches, threads):
     import gkgpu
     from gkgpu.client import Client
     from oracle import cpu_baseline as CB
-    threads = threads or min(16, os.cpu_count() or 1)
+    hc = host_cpus()
+    threads = threads or hc["lease"]
     d = gkgpu.Driver(host_only=True)
     cl = Client(d)
     for t in templates:
@@ -684,7 +711,7 @@ def webhook_native_cpu_baseline(templates, constraints, batches, threads):
     secs, evals, viol, mbytes, flagged = CB.sweep(d, b, threads=threads)
     b.free()
     d.close()
-    return {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port",
+    return {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port", "host_cpus": hc,
             "sample": "%d AdmissionReviews (the benchmark's %d micro-batches) x %d constraints; oracle/cpuvm.cc: the "
                       "engine's compiled bytecode + device runtime on host threads, NOT OPA (Go/OPA not buildable "
                       "offline)" % (len(inputs), len(batches), len(constraints)),

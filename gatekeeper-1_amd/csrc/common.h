@@ -73,6 +73,8 @@ enum Tag : uint32_t {
   V_SLICE = 10,                                    // SLICE: string id:32 | start:14 | len:14
   V_FMT = 11,                                      // FMT: deferred sprintf (template kernels only): fidx:24 <<32 | args (bit31: node, else heap list offset)
   V_GSTR = 12,                                     // GSTR: string in the evaluation's memo-string arena (off:40 << 20 | len:20)
+  V_GLIST = 13,                                    // GLIST: a list copied out at emission (devrt.h gval_copy): kind in bits
+                                                   // 56..59, the word offset of [len, 0, words...] in ebytes
 };
 enum ListKind : uint32_t { LK_SET = 1, LK_ARR = 2, LK_OBJ = 3 };
 
@@ -323,10 +325,15 @@ constexpr uint32_t FMT_MAXARGS = 6;
 //   VF_DEFER   msg_len = fidx | nargs << 24, the arguments in frec; the size
 //              pass prints its length, the format pass the bytes
 //   VF_DET_OBJ the details are the hook default `{}` (no staged bytes)
+//   VF_DET_VAL the details are the JSON of one frec word (index: the message's
+//              argument count when VF_DEFER, else 0), printed by the passes;
+//              the size pass stores their length in det_len
 // otherwise msg_len is the message length and ebytes[msg_off, ...) holds the
-// message (eager) followed by the details (unless VF_DET_OBJ); a deferred
-// message's details (unless VF_DET_OBJ) are at ebytes[msg_off, +det_len)
-constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2;
+// message (eager) followed by the details (unless VF_DET_OBJ / VF_DET_VAL); a
+// deferred message's details (unless VF_DET_*) are at ebytes[msg_off, +det_len)
+//   VF_NOPRINT set by the size pass: the message or details cannot be printed
+//              on the GPU (the review goes to the CPU); the tuple gets no bytes
+constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2, VF_DET_VAL = 4, VF_NOPRINT = 8;
 // the size / format passes work in tiles of FTILE consecutive tuples
 constexpr uint32_t FTILE = 256;  // one block pass: a small output still spreads over many blocks
 

@@ -78,6 +78,12 @@ constexpr int HCAP = GK_HCAP;  // heap words per lane (lists, big floats)
 #define GK_LDS_HWORDS_DEF GK_LDS_HWORDS
 static_assert(GK_LDS_HWORDS < GK_HCAP, "LDS heap words must leave a private-segment tail");
 constexpr int MAXLOOP = 16;    // loop nesting levels with per-iteration heap reclamation
+// loop levels a kernel's programs use (the template JIT defines it from the
+// program's deepest loop; audit_body clears only those watermarks)
+#ifndef GK_MAXDEPTH
+#define GK_MAXDEPTH MAXLOOP
+#endif
+static_assert(GK_MAXDEPTH >= 1 && GK_MAXDEPTH <= MAXLOOP, "GK_MAXDEPTH: 1..MAXLOOP loop levels");
 constexpr int BCAP = GK_BCAP;  // byte buffer per lane (computed strings; an emission's bytes in transit)
 // emission order key of a tuple (Viol.seq): (OP_ORD key << 8) | the lane's
 // emission index; a lane past either limit goes to the CPU fallback
@@ -291,7 +297,7 @@ __device__ __forceinline__ bool heap_val(uint64_t v) {
 }
 __device__ __forceinline__ void pin_escape(PLane& L, uint32_t range) {
   uint32_t lo = range & 0xff, hi = (range >> 8) & 0xff;
-  for (uint32_t d = lo; d <= hi && d < MAXLOOP; ++d) {
+  for (uint32_t d = lo; d <= hi && d < GK_MAXDEPTH; ++d) {
     if (L.keepH[d] < L.hp) L.keepH[d] = (uint16_t)L.hp;
     if (L.keepB[d] < L.bp) L.keepB[d] = (uint16_t)L.bp;
   }
@@ -483,15 +489,21 @@ __device__ __forceinline__ int tclass(uint64_t v) {
     case V_NUM: case V_INT: case V_BFN: return 3;
     case V_STR: case V_HSTR: case V_SLICE: case V_GSTR: return 4;
     case V_NODE: GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
-    case V_LIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
+    case V_LIST: case V_GLIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
   }
   return 0;
+}
+
+// a list copied out at emission (gval_copy), read by the size / format passes
+__device__ __forceinline__ const uint64_t* glist_words(uint64_t v) {
+  return (const uint64_t*)gk_args.ebytes + list_off(v);
 }
 
 // collection view helpers (NODE arrays/objects and heap lists)
 __device__ uint32_t coll_len(const PLane& L, uint64_t v) {
   if (vtag(v) == V_NODE) { GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].n; }
   if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
+  if (vtag(v) == V_GLIST) { uint32_t n = (uint32_t)glist_words(v)[0]; return list_kind(v) == LK_OBJ ? n / 2 : n; }
   return 0;
 }
 // i-th (key, value) of a collection
@@ -504,6 +516,13 @@ __device__ void coll_at(const PLane& L, uint64_t v, uint32_t i, uint64_t& k, uin
     return;
   }
   uint32_t kind = list_kind(v);
+  if (vtag(v) == V_GLIST) {
+    const uint64_t* w = glist_words(v) + 2;
+    if (kind == LK_OBJ) { k = w[2 * i]; val = w[2 * i + 1]; return; }
+    val = w[i];
+    k = kind == LK_SET ? val : mkint(i);
+    return;
+  }
   if (kind == LK_OBJ) { k = list_at(L, v, 2 * i); val = list_at(L, v, 2 * i + 1); return; }
   val = list_at(L, v, i);
   k = kind == LK_SET ? val : mkint(i);
@@ -2146,39 +2165,105 @@ __device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k
   e[0] = k0; e[1] = k1; e[2] = v; e[3] = gm_check(h, v);
 }
 
+// ------------------------------------------------------------------ values copied out at emission
+// A deferred message's argument or a details value that lives in the lane heap
+// -- a set, array or object such as k8srequiredlabels' `missing` and
+// {"missing_labels": missing} (demo/agilebank/templates/
+// k8srequiredlabels_template.yaml:39-46) -- is copied out with its tuple
+// instead of being printed into the lane's byte buffer: its words go to the
+// emission's ebytes reservation as [len, 0, words...] and the tuple's frec word
+// names them (V_GLIST); the size and format passes print it (coll_len /
+// coll_at read V_GLIST).  Members must be heap-free (memo_stable: interned
+// strings, numbers, document nodes) or, one level down, heap lists of such.
+constexpr uint32_t GVAL_MAXWORDS = 64;
+// words a copy of v takes (0: v is heap-free as it is); > GVAL_MAXWORDS: no copy
+__device__ __forceinline__ uint32_t gval_words(const PLane& L, uint64_t v) {
+  if (memo_stable(v)) return 0;
+  if (vtag(v) != V_LIST) return GVAL_MAXWORDS + 1;
+  const uint32_t n = list_len(L, v);
+  uint32_t w = 2 + n;
+  for (uint32_t i = 0; i < n && w <= GVAL_MAXWORDS; ++i) {
+    const uint64_t e = list_at(L, v, i);
+    if (memo_stable(e)) continue;
+    if (vtag(e) != V_LIST) return GVAL_MAXWORDS + 1;
+    const uint32_t m = list_len(L, e);
+    w += 2 + m;
+    for (uint32_t j = 0; j < m; ++j)
+      if (!memo_stable(list_at(L, e, j))) return GVAL_MAXWORDS + 1;
+  }
+  return w;
+}
+// copies v (gval_words(v) words) to ebytes word `at` onwards; the heap-free value
+__device__ __forceinline__ uint64_t gval_put(const PLane& L, uint64_t v, uint64_t* dst, uint32_t& at) {
+  if (memo_stable(v)) return v;
+  const uint32_t n = list_len(L, v), me = at;
+  at += 2 + n;
+  dst[me] = n;
+  dst[me + 1] = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t e = list_at(L, v, i);
+    if (memo_stable(e)) { dst[me + 2 + i] = e; continue; }
+    const uint32_t m = list_len(L, e), ce = at;
+    at += 2 + m;
+    dst[ce] = m;
+    dst[ce + 1] = 0;
+    for (uint32_t j = 0; j < m; ++j) dst[ce + 2 + j] = list_at(L, e, j);
+    dst[me + 2 + i] = mkv(V_GLIST, ((uint64_t)list_kind(e) << 56) | ce);
+  }
+  return mkv(V_GLIST, ((uint64_t)list_kind(v) << 56) | me);
+}
+
 // m: message register, d: details register (undefined when absent).  Every
 // active lane at the emission site calls it (the output reservations are
 // wave-level); a lane that already failed emits nothing.
 __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
   bool ok = !L.fail;
   bool defer = false;
-  uint32_t fidx = 0, n = 0;
+  uint32_t fidx = 0, n = 0, gw = 0;
   uint64_t args = 0;
   if (ok && vtag(m) == V_FMT) {
-    // a deferred message whose arguments are heap-free values (the record
-    // outlives this iteration's heap) goes to the format pass as its record;
-    // otherwise it is built in the lane buffer now
+    // a deferred message whose arguments are heap-free (or copied out,
+    // gval_words) goes to the format pass as its record -- it outlives this
+    // iteration's heap; otherwise it is built in the lane buffer now
     args = fmt_args(m);
     fidx = fmt_fidx(m);
     n = coll_len(L, args);
     defer = n <= FMT_MAXARGS;
-    for (uint32_t i = 0; i < n && defer; ++i) { uint64_t k, v; coll_at(L, args, i, k, v); defer = memo_stable(v); }
-    if (!defer) { m = force_fmt(L, m); ok = !L.fail; }
+    for (uint32_t i = 0; i < n && defer; ++i) {
+      uint64_t k, v;
+      coll_at(L, args, i, k, v);
+      gw += gval_words(L, v);
+      defer = gw <= GVAL_MAXWORDS;
+    }
+    if (!defer) { m = force_fmt(L, m); ok = !L.fail; gw = 0; }
   }
   if (ok && !defer && !is_strv(m)) { lane_error(L); ok = false; }  // types.Result.msg must unmarshal as a string
-  // details JSON in the lane buffer above everything live (not kept: copied out below)
+  // details: a value the passes print as JSON (VF_DET_VAL, in the frec word
+  // after the message's arguments), else JSON in the lane buffer above
+  // everything live (not kept: copied out below)
   const char* det = nullptr;
-  uint32_t dlen = 2;
+  uint32_t dlen = 2, dw = 0;
+  bool dval = false;
+  const uint32_t di = defer ? n : 0u;
   if (ok && vtag(d) != V_UNDEF) {
-    Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
-    if (!put_json(L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); ok = false; }
-    else if (!(o.n == 2 && o.p[0] == '{' && o.p[1] == '}')) { det = o.p; dlen = o.n; }
+    if (di < FMT_MAXARGS) {
+      dw = gval_words(L, d);
+      dval = gw + dw <= GVAL_MAXWORDS;
+    }
+    if (!dval) {
+      dw = 0;
+      Out o{L.B + L.bp, 0, (uint32_t)(BCAP - L.bp), false};
+      if (!put_json(L, o, d) || o.ovf) { lane_fallback(L, o.ovf ? FB_MSG_LEN : FB_PRINT); ok = false; }
+      else if (!(o.n == 2 && o.p[0] == '{' && o.p[1] == '}')) { det = o.p; dlen = o.n; }
+    }
   }
   SView ms{nullptr, 0};
   if (ok && !defer) ms = sview(L, m);
   uint32_t seq = 0;
   if (ok) ok = next_seq(L, seq);
-  const uint32_t eb = ok ? (defer ? 0u : ms.n) + (det ? dlen : 0u) : 0u;
+  const uint32_t sb = ok ? (defer ? 0u : ms.n) + (det ? dlen : 0u) : 0u;  // staged bytes
+  const uint32_t words = ok ? gw + dw : 0u;                               // copied-out words (8-B aligned)
+  const uint32_t eb = sb + (words ? 8u * words + 7u : 0u);
   const uint64_t eoff = wave_reserve_bytes(&gk_args.counters[1], ok, eb);
   const uint64_t slot = wave_reserve(&gk_args.counters[0], ok);
   if (!ok) return false;
@@ -2186,6 +2271,8 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
   if (slot >= gk_args.out_cap || eoff + eb > gk_args.ebytes_cap) { slot_overflow(L); return true; }
   if (!defer) copy_out(eoff, ms.p, ms.n);
   if (det) copy_out(eoff + (defer ? 0u : ms.n), det, dlen);
+  uint64_t* gdst = (uint64_t*)gk_args.ebytes;
+  uint32_t at = (uint32_t)((eoff + sb + 7) >> 3);
   Viol v;
   v.review = L.rv;
   v.constraint = L.cn;
@@ -2193,15 +2280,16 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
   v.rule = (uint16_t)rule;
   v.msg_len = defer ? (fidx | (n << 24)) : ms.n;
   v.msg_off = eoff;
-  v.det_len = dlen;
-  v.pad = (defer ? VF_DEFER : 0u) | (det ? 0u : VF_DET_OBJ);
+  v.det_len = dval ? 0u : dlen;
+  v.pad = (defer ? VF_DEFER : 0u) | (dval ? VF_DET_VAL : det ? 0u : VF_DET_OBJ);
   gk_args.out[slot] = v;
   if (defer)
     for (uint32_t i = 0; i < n; ++i) {
       uint64_t k, a;
       coll_at(L, args, i, k, a);
-      gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = a;
+      gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = gval_put(L, a, gdst, at);
     }
+  if (dval) gk_args.frec[(uint64_t)di * gk_args.out_cap + slot] = gval_put(L, d, gdst, at);
   return true;
 }
 
@@ -2314,8 +2402,12 @@ __device__ __forceinline__ void audit_body(Run run) {
   uint32_t r = rp;                   // the review's index in the caller's batch
   Lane L0;
   PLane& L = *(PLane*)&L0;
-  L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0; L.memo_ok = 0;
-  for (int d = 0; d < MAXLOOP; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
+  // the lane scalars (LDS in template kernels); the private-segment fields
+  // the predicate reads (loop watermarks, VM memo flags) are set only for a
+  // matched lane, right before it runs: a scratch store is HBM write traffic
+  // once the line leaves L2, and most lanes of a wide constraint set fail the
+  // match
+  L.hp = 0; L.bp = 0; L.ord = 0; L.ord_base = 0; L.fail = 0; L.reason = 0; L.en = 0; L.steps = 0;
   bool live = rp < gk_args.nrev;
   ReviewCol rc{};
   if (live) {
@@ -2346,6 +2438,8 @@ __device__ __forceinline__ void audit_body(Run run) {
       else if (mr == -2) L.fail = RF_FALLBACK;
       else if (mr == 1 && (m.flags & MF_FALLBACK)) lane_fallback(L, FB_TEMPLATE);  // template served by CPU OPA
       else if (mr == 1 && m.prog != NO_ID) {
+        L.memo_ok = 0;
+        for (int d = 0; d < GK_MAXDEPTH; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
         uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
         run(L, mkv(V_NODE, rc.root), params, m.prog, plo, pn);
       }

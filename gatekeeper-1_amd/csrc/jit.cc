@@ -43,12 +43,16 @@ std::string hex16(uint64_t v) {
 // deferred sprintf is forced into the lane buffer first).  Not listed: MOV and
 // YIELD (copy the deferred value; op_yield forces before a conflict check),
 // EMIT's message (formatted into the output at flush), jumps (a V_FMT is
-// neither undefined nor a boolean) and MEMO_PUT (never caches a V_FMT).
+// neither undefined nor a boolean), MEMO_PUT (never caches a V_FMT) and
+// MEMO_GET: a V_FMT argument is no memo key (gm_key), so the call is
+// evaluated with the deferred value -- get_message(parameters, def_msg) in
+// demo/agilebank's k8srequiredlabels returns def_msg still unprinted, and a
+// constraint with a `message` parameter never prints it at all.
 std::vector<uint32_t> fmt_reads(const Ins& in) {
   std::vector<uint32_t> rs;
   auto add = [&](uint32_t r) { if (r != 0xffff) rs.push_back(r); };
   switch (in.op) {
-    case OP_GET: case OP_CMP: case OP_ARITH: case OP_MEMO_GET: add(in.b); add(in.c); break;
+    case OP_GET: case OP_CMP: case OP_ARITH: add(in.b); add(in.c); break;
     case OP_GETK: case OP_ITER_INIT: case OP_SPRINTF: case OP_LEN_EQ: case OP_TABLE: case OP_EMIT: case OP_JPROBE:
       add(in.b);
       break;
@@ -793,6 +797,25 @@ static StagePlan stage_plan(const Program& p, const Gen& g) {
   return sp;
 }
 
+// the loop levels a program's lane uses (devrt.h GK_MAXDEPTH): loop depths
+// of its iterations and probes, and the ranges values escaping loops pin
+constexpr uint32_t kMaxLoop = 16;  // devrt.h MAXLOOP
+static int max_depth(const Program& p, const CodeBank& bank) {
+  uint32_t m = 0;
+  for (uint32_t k = 0; k < p.code_len; ++k) {
+    const Ins& in = bank.code[p.code_off + k];
+    uint32_t d = 0;
+    switch (in.op) {
+      case OP_ITER_INIT: case OP_ITER_NEXT: case OP_JNEXT: d = in.y < kMaxLoop ? in.y : 0; break;
+      case OP_JPROBE: d = (in.y & 0xff) < kMaxLoop ? (in.y & 0xff) : 0; break;
+      case OP_LIST_ADD: case OP_OBJ_PUT: case OP_YIELD: d = (in.y >> 8) & 0xff; break;
+      default: break;
+    }
+    m = std::max(m, d);
+  }
+  return (int)std::min<uint32_t>(m + 1, kMaxLoop);
+}
+
 static std::string inline_hot_tag(const Program& p) {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
@@ -827,6 +850,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words(p) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(p) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
+  o << "#define GK_MAXDEPTH " << max_depth(p, bank) << "\n";
   const StagePlan sp = stage_plan(p, g);
   if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
   if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
@@ -881,6 +905,9 @@ std::string jit_fused_source(const std::vector<const Program*>& progs, const std
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words(*big) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(*big) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
+  int depth = 1;
+  for (auto* p : progs) depth = std::max(depth, max_depth(*p, bank));
+  o << "#define GK_MAXDEPTH " << depth << "\n";
   if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
   if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
   o << "#include \"devrt.h\"\n"

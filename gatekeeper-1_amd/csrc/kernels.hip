@@ -193,7 +193,16 @@ __device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint6
   return true;
 }
 
-__device__ __forceinline__ uint32_t det_bytes(const Viol& v) { return (v.pad & VF_DET_OBJ) ? 2u : v.det_len; }
+// a tuple's details bytes: the hook default `{}`, staged bytes, or (VF_DET_VAL)
+// the length the size pass printed and stored in det_len
+__device__ __forceinline__ uint32_t det_bytes(const Viol& v) {
+  return (v.pad & VF_NOPRINT) ? 0u : (v.pad & VF_DET_OBJ) ? 2u : v.det_len;
+}
+// VF_DET_VAL: the frec word holding the details value
+__device__ __forceinline__ uint64_t det_word(const Viol& v, uint64_t i) {
+  const uint32_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
+  return gk_args.frec[(uint64_t)di * gk_args.out_cap + i];
+}
 
 // The lane the size / format passes hand to the printers.  Deferred arguments
 // are heap-free values, so nothing reads it; a failing print only sets its
@@ -217,17 +226,26 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
       const uint64_t i = t * FTILE + k + threadIdx.x;
       if (i >= n) break;
       const Viol v = gk_args.out[i];
-      uint32_t ml = v.msg_len;
-      if (v.pad & VF_DEFER) {
-        if (!size_deferred_msg(L, v, i, ml)) {
-          // the emission-time outcome: this review goes to CPU OPA
-          atomicOr(&gk_args.rflags[v.review], (uint32_t)RF_FALLBACK);
-          if (gk_args.rreason) atomicMax(&gk_args.rreason[v.review], (uint32_t)FB_PRINT);
-          atomicAdd(&gk_args.counters[2], 1ull);
-          ml = 0;
-        }
+      uint32_t ml = v.msg_len, dl = det_bytes(v);
+      bool printable = true;
+      if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml);
+      if (v.pad & VF_DET_VAL) {
+        Cnt cn{0, false};
+        printable = put_json(L, cn, det_word(v, i)) && printable;
+        dl = cn.n;
+        gk_args.out[i].det_len = dl;  // the format pass's det_bytes
       }
-      const uint32_t len = ml + det_bytes(v);
+      if (!printable) {
+        // the emission-time outcome: this review goes to CPU OPA; the tuple
+        // gets no bytes (the format pass prints nothing for it, and every
+        // consumer drops the rows of a flagged review)
+        atomicOr(&gk_args.rflags[v.review], (uint32_t)RF_FALLBACK);
+        if (gk_args.rreason) atomicMax(&gk_args.rreason[v.review], (uint32_t)FB_PRINT);
+        atomicAdd(&gk_args.counters[2], 1ull);
+        gk_args.out[i].pad = v.pad | VF_NOPRINT;
+        ml = dl = 0;
+      }
+      const uint32_t len = ml + dl;
       gk_args.lens[i] = len;
       s += len;
     }
@@ -326,6 +344,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         if (defer) fmt_run(L, o, v.msg_len & 0xffffffu, [&](uint32_t j) { return a[j]; });
         else puts_(o, gk_args.ebytes + v.msg_off, ml);
         if (v.pad & VF_DET_OBJ) { o.put('{'); o.put('}'); }
+        else if (v.pad & VF_DET_VAL) { if (dl) put_json(L, o, det_word(v, i)); }
         else puts_(o, gk_args.ebytes + v.msg_off + (defer ? 0u : ml), dl);
       };
       if (hi > lo && hi4 - lo4 <= FSTAGE) {

@@ -237,6 +237,15 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
     } else {
       k.msg_bytes += v.msg_len;
     }
+    if (v.pad & VF_DET_VAL) {
+      // details copied out at emission: the size pass prints them (JSON)
+      const uint32_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
+      Cnt cn{0, false};
+      if (!put_json(L, cn, gk_args.frec[(uint64_t)di * gk_args.out_cap + i])) {
+        ++k.flagged;
+        return;
+      }
+    }
     ++k.violations;
   }
 }

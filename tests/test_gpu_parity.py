@@ -58,7 +58,7 @@ def _assert_clean(rep, max_fallback_frac=0.0):
 
 def test_config1_namespaces_required_labels():
     ts, cs = W.config1()
-    nss = W.gen_namespaces(3000, seed=1)
+    nss = W.gen_namespaces(10000, seed=1)  # BASELINE configs[0]: all 10k Namespaces
     rep, res = run_objects(Driver(), ts, cs, nss, [None] * len(nss))
     _assert_clean(rep)
     assert rep.violations > 1000

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 N_SAMPLE = 2000
 
 
-def _run(cfg, n, gen, max_fallback_frac):
+def _run(cfg, n, gen, max_fallback_frac, inventory=(), oracle_factory=None):
     import torch
     import gkgpu
     from gkgpu import workloads as W
@@ -47,6 +47,8 @@ def _run(cfg, n, gen, max_fallback_frac):
         cl.add_template(t)
     for c in cs:
         cl.add_constraint(c)
+    for path, js in inventory:
+        drv.put_data(path, json.loads(js))
     batch = drv.stage_page(Page.from_lists(objs, nss))
     dev = torch.device("cuda", 0)
     dout = DeviceOutput(dev)
@@ -78,7 +80,7 @@ def _run(cfg, n, gen, max_fallback_frac):
         rows.append(Result(pos[rv], c, kind, name, b[:ml].decode("utf-8", "surrogateescape"),
                            b[ml:].decode("utf-8", "surrogateescape"), ea[(kind, name)]))
     sub = Results(rows, [int(status[i]) if len(status) else 0 for i in sample], [0] * len(sample), [])
-    od = oracle_for(ts, cs)
+    od = oracle_factory(ts, cs) if oracle_factory else oracle_for(ts, cs)
     reviews = [augmented_review(json.loads(objs[i]), None if nss[i] is None else json.loads(nss[i])) for i in sample]
     rep = compare(od, reviews, sub)
     print("config %d sample:" % cfg, rep, "heaviest lane emitted", int(counts.max()), flush=True)
@@ -100,3 +102,63 @@ def test_config2_bench_workload_parity_at_1m():
 def test_config4_bench_workload_parity_at_1_25m():
     from gkgpu import workloads as W
     _run(4, 1_250_000, lambda n: W.gen_config4_json(n, seed=1234, start=0), 0.01)
+
+
+def test_config3_bench_workload_parity_at_1m():
+    """config 3: 1M Deployments + Services x the 10 allowedRegex constraints"""
+    from gkgpu import workloads as W
+    _run(3, 1_000_000, lambda n: W.gen_config3_json(n, seed=7, start=0), 0.0)
+
+
+class _KeyGroupOracle:
+    """The oracle for config 6 at 200K synced objects.  Scanning the whole
+    inventory per review (what topdown does for unique-label /
+    unique-service-selector) is out of reach for the Python restatement at
+    this size, so per sampled review the oracle's data.inventory holds every
+    synced object whose JSON carries the review's own `app` value as a string
+    token -- a superset of the objects whose label value / flattened selector
+    can equal the review's, the only ones the templates' equality literal lets
+    produce a row (k8suniquelabel_template.yaml:49-55,
+    k8suniqueserviceselector_template.yaml:40-46) -- plus 24 objects of other
+    keys.  The device evaluated against all 200K."""
+
+    def __init__(self, od, inventory, seed=6):
+        import re
+        self.od = od
+        self.app = re.compile(r'"app":"(app-[0-9]+)"')
+        self.groups = {}
+        for path, js in inventory:
+            for a in set(self.app.findall(js)):
+                self.groups.setdefault(a, []).append((path, js))
+        self.inv = inventory
+        self.rng = random.Random(seed)
+
+    def query(self, path, input_json):
+        rv = json.loads(input_json)["review"]
+        obj = rv.get("object") or {}
+        a = ((obj.get("metadata") or {}).get("labels") or {}).get("app") or \
+            ((obj.get("spec") or {}).get("selector") or {}).get("app")
+        put = list(self.groups.get(a, [])) if isinstance(a, str) else []
+        put += [self.inv[self.rng.randrange(len(self.inv))] for _ in range(24)]
+        seen = set()
+        put = [(p, js) for p, js in put if not (p in seen or seen.add(p))]
+        for p, js in put:
+            self.od.put_data(p, js)
+        try:
+            return self.od.query(path, input_json)
+        finally:
+            for p, _ in put:
+                self.od.delete_data(p)
+
+
+def test_config6_bench_workload_parity_at_200k():
+    """config 6: the agilebank constraints + unique-label over 200K objects
+    that are also the synced inventory (the bench's join workload); the
+    stratified sample against the key-group oracle above"""
+    from gkgpu import workloads as W
+    from parity import oracle_for
+    objs, nss = W.gen_config6_json(200_000)
+    inv = W.inventory_paths(objs)
+    rep = _run(6, len(objs), lambda n: (objs, nss), 0.0, inventory=inv,
+               oracle_factory=lambda ts, cs: _KeyGroupOracle(oracle_for(ts, cs), inv))
+    assert rep.violations > 200, rep
