@@ -707,15 +707,26 @@ def webhook_native_cpu_baseline(templates, constraints, batches, threads):
     for c in constraints:
         cl.add_constraint(c)
     inputs = [x for b in batches for x in b]
+    # the port parses and flattens the requests' JSON as the GPU path does
+    # (the engine's parallel flattener, micro-batch by micro-batch), then
+    # evaluates them: `value` counts both, as the GPU latency does
+    stage_s = 0.0
+    for bt in batches:
+        t0 = time.perf_counter()
+        sb = d.debug_stage_inputs(bt)
+        stage_s += time.perf_counter() - t0
+        sb.free()
     b = d.debug_stage_inputs(inputs)
     secs, evals, viol, mbytes, flagged = CB.sweep(d, b, threads=threads)
     b.free()
     d.close()
-    return {"value": evals / secs, "unit": "evals/s", "cores": threads, "kind": "port", "host_cpus": hc,
-            "sample": "%d AdmissionReviews (the benchmark's %d micro-batches) x %d constraints; oracle/cpuvm.cc: the "
-                      "engine's compiled bytecode + device runtime on host threads, NOT OPA (Go/OPA not buildable "
-                      "offline)" % (len(inputs), len(batches), len(constraints)),
-            "seconds": secs, "violations": viol, "message_bytes": mbytes, "flagged_pairs": flagged,
+    return {"value": evals / (secs + stage_s), "unit": "evals/s", "cores": threads, "kind": "port", "host_cpus": hc,
+            "value_eval_only": evals / secs, "stage_seconds": stage_s,
+            "sample": "%d AdmissionReviews (the benchmark's %d micro-batches) x %d constraints; request JSON parsed and "
+                      "flattened per micro-batch, then oracle/cpuvm.cc: the engine's compiled bytecode + device runtime "
+                      "on host threads, NOT OPA (Go/OPA not buildable offline)" % (len(inputs), len(batches),
+                                                                                   len(constraints)),
+            "seconds": secs + stage_s, "violations": viol, "message_bytes": mbytes, "flagged_pairs": flagged,
             "cpu_model": cpu_model()}
 
 

@@ -231,7 +231,24 @@ struct EvalCtx {
   uint32_t perm_nodes = 0;
   void* perm_buf = nullptr;  // the d_nodes buffer that copy went to
   NodeArena arena;           // host documents of the current query (node id perm_nodes + k)
+  // pinned host staging for the readback: several device-to-host copies are
+  // queued back to back and waited for once (a pageable copy syncs each time)
+  char* h_pin = nullptr;
+  size_t h_pin_cap = 0;
+  char* pin(size_t n) {
+    if (n <= h_pin_cap) return h_pin;
+    if (h_pin) hipHostFree(h_pin);
+    h_pin = nullptr;
+    h_pin_cap = 0;
+    const size_t cap = std::max<size_t>(n + (n >> 1), 1 << 16);
+    if (hipHostMalloc((void**)&h_pin, cap, hipHostMallocDefault) != hipSuccess) { h_pin = nullptr; return nullptr; }
+    h_pin_cap = cap;
+    return h_pin;
+  }
   void release_all() {
+    if (h_pin) hipHostFree(h_pin);
+    h_pin = nullptr;
+    h_pin_cap = 0;
     for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
                     &d_clist, &d_gmemo, &d_mstr, &d_mtop, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
                     &d_part})
@@ -1671,10 +1688,28 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     // size, spine and format passes over the tuples of every launch above
     int flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 1]);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)flr));
-    if (hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
+    // one wait for the kernels and the small readbacks: counters, per-launch
+    // counter snapshots, totals, and the per-review flags and reasons, queued
+    // into the context's pinned buffer
+    const size_t o_snap = 32, o_tot = o_snap + 16 * plan.size(), o_fl = o_tot + 8 * (size_t)ncons,
+                 o_rs = o_fl + 4 * (size_t)nrev, o_end = o_rs + 4 * (size_t)nrev;
+    char* hp = x->pin(o_end);
+    if (!hp) return fail(e, GK_EDEVICE, "pinned host allocation failed");
+    bool qok = hipMemcpyAsync(hp, x->d_counters.p, 32, hipMemcpyDeviceToHost, x->stream) == hipSuccess &&
+               hipMemcpyAsync(hp + o_snap, (char*)x->d_counters.p + 64, 16 * plan.size(), hipMemcpyDeviceToHost,
+                              x->stream) == hipSuccess &&
+               hipMemcpyAsync(hp + o_tot, x->d_totals.p, 8 * (size_t)ncons, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
+    // a large batch (an audit sweep) reads the per-review words only when
+    // something was flagged (below); a micro-batch reads them right away
+    const bool early_flags = nrev <= 65536;
+    if (early_flags)
+      qok = qok &&
+            hipMemcpyAsync(hp + o_fl, x->d_rflags.p, 4 * (size_t)nrev, hipMemcpyDeviceToHost, x->stream) == hipSuccess &&
+            hipMemcpyAsync(hp + o_rs, x->d_rreason.p, 4 * (size_t)nrev, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
+    if (!qok || hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "kernel execution failed");
     // [0] tuples, [1] staged bytes, [2] lanes that flagged their review (error/fallback), [3] output bytes
     uint64_t counters[4];
-    d2h(x, counters, x->d_counters.p, 32);
+    memcpy(counters, hp, 32);
     if (counters[0] > x->out_cap || counters[1] > x->ebytes_cap) {
       x->out_cap = std::max<size_t>(x->out_cap * 2, counters[0] + 1024);
       x->ebytes_cap = std::max<size_t>(x->ebytes_cap * 2, (size_t)counters[1] + 65536);
@@ -1694,7 +1729,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     res->launches.clear();
     std::vector<uint64_t> snap(2 * plan.size());
-    d2h(x, snap.data(), (char*)x->d_counters.p + 64, 16 * plan.size());
+    memcpy(snap.data(), hp + o_snap, 16 * plan.size());
     for (size_t i = 0; i < plan.size(); ++i) {
       float kms = 0;
       hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
@@ -1718,7 +1753,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     res->failed_lanes = counters[2];
     res->epoch = ++x->eval_epoch;
     std::vector<uint64_t> tot(ncons);
-    d2h(x, tot.data(), x->d_totals.p, ncons * 8);
+    memcpy(tot.data(), hp + o_tot, ncons * 8);
     for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = tot[c];
     bool ea_err = false;
     for (auto* c : e->corder) ea_err |= c->ea_error;
@@ -1731,8 +1766,13 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     res->status.assign(nrev, 0);
     res->reason.assign(nrev, 0);
-    d2h(x, res->status.data(), x->d_rflags.p, nrev * 4);
-    d2h(x, res->reason.data(), x->d_rreason.p, nrev * 4);
+    if (early_flags) {
+      memcpy(res->status.data(), hp + o_fl, nrev * 4);
+      memcpy(res->reason.data(), hp + o_rs, nrev * 4);
+    } else {
+      d2h(x, res->status.data(), x->d_rflags.p, nrev * 4);
+      d2h(x, res->reason.data(), x->d_rreason.p, nrev * 4);
+    }
     if (hist) {
       std::lock_guard<std::mutex> g(e->dbg_mu);
       e->pchist.assign(ncode, 0);
@@ -1756,10 +1796,27 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     std::vector<Viol> vs(counters[0]);
     std::string bytes;
-    if (counters[0]) d2h(x, vs.data(), x->d_out.p, counters[0] * sizeof(Viol));
-    if (decode) {
-      bytes.assign(counters[3], '\0');
-      if (counters[3]) d2h(x, &bytes[0], x->d_bytes.p, counters[3]);
+    {
+      // tuples and (decoding) message bytes: two copies into the pinned
+      // buffer, one wait (a large output goes through pageable copies: no
+      // pinned buffer of its size is kept)
+      const size_t tb = counters[0] * sizeof(Viol), bb = decode ? counters[3] : 0;
+      char* hq = tb + bb <= ((size_t)64 << 20) ? x->pin(tb + bb) : nullptr;
+      if (hq) {
+        bool cok = true;
+        if (tb) cok = hipMemcpyAsync(hq, x->d_out.p, tb, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
+        if (bb && cok) cok = hipMemcpyAsync(hq + tb, x->d_bytes.p, bb, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
+        if (!cok || ((tb || bb) && hipStreamSynchronize(x->stream) != hipSuccess))
+          return fail(e, GK_EDEVICE, "result download failed");
+        if (tb) memcpy(vs.data(), hq, tb);
+        if (decode) bytes.assign(hq + tb, bb);
+      } else {
+        if (tb) d2h(x, vs.data(), x->d_out.p, tb);
+        if (decode) {
+          bytes.assign(bb, '\0');
+          if (bb) d2h(x, &bytes[0], x->d_bytes.p, bb);
+        }
+      }
     }
     res->ms[3] = ms_since(t1);
     auto t2 = Clock::now();

@@ -15,6 +15,11 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <thread>
 #include <mutex>
 #include <unordered_map>
@@ -37,6 +42,82 @@ int default_threads() {
   // the GPU box grants a 16-CPU share whatever the machine's CPU count
   return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
 }
+
+// ------------------------------------------------------------------ worker pool
+namespace {
+struct PoolJob {
+  const std::function<void(int)>* f;
+  int n;
+  std::atomic<int> left;
+  std::mutex mu;
+  std::condition_variable cv;
+};
+struct WorkPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<std::shared_ptr<PoolJob>, int>> q;  // (job, index)
+  int workers = 0;
+  static void finish(PoolJob& j) {
+    if (j.left.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> g(j.mu);
+      j.cv.notify_all();
+    }
+  }
+  void worker() {
+    for (;;) {
+      std::pair<std::shared_ptr<PoolJob>, int> t;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !q.empty(); });
+        t = q.front();
+        q.pop_front();
+      }
+      (*t.first->f)(t.second);
+      finish(*t.first);
+    }
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    if (n <= 0) return;
+    if (n == 1) { f(0); return; }
+    auto job = std::make_shared<PoolJob>();
+    job->f = &f;
+    job->n = n;
+    job->left = n;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      const int want = std::max(1, default_threads() - 1);
+      while (workers < want) {
+        std::thread([this] { worker(); }).detach();
+        ++workers;
+      }
+      for (int i = 1; i < n; ++i) q.push_back({job, i});
+    }
+    cv.notify_all();
+    f(0);
+    finish(*job);
+    // help with whatever is queued (this job's indices or another caller's)
+    for (;;) {
+      std::pair<std::shared_ptr<PoolJob>, int> t;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (q.empty()) break;
+        t = q.front();
+        q.pop_front();
+      }
+      (*t.first->f)(t.second);
+      finish(*t.first);
+    }
+    std::unique_lock<std::mutex> lk(job->mu);
+    job->cv.wait(lk, [&] { return job->left.load() == 0; });
+  }
+};
+WorkPool& pool() {
+  static WorkPool* p = new WorkPool();  // never destroyed: detached workers outlive static destructors
+  return *p;
+}
+}  // namespace
+
+void parallel_run(int n, const std::function<void(int)>& f) { pool().run(n, f); }
 
 ReviewCol review_columns(const Store& st, const Store& gst, const NsCache& ns_cache, uint32_t root,
                          bool* ns_labels_global) {
@@ -437,12 +518,7 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
   using Clock = std::chrono::steady_clock;
   auto ms = [](Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   const int T = (int)parts.size();
-  auto pfor = [&](const std::function<void(int)>& f) {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(f, t);
-    f(0);
-    for (auto& x : th) x.join();
-  };
+  auto pfor = [&](const std::function<void(int)>& f) { parallel_run(T, f); };
   // 1.
   out.cols.resize(n);
   out.weight.resize(n);
@@ -726,10 +802,7 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
         out.resources[p.lo + i] = ResourceIds{str(r.api_version), str(r.kind), str(r.name), str(r.ns)};
       }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { relocate(parts[t]); });
-    relocate(parts[0]);
-    for (auto& x : th) x.join();
+    parallel_run(T, [&](int t) { relocate(parts[t]); });
   }
   if (getenv("GKGPU_FLATTEN_TRACE"))
     fprintf(stderr, "flatten: relocate %.1f ms\n", std::chrono::duration<double, std::milli>(Clock::now() - t15).count());
@@ -756,10 +829,7 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
     parts[t].count_paths = order != nullptr;
   }
   {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { run_part(parts[t], gst, ns_cache, excluded, pg); });
-    run_part(parts[0], gst, ns_cache, excluded, pg);
-    for (auto& x : th) x.join();
+    parallel_run(T, [&](int t) { run_part(parts[t], gst, ns_cache, excluded, pg); });
   }
   for (auto& p : parts)
     if (!p.err.empty()) { err = p.err; return false; }
@@ -772,25 +842,35 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
 bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,
                      const std::vector<std::pair<const char*, size_t>>& inputs, uint32_t base, NodeArena& dst,
                      std::vector<ReviewCol>& cols, std::string& err) {
-  std::vector<Part> parts(1);
-  Part& p = parts[0];
-  p.lo = 0;
-  p.hi = inputs.size();
-  JDoc d;
-  for (size_t i = 0; i < inputs.size(); ++i) {
-    JsonReader rd(inputs[i].first, inputs[i].second, &d);
-    int root = rd.parse();
-    if (root < 0) { err = "invalid input JSON: " + d.err; return false; }
-    int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
-    uint32_t rn = rv >= 0 ? p.st.add_doc(d, rv) : NO_ID;
-    bool glob = false;
-    p.cols.push_back(review_columns(p.st, gst, ns_cache, rn, &glob));
-    p.nsglob.push_back(glob);
-    p.weight.push_back(0);
-    p.res.push_back(ResourceIds{p.st.s_empty, p.st.s_empty, p.st.s_empty, p.st.s_empty});
+  // parts of >= 16 inputs on the worker pool (a webhook micro-batch of 256
+  // AdmissionReviews: 16 parts); the first input that is not JSON fails the call
+  const size_t n = inputs.size();
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 16));
+  std::vector<Part> parts(T);
+  for (int t = 0; t < T; ++t) {
+    parts[t].lo = n * t / T;
+    parts[t].hi = n * (t + 1) / T;
   }
+  parallel_run(T, [&](int t) {
+    Part& p = parts[t];
+    JDoc d;
+    for (size_t i = p.lo; i < p.hi; ++i) {
+      JsonReader rd(inputs[i].first, inputs[i].second, &d);
+      int root = rd.parse();
+      if (root < 0) { p.err = "invalid input JSON: " + d.err; return; }
+      int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
+      uint32_t rn = rv >= 0 ? p.st.add_doc(d, rv) : NO_ID;
+      bool glob = false;
+      p.cols.push_back(review_columns(p.st, gst, ns_cache, rn, &glob));
+      p.nsglob.push_back(glob);
+      p.weight.push_back(0);
+      p.res.push_back(ResourceIds{p.st.s_empty, p.st.s_empty, p.st.s_empty, p.st.s_empty});
+    }
+  });
+  for (auto& p : parts)
+    if (!p.err.empty()) { err = p.err; return false; }
   FlatResult out;
-  if (!merge_parts(gst, smu, parts, base, dst, out, inputs.size(), err)) return false;
+  if (!merge_parts(gst, smu, parts, base, dst, out, n, err)) return false;
   cols.swap(out.cols);
   return true;
 }

@@ -126,6 +126,12 @@ bool flatten_reviews(Store& st, std::mutex& smu, const NsCache& ns_cache,
 
 int default_threads();
 
+// Runs f(0) .. f(n-1) in parallel on the engine's persistent host workers
+// (created once, sized to default_threads()) and the calling thread; returns
+// when all are done.  Concurrent callers share the workers.  A webhook
+// micro-batch is too small to pay for starting threads per call.
+void parallel_run(int n, const std::function<void(int)>& f);
+
 // id-independent content hash of the document rooted at `node` (`nodes`: the
 // node array its ids index; strings and numbers of `st`)
 uint64_t doc_hash(const Store& st, const Node* nodes, uint32_t node);

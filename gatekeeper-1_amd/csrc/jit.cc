@@ -453,6 +453,52 @@ std::string table_inline(const CodeBank& bank, const Store& st, uint32_t off, co
   return o.str();
 }
 
+// Registers an instruction reads and writes (the VM's semantics,
+// kernels.hip run_program); MEMO_GET's write is the hit path's.
+void ins_regs(const Ins& in, std::vector<uint32_t>& rd, std::vector<uint32_t>& wr) {
+  rd.clear();
+  wr.clear();
+  auto R = [&](uint32_t r) { if (r != 0xffff) rd.push_back(r); };
+  auto W = [&](uint32_t r) { if (r != 0xffff) wr.push_back(r); };
+  switch (in.op) {
+    case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_KEYOUT: R(in.a); break;
+    case OP_LOADK: case OP_LOADREV: case OP_LOADPARAM: case OP_LIST_NEW: W(in.a); break;
+    case OP_MOV: case OP_GETK: case OP_SPRINTF: case OP_TABLE: case OP_LEN_EQ: R(in.b); W(in.a); break;
+    case OP_GET: case OP_CMP: case OP_ARITH: R(in.b); R(in.c); W(in.a); break;
+    case OP_ITER_INIT: R(in.b); W(in.a); W(in.a + 1u); break;
+    case OP_ITER_NEXT: R(in.a); R(in.a + 1u); W(in.a + 1u); W(in.b); W(in.c); break;
+    case OP_LIST_ADD: case OP_YIELD: R(in.a); R(in.b); W(in.a); break;
+    case OP_OBJ_PUT: R(in.a); R(in.b); R(in.c); W(in.a); break;
+    case OP_CALL: for (uint32_t i = 0; i < in.c; ++i) R(in.b + i); W(in.a); break;
+    case OP_EMIT: R(in.a); R(in.b); break;
+    case OP_MEMO_GET: R(in.b); R(in.c); W(in.a); break;
+    case OP_MEMO_PUT: R(in.a); R(in.b); R(in.c); break;
+    case OP_JPROBE: R(in.b); W(in.a); W(in.a + 1u); break;
+    case OP_JNEXT: R(in.a); R(in.a + 1u); W(in.a + 1u); W(in.b); break;
+    case OP_JVAR: R(in.b); R(in.b + 1u); W(in.a); break;
+    default: break;
+  }
+}
+
+// successors of the instruction at pc (absolute), for data flow
+void ins_succ(const Ins& in, uint32_t pc, std::vector<uint32_t>& out) {
+  out.clear();
+  switch (in.op) {
+    case OP_END: case OP_FAIL_FALLBACK: return;
+    case OP_JMP: out.push_back(in.x); return;
+    case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: case OP_ITER_NEXT: case OP_MEMO_GET: case OP_JPROBE: case OP_JNEXT:
+      out.push_back(in.x);
+      out.push_back(pc + 1);
+      return;
+    default: out.push_back(pc + 1); return;
+  }
+}
+
+bool jump_op(uint16_t op) {
+  return op == OP_JMP || op == OP_JUNDEF || op == OP_JFALSE || op == OP_JTRUE || op == OP_ITER_NEXT ||
+         op == OP_MEMO_GET || op == OP_JPROBE || op == OP_JNEXT;
+}
+
 struct Gen {
   std::string pre;   // helper functions (literal regex DFAs)
   std::string body;  // body of the predicate function
@@ -533,13 +579,35 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
     if (memo2.count(m))
       o << "  uint64_t mkb0_" << m << ", mkb1_" << m << ", mvb_" << m << "; bool mokb_" << m << " = false;\n";
   }
+  // Param-keyed register memo (GKGPU_JIT_PMEMO, default on): a pure call whose
+  // arguments are derived from the constraint's parameters (jit.cc
+  // param_flow) -- canonify_cpu(input.parameters.cpu) in K8sContainerLimits,
+  // evaluated once per container -- keeps its last (arguments, value) in
+  // registers at that call site, so only the lane's first call probes the
+  // cross-lane memo.  The key is compared, so a varying parameter (an
+  // iteration over a parameter list) only misses.
+  std::set<uint32_t> psite;            // MEMO_GET pcs with a register entry
+  std::map<uint32_t, uint32_t> put_site;  // their MEMO_PUT pc -> MEMO_GET pc
+  {
+    const char* pm = getenv("GKGPU_JIT_PMEMO");
+    if (!pm || atoi(pm) != 0)
+      for (uint32_t pc = b0; pc < b1; ++pc) {
+        const Ins& in = bank.code[pc];
+        const uint32_t k = pc - b0;
+        if (in.op != OP_MEMO_GET || !gslots.count(in.y) || lslots.count(in.y) || !PF.reached[k]) continue;
+        if (!PF.has(k, in.b) || (in.c != 0xffff && !PF.has(k, in.c))) continue;
+        if (in.x < 1 || in.x > b1 || bank.code[in.x - 1].op != OP_MEMO_PUT || bank.code[in.x - 1].y != in.y) continue;
+        psite.insert(pc);
+        put_site[in.x - 1] = pc;
+      }
+  }
   const char* UND = "0x0000000000000000ull";
   std::function<std::string(uint64_t)> lit = [](uint64_t v) {
     char kb[40];
     snprintf(kb, sizeof kb, "0x%016llxull", (unsigned long long)v);
     return std::string(kb);
   };
-  for (uint32_t pc = b0; pc < b1; ++pc) {
+  auto emit = [&](uint32_t pc, std::ostringstream& o, const std::string& RET) {
     const Ins& in = bank.code[pc];
     const uint32_t k = pc - b0;
     if (labels.count(pc)) o << "L" << pc << ":;\n";
@@ -550,7 +618,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (F.has(k, r)) o << "  if (vtag(" << R(r) << ") == V_FMT) " << R(r) << " = force_fmt(L, " << R(r) << ");\n";
     o << "  ";
     switch (in.op) {
-      case OP_END: o << "return;"; break;
+      case OP_END: o << RET; break;
       case OP_JMP: o << "goto " << x << ";"; break;
       case OP_JUNDEF: o << "if (vtag(" << a << ") == V_UNDEF) goto " << x << ";"; break;
       case OP_JFALSE: o << "if (" << a << " == " << lit(((uint64_t)V_BOOL << 60) | 0) << ") goto " << x << ";"; break;
@@ -592,12 +660,12 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (in.c != 0xffff) o << " " << c << " = v_;";
         o << " }";
         break;
-      case OP_CMP: o << "if (!op_cmp(L, " << y << ", " << b << ", " << c << ", " << a << ")) return;"; break;
+      case OP_CMP: o << "if (!op_cmp(L, " << y << ", " << b << ", " << c << ", " << a << ")) " << RET; break;
       case OP_ARITH: o << a << " = arith(L, " << y << ", " << b << ", " << c << ");"; break;
       case OP_LIST_NEW: o << a << " = list_new(L, " << y << ", 4);"; break;
-      case OP_LIST_ADD: o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) return;"; break;
-      case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) return;"; break;
-      case OP_YIELD: o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) return;"; break;
+      case OP_LIST_ADD: o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) " << RET; break;
+      case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) " << RET; break;
+      case OP_YIELD: o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) " << RET; break;
       case OP_CALL: {
         // builtins are called directly with register operands (no argument
         // array, no dispatch on the builtin id)
@@ -658,7 +726,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       case OP_LEN_EQ: o << a << " = op_len_eq(L, " << b << ", " << y << ");"; break;
       case OP_EMIT:
         o << "if (!op_emit(L, " << a << ", " << (in.b == 0xffff ? std::string(UND) : b) << ", " << in.c << "u, " << y
-          << ")) return;";
+          << ")) " << RET;
         break;
       case OP_MEMO_GET: {
         // two entries per slot (most recent first): call sites of one function
@@ -670,7 +738,17 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (memo2.count(in.y))
           o << " if (mokb_" << m << " && mkb0_" << m << " == " << b << " && mkb1_" << m << " == " << k1 << ") { " << a
             << " = mvb_" << m << "; goto " << x << "; }";
-        if (gslots.count(in.y)) o << " if (gm_get(" << m << "u, " << b << ", " << k1 << ", " << a << ")) goto " << x << ";";
+        if (psite.count(pc)) {
+          const std::string ps = std::to_string(pc);
+          o << " if (psok_" << ps << " && psk0_" << ps << " == " << b << " && psk1_" << ps << " == " << k1 << ") { " << a
+            << " = psv_" << ps << "; goto " << x << "; }";
+          if (gslots.count(in.y))
+            o << " if (gm_get(" << m << "u, " << b << ", " << k1 << ", " << a << ")) { psk0_" << ps << " = " << b
+              << "; psk1_" << ps << " = " << k1 << "; psv_" << ps << " = " << a << "; psok_" << ps << " = true; goto " << x
+              << "; }";
+        } else if (gslots.count(in.y)) {
+          o << " if (gm_get(" << m << "u, " << b << ", " << k1 << ", " << a << ")) goto " << x << ";";
+        }
         break;
       }
       case OP_MEMO_PUT: {
@@ -684,6 +762,12 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
             << " = true; }";
         }
         if (gslots.count(in.y)) o << " gm_put(L, " << m << "u, " << b << ", " << k1 << ", " << a << ");";
+        auto pg = put_site.find(pc);
+        if (pg != put_site.end()) {
+          const std::string ps = std::to_string(pg->second);
+          o << " if (memo_stable(" << a << ")) { psk0_" << ps << " = " << b << "; psk1_" << ps << " = " << k1 << "; psv_"
+            << ps << " = " << a << "; psok_" << ps << " = true; }";
+        }
         break;
       }
       case OP_TABLE: {
@@ -692,7 +776,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         else o << t;
         break;
       }
-      case OP_FAIL_FALLBACK: o << "lane_fallback(L, " << y << "); return;"; break;
+      case OP_FAIL_FALLBACK: o << "lane_fallback(L, " << y << "); " << RET; break;
       case OP_ORD: o << "op_ord(L, " << y << ");"; break;
       case OP_JPROBE:
         o << "if (!op_jprobe(L, " << a << ", " << R(in.a + 1) << ", " << b << ", " << y << ")) goto " << x << ";";
@@ -702,10 +786,154 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           << x << "; " << b << " = v_; }";
         break;
       case OP_JVAR: o << a << " = op_jvar(" << b << ", " << R(in.b + 1) << ", " << y << ");"; break;
-      default: o << "lane_fallback(L, FB_UNSUPPORTED); return;"; break;
+      default: o << "lane_fallback(L, FB_UNSUPPORTED); " << RET; break;
     }
     o << "\n";
+  };
+
+  // Outlined pure-function bodies (GKGPU_JIT_OUTLINE, default on): the code a
+  // cross-lane memo miss runs -- the function inlined between MEMO_GET and its
+  // MEMO_PUT, e.g. K8sContainerLimits' canonify_mem with get_suffix's six
+  // bodies -- becomes a __noinline__ function of its live-in registers, so the
+  // predicate keeps only the memo probe and a call.  Misses are rare (a few
+  // distinct arguments per launch), and the predicate shrinks: instruction
+  // cache footprint and register pressure of the code every lane runs.
+  std::map<uint32_t, uint32_t> outl;  // region start (MEMO_GET pc) -> its MEMO_PUT pc
+  std::map<uint32_t, std::vector<uint32_t>> outl_in;  // live-in registers of the region
+  {
+    const char* ov = getenv("GKGPU_JIT_OUTLINE");
+    const bool on = !ov || atoi(ov) != 0;
+    // global liveness (backward may-analysis)
+    const uint32_t nw = (p.nregs + 64) / 64;
+    std::vector<std::vector<uint64_t>> live(p.code_len, std::vector<uint64_t>(nw, 0));
+    std::vector<uint32_t> rd, wr, sc;
+    auto reads_of = [&](uint32_t pc, std::vector<uint32_t>& r) {
+      std::vector<uint32_t> w;
+      ins_regs(bank.code[pc], r, w);
+      const Ins& in = bank.code[pc];
+      const uint32_t k = pc - b0;
+      // lookups answered by an available register read that register
+      if (in.op == OP_GETK) { const int h = LK.find(k, in.b, in.x); if (h >= 0) r.push_back((uint32_t)h); }
+      if (in.op == OP_GET) {
+        const int kc = LK.konst(k, in.c);
+        const int h = kc >= 0 ? LK.find(k, in.b, (uint32_t)kc) : -1;
+        if (h >= 0) r.push_back((uint32_t)h);
+      }
+    };
+    for (bool changed = on; changed;) {
+      changed = false;
+      for (uint32_t k = p.code_len; k-- > 0;) {
+        const uint32_t pc = b0 + k;
+        std::vector<uint64_t> out(nw, 0);
+        ins_succ(bank.code[pc], pc, sc);
+        for (uint32_t t : sc)
+          if (t >= b0 && t < b1) for (uint32_t w = 0; w < nw; ++w) out[w] |= live[t - b0][w];
+        ins_regs(bank.code[pc], rd, wr);
+        for (uint32_t r : wr) if (r < 64 * nw) out[r >> 6] &= ~(1ull << (r & 63));
+        reads_of(pc, rd);
+        for (uint32_t r : rd) if (r < 64 * nw) out[r >> 6] |= 1ull << (r & 63);
+        if (out != live[k]) { live[k] = out; changed = true; }
+      }
+    }
+    auto is_live = [&](uint32_t pc, uint32_t r) {
+      return pc >= b0 && pc < b1 && r < 64 * nw && ((live[pc - b0][r >> 6] >> (r & 63)) & 1);
+    };
+    // jump targets from each instruction
+    std::vector<std::pair<uint32_t, uint32_t>> jumps;  // (from, to)
+    for (uint32_t pc = b0; pc < b1; ++pc)
+      if (jump_op(bank.code[pc].op)) jumps.push_back({pc, bank.code[pc].x});
+    for (uint32_t pc = b0; on && pc < b1; ++pc) {
+      const Ins& in = bank.code[pc];
+      if (in.op != OP_MEMO_GET || !gslots.count(in.y)) continue;
+      const uint32_t x = in.x, put = x - 1;
+      if (x <= pc + 1 || x > b1 || bank.code[put].op != OP_MEMO_PUT || bank.code[put].y != in.y) continue;
+      if (put - (pc + 1) < 12) continue;  // small bodies stay inline
+      bool ok = true;
+      for (auto& j : jumps) {
+        const bool from_in = j.first > pc && j.first < put, to_in = j.second > pc && j.second < put;
+        if (from_in && !(to_in || j.second == put || j.second == x)) ok = false;  // leaves the region
+        if (!from_in && to_in) ok = false;                                      // enters it
+      }
+      // what the region writes must be dead after it (its value register aside)
+      std::set<uint32_t> wrs;
+      for (uint32_t q = pc + 1; q < put && ok; ++q) {
+        ins_regs(bank.code[q], rd, wr);
+        wrs.insert(wr.begin(), wr.end());
+      }
+      for (uint32_t r : wrs)
+        if (r != in.a && (is_live(x, r) || r == in.b || r == in.c)) ok = false;
+      if (!ok) continue;
+      // live-in registers of the region (its exits read nothing)
+      std::vector<std::vector<uint64_t>> rl(put - pc - 1, std::vector<uint64_t>(nw, 0));
+      for (bool ch = true; ch;) {
+        ch = false;
+        for (uint32_t q = put; q-- > pc + 1;) {
+          std::vector<uint64_t> out(nw, 0);
+          ins_succ(bank.code[q], q, sc);
+          for (uint32_t t : sc)
+            if (t > pc && t < put) for (uint32_t w = 0; w < nw; ++w) out[w] |= rl[t - pc - 1][w];
+          ins_regs(bank.code[q], rd, wr);
+          for (uint32_t r : wr) if (r < 64 * nw) out[r >> 6] &= ~(1ull << (r & 63));
+          reads_of(q, rd);
+          for (uint32_t r : rd) if (r < 64 * nw) out[r >> 6] |= 1ull << (r & 63);
+          if (out != rl[q - pc - 1]) { rl[q - pc - 1] = out; ch = true; }
+        }
+      }
+      std::vector<uint32_t> lin;
+      for (uint32_t r = 0; r < 64 * nw && r < p.nregs; ++r)
+        if ((rl[0][r >> 6] >> (r & 63)) & 1) lin.push_back(r);
+      if (std::find(lin.begin(), lin.end(), (uint32_t)in.a) == lin.end()) lin.insert(lin.begin(), in.a);
+      outl[pc] = put;
+      outl_in[pc] = lin;
+      pc = put;  // outermost regions only
+    }
   }
+  // register memo sites inside an outlined body stay memo-only (their
+  // registers are the predicate's locals)
+  for (auto& kv : outl)
+    for (uint32_t q = kv.first + 1; q < kv.second; ++q) {
+      if (psite.erase(q)) put_site.erase(bank.code[q].x - 1);
+    }
+  for (uint32_t ps : psite)
+    o << "  uint64_t psk0_" << ps << ", psk1_" << ps << ", psv_" << ps << "; bool psok_" << ps << " = false;\n";
+  std::ostringstream fo;  // the outlined functions (before the predicate)
+  for (auto& kv : outl) {
+    const uint32_t g0 = kv.first, put = kv.second;
+    const Ins& gi = bank.code[g0];
+    const std::vector<uint32_t>& lin = outl_in[g0];
+    std::set<uint32_t> used;
+    std::vector<uint32_t> rd, wr;
+    for (uint32_t q = g0 + 1; q < put; ++q) {
+      ins_regs(bank.code[q], rd, wr);
+      used.insert(rd.begin(), rd.end());
+      used.insert(wr.begin(), wr.end());
+    }
+    for (uint32_t r : lin) used.erase(r);
+    fo << "__device__ __noinline__ uint64_t gk_o" << g0 << "(PLane& L, uint32_t plo, uint32_t pn";
+    for (uint32_t r : lin) fo << ", uint64_t " << R(r);
+    fo << ") {\n";
+    if (!used.empty()) {
+      fo << "  uint64_t ";
+      bool first = true;
+      for (uint32_t r : used) { fo << (first ? "" : ", ") << R(r); first = false; }
+      fo << ";\n";
+    }
+    const std::string ret = "return " + R(gi.a) + ";";
+    std::ostringstream ob;
+    for (uint32_t q = g0 + 1; q < put; ++q) emit(q, ob, ret);
+    fo << ob.str() << "L" << put << ":;\nL" << gi.x << ":;\n  " << ret << "\n}\n";
+  }
+  for (uint32_t pc = b0; pc < b1; ++pc) {
+    emit(pc, o, "return;");
+    auto ol = outl.find(pc);
+    if (ol == outl.end()) continue;
+    const Ins& in = bank.code[pc];
+    o << "  " << R(in.a) << " = gk_o" << pc << "(L, plo, pn";
+    for (uint32_t r : outl_in[pc]) o << ", " << R(r);
+    o << "); if (L.fail) return;\n";
+    pc = ol->second - 1;  // continue at the MEMO_PUT
+  }
+  g.pre += fo.str();
   o << "  lane_fallback(L, FB_UNSUPPORTED);\n";
   g.body = o.str();
   return g;

@@ -1,6 +1,7 @@
 // Host-side interned store (strings, numbers, node arena) + exact number
 // conversions matching Go's math/big / strconv behaviour.
 #include "store.h"
+#include "flatten.h"
 
 #include <atomic>
 #include <charconv>
@@ -688,10 +689,7 @@ void Store::intern_parts(const std::vector<const Store*>& src, uint32_t first,
   auto pfor = [&](size_t n, const std::function<void(size_t)>& f) {
     std::atomic<size_t> next{0};
     auto work = [&] { for (size_t i; (i = next.fetch_add(1)) < n;) f(i); };
-    std::vector<std::thread> th;
-    for (int t = 1; t < std::max(1, threads); ++t) th.emplace_back(work);
-    work();
-    for (auto& x : th) x.join();
+    parallel_run(std::max(1, threads), [&](int) { work(); });
   };
   // A
   pfor(P, [&](size_t p) {
