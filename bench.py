@@ -51,6 +51,10 @@ def parse():
                          "capped by a cgroup CPU quota when one is set)")
     ap.add_argument("--oracle-sample", type=int, default=0,
                     help="resources also timed on the Python oracle (1 core; 0 = skip)")
+    ap.add_argument("--from-cache", action="store_true",
+                    help="audit from the cache: the config's objects (and their Namespaces) synced into the "
+                         "inventory with PutData, a step = one Client.Audit (hooks.audit) over all of them, every "
+                         "result row decoded on the host (--audit-from-cache, manager.go:195-197)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch for this workload (rocprofv3 --pmc), if measured")
     return ap.parse_args()
@@ -107,6 +111,8 @@ def main():
         sys.exit(spawn(args))
     if args.config == "5":
         return webhook_main(args)
+    if args.from_cache:
+        return from_cache_main(args)
     if args.steps is None:
         args.steps = 20
     cfg_templates, cfg_gen, cfg_default_n, cfg_desc = _configs()[args.config]
@@ -404,6 +410,88 @@ def main():
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def from_cache_main(args):
+    """--from-cache (one GPU): Client.Audit over the synced inventory.  The
+    engine keeps the inventory as a device-resident staged batch of
+    make_review documents (target_template_source.go:46-89), built by the first
+    audit after a change; every step evaluates it and decodes all result rows
+    (Client.Audit returns every result, client.go:805-833)."""
+    import re
+    import gkgpu
+    from gkgpu.client import Client, TARGET
+    if args.steps is None:
+        args.steps = 5
+    cfg_templates, cfg_gen, cfg_default_n, cfg_desc = _configs()[args.config]
+    n = args.pods or cfg_default_n
+    templates, constraints = cfg_templates()
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    objs, nss = cfg_gen(n, 0)
+    t0 = time.time()
+    ident = re.compile(r'"apiVersion":"([^"]*)","kind":"([^"]*)","metadata":\{"name":"([^"]*)"(?:,"namespace":"([^"]*)")?')
+    seen_ns = set()
+    for js, ns in zip(objs, nss):
+        if ns is not None and id(ns) not in seen_ns:
+            seen_ns.add(id(ns))
+            nm = json.loads(ns)["metadata"]["name"]
+            drv.put_data("/external/%s/cluster/v1/Namespace/%s" % (TARGET, nm), ns)
+        m = ident.match(js)
+        av, kind, name, ons = m.group(1), m.group(2), m.group(3), m.group(4)
+        gv = av.replace("/", "%2F")
+        path = ("/external/%s/namespace/%s/%s/%s/%s" % (TARGET, ons, gv, kind, name) if ons
+                else "/external/%s/cluster/%s/%s/%s" % (TARGET, gv, kind, name))
+        drv.put_data(path, js)
+    t_sync = time.time() - t0
+    del objs, nss
+    t0 = time.perf_counter()
+    first = drv.audit_summary()
+    t_first = time.perf_counter() - t0
+    for _ in range(args.warmup):
+        drv.audit_summary()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = drv.audit_summary()
+    elapsed = time.perf_counter() - t0
+    builds, reviews = drv.audit_cache_stats()
+    n_cons = len(constraints)
+    ms = elapsed / args.steps * 1000.0
+    out = {
+        "metric": "resource x constraint evals/sec (1/2/4/8 GPU) + % HBM roofline; vs host-CPU OPA",
+        "value": reviews * n_cons / (ms / 1000.0),
+        "unit": "evals/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded generator, SURVEY 8(d) config %s distribution), synced with PutData" % args.config,
+        "config": {
+            "workload": cfg_desc + " -- audit from the cache (hooks.audit over the synced inventory)",
+            "reviews": reviews,
+            "constraints": n_cons,
+            "results_per_audit": last["results"],
+            "status_totals": sum(last["totals"]),
+            "cache_builds": builds,
+            "first_audit_s": round(t_first, 3),
+            "first_audit_timing_ms": [round(x, 2) for x in first["timing_ms"]],
+            "steady_timing_ms": [round(x, 2) for x in last["timing_ms"]],
+            "timing_fields": "flatten, upload, kernels, download, decode (engine phases of one gk_query)",
+            "sync_s": round(t_sync, 1),
+        },
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(out))
 
 
 def referenced_bytes(drv, batch, kind, cons_ids, threads, every=False):

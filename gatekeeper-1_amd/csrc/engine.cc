@@ -386,6 +386,11 @@ struct gk_engine {
   std::vector<uint32_t> mwords;
   bool constraints_dirty = true;
   std::map<std::string, std::string> inventory;  // external path -> json
+  // hooks.audit: the synced inventory as a staged batch of make_review
+  // documents, device-resident until the engine state changes (gen)
+  std::mutex cache_mu;
+  std::shared_ptr<gk_batch> cache_batch;
+  uint64_t cache_builds = 0;
   std::map<std::string, std::pair<uint32_t, uint32_t>> ns_nodes;  // namespace name -> (node, node count)
   gk::NsCache ns_cache;                           // namespace name -> node (permanent)
   std::map<std::string, std::string> other_data;
@@ -1908,6 +1913,7 @@ int gk_engine_create(const char* opts_json, gk_engine** out) {
 
 void gk_engine_destroy(gk_engine* e) {
   if (!e) return;
+  e->cache_batch.reset();
   for (auto& x : e->ctxs) x->release_all();
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
                   &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
@@ -2203,11 +2209,111 @@ static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_resul
   return GK_OK;
 }
 
+int gk_audit_cache_stats(gk_engine* e, uint64_t* builds, uint64_t* reviews) {
+  if (!e) return GK_EINVAL;
+  std::lock_guard<std::mutex> g(e->cache_mu);
+  if (builds) *builds = e->cache_builds;
+  if (reviews) *reviews = e->cache_batch ? e->cache_batch->nrev : 0;
+  return GK_OK;
+}
+
 int gk_coalesce_stats(gk_engine* e, uint64_t* batches, uint64_t* requests) {
   if (!e) return GK_EINVAL;
   std::lock_guard<std::mutex> g(e->co.mu);
   if (batches) *batches = e->co.batches;
   if (requests) *requests = e->co.requests;
+  return GK_OK;
+}
+
+// hooks.audit (Client.Audit, client.go:805-833): every synced object of the
+// inventory reviewed against every constraint in one query
+// (target_template_source.go:46-89 matching_reviews_and_constraints).  The
+// inventory is kept as a staged batch -- make_review / add_field documents in
+// the path-grouped layout, device-resident -- built on the first audit after a
+// change of the engine state (a mutation bumps gen) and evaluated as it is by
+// every later one: repeated audits do no per-object JSON work.  Reviews are
+// numbered in inventory path order (the row's review index).
+// The from-cache page of the synced inventory (shared lock held): objects in
+// inventory path order, each with its path's fields; paths that name no
+// review (a group/version with two slashes, another depth) are skipped.
+struct CachePage {
+  std::vector<std::vector<std::string>> segs;
+  std::vector<Page::CacheKey> keys;
+  std::vector<uint64_t> offs;
+  std::string objs;
+  Page pg;
+};
+static void build_cache_page(gk_engine* e, CachePage& c) {
+  std::vector<const std::string*> js;
+  c.segs.reserve(e->inventory.size());
+  for (auto& kv : e->inventory) {
+    auto q = split_path(kv.first);
+    bool ok = q.size() >= 2 && q[0] == "external" && q[1] == TARGET &&
+              ((q.size() == 7 && q[2] == "namespace") || (q.size() == 6 && q[2] == "cluster"));
+    if (ok) {
+      // make_group_version: "g/v" -> (g, v), "v" -> ("", v); more slashes: no review
+      const std::string& gv = q[q.size() - 3];
+      const size_t sl = gv.find('/');
+      ok = sl == std::string::npos || gv.find('/', sl + 1) == std::string::npos;
+    }
+    if (!ok) continue;
+    c.segs.push_back(std::move(q));
+    js.push_back(&kv.second);
+  }
+  const size_t n = c.segs.size();
+  c.keys.resize(n);
+  c.offs.assign(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) c.offs[i + 1] = c.offs[i] + js[i]->size();
+  c.objs.assign(c.offs[n], '\0');
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 4096));
+  parallel_run(T, [&](int t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      if (!js[i]->empty()) memcpy(&c.objs[c.offs[i]], js[i]->data(), js[i]->size());
+      const auto& q = c.segs[i];
+      const bool nsd = q.size() == 7;
+      const std::string& gv = q[q.size() - 3];
+      const size_t sl = gv.find('/');
+      Page::CacheKey& k = c.keys[i];
+      k.namespaced = nsd;
+      k.ns = nsd ? std::string_view(q[3]) : std::string_view();
+      k.group = sl == std::string::npos ? std::string_view() : std::string_view(gv).substr(0, sl);
+      k.version = sl == std::string::npos ? std::string_view(gv) : std::string_view(gv).substr(sl + 1);
+      k.kind = q[q.size() - 2];
+      k.name = q[q.size() - 1];
+    }
+  });
+  c.pg = Page{c.objs.data(), c.offs.data(), n, nullptr, nullptr, 0, nullptr};
+  c.pg.cache = c.keys.data();
+}
+
+static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out);
+static int audit_from_cache(gk_engine* e, gk_results** out) {
+  ReadLock rl;
+  int rc = read_lock(e, rl, !e->host_only);
+  if (rc != GK_OK) return rc;
+  std::shared_ptr<gk_batch> b;
+  {
+    std::lock_guard<std::mutex> g(e->cache_mu);
+    if (!e->cache_batch || e->cache_batch->gen != e->gen) {
+      e->cache_batch.reset();
+      CachePage cp;
+      build_cache_page(e, cp);
+      gk_batch* nb = nullptr;
+      rc = stage_page_locked(e, cp.pg, &nb);
+      if (rc != GK_OK) return rc;
+      e->cache_batch = std::shared_ptr<gk_batch>(nb, gk_batch_free);
+      ++e->cache_builds;
+    }
+    b = e->cache_batch;
+  }
+  if (!e->dev_ok || !b->d_nodes.p) return fail(e, GK_EDEVICE, "no HIP device available");
+  CtxLease lease(e);
+  TablePtrs tp;
+  if (!ctx_device(e, lease.x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
+  auto res = std::make_unique<gk_results>();
+  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, true, res.get(), b->d_nodes.p, 0, b->node_begin);
+  if (rc != GK_OK) return rc;
+  *out = res.release();
   return GK_OK;
 }
 
@@ -2222,42 +2328,7 @@ int gk_query(gk_engine* e, const char* path, const char* input_json, size_t len,
     in.push_back({input_json ? input_json : "null", input_json ? len : 4});
     return eval_inputs(e, in, out);
   }
-  if (p == aud) {
-    // hooks.audit: reviews synthesized from the synced inventory
-    // (target_template_source.go:46-89: make_review / add_field); the
-    // inventory is read under the shared lock, evaluated in a second hold
-    // (a mutation in between is a later state, as for two Queries)
-    std::vector<std::string> docs;
-    ReadLock rl;
-    int rc = read_lock(e, rl, false);
-    if (rc != GK_OK) return rc;
-    std::string prefix = std::string("/external/") + TARGET + "/";
-    for (auto& kv : e->inventory) {
-      auto q = split_path(kv.first);
-      std::string ns, gv, kind, name;
-      if (q.size() == 7 && q[2] == "namespace") { ns = q[3]; gv = q[4]; kind = q[5]; name = q[6]; }
-      else if (q.size() == 6 && q[2] == "cluster") { gv = q[3]; kind = q[4]; name = q[5]; }
-      else continue;
-      std::string group, version;
-      size_t s = gv.find('/');
-      if (s == std::string::npos) version = gv;
-      else if (gv.find('/', s + 1) == std::string::npos) { group = gv.substr(0, s); version = gv.substr(s + 1); }
-      else continue;
-      auto js = [](const std::string& v) {
-        std::string o = "\"";
-        for (char c : v) { if (c == '"' || c == '\\') o.push_back('\\'); o.push_back(c); }
-        return o + "\"";
-      };
-      std::string r = "{\"review\":{\"kind\":{\"group\":" + js(group) + ",\"version\":" + js(version) + ",\"kind\":" +
-                      js(kind) + "},\"name\":" + js(name) + ",\"object\":" + kv.second +
-                      (q.size() == 7 ? ",\"namespace\":" + js(ns) : std::string()) + "}}";
-      docs.push_back(r);
-    }
-    rl.lk.unlock();
-    std::vector<std::pair<const char*, size_t>> in;
-    for (auto& s : docs) in.push_back({s.data(), s.size()});
-    return eval_inputs(e, in, out);
-  }
+  if (p == aud) return audit_from_cache(e, out);
   return fail(e, GK_EQUERY, "unsupported query path: " + p);
 }
 
@@ -2385,7 +2456,8 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
   FlatResult fr;
   std::string err;
   auto exit_ = e->excluded.find("audit");
-  const std::set<std::string>* ex = exit_ == e->excluded.end() ? nullptr : &exit_->second;
+  // (Client.Audit from the cache applies no excluder: manager.go:195-197)
+  const std::set<std::string>* ex = exit_ == e->excluded.end() || page.cache ? nullptr : &exit_->second;
   // GKGPU_PATH_LAYOUT (A/B switch, default on): staged batches' documents in
   // the path-grouped layout (flatten.h), ordered with the reviews
   const bool path_layout = order_by_size && env_mode("GKGPU_PATH_LAYOUT", 1, 1) != 0;
@@ -2537,6 +2609,12 @@ static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
   ReadLock rl;
   int rc = read_lock(e, rl, !e->host_only);
   if (rc != GK_OK) return rc;
+  return stage_page_locked(e, page, out);
+}
+
+// stage_page under the caller's shared lock
+static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
+  int rc = GK_OK;
   auto t0 = Clock::now();
   auto b = std::make_unique<gk_batch>();
   b->eng = e;
@@ -3108,6 +3186,18 @@ extern "C" int gk_debug_store_sizes(gk_engine* e, uint64_t* nodes, uint64_t* str
 // A staged batch of Query inputs ({"review": ...} documents, as gk_query_batch
 // takes them): lets tests evaluate arbitrary review documents through
 // gk_batch_eval, and through the CPU baseline on a host-only engine.
+// a fresh staged batch of the from-cache reviews (hooks.audit's documents;
+// tests run the CPU checker over it)
+extern "C" int gk_debug_stage_cache(gk_engine* e, gk_batch** out) {
+  if (!e || !out) return GK_EINVAL;
+  ReadLock rl;
+  int rc = read_lock(e, rl, !e->host_only);
+  if (rc != GK_OK) return rc;
+  CachePage cp;
+  build_cache_page(e, cp);
+  return stage_page_locked(e, cp.pg, out);
+}
+
 extern "C" int gk_debug_stage_inputs(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n,
                                      gk_batch** out) {
   if (!e || !out || (n && !inputs)) return GK_EINVAL;

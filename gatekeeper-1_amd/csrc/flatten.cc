@@ -323,6 +323,63 @@ uint32_t build_object_review(Store& st, const Keys& K, const Node& obj, const Ns
   return root;
 }
 
+// hooks.audit's review of a synced object (target_template_source.go:46-89):
+//   make_review: {"kind": {"group", "version", "kind"}, "name": name, "object": obj}
+//   add_field(r, "namespace", ns) for namespaced objects: the keys of r whose
+//   values are truthy plus "namespace", each value get_default(r, k, ns) -- so
+//   a null object becomes the namespace string, and the members keep that order
+// `obj` is the object's parsed root record.
+uint32_t build_cache_review(Store& st, const Keys& K, const Node& obj, const Page::CacheKey& ck, ResourceIds* res) {
+  const uint32_t s_group = st.intern(ck.group.data(), ck.group.size());
+  const uint32_t s_version = st.intern(ck.version.data(), ck.version.size());
+  const uint32_t s_kind = st.intern(ck.kind.data(), ck.kind.size());
+  const uint32_t s_name = st.intern(ck.name.data(), ck.name.size());
+  const uint32_t s_ns = ck.namespaced ? st.intern(ck.ns.data(), ck.ns.size()) : st.s_empty;
+  // add_field drops a falsy member: an object that is JSON `false`
+  const bool has_obj = !(ck.namespaced && obj.type == NT_FALSE);
+  const uint32_t nch = 2 + (has_obj ? 1 : 0) + (ck.namespaced ? 1 : 0);
+  const uint32_t root = (uint32_t)st.nodes().size();
+  st.nodes().resize(root + 1 + nch + 3);
+  Node* N = st.nodes().data();
+  const uint32_t first = root + 1, kf = first + nch;
+  auto obj_node = [&](uint32_t key, uint32_t f, uint32_t n) { Node x{}; x.key = key; x.type = NT_OBJ; x.first = f; x.n = (uint16_t)n; return x; };
+  auto str_node = [&](uint32_t key, uint32_t sid) { Node x{}; x.key = key; x.type = NT_STR; x.val = sid; return x; };
+  N[root] = obj_node(0, first, nch);
+  uint32_t i = first;
+  N[i++] = obj_node(st.s_kind, kf, 3);
+  N[i++] = str_node(st.s_name, s_name);
+  if (has_obj) {
+    if (ck.namespaced && obj.type == NT_NULL) {
+      N[i++] = str_node(st.s_object, s_ns);  // get_default(r, "object", namespace)
+    } else {
+      Node o = obj;
+      o.key = st.s_object;
+      N[i++] = o;
+    }
+  }
+  if (ck.namespaced) N[i++] = str_node(st.s_namespace, s_ns);
+  N[kf] = str_node(st.s_group, s_group);
+  N[kf + 1] = str_node(st.s_version, s_version);
+  N[kf + 2] = str_node(st.s_kind, s_kind);
+  // HandleViolation (target.go:193-244): apiVersion from review.kind, the
+  // object's own metadata name / namespace
+  uint32_t s_oname = NO_ID, s_ons = NO_ID;
+  if (const Node* md = member(st, obj, st.s_metadata)) {
+    s_oname = member_str(st, *md, st.s_name);
+    s_ons = member_str(st, *md, st.s_namespace);
+  }
+  if (s_group == st.s_empty) res->api_version = s_version;
+  else {
+    std::string av = std::string(ck.group) + "/" + std::string(ck.version);
+    res->api_version = st.intern(av.data(), av.size());
+  }
+  res->kind = s_kind;
+  res->name = s_oname == NO_ID ? st.s_empty : s_oname;
+  res->ns = s_ons == NO_ID ? st.s_empty : s_ons;
+  (void)K;
+  return root;
+}
+
 // ------------------------------------------------------------------ path-grouped layout (flatten.h)
 constexpr uint32_t kElem = 0xfffffffeu;   // path key of array elements
 constexpr uint32_t kMaxPaths = 1u << 16;  // per part; further distinct paths share their parent's region
@@ -447,6 +504,22 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
     if (!st.parse_doc(pg.objs + pg.obj_offs[i], pg.obj_offs[i + 1] - pg.obj_offs[i], &obj, &err)) {
       p.err = "invalid object JSON at " + std::to_string(i) + ": " + err;
       return;
+    }
+    if (pg.cache) {
+      ResourceIds rid{};
+      const uint32_t root = build_cache_review(st, K, obj, pg.cache[i], &rid);
+      bool glob = false;
+      p.cols.push_back(review_columns(st, gst, ns_cache, root, &glob));
+      p.nsglob.push_back(glob);
+      p.res.push_back(rid);
+      if (p.count_paths) count_paths(root);
+      uint32_t elems = 0;
+      const Node* nv = st.nodes().data();
+      const size_t n1 = st.nodes().size();
+      for (size_t k = n0; k < n1; ++k)
+        if (nv[k].type == NT_ARR) elems += nv[k].n;
+      p.weight.push_back((std::min<uint32_t>(elems, 0xfff) << 20) | std::min<uint32_t>((uint32_t)(n1 - n0), 0xfffff));
+      continue;
     }
     if (ex && !ex->empty()) {
       uint32_t ons = NO_ID;

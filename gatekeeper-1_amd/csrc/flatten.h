@@ -13,6 +13,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "common.h"
@@ -69,6 +70,15 @@ struct Page {
   const uint64_t* ns_offs = nullptr;   // n_ns + 1 offsets
   size_t n_ns = 0;
   const uint32_t* obj_ns = nullptr;    // per object: namespace index or NO_ID
+  // From-cache reviews (hooks.audit over the synced inventory,
+  // target_template_source.go:46-89): per object, the fields of its inventory
+  // path; each review is then make_review / add_field's document instead of
+  // the audit envelope, and no namespace is excluded or attached.
+  struct CacheKey {
+    std::string_view group, version, kind, name, ns;
+    bool namespaced;
+  };
+  const CacheKey* cache = nullptr;
 };
 
 // HandleViolation's Resource identity of a review (pkg/target/target.go:193-244):

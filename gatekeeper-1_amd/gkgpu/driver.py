@@ -567,6 +567,29 @@ class Driver:
         self._check(self._lib.gk_query(self._e, _b(path), js, len(js), C.byref(out)))
         return _collect(self._lib, out)
 
+    def audit_cache_stats(self):
+        """(builds, reviews) of the device-resident from-cache batch hooks.audit
+        evaluates (gk_audit_cache_stats): a build per engine state"""
+        b, r = C.c_uint64(), C.c_uint64()
+        self._lib.gk_audit_cache_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        self._check(self._lib.gk_audit_cache_stats(self._e, C.byref(b), C.byref(r)))
+        return b.value, r.value
+
+    def audit_summary(self):
+        """Client.Audit (hooks.audit) without materializing Python rows: the
+        per-constraint totals, the result count and the engine phase timings"""
+        out = C.c_void_p()
+        self._check(self._lib.gk_query(self._e, _b('hooks["%s"].audit' % TARGET), b"null", 4, C.byref(out)))
+        try:
+            n = self._lib.gk_results_count(out)
+            nc = self._lib.gk_results_constraints(out)
+            totals = [self._lib.gk_results_constraint_total(out, i) for i in range(nc)]
+            ms = (C.c_double * 5)()
+            self._lib.gk_results_timing(out, ms)
+            return {"results": n, "totals": totals, "timing_ms": list(ms)}
+        finally:
+            self._lib.gk_results_free(out)
+
     def coalesce_stats(self):
         """(launches, gk_query calls served) of the micro-batch coalescer"""
         b, r = C.c_uint64(), C.c_uint64()
@@ -683,6 +706,16 @@ class Driver:
     def is_namespace_excluded(self, process: str, namespace: str) -> bool:
         """Excluder.IsNamespaceExcluded (excluder.go:82-86)"""
         return bool(self._lib.gk_excluder_is_excluded(self._e, _b(process), _b(namespace)))
+
+    def debug_stage_cache(self) -> Batch:
+        """a staged batch of hooks.audit's from-cache reviews of the synced
+        inventory, in inventory path order (tests: the CPU checker)"""
+        out = C.c_void_p()
+        self._lib.gk_debug_stage_cache.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        self._check(self._lib.gk_debug_stage_cache(self._e, C.byref(out)))
+        n = C.c_uint64()
+        self._lib.gk_batch_stats(out, C.byref(n), None, None, None)
+        return Batch(self, out, n.value)
 
     def debug_stage_inputs(self, inputs: Sequence) -> Batch:
         """a staged batch of Query inputs ({"review": ...}; diagnostics / tests)"""

@@ -103,6 +103,10 @@ void gk_free_string(char* s);
 int gk_query_batch(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n, gk_results** out);
 /* the coalescer's launches and the gk_query calls they served (diagnostics) */
 int gk_coalesce_stats(gk_engine* e, uint64_t* batches, uint64_t* requests);
+/* hooks.audit (Client.Audit, client.go:805-833) keeps the synced inventory as a
+ * device-resident staged batch, rebuilt after any mutation: how many times it
+ * was built, and the reviews of the current one. */
+int gk_audit_cache_stats(gk_engine* e, uint64_t* builds, uint64_t* reviews);
 /* audit discovery mode: Review(AugmentedUnstructured{objs[i], ns(objs[i])}) for
  * every object (pkg/audit/manager.go:361-389, pkg/target/target.go:129-163).
  * ns_json[i] is the JSON of the object's corev1.Namespace (NULL / len 0 for

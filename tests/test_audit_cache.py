@@ -1,0 +1,124 @@
+"""hooks.audit over the synced inventory (Client.Audit, client.go:805-833) as a
+staged, device-resident batch (engine.cc audit_from_cache): the review of
+each synced object is make_review / add_field's document
+(target_template_source.go:46-89), built once per engine state.
+
+CPU: the from-cache batch run by the CPU checker (oracle/cpuvm.cc) against
+the oracle's own hooks.audit, with edge objects -- a JSON null (add_field
+puts the namespace string in its place), a JSON false (dropped), an escaped
+group/version, a group/version with two slashes (no review).  GPU: rows equal
+the oracle's, and repeated audits reuse the batch until a mutation."""
+import json
+
+import pytest
+
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, TARGET, data_path
+
+from parity import oracle_for
+
+AUDIT = 'hooks["%s"].audit' % TARGET
+
+
+def _inventory(n_pods, seed):
+    pods, ns_of, ns_objs = W.gen_pods(n_pods, seed=seed, n_namespaces=12)
+    items = [(data_path(o), o) for o in list(ns_objs.values()) + pods]
+    base = "/external/%s/namespace/team-0001" % TARGET
+    items += [
+        (base + "/v1/Pod/null-pod", None),                       # add_field: object := namespace
+        (base + "/v1/Pod/false-pod", False),                     # add_field drops a falsy member
+        (base + "/apps%2Fv1/Deployment/dep", {"apiVersion": "apps/v1", "kind": "Deployment",
+                                              "metadata": {"name": "dep", "namespace": "team-0001"},
+                                              "spec": {"template": {"spec": {"containers": []}}}}),
+        (base + "/a%2Fb%2Fv1/Pod/two-slashes", pods[0]),         # make_group_version fails: no review
+        ("/external/%s/cluster/v1/ConfigMap/cm" % TARGET, {"apiVersion": "v1", "kind": "ConfigMap",
+                                                           "metadata": {"name": "cm"}}),
+    ]
+    return items
+
+
+def _oracle_rows(od):
+    return list(od.query(AUDIT))
+
+
+def test_cache_batch_checker_equals_the_oracle_audit():
+    from oracle import cpu_baseline
+    ts, cs = W.config2()
+    items = _inventory(200, 31)
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, cs)
+    for p, o in items:
+        d.put_data(p, o)
+        od.put_data(p, json.dumps(o))
+    b = d.debug_stage_cache()
+    assert b.n == len(items) - 1  # the two-slash group/version names no review
+    _s, evals, viol, _mb, flagged = cpu_baseline.sweep(d, b, threads=4)
+    # the null object's review (object: a string) goes to the CPU driver for
+    # its five constraints (ReviewCol fallback); nothing else is flagged
+    assert flagged in (0, len(cs)), flagged
+    want = _oracle_rows(od)
+    assert viol == len(want) > 100, (viol, len(want))
+
+
+@pytest.mark.gpu
+def test_audit_from_cache_reuses_the_staged_batch():
+    """2,000 synced Pods + their Namespaces + the edge objects: Client.Audit's
+    rows equal the oracle's (multiset of (kind, namespace, name, constraint,
+    msg, details, action)); a second audit reuses the device batch; a put of
+    a new object rebuilds it and the rows follow."""
+    from oracle.driver import details_json
+    ts, cs = W.config2()
+    items = _inventory(2000, 32)
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, cs)
+    for p, o in items:
+        drv.put_data(p, o)
+        od.put_data(p, json.dumps(o))
+
+    def eng_rows():
+        res = cl.audit()
+        order = sorted(p for p, _ in items if "%2Fb%2F" not in p)
+        # only the null object's review may go to the CPU driver
+        assert all(order[i].endswith("/null-pod") for i, s in enumerate(res.status) if s), res.status
+        out = []
+        for r in res.results:
+            seg = order[r.review].split("/")
+            ns = seg[4] if seg[3] == "namespace" else ""
+            out.append((seg[-2], ns, seg[-1], r.constraint_kind, r.constraint_name, r.msg, r.details_json,
+                        r.enforcement_action))
+        return sorted(out)
+
+    def ref_rows():
+        rows = []
+        for r in _oracle_rows(od):
+            rv, c = r["review"], r["constraint"]
+            ns = rv.get("namespace") if hasattr(rv, "get") else None
+            rows.append((rv.get("kind").get("kind"), ns if isinstance(ns, str) else "", rv.get("name"), c.get("kind"),
+                         c.get("metadata").get("name"), r["msg"], details_json(r["details"]), r["enforcementAction"]))
+        return sorted(rows)
+
+    want = ref_rows()
+    assert len(want) > 1000
+    assert eng_rows() == want
+    assert eng_rows() == want
+    builds, reviews = drv.audit_cache_stats()
+    assert builds == 1 and reviews == len(items) - 1, (builds, reviews)
+    extra = W.gen_pods(1, seed=77, n_namespaces=12)[0][0]
+    extra["metadata"]["name"] = "late-pod"
+    p = data_path(extra)
+    items.append((p, extra))
+    drv.put_data(p, extra)
+    od.put_data(p, json.dumps(extra))
+    assert eng_rows() == ref_rows()
+    assert drv.audit_cache_stats()[0] == 2
