@@ -848,6 +848,12 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       const uint32_t x = in.x, put = x - 1;
       if (x <= pc + 1 || x > b1 || bank.code[put].op != OP_MEMO_PUT || bank.code[put].y != in.y) continue;
       if (put - (pc + 1) < 12) continue;  // small bodies stay inline
+      // an argument that may be a deferred sprintf is no memo key (gm_key):
+      // every call would miss and pay the out-of-line call
+      {
+        const uint32_t k = pc - b0;
+        if (F.reached[k] && (F.has(k, in.b) || (in.c != 0xffff && F.has(k, in.c)))) continue;
+      }
       bool ok = true;
       for (auto& j : jumps) {
         const bool from_in = j.first > pc && j.first < put, to_in = j.second > pc && j.second < put;
