@@ -157,8 +157,22 @@ struct LdsField {
   __device__ __forceinline__ T operator++(int) { T o = *this; *this += 1u; return o; }
 };
 #define GK_LSCAL(T, name, F) LdsField<T, F> name
+// the loop watermarks (keepH / keepB per loop level, read at every iteration)
+// likewise: GK_MAXDEPTH levels x 2 x 256 threads x 2 B in LDS
+__shared__ uint16_t gk_lds_keep[2][GK_MAXDEPTH][256];
+template <int F>
+struct LdsKeep {
+  struct Ref {
+    uint32_t d;
+    __device__ __forceinline__ operator uint16_t() const { return gk_lds_keep[F][d][threadIdx.x]; }
+    __device__ __forceinline__ Ref& operator=(uint32_t v) { gk_lds_keep[F][d][threadIdx.x] = (uint16_t)v; return *this; }
+  };
+  __device__ __forceinline__ Ref operator[](uint32_t d) const { return Ref{d < GK_MAXDEPTH ? d : 0u}; }
+};
+#define GK_LKEEP(name, F) LdsKeep<F> name
 #else
 #define GK_LSCAL(T, name, F) T name
+#define GK_LKEEP(name, F) uint16_t name[MAXLOOP]
 #endif
 
 struct Lane {
@@ -173,7 +187,8 @@ struct Lane {
   GK_LSCAL(uint16_t, ord_base, 4);
   GK_LSCAL(uint32_t, reason, 5);
   // per loop depth: heap / byte watermarks that values escaping the loop pinned
-  uint16_t keepH[MAXLOOP], keepB[MAXLOOP];
+  GK_LKEEP(keepH, 0);
+  GK_LKEEP(keepB, 1);
   GK_LSCAL(uint32_t, en, 6);  // tuples this lane emitted (written straight to the output)
   uint32_t steps;
   GK_LSCAL(uint32_t, rv, 7);  // the review's index in the caller's batch (Viol.review)

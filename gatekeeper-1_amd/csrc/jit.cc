@@ -1017,22 +1017,6 @@ static bool lds_scalars() {
 // add to the lane heap words and scalars and still fit the blocks per CU its
 // waves-per-EU asks for (160 KB per CU).  2-wave kernels (32 heap words, 73 KB)
 // take one of the two, 3-wave kernels (16 words, 41 KB) both.
-struct StagePlan { bool params = false, dfa = false; };
-static StagePlan stage_plan(const Program& p, const Gen& g) {
-  StagePlan sp;
-  if (!lds_stage_on()) return sp;
-  const char* w = getenv("GKGPU_JIT_WPE");
-  const int wpe = w ? atoi(w) : (small_program(p) ? 3 : 2);
-  const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
-  uint32_t used = (uint32_t)lds_heap_words(p) * 8u * 256u + (lds_scalars() ? 9u * 4u * 256u : 0u);
-  const uint32_t pbytes = 4u * 64u * 16u, dbytes = 4u * 1024u + 4u * 17u * 4u;  // devrt.h LDS_PCAP / LDS_DFA_*
-  if (g.param_regex && used + dbytes <= limit) { sp.dfa = true; used += dbytes; }
-  if (g.param_reads && used + pbytes <= limit) { sp.params = true; used += pbytes; }
-  return sp;
-}
-
-// the loop levels a program's lane uses (devrt.h GK_MAXDEPTH): loop depths
-// of its iterations and probes, and the ranges values escaping loops pin
 constexpr uint32_t kMaxLoop = 16;  // devrt.h MAXLOOP
 static int max_depth(const Program& p, const CodeBank& bank) {
   uint32_t m = 0;
@@ -1050,6 +1034,23 @@ static int max_depth(const Program& p, const CodeBank& bank) {
   return (int)std::min<uint32_t>(m + 1, kMaxLoop);
 }
 
+struct StagePlan { bool params = false, dfa = false; };
+static StagePlan stage_plan(const Program& p, const Gen& g, int depth) {
+  StagePlan sp;
+  if (!lds_stage_on()) return sp;
+  const char* w = getenv("GKGPU_JIT_WPE");
+  const int wpe = w ? atoi(w) : (small_program(p) ? 3 : 2);
+  const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
+  // lane heap words, lane scalars and (with the scalars) the loop watermarks
+  uint32_t used = (uint32_t)lds_heap_words(p) * 8u * 256u + (lds_scalars() ? 9u * 4u * 256u + 4u * 256u * (uint32_t)depth : 0u);
+  const uint32_t pbytes = 4u * 64u * 16u, dbytes = 4u * 1024u + 4u * 17u * 4u;  // devrt.h LDS_PCAP / LDS_DFA_*
+  if (g.param_regex && used + dbytes <= limit) { sp.dfa = true; used += dbytes; }
+  if (g.param_reads && used + pbytes <= limit) { sp.params = true; used += pbytes; }
+  return sp;
+}
+
+// the loop levels a program's lane uses (devrt.h GK_MAXDEPTH): loop depths
+// of its iterations and probes, and the ranges values escaping loops pin
 static std::string inline_hot_tag(const Program& p) {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
@@ -1084,8 +1085,9 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words(p) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(p) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
-  o << "#define GK_MAXDEPTH " << max_depth(p, bank) << "\n";
-  const StagePlan sp = stage_plan(p, g);
+  const int depth = max_depth(p, bank);
+  o << "#define GK_MAXDEPTH " << depth << "\n";
+  const StagePlan sp = stage_plan(p, g, depth);
   if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
   if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
   o << "#include \"devrt.h\"\n"
@@ -1119,7 +1121,9 @@ std::string jit_fused_source(const std::vector<const Program*>& progs, const std
   Gen u;
   u.param_reads = preads;
   u.param_regex = pregex;
-  const StagePlan sp = stage_plan(*big, u);
+  int depth = 1;
+  for (auto* q : progs) depth = std::max(depth, max_depth(*q, bank));
+  const StagePlan sp = stage_plan(*big, u, depth);
   std::ostringstream body;
   std::string key = wpe_suffix(*big) + inline_hot_tag(*big);
   for (size_t i = 0; i < gs.size(); ++i) {
@@ -1139,8 +1143,6 @@ std::string jit_fused_source(const std::vector<const Program*>& progs, const std
   if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
   if (lds_heap_words(*big) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(*big) << "\n";
   if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
-  int depth = 1;
-  for (auto* p : progs) depth = std::max(depth, max_depth(*p, bank));
   o << "#define GK_MAXDEPTH " << depth << "\n";
   if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
   if (sp.dfa) o << "#define GK_LDS_DFA 1\n";

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU call of measurements after the suite: same-call A/Bs of JIT
+# switches on config 2 (and config 4), the config-5 phase breakdown and batch
+# bench, and the from-cache bench.  Summaries print as AB lines; JSON under
+# gpurun_out/<tag>/.   bash tools/gpu_measure.sh <tag> [c2|c4|c5|cache ...]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r04m}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT" gpurun_out/jitcache
+cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
+export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+for what in "${@:-c2 c4 c5 cache}"; do
+  case $what in
+    c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_JIT_OUTLINE=0 GKGPU_JIT_PMEMO=0" \
+          "GKGPU_JIT_LMEMO=1" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=32" "GKGPU_INLINE_HOT=0" "GKGPU_FN_EARLY=1" || exit 1 ;;
+    c4) bash tools/gpu_bench_ab.sh "$TAG/c4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
+    c5) timeout -k 10 300 python -u tools/probe_c5_time.py 256 > "$OUT/c5_phases.txt" 2>&1 || { echo C5P_FAIL; tail "$OUT/c5_phases.txt"; exit 1; }
+        cat "$OUT/c5_phases.txt"
+        timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 > "$OUT/c5_batch.json" 2> "$OUT/c5_batch.err" || { echo C5_FAIL; tail "$OUT/c5_batch.err"; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5', d['config']['latency_ms'], round(d['value']/1e6,2), 'M/s; cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']/1e6,2))" "$OUT/c5_batch.json" ;;
+    cache) timeout -k 10 600 python -u bench.py --from-cache --steps 3 --warmup 1 > "$OUT/cache.json" 2> "$OUT/cache.err" || { echo CACHE_FAIL; tail "$OUT/cache.err"; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('CACHE', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],1), 'ms', c['results_per_audit'], c['cache_builds'], c['first_audit_s'], c['steady_timing_ms'])" "$OUT/cache.json" ;;
+  esac
+done
