@@ -63,6 +63,37 @@ def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1, joins: bool = T
     return s, out[0], out[1], out[2], out[3]
 
 
+def sweep_digest(driver, batch, threads: int = 1, joins: bool = True):
+    """sweep() over the whole batch plus an order-free digest of every result
+    row (oracle/cpuvm.cc gkcpu_sweep_digest): (evals, violations, flagged,
+    digest).  row_digest computes the same over rows from elsewhere (the
+    oracle), so tests compare rows, not just counts."""
+    lib = load()
+    lib.gkcpu_sweep_digest.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]
+    lib.gkcpu_sweep_digest.restype = C.c_double
+    buf = _host_args(driver, batch, joins, threads)
+    out = (C.c_uint64 * 5)()
+    lib.gkcpu_sweep_digest(buf, 0, batch.n, threads, out)
+    return out[0], out[1], out[3], out[4]
+
+
+def row_hash(review: int, constraint: int, msg: bytes, details: bytes) -> int:
+    """FNV-1a 64 over (u32 review LE, u32 constraint LE, msg, 0xff, details)"""
+    h = 1469598103934665603
+    for b in review.to_bytes(4, "little") + constraint.to_bytes(4, "little") + msg + b"\xff" + details:
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def row_digest(rows) -> int:
+    """rows: iterable of (review, constraint, msg str, details JSON str)"""
+    d = 0
+    for rv, c, m, det in rows:
+        d = (d + row_hash(rv, c, m.encode("utf-8", "surrogateescape"), det.encode("utf-8", "surrogateescape"))) \
+            & 0xFFFFFFFFFFFFFFFF
+    return d
+
+
 def referenced(driver, batch, only: int = -1, lo: int = 0, hi=None, threads: int = 1, pc_hist=None, joins: bool = True):
     """SURVEY 8(d) reference accounting of reviews [lo, hi) x constraint `only`
     (all when < 0): dict(nodes, strings, string_bytes, violations, flagged);

@@ -165,7 +165,19 @@ static void run_program(Lane& L, uint32_t pc, uint64_t review, uint64_t params) 
 
 struct Counts {
   uint64_t evals = 0, violations = 0, msg_bytes = 0, flagged = 0;
+  uint64_t digest = 0;  // sum over result rows of row_hash (an order-free multiset digest)
 };
+
+// gkcpu_sweep_digest: rows are hashed as FNV-1a 64 over (u32 batch review index
+// LE, u32 constraint LE, message bytes, 0xff, details JSON bytes); tests compute
+// the same over the oracle's rows (oracle/cpu_baseline.py row_hash)
+static bool g_digest = false;
+static uint64_t g_last_digest = 0;
+static uint64_t fnv_bytes(uint64_t h, const void* p, size_t n) {
+  const unsigned char* b = (const unsigned char*)p;
+  for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+  return h;
+}
 
 // A worker thread's output buffers: its copy of the launch arguments points
 // the emission path (devrt.h op_emit / emit_eager) at them.  One pair emits
@@ -224,8 +236,12 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
   }
   if (L.fail) { ++k.flagged; return; }
   const uint64_t n = gk_args.counters[0];
+  const uint32_t review = rc.orig != NO_ID ? rc.orig : rp;
+  std::vector<char> dbuf;
   for (uint64_t i = 0; i < n; ++i) {
     const Viol& v = gk_args.out[i];
+    const char* mp = gk_args.ebytes + v.msg_off;
+    uint32_t ml = v.msg_len;
     if (v.pad & VF_DEFER) {
       const uint32_t fidx = v.msg_len & 0xffffffu, na = v.msg_len >> 24;
       Out out{fbuf, 0, fcap, false};
@@ -234,17 +250,42 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
         return;
       }
       k.msg_bytes += out.n;
+      mp = fbuf;
+      ml = out.n;
     } else {
       k.msg_bytes += v.msg_len;
     }
+    const char* dp = "{}";
+    uint32_t dl = 2;
     if (v.pad & VF_DET_VAL) {
       // details copied out at emission: the size pass prints them (JSON)
       const uint32_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
+      const uint64_t dv = gk_args.frec[(uint64_t)di * gk_args.out_cap + i];
       Cnt cn{0, false};
-      if (!put_json(L, cn, gk_args.frec[(uint64_t)di * gk_args.out_cap + i])) {
+      if (!put_json(L, cn, dv)) {
         ++k.flagged;
         return;
       }
+      if (g_digest) {
+        dbuf.resize(cn.n + 1);
+        Out o{dbuf.data(), 0, (uint32_t)dbuf.size(), false};
+        put_json(L, o, dv);
+        dp = dbuf.data();
+        dl = o.n;
+      }
+    } else if (!(v.pad & VF_DET_OBJ)) {
+      dp = gk_args.ebytes + v.msg_off + ((v.pad & VF_DEFER) ? 0u : v.msg_len);
+      dl = v.det_len;
+    }
+    if (g_digest) {
+      uint64_t h = 1469598103934665603ull;
+      const uint32_t rc4[2] = {review, v.constraint};
+      h = fnv_bytes(h, rc4, 8);
+      h = fnv_bytes(h, mp, ml);
+      const unsigned char sep = 0xff;
+      h = fnv_bytes(h, &sep, 1);
+      h = fnv_bytes(h, dp, dl);
+      k.digest += h;
     }
     ++k.violations;
   }
@@ -370,8 +411,21 @@ double gkcpu_sweep(const void* args, uint32_t lo, uint32_t hi, int threads, uint
   for (auto& x : th) x.join();
   double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   uint64_t tot[4] = {0, 0, 0, 0};
-  for (auto& k : per) { tot[0] += k.evals; tot[1] += k.violations; tot[2] += k.msg_bytes; tot[3] += k.flagged; }
+  uint64_t dig = 0;
+  for (auto& k : per) { tot[0] += k.evals; tot[1] += k.violations; tot[2] += k.msg_bytes; tot[3] += k.flagged; dig += k.digest; }
+  gk::cpu::g_last_digest = dig;
   if (out4) memcpy(out4, tot, sizeof tot);
+  return s;
+}
+
+// gkcpu_sweep plus out5[4] = the digest of every result row (Counts::digest)
+double gkcpu_sweep_digest(const void* args, uint32_t lo, uint32_t hi, int threads, uint64_t* out5) {
+  gk::cpu::g_digest = true;
+  uint64_t o4[4];
+  const double s = gkcpu_sweep(args, lo, hi, threads, o4);
+  gk::cpu::g_digest = false;
+  memcpy(out5, o4, sizeof o4);
+  out5[4] = gk::cpu::g_last_digest;
   return s;
 }
 

@@ -58,12 +58,30 @@ def test_cache_batch_checker_equals_the_oracle_audit():
         od.put_data(p, json.dumps(o))
     b = d.debug_stage_cache()
     assert b.n == len(items) - 1  # the two-slash group/version names no review
-    _s, evals, viol, _mb, flagged = cpu_baseline.sweep(d, b, threads=4)
+    evals, viol, flagged, digest = cpu_baseline.sweep_digest(d, b, threads=4)
     # the null object's review (object: a string) goes to the CPU driver for
     # its five constraints (ReviewCol fallback); nothing else is flagged
     assert flagged in (0, len(cs)), flagged
     want = _oracle_rows(od)
     assert viol == len(want) > 100, (viol, len(want))
+    # row by row: the review's position in inventory path order, the engine's
+    # constraint index, message and details (an order-free digest)
+    import urllib.parse
+    from oracle.driver import details_json
+    order = {p: i for i, p in enumerate(sorted(p for p, _ in items if "%2Fb%2F" not in p))}
+    cidx = {kn: i for i, kn in enumerate(d.constraints())}
+    rows = []
+    for r in want:
+        rv, c = r["review"], r["constraint"]
+        k = rv.get("kind")
+        gv = k.get("version") if not k.get("group") else "%s/%s" % (k.get("group"), k.get("version"))
+        ns = rv.get("namespace") if hasattr(rv, "get") else None
+        path = ("/external/%s/namespace/%s/%s/%s/%s" % (TARGET, ns, urllib.parse.quote(gv, safe=""), k.get("kind"),
+                                                         rv.get("name")) if isinstance(ns, str) else
+                "/external/%s/cluster/%s/%s/%s" % (TARGET, urllib.parse.quote(gv, safe=""), k.get("kind"), rv.get("name")))
+        rows.append((order[path], cidx[(c.get("kind"), c.get("metadata").get("name"))], r["msg"],
+                     details_json(r["details"])))
+    assert digest == cpu_baseline.row_digest(rows)
 
 
 @pytest.mark.gpu

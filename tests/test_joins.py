@@ -350,8 +350,10 @@ def test_function_early_exit_keeps_results():
     """GKGPU_FN_EARLY=1 (compiler.cc early_exit_ok): a function whose bodies
     all yield one constant and cannot err stops at its first solution --
     probe_is_missing / missing / identical in the agilebank templates.  The
-    CPU checker's counts with it equal the oracle's on config 2 Pods and on
-    config 6 (a subprocess: the switch is read once per process)."""
+    CPU checker's result ROWS with it (an order-free digest of (review,
+    constraint, message, details), oracle/cpuvm.cc gkcpu_sweep_digest) equal
+    the oracle's on config 2 Pods and on config 6 (a subprocess: the switch is
+    read once per process)."""
     import os
     import subprocess
     import sys
@@ -369,25 +371,32 @@ def drv(ts, cs, extra=()):
     for c in cs: cl.add_constraint(c)
     for p, o in extra: d.put_data(p, o)
     return d
+def want_digest(d, od, objs, nss):
+    cidx = {kn: i for i, kn in enumerate(d.constraints())}
+    rows = []
+    for i, (o, n) in enumerate(zip(objs, nss)):
+        for kind, name, msg, det, _ea in oracle_review(od, augmented_review(o, n)):
+            rows.append((i, cidx[(kind, name)], msg, det))
+    return cpu_baseline.row_digest(rows), len(rows)
 ts, cs = W.config2()
 pods, ns_of, ns_objs = W.gen_pods(400, seed=9, n_namespaces=20)
 nss = [ns_objs[n] for n in ns_of]
 d = drv(ts, cs)
-got = cpu_baseline.sweep(d, d.stage_objects(pods, nss), threads=2)
-od = oracle_for(ts, cs)
-want = sum(len(oracle_review(od, augmented_review(p, n))) for p, n in zip(pods, nss))
+got = cpu_baseline.sweep_digest(d, d.stage_objects(pods, nss), threads=2)
+want = want_digest(d, oracle_for(ts, cs), pods, nss)
 ts6, cs6 = W.config6()
 objs, onss = W.gen_config6_json(200)
 inv = [(p, json.loads(o)) for p, o in W.inventory_paths(objs)]
 d6 = drv(ts6, cs6, inv)
-got6 = cpu_baseline.sweep(d6, d6.stage_objects(objs, onss), threads=2)
-od6 = oracle_for(ts6, cs6, inv)
-want6 = sum(len(oracle_review(od6, augmented_review(json.loads(o), json.loads(n)))) for o, n in zip(objs, onss))
-print(json.dumps([got[2], got[4], want, got6[2], got6[4], want6]))
+got6 = cpu_baseline.sweep_digest(d6, d6.stage_objects(objs, onss), threads=2)
+want6 = want_digest(d6, oracle_for(ts6, cs6, inv), [json.loads(o) for o in objs], [json.loads(n) for n in onss])
+print(json.dumps([got[1], got[2], got[3], want[0], want[1], got6[1], got6[2], got6[3], want6[0], want6[1]]))
 ''' % (os.path.join(ROOT, "gatekeeper-1_amd"), ROOT, os.path.join(ROOT, "tests"))
-    env = dict(os.environ, GKGPU_FN_EARLY="1")
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
-    assert out.returncode == 0, out.stderr[-2000:]
-    v, fl, want, v6, fl6, want6 = json.loads(out.stdout.strip().splitlines()[-1])
-    assert fl == 0 and fl6 == 0
-    assert v == want > 100 and v6 == want6 > 20, (v, want, v6, want6)
+    for early in ("0", "1"):
+        env = dict(os.environ, GKGPU_FN_EARLY=early)
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-2000:]
+        v, fl, dg, wd, wn, v6, fl6, dg6, wd6, wn6 = json.loads(out.stdout.strip().splitlines()[-1])
+        assert fl == 0 and fl6 == 0
+        assert v == wn > 100 and v6 == wn6 > 20, (early, v, wn, v6, wn6)
+        assert dg == wd and dg6 == wd6, (early, "row digests differ from the oracle's")
