@@ -12,6 +12,8 @@
 #include "flatten.h"
 
 #include <algorithm>
+#include <sched.h>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -38,9 +40,31 @@ int default_threads() {
     int n = atoi(v);
     if (n >= 1 && n <= 256) return n;
   }
-  unsigned hc = std::thread::hardware_concurrency();
-  // the GPU box grants a 16-CPU share whatever the machine's CPU count
-  return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+  // the host cores this process is leased: its CPU affinity set, capped by a
+  // cgroup CPU quota (the GPU box grants a 16-CPU share of a 256-CPU host:
+  // cpu.max "1600000 100000", affinity 0-255)
+  static const int leased = [] {
+    int n = 0;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+    long long q = 0, per = 0;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char a[32] = {0};
+      if (fscanf(f, "%31s %lld", a, &per) == 2 && strcmp(a, "max") != 0) q = atoll(a);
+      fclose(f);
+    } else if (FILE* f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+      if (fscanf(f2, "%lld", &q) != 1) q = 0;
+      fclose(f2);
+      if (FILE* f3 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (fscanf(f3, "%lld", &per) != 1) per = 0;
+        fclose(f3);
+      }
+    }
+    if (q > 0 && per > 0) n = std::min<int>(n, (int)std::max<long long>(1, (q + per - 1) / per));
+    return std::max(1, std::min(n, 256));
+  }();
+  return leased;
 }
 
 // ------------------------------------------------------------------ worker pool

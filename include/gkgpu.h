@@ -124,7 +124,8 @@ int gk_batch_stage_objects(gk_engine* e, const char* const* objs, const size_t* 
  * manager.go:96-115) with n_ns + 1 offsets, and per object the index of its
  * Namespace (UINT32_MAX = cluster-scoped: reviewed with an empty
  * corev1.Namespace{}, target.go:137-139).  Objects are parsed and flattened on
- * GKGPU_THREADS host threads (default: hardware threads, at most 16). */
+ * GKGPU_THREADS host threads (default: the leased host cores -- the CPU affinity
+ * set, capped by a cgroup CPU quota). */
 int gk_review_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
                    const uint64_t* ns_offs, size_t n_ns, const uint32_t* obj_ns, gk_results** out);
 int gk_batch_stage_page(gk_engine* e, const char* objs, const uint64_t* obj_offs, size_t n, const char* nss,
