@@ -111,14 +111,10 @@ static bool upload_bounce(void* dst, const char* src, size_t n) {
     ms_wait += std::chrono::duration<double, std::milli>(tc - tw).count();
     char* dstp = pin[b];
     const char* srcp = src + off;
-    std::vector<std::thread> th;
-    auto part = [&](int t) {
+    parallel_run(T, [&](int t) {
       const size_t lo = len * t / T, hi = len * (t + 1) / T;
       memcpy(dstp + lo, srcp + lo, hi - lo);
-    };
-    for (int t = 1; t < T; ++t) th.emplace_back(part, t);
-    part(0);
-    for (auto& x : th) x.join();
+    });
     ms_copy += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
     if (hipMemcpyAsync((char*)dst + off, dstp, len, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipEventRecord(ev[b], st) != hipSuccess) {
@@ -299,6 +295,7 @@ struct gk_batch {
   gk::DBuf d_revs;
   gk::DBuf d_nodes;  // the batch's own device node array: permanent region + its documents
   uint64_t dev_bytes = 0;
+  bool device_layout = false;  // d_nodes / d_revs hold the device-built path layout (node ids differ from arena's)
 };
 
 // Webhook micro-batch coalescer: concurrent single-review
@@ -2452,7 +2449,7 @@ static void review_order(gk_engine* e, const std::vector<ReviewCol>& cols, const
 // number of reviews the process excluder skipped.
 static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size, NodeArena& arena,
                              std::vector<ReviewCol>& cols, std::vector<ResourceIds>* resources, uint64_t* excluded,
-                             double* ms_parse = nullptr, uint32_t* paths = nullptr) {
+                             double* ms_parse = nullptr, uint32_t* paths = nullptr, DevLayout* dl = nullptr) {
   FlatResult fr;
   std::string err;
   auto exit_ = e->excluded.find("audit");
@@ -2466,8 +2463,9 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
     review_order(e, f.cols, f.weight, lo, hi, p);
   };
   if (!flatten_page(e->st, e->smu, e->ns_cache, ex, page, default_threads(), e->perm_nodes, arena, fr, err,
-                    path_layout ? &ord : nullptr, path_layout ? &perm : nullptr))
+                    path_layout ? &ord : nullptr, path_layout ? &perm : nullptr, path_layout ? dl : nullptr))
     return fail(e, GK_EINVAL, err);
+  if (dl && !path_layout) dl->nroots = NO_ID;  // no device layout: the host arena is uploaded as it is
   if (ms_parse) *ms_parse = fr.ms_parse;
   if (paths) *paths = fr.paths;
   if (resources) resources->swap(fr.resources);
@@ -2480,13 +2478,9 @@ static int flatten_page_into(gk_engine* e, const Page& page, bool order_by_size,
     std::vector<ReviewCol> sorted(cols.size());
     const size_t n = perm.size();
     const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 65536));
-    auto gather = [&](int t) {
+    parallel_run(T, [&](int t) {
       for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) { sorted[i] = cols[perm[i]]; sorted[i].orig = perm[i]; }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(gather, t);
-    gather(0);
-    for (auto& x : th) x.join();
+    });
     cols.swap(sorted);
     if (trace) fprintf(stderr, "flatten: review order %.1f ms\n", ms_since(t_ord));
   }
@@ -2605,6 +2599,51 @@ static bool batch_upload(gk_engine* e, gk_batch* b) {
   return true;
 }
 
+extern "C" int gk_device_layout(const Node* D, uint64_t nD, uint32_t base, const uint32_t* beg, const uint32_t* evalpos,
+                                const uint32_t* root_d, const uint32_t* slot, uint32_t nrev, uint32_t nroots, Node* N,
+                                ReviewCol* cols, uint32_t ncols, uint64_t* n_out, hipStream_t s);
+
+// batch_upload for the device layout: the permanent region as batch_upload
+// does, the per-document arena D into a scratch buffer, then layout.hip
+// permutes it into the batch's node array and rewrites the uploaded review
+// columns' node ids.  The host arena keeps D (the CPU checker reads it).
+static bool batch_upload_layout(gk_engine* e, gk_batch* b, const DevLayout& dl) {
+  const size_t perm = b->node_begin, docs = b->arena.size();
+  const uint32_t nrev = (uint32_t)dl.beg.size();
+  if (!docs || !nrev || b->cols.size() != nrev || dl.evalpos.size() != nrev || dl.root_d.size() != nrev ||
+      dl.slot.size() != nrev)
+    return batch_upload(e, b);
+  if (!b->d_nodes.reserve((perm + docs + 1) * sizeof(Node))) return false;
+  if (perm && (hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess ||
+               hipStreamSynchronize(nullptr) != hipSuccess))
+    return false;
+  DBuf dD, dbeg, deval, droot, dslot;
+  bool ok = dD.reserve(docs * sizeof(Node)) && dbeg.reserve(nrev * 4) && deval.reserve(nrev * 4) &&
+            droot.reserve(nrev * 4) && dslot.reserve(nrev * 4);
+  const size_t bytes = docs * sizeof(Node);
+  const char* bm = getenv("GKGPU_BOUNCE_MIN");
+  const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+  if (ok) ok = bytes >= bounce_min ? upload_bounce(dD.p, (const char*)b->arena.data(), bytes)
+                                   : hipMemcpy(dD.p, b->arena.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && hipMemcpy(dbeg.p, dl.beg.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(deval.p, dl.evalpos.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(droot.p, dl.root_d.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(dslot.p, dl.slot.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess;
+  hipStream_t st = nullptr;
+  uint64_t nout = 0;
+  if (ok) ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+  if (ok)
+    ok = gk_device_layout((const Node*)dD.p, docs, b->node_begin, (const uint32_t*)dbeg.p, (const uint32_t*)deval.p,
+                          (const uint32_t*)droot.p, (const uint32_t*)dslot.p, nrev, dl.nroots,
+                          (Node*)b->d_nodes.p + perm, (ReviewCol*)b->d_revs.p, nrev, &nout, st) == 0;
+  if (st) hipStreamDestroy(st);
+  for (DBuf* x : {&dD, &dbeg, &deval, &droot, &dslot}) x->free_();
+  if (!ok) return false;
+  b->d_nodes.used = (perm + docs) * sizeof(Node);
+  b->device_layout = true;
+  return true;
+}
+
 static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
   ReadLock rl;
   int rc = read_lock(e, rl, !e->host_only);
@@ -2620,7 +2659,12 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   b->eng = e;
   b->node_begin = e->perm_nodes;
   const bool size_order = env_mode("GKGPU_SIZE_ORDER", 1, 1) != 0;  // A/B switch (default on)
-  rc = flatten_page_into(e, page, size_order, b->arena, b->cols, &b->resources, &b->excluded, &b->ms_parse);
+  // GKGPU_DEVICE_LAYOUT (A/B switch, default on): the path-grouped layout is
+  // built on the device (layout.hip) from the per-document arena
+  DevLayout dl;
+  const bool dev_layout = !e->host_only && e->dev_ok && env_mode("GKGPU_DEVICE_LAYOUT", 1, 1) != 0;
+  rc = flatten_page_into(e, page, size_order, b->arena, b->cols, &b->resources, &b->excluded, &b->ms_parse, nullptr,
+                         dev_layout ? &dl : nullptr);
   if (rc != GK_OK) return rc;
   b->ms_flatten = ms_since(t0);
   b->node_end = b->node_begin + (uint32_t)b->arena.size();
@@ -2638,7 +2682,8 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   const double ms_tables = ms_since(t1);
   up_ok = up_ok && up(b->d_revs, b->cols, false);
   const double ms_cols = ms_since(t1);
-  up_ok = up_ok && batch_upload(e, b.get());
+  if (dev_layout && dl.nroots != NO_ID) up_ok = up_ok && batch_upload_layout(e, b.get(), dl);
+  else up_ok = up_ok && batch_upload(e, b.get());
   if (trace)
     fprintf(stderr, "stage upload: strings %.1f ms, columns %.1f ms, nodes %.1f ms\n", ms_tables, ms_cols - ms_tables,
             ms_since(t1) - ms_cols);
@@ -3331,6 +3376,67 @@ extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, si
   return GK_OK;
 }
 
+// Content hash over a staged batch's review columns (in order), the documents
+// and label objects they reference in `all` (node ids as the columns give
+// them) and the resource ids: equal for every layout of the same batch.
+// Caller holds e->smu.
+static uint64_t columns_hash(gk_engine* e, const Node* all, const std::vector<ReviewCol>& cols,
+                             const std::vector<ResourceIds>& resources) {
+  uint64_t h = 0;
+  for (size_t i = 0; i < cols.size(); ++i) {
+    const ReviewCol& c = cols[i];
+    auto sh = [&](uint32_t sid) -> uint64_t {
+      if (sid == NO_ID) return 7;
+      std::string_view v = e->st.str(sid);
+      return fnv1a(v.data(), v.size());
+    };
+    uint64_t x = doc_hash(e->st, all, c.root) * 31 + sh(c.group);
+    x = x * 31 + sh(c.kind);
+    x = x * 31 + sh(c.ns);
+    x = x * 31 + sh(c.nsname);
+    x = x * 31 + doc_hash(e->st, all, c.labels);
+    x = x * 31 + doc_hash(e->st, all, c.old_labels);
+    x = x * 31 + doc_hash(e->st, all, c.ns_labels);
+    x = x * 31 + c.flags;
+    const ResourceIds& r = resources[i];
+    x = x * 31 + sh(r.api_version);
+    x = x * 31 + sh(r.kind);
+    x = x * 31 + sh(r.name);
+    x = x * 31 + sh(r.ns);
+    h = (h ^ x) * 1099511628211ull + i;
+  }
+  return h;
+}
+
+// The staged batch as the kernels see it: the device node array and review
+// columns downloaded and hashed as gk_debug_flatten_page hashes the host
+// forms (GPU tests of the device-built layout, layout.hip).
+extern "C" int gk_debug_batch_hash(gk_engine* e, const gk_batch* b, uint64_t* hash) {
+  if (!e || !b || !hash) return GK_EINVAL;
+  ReadLock rl;
+  int rc = read_lock(e, rl, false);
+  if (rc != GK_OK) return rc;
+  if (!b->d_nodes.p || !b->d_revs.p) return fail(e, GK_EINVAL, "batch has no device copy");
+  const size_t nn = b->node_end;
+  std::vector<Node> all(nn);
+  std::vector<ReviewCol> cols(b->cols.size());
+  if (hipMemcpy(all.data(), b->d_nodes.p, nn * sizeof(Node), hipMemcpyDeviceToHost) != hipSuccess ||
+      (cols.size() && hipMemcpy(cols.data(), b->d_revs.p, cols.size() * sizeof(ReviewCol), hipMemcpyDeviceToHost) != hipSuccess))
+    return fail(e, GK_EDEVICE, "device download failed");
+  // columns back to batch order (the resource ids' and gk_debug_flatten_page's)
+  std::vector<ReviewCol> bcols(cols.size());
+  if (b->resources.size() != cols.size()) return fail(e, GK_EINVAL, "column without resource ids");
+  for (size_t i = 0; i < cols.size(); ++i) {
+    const uint32_t o = b->cols[i].orig == NO_ID ? (uint32_t)i : b->cols[i].orig;
+    if (o >= cols.size()) return fail(e, GK_EINVAL, "column order out of range");
+    bcols[o] = cols[i];
+    bcols[o].orig = NO_ID;
+  }
+  std::lock_guard<std::mutex> sg(e->smu);
+  *hash = columns_hash(e, all.data(), bcols, b->resources);
+  return GK_OK;
+}
+
 // Flattens a page on `threads` host threads without a device (diagnostics and
 // CPU tests): *hash = content hash over every review's columns and document,
 // ms2 = [parse + build, total flatten].  The documents are dropped afterwards.
@@ -3354,36 +3460,20 @@ extern "C" int gk_debug_flatten_page(gk_engine* e, const char* objs, const uint6
     review_order(e, f.cols, f.weight, lo, hi, p);
   };
   const int nt = threads > 0 ? threads : threads < 0 ? -threads : default_threads();
+  // GKGPU_DEBUG_DEVICE_FORM (with threads < 0): the per-document arena the
+  // device layout pass (layout.hip) starts from
+  DevLayout dl;
+  const bool dform = threads < 0 && getenv("GKGPU_DEBUG_DEVICE_FORM");
   if (!flatten_page(e->st, e->smu, e->ns_cache, ex, pg, nt, e->perm_nodes, arena, fr, err, threads < 0 ? &ord : nullptr,
-                    threads < 0 ? &perm : nullptr))
+                    threads < 0 ? &perm : nullptr, dform ? &dl : nullptr))
     return fail(e, GK_EINVAL, err);
+  if (dform && (dl.beg.size() != fr.cols.size() || dl.nroots > fr.cols.size()))
+    return fail(e, GK_EINVAL, "device layout inputs do not match the columns");
   double tot = ms_since(t0);
   std::vector<Node> all(e->st.nodes().begin(), e->st.nodes().begin() + e->perm_nodes);
   all.insert(all.end(), arena.begin(), arena.end());
   std::lock_guard<std::mutex> sg(e->smu);
-  uint64_t h = 0;
-  for (size_t i = 0; i < fr.cols.size(); ++i) {
-    const ReviewCol& c = fr.cols[i];
-    auto sh = [&](uint32_t sid) -> uint64_t {
-      if (sid == NO_ID) return 7;
-      std::string_view v = e->st.str(sid);
-      return fnv1a(v.data(), v.size());
-    };
-    uint64_t x = doc_hash(e->st, all.data(), c.root) * 31 + sh(c.group);
-    x = x * 31 + sh(c.kind);
-    x = x * 31 + sh(c.ns);
-    x = x * 31 + sh(c.nsname);
-    x = x * 31 + doc_hash(e->st, all.data(), c.labels);
-    x = x * 31 + doc_hash(e->st, all.data(), c.old_labels);
-    x = x * 31 + doc_hash(e->st, all.data(), c.ns_labels);
-    x = x * 31 + c.flags;
-    const ResourceIds& r = fr.resources[i];
-    x = x * 31 + sh(r.api_version);
-    x = x * 31 + sh(r.kind);
-    x = x * 31 + sh(r.name);
-    x = x * 31 + sh(r.ns);
-    h = (h ^ x) * 1099511628211ull + i;
-  }
+  const uint64_t h = columns_hash(e, all.data(), fr.cols, fr.resources);
   if (hash) *hash = h;
   if (nodes) *nodes = fr.node_count;
   if (ms2) { ms2[0] = fr.ms_parse; ms2[1] = tot; }

@@ -455,6 +455,7 @@ struct Part {
   // phase 2 maps (local id -> global id)
   std::vector<uint32_t> smap, nmap;
   uint64_t node_off = 0;             // global index of this part's node kFixedNodes
+  std::vector<uint32_t> rbeg;        // per review: its first local node (device layout)
 };
 
 void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set<std::string>* ex, const Page& pg) {
@@ -524,6 +525,7 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
   };
   for (size_t i = p.lo; i < p.hi; ++i) {
     size_t n0 = st.nodes().size();
+    p.rbeg.push_back((uint32_t)n0);
     Node obj;
     if (!st.parse_doc(pg.objs + pg.obj_offs[i], pg.obj_offs[i + 1] - pg.obj_offs[i], &obj, &err)) {
       p.err = "invalid object JSON at " + std::to_string(i) + ": " + err;
@@ -813,6 +815,116 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
 
 }  // namespace
 
+// Phase 3 for the device layout (flatten.h DevLayout, layout.hip): the parts'
+// nodes relocated into one per-document arena D (as without a layout), every
+// container's `val` its global document path (kSharedPath for the shared
+// Namespace runs), plus what the device pass needs per review: where its
+// document starts in D, its evaluation position and its root's slot.
+static bool relocate_for_device(std::vector<Part>& parts, uint32_t base, NodeArena& dst, FlatResult& out, size_t n,
+                                std::string& err, const OrderFn& order, std::vector<uint32_t>& perm, DevLayout& dl) {
+  const int T = (int)parts.size();
+  auto pfor = [&](const std::function<void(int)>& f) { parallel_run(T, f); };
+  // columns with global string ids (node ids below), each part's evaluation order
+  out.cols.resize(n);
+  out.weight.resize(n);
+  out.resources.resize(n);
+  pfor([&](int t) {
+    Part& p = parts[t];
+    auto str = [&](uint32_t s) { return s == NO_ID ? NO_ID : p.smap[s]; };
+    for (size_t i = 0; i < p.cols.size(); ++i) {
+      ReviewCol rc = p.cols[i];
+      rc.group = str(rc.group);
+      rc.kind = str(rc.kind);
+      rc.ns = str(rc.ns);
+      rc.nsname = str(rc.nsname);
+      out.cols[p.lo + i] = rc;
+      out.weight[p.lo + i] = p.weight[i];
+      const ResourceIds& r = p.res[i];
+      out.resources[p.lo + i] = ResourceIds{str(r.api_version), str(r.kind), str(r.name), str(r.ns)};
+    }
+  });
+  std::vector<std::vector<uint32_t>> porder(T);
+  pfor([&](int t) { order(out, parts[t].lo, parts[t].hi, porder[t]); });
+  perm.clear();
+  perm.reserve(n);
+  for (int t = 0; t < T; ++t) {
+    if (porder[t].size() != parts[t].hi - parts[t].lo) { err = "review order: bad permutation"; return false; }
+    perm.insert(perm.end(), porder[t].begin(), porder[t].end());
+  }
+  // global paths (a part's paths are numbered parent first)
+  std::unordered_map<uint64_t, uint32_t> gm;
+  std::vector<std::vector<uint32_t>> g_of(T);
+  uint32_t G = 1;
+  for (int t = 0; t < T; ++t) {
+    const PathTab& pt = parts[t].paths;
+    g_of[t].assign(pt.def.size(), 0);
+    for (uint32_t l = 1; l < pt.def.size(); ++l) {
+      const uint32_t key = pt.def[l].second == kElem ? kElem : parts[t].smap[pt.def[l].second];
+      const uint64_t k = ((uint64_t)g_of[t][pt.def[l].first] << 32) | key;
+      auto it = gm.find(k);
+      if (it == gm.end()) it = gm.emplace(k, G++).first;
+      g_of[t][l] = it->second;
+    }
+  }
+  uint64_t total = 0;
+  for (auto& p : parts) {
+    p.node_off = total;
+    total += p.st.nodes().size() - kFixedNodes;
+  }
+  if ((uint64_t)base + total >= NO_ID) { err = "node arena exceeds 2^32 nodes"; return false; }
+  dst.resize(total);
+  dl.beg.assign(n, 0);
+  Node* dn = dst.data();
+  pfor([&](int t) {
+    Part& p = parts[t];
+    const auto& ln = p.st.nodes();
+    const uint32_t goff = base + (uint32_t)p.node_off - kFixedNodes;
+    Node* d = dn + p.node_off - kFixedNodes;
+    auto node = [&](uint32_t x) { return x == NO_ID ? NO_ID : (x < kFixedNodes ? x : x + goff); };
+    const std::vector<uint32_t>& gp = g_of[t];
+    for (size_t k = kFixedNodes; k < ln.size(); ++k) {
+      Node x = ln[k];
+      if (x.type == NT_STR) x.val = p.smap[x.val];
+      else if (x.type == NT_NUM) x.val = p.nmap[x.val];
+      else if (x.type == NT_ARR || x.type == NT_OBJ) {
+        if (x.flags & kShared) x.val = DevLayout::kSharedPath;
+        else x.val = x.n && x.val < gp.size() ? gp[x.val] : 0;
+        if (x.n) x.first += goff;
+      }
+      d[k] = x;  // kShared stays: the device pass reads and clears it
+    }
+    for (size_t k = kFixedNodes; k < ln.size(); ++k) {
+      const Node& x = ln[k];
+      if (x.type != NT_OBJ) continue;
+      for (uint32_t c = 0; c < x.n; ++c) d[x.first + c].key = p.smap[ln[x.first + c].key];
+    }
+    for (size_t i = 0; i < p.cols.size(); ++i) {
+      ReviewCol& rc = out.cols[p.lo + i];
+      rc.root = node(p.cols[i].root);
+      rc.labels = node(p.cols[i].labels);
+      rc.old_labels = node(p.cols[i].old_labels);
+      if (!p.nsglob[i]) rc.ns_labels = node(p.cols[i].ns_labels);
+      dl.beg[p.lo + i] = (uint32_t)(p.node_off + (i < p.rbeg.size() ? p.rbeg[i] : ln.size()) - kFixedNodes);
+    }
+  });
+  dl.evalpos.assign(n, 0);
+  dl.slot.assign(n, NO_ID);
+  dl.root_d.assign(n, NO_ID);
+  uint32_t live = 0;
+  for (size_t k = 0; k < perm.size(); ++k) {
+    const uint32_t b = perm[k];
+    dl.evalpos[b] = (uint32_t)k;
+    dl.root_d[b] = out.cols[b].root;
+    if (out.cols[b].root != NO_ID) dl.slot[b] = live++;
+  }
+  dl.nroots = live;
+  out.excluded = 0;
+  for (auto& p : parts) out.excluded += p.excluded;
+  out.node_count = total;
+  out.paths = G;
+  return true;
+}
+
 // Phases 2 and 3 of every flattening: the parts' strings and numbers are
 // interned into the engine store (under `smu`: concurrent evaluations intern
 // into the one table), then each part's nodes are copied into `dst` -- node id
@@ -820,7 +932,7 @@ static bool layout_parts(std::vector<Part>& parts, uint32_t base, NodeArena& dst
 // rewritten, and its columns relocated.
 static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, uint32_t base, NodeArena& dst,
                         FlatResult& out, size_t n, std::string& err, const OrderFn* order = nullptr,
-                        std::vector<uint32_t>* perm = nullptr) {
+                        std::vector<uint32_t>* perm = nullptr, DevLayout* dl = nullptr) {
   using Clock = std::chrono::steady_clock;
   auto t1 = Clock::now();
   const int T = (int)parts.size();
@@ -848,6 +960,7 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
   if (getenv("GKGPU_FLATTEN_TRACE"))
     fprintf(stderr, "flatten: intern %.1f ms (%zu strings)\n", std::chrono::duration<double, std::milli>(t15 - t1).count(),
             extra);
+  if (order && dl) return relocate_for_device(parts, base, dst, out, n, err, *order, *perm, *dl);
   if (order) return layout_parts(parts, base, dst, out, n, err, *order, *perm, t1);
   uint64_t total = 0;
   for (auto& p : parts) {
@@ -912,7 +1025,7 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
 
 bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded,
                   const Page& pg, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err,
-                  const OrderFn* order, std::vector<uint32_t>* perm) {
+                  const OrderFn* order, std::vector<uint32_t>* perm, DevLayout* dl) {
   using Clock = std::chrono::steady_clock;
   auto t0 = Clock::now();
   const size_t n = pg.n;
@@ -933,7 +1046,7 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
   out.ms_parse = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   if (getenv("GKGPU_FLATTEN_TRACE")) fprintf(stderr, "flatten: parse %.1f ms\n", out.ms_parse);
   if (order && !perm) { err = "flatten_page: order without perm"; return false; }
-  return merge_parts(gst, smu, parts, base, dst, out, n, err, order, perm);
+  return merge_parts(gst, smu, parts, base, dst, out, n, err, order, perm, dl);
 }
 
 bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,

@@ -124,9 +124,21 @@ using OrderFn = std::function<void(const FlatResult&, size_t lo, size_t hi, std:
 // every consumer of the node store reads it unchanged; what changes is that
 // the wavefront's 64 consecutive reviews find their nodes at one path next to
 // each other (a column of node runs per path) instead of in 64 documents.
+// With `order` and `dl` (staged batches on a device), the path-grouped layout
+// is built on the device instead (layout.hip gk_device_layout): `dst` is the
+// per-document arena D -- every container's `val` its global document path --
+// and `dl` what the device pass needs per review.
+struct DevLayout {
+  static constexpr uint32_t kSharedPath = 0xffffffffu;  // a shared Namespace run
+  std::vector<uint32_t> beg;      // per batch index: the D index of its document's first node
+  std::vector<uint32_t> evalpos;  // per batch index: its evaluation position
+  std::vector<uint32_t> root_d;   // per batch index: its root's id in D (NO_ID: excluded)
+  std::vector<uint32_t> slot;     // per batch index: its root's index in the layout (NO_ID: excluded)
+  uint32_t nroots = 0;            // live reviews
+};
 bool flatten_page(Store& st, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded_ns,
                   const Page& page, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err,
-                  const OrderFn* order = nullptr, std::vector<uint32_t>* perm = nullptr);
+                  const OrderFn* order = nullptr, std::vector<uint32_t>* perm = nullptr, DevLayout* dl = nullptr);
 
 // Query inputs ({"review": ...} documents, Driver.Query's input) into `dst`
 // likewise, with their match columns.

@@ -693,6 +693,15 @@ class Driver:
         self._check(self._lib.gk_debug_flatten_page(self._e, *args, threads, C.byref(h), C.byref(n), ms))
         return h.value, n.value, ms[0], ms[1]
 
+    def debug_batch_hash(self, batch) -> int:
+        """content hash of a staged batch as the kernels see it (its device node
+        array and review columns downloaded; equal to debug_flatten's hash of
+        the same page)"""
+        h = C.c_uint64()
+        self._lib.gk_debug_batch_hash.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+        self._check(self._lib.gk_debug_batch_hash(self._e, batch._h, C.byref(h)))
+        return h.value
+
     # -- process excluder (excluder.go)
     def excluder_add(self, processes: Sequence[str], namespaces: Sequence[str]):
         """Excluder.Add(MatchEntry{ExcludedNamespaces, Processes}) (excluder.go:44-68)"""

@@ -137,3 +137,18 @@ def test_unparsable_api_version_gives_an_empty_gvk():
     b = d.stage_objects([obj, ok], [None, None])
     assert b.resource(0) == ("", "", "p", "n")
     assert b.resource(1) == ("apps/v1", "Deployment", "d", "n")
+
+
+def test_device_layout_input_holds_the_same_documents(drv, monkeypatch):
+    """The per-document arena the device layout pass (layout.hip) permutes --
+    containers carrying their document path, shared Namespace runs flagged --
+    holds the same documents and columns as both host layouts."""
+    for gen, n in ((lambda: W.gen_pods_json(9000, seed=42, n_namespaces=50), 9000),
+                   (lambda: W.gen_config4_json(6000, seed=99), 6000)):
+        objs, nss = gen()
+        pg = Page.from_lists(objs, nss)
+        for t in (1, 3):
+            monkeypatch.delenv("GKGPU_DEBUG_DEVICE_FORM", raising=False)
+            host = drv.debug_flatten(pg, -t)[0]
+            monkeypatch.setenv("GKGPU_DEBUG_DEVICE_FORM", "1")
+            assert drv.debug_flatten(pg, -t)[0] == host == drv.debug_flatten(pg, t)[0]

@@ -13,7 +13,7 @@ export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
 for what in "${@:-c2 c4 c5 cache}"; do
   case $what in
     c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_JIT_OUTLINE=0 GKGPU_JIT_PMEMO=0" \
-          "GKGPU_JIT_LMEMO=1" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=32" "GKGPU_INLINE_HOT=0" "GKGPU_FN_EARLY=1" || exit 1 ;;
+          "GKGPU_JIT_LMEMO=1" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=32" "GKGPU_INLINE_HOT=0" "GKGPU_FN_EARLY=1" "GKGPU_DEVICE_LAYOUT=0" || exit 1 ;;
     c4) bash tools/gpu_bench_ab.sh "$TAG/c4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
     c5) timeout -k 10 300 python -u tools/probe_c5_time.py 256 > "$OUT/c5_phases.txt" 2>&1 || { echo C5P_FAIL; tail "$OUT/c5_phases.txt"; exit 1; }
         cat "$OUT/c5_phases.txt"
