@@ -1,6 +1,8 @@
 // Host-side interned store (strings, numbers, node arena) + exact number
 // conversions matching Go's math/big / strconv behaviour.
 #include "store.h"
+
+#include <emmintrin.h>
 #include "flatten.h"
 
 #include <atomic>
@@ -323,8 +325,26 @@ static uint8_t str_flags_of(const char* p, size_t n) {
 }
 
 uint32_t Store::intern(const char* p, size_t n) {
+  if (n <= 32) {
+    // the string as four words (overlapping loads; with n they determine it)
+    uint64_t w[4] = {0, 0, 0, 0};
+    if (n > 16) { memcpy(&w[0], p, 8); memcpy(&w[1], p + 8, 8); memcpy(&w[2], p + n - 16, 8); memcpy(&w[3], p + n - 8, 8); }
+    else if (n >= 8) { memcpy(&w[0], p, 8); memcpy(&w[1], p + n - 8, 8); }
+    else if (n) memcpy(&w[0], p, n);
+    const uint64_t k = (w[0] * 0x9e3779b97f4a7c15ull) ^ (w[1] * 0xc2b2ae3d27d4eb4full) ^
+                       ((w[2] ^ (w[3] << 1)) * 0x94d049bb133111ebull) ^ (n * 0x165667b19e3779f9ull);
+    if (short_.empty()) short_.assign(kShortCache, ShortEnt{{0, 0, 0, 0}, ~0u, 0});
+    ShortEnt& e = short_[(k >> 40) & (kShortCache - 1)];
+    if (e.len == n && e.w[0] == w[0] && e.w[1] == w[1] && e.w[2] == w[2] && e.w[3] == w[3]) return e.id;
+    const uint32_t id = intern_slow(p, n, str_hash(p, n));
+    e = ShortEnt{{w[0], w[1], w[2], w[3]}, (uint32_t)n, id};
+    return id;
+  }
+  return intern_slow(p, n, str_hash(p, n));
+}
+
+uint32_t Store::intern_slow(const char* p, size_t n, uint64_t hv) {
   size_t mask = table_.size() - 1;
-  uint64_t hv = str_hash(p, n);
   uint64_t tag = hv & 0xffffffff00000000ull;
   size_t h = hv & mask;
   while (uint64_t e = table_[h]) {
@@ -482,7 +502,18 @@ class DocParser {
     if (p_ >= e_ || *p_ != '"') return false;
     ++p_;
     const char* s = p_;
+    // 16 bytes at a time to the first quote, backslash or control byte
+    const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), c1f = _mm_set1_epi8(0x1f);
+    while (e_ - p_ >= 16) {
+      const __m128i v = _mm_loadu_si128((const __m128i*)p_);
+      const __m128i hit = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)),
+                                       _mm_cmpeq_epi8(_mm_max_epu8(v, c1f), c1f));
+      const unsigned m = (unsigned)_mm_movemask_epi8(hit);
+      if (m) { p_ += __builtin_ctz(m); goto scanned; }
+      p_ += 16;
+    }
     while (p_ < e_ && *p_ != '"' && *p_ != '\\' && (unsigned char)*p_ >= 0x20) ++p_;
+  scanned:
     if (p_ < e_ && *p_ == '"') {  // no escapes: intern straight from the input
       *sid = st_.intern(s, (size_t)(p_ - s));
       ++p_;

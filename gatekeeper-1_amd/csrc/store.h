@@ -142,6 +142,13 @@ class Store {
   std::vector<BfsEnt> bfs_;  // add_doc work queue (reused)
   std::vector<Node> pend_;   // parse_doc: children of the open objects / arrays
   std::string scratch_;      // parse_doc: unescaped string bytes
+  // direct-mapped cache of short strings (<= 32 bytes: the bytes themselves are
+  // the tag, so a hit touches one 40-byte entry instead of the table, the
+  // string entry and the pool -- object keys and repeated values)
+  struct ShortEnt { uint64_t w[4]; uint32_t len, id; };
+  static constexpr size_t kShortCache = 4096;
+  std::vector<ShortEnt> short_;
+  uint32_t intern_slow(const char* p, size_t n, uint64_t hv);
   friend class DocParser;
   void grow();
   void rehash(size_t sz);
