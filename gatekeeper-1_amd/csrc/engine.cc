@@ -2965,6 +2965,12 @@ int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double
   return GK_OK;
 }
 
+int gk_engine_prepare(gk_engine* e, int device) {
+  if (!e) return GK_EINVAL;
+  ReadLock rl;
+  return read_lock(e, rl, device != 0 && !e->host_only);
+}
+
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail) {
   if (!e || !kind) return GK_EINVAL;
   WriteLock g(e);  // compiles on demand

@@ -330,7 +330,14 @@ uint32_t Store::intern(const char* p, size_t n) {
     uint64_t w[4] = {0, 0, 0, 0};
     if (n > 16) { memcpy(&w[0], p, 8); memcpy(&w[1], p + 8, 8); memcpy(&w[2], p + n - 16, 8); memcpy(&w[3], p + n - 8, 8); }
     else if (n >= 8) { memcpy(&w[0], p, 8); memcpy(&w[1], p + n - 8, 8); }
-    else if (n) memcpy(&w[0], p, n);
+    else if (n >= 4) {
+      uint32_t lo, hi;
+      memcpy(&lo, p, 4);
+      memcpy(&hi, p + n - 4, 4);
+      w[0] = lo | (uint64_t)hi << 32;
+    } else if (n) {
+      w[0] = (uint8_t)p[0] | (uint32_t)(uint8_t)p[n >> 1] << 8 | (uint32_t)(uint8_t)p[n - 1] << 16;
+    }
     const uint64_t k = (w[0] * 0x9e3779b97f4a7c15ull) ^ (w[1] * 0xc2b2ae3d27d4eb4full) ^
                        ((w[2] ^ (w[3] << 1)) * 0x94d049bb133111ebull) ^ (n * 0x165667b19e3779f9ull);
     if (short_.empty()) short_.assign(kShortCache, ShortEnt{{0, 0, 0, 0}, ~0u, 0});

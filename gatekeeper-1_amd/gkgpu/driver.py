@@ -32,7 +32,7 @@ EXPORTS = [
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
     "gk_results_export", "gk_results_samples_export", "gk_results_generation", "gk_coalesce_stats",
-    "gk_template_joins", "gk_join_stats",
+    "gk_template_joins", "gk_join_stats", "gk_engine_prepare",
 ]
 
 
@@ -770,6 +770,13 @@ class Driver:
         s = C.string_at(p).decode()
         self._lib.gk_free_string(p)
         return s
+
+    def prepare(self, device: bool = True):
+        """gk_engine_prepare: compile and upload the current templates and
+        constraints now (the reference compiles at AddTemplate), so the next
+        staging / evaluation does not"""
+        self._lib.gk_engine_prepare.argtypes = [C.c_void_p, C.c_int]
+        self._check(self._lib.gk_engine_prepare(self._e, 1 if device else 0))
 
     def template_backend(self, kind: str):
         """(backend, detail): 2 template kernel (hipRTC), 1 bytecode VM, 3 guard program on

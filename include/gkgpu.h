@@ -277,6 +277,14 @@ int gk_template_status(gk_engine* e, const char* kind, const char** reason);
  * flagged GK_REVIEW_FALLBACK (detail = reason), 0 = CPU fallback for every
  * matched review (detail = reason).  Compiles on demand. */
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail);
+/* Prepares the engine's current state for evaluation now instead of at the
+ * next staging / evaluation: rules and constraints compiled, match tables and
+ * constants uploaded, template kernels compiled (hipRTC or the code-object
+ * cache) and loaded, join indexes built.  The reference compiles a template's
+ * Rego when it is added (client.go AddTemplate), not inside the audit sweep;
+ * an audit loop calls this after syncing templates and constraints.
+ * device = 0: host state only.  0 = success. */
+int gk_engine_prepare(gk_engine* e, int device);
 /* inventory join sites of a template (compiler.cc join_site): iterations of
  * data.inventory whose body filters on `A == key(leaf)` run as probes of a
  * per-constraint hash index built on the device (the reference scans:

@@ -29,19 +29,22 @@ import gkgpu
 from gkgpu import workloads as W
 from gkgpu.client import Client
 ts, cs = getattr(W, "config%d")()
-d = gkgpu.Driver()
-cl = Client(d)
+import os
 for t in ts:
-    cl.add_template(t)
-for t in ts:
+    # one engine per template: its kernel source alone in its own directory
     k = t["spec"]["crd"]["spec"]["names"]["kind"]
+    os.makedirs(os.path.join(%r, k), exist_ok=True)
+    os.environ["GKGPU_JIT_DUMP"] = os.path.join(%r, k)
+    d = gkgpu.Driver()
+    Client(d).add_template(t)
     print(k, d.template_backend(k))
-''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), config)
+''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), config, d, d)
     env = dict(os.environ, GKGPU_JIT_CACHE="0", GKGPU_JIT_DUMP=d, GKGPU_JIT_DUMP_ONLY="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         raise SystemExit(r.stderr[-3000:])
-    return sorted(glob.glob(os.path.join(d, "*.hip"))), r.stdout
+    files = [(os.path.basename(os.path.dirname(f)), f) for f in sorted(glob.glob(os.path.join(d, "*", "*.hip")))]
+    return files, r.stdout
 
 
 FIELDS = ("VGPRs:", "AGPRs:", "SGPRs:", "ScratchSize", "Occupancy", "LDS Size", "VGPRs Spill", "SGPRs Spill")
@@ -66,9 +69,9 @@ def main():
     a = ap.parse_args()
     files, backends = dump_sources(a.config)
     rep = ["config %d template kernels (hipcc gfx950 -O3, kernel-resource-usage)" % a.config, backends.strip(), ""]
-    for f in files:
+    for kind, f in files:
         name, rc, keep = resources(f)
-        rep.append("%s (rc %d)" % (name, rc))
+        rep.append("%s %s (rc %d)" % (kind, name, rc))
         rep.extend("  " + k for k in keep)
     text = "\n".join(rep) + "\n"
     print(text)
