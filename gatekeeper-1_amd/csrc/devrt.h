@@ -265,11 +265,30 @@ __shared__ uint32_t gk_lds_dfa[4][LDS_DFA_BYTES / 4];
 __shared__ uint32_t gk_lds_dfadir[4][1 + 4 * LDS_DFA_MAX];
 #endif
 
+// GK_LDS_MEMO (template kernels, jit.cc): a direct-mapped cache in front of
+// the cross-lane memo (gm_get / gm_put below), GK_LDS_MEMO entries of
+// (key0, key1, value, check) per wavefront.  A pure call's arguments repeat
+// within a wave -- K8sContainerLimits' canonify_cpu("2000m") at every
+// container of the 64 Pods -- and each probe of the global table is a
+// dependent L2 round trip; the wave's own copy answers in LDS.  Entries are
+// guarded by the same check word as the global table, so racing lanes of
+// the wave and collisions read as misses.  Cleared at wave start.
+#ifndef GK_LDS_MEMO
+#define GK_LDS_MEMO 0
+#endif
+static_assert((GK_LDS_MEMO & (GK_LDS_MEMO - 1)) == 0, "GK_LDS_MEMO: a power of two");
+#if GK_LDS_MEMO && !defined(GK_HOST)
+__shared__ uint64_t gk_lds_memo[4][GK_LDS_MEMO][4];
+#endif
+
 // copies this wave's stage (all 64 lanes, wave-uniform m); the wave's own
 // lanes read it after the wave barrier
 __device__ __forceinline__ void stage_wave(const MatchSpec& m, uint32_t lane) {
-#if GK_LDS_PARAMS || GK_LDS_DFA
+#if GK_LDS_PARAMS || GK_LDS_DFA || (GK_LDS_MEMO && !defined(GK_HOST))
   const uint32_t wv = threadIdx.x >> 6;
+#endif
+#if GK_LDS_MEMO && !defined(GK_HOST)
+  for (uint32_t k = lane; k < GK_LDS_MEMO * 4u; k += 64) (&gk_lds_memo[wv][0][0])[k] = 0;
 #endif
 #if GK_LDS_PARAMS
   const uint32_t pn = m.pn <= LDS_PCAP ? m.pn : 0;
@@ -297,7 +316,7 @@ __device__ __forceinline__ void stage_wave(const MatchSpec& m, uint32_t lane) {
   }
   if (lane == 0) gk_lds_dfadir[wv][0] = nd;
 #endif
-#if GK_LDS_PARAMS || GK_LDS_DFA
+#if GK_LDS_PARAMS || GK_LDS_DFA || (GK_LDS_MEMO && !defined(GK_HOST))
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2157,15 +2176,38 @@ __device__ __noinline__ uint64_t gm_value_slow(const PLane& L, uint64_t v) {
   return mkv(V_GSTR, ((uint64_t)at << 20) | s.n);
 }
 
+#if GK_LDS_MEMO && !defined(GK_HOST)
+__device__ __forceinline__ uint64_t* lds_memo_entry(uint64_t h) {
+  return gk_lds_memo[threadIdx.x >> 6][(uint32_t)(h >> 40) & (GK_LDS_MEMO - 1)];
+}
+__device__ __forceinline__ void lds_memo_put(uint64_t h, uint64_t k0, uint64_t k1, uint64_t v, uint64_t c) {
+  uint64_t* le = lds_memo_entry(h);
+  le[0] = k0; le[1] = k1; le[2] = v; le[3] = c;
+}
+#endif
+
 __device__ __forceinline__ bool gm_get(uint32_t site, uint64_t k0, uint64_t k1, uint64_t& out) {
   if (!gk_args.gmemo || !gm_key(k0) || !gm_key(k1)) return false;
   uint64_t h = gm_hash(site, k0, k1);
+#if GK_LDS_MEMO && !defined(GK_HOST)
+  {
+    const uint64_t* le = lds_memo_entry(h);
+    const uint64_t a = le[0], b = le[1], v = le[2], c = le[3];
+    if (a == k0 && b == k1 && c == gm_check(h, v)) { out = v; return true; }
+  }
+#endif
   uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
 #pragma unroll
   for (uint32_t p = 0; p < 2; ++p) {
     const uint64_t* e = gk_args.gmemo + 4 * (i ^ p);
     uint64_t a = e[0], b = e[1], v = e[2], c = e[3];
-    if (a == k0 && b == k1 && c == gm_check(h, v)) { out = v; return true; }
+    if (a == k0 && b == k1 && c == gm_check(h, v)) {
+#if GK_LDS_MEMO && !defined(GK_HOST)
+      lds_memo_put(h, a, b, v, c);
+#endif
+      out = v;
+      return true;
+    }
   }
   return false;
 }
@@ -2177,7 +2219,11 @@ __device__ __forceinline__ void gm_put(const PLane& L, uint32_t site, uint64_t k
   uint32_t i = (uint32_t)h & gk_args.gmemo_mask;
   if (gk_args.gmemo[4 * i + 3] != 0) i ^= 1;
   uint64_t* e = gk_args.gmemo + 4 * i;
-  e[0] = k0; e[1] = k1; e[2] = v; e[3] = gm_check(h, v);
+  const uint64_t c = gm_check(h, v);
+  e[0] = k0; e[1] = k1; e[2] = v; e[3] = c;
+#if GK_LDS_MEMO && !defined(GK_HOST)
+  lds_memo_put(h, k0, k1, v, c);
+#endif
 }
 
 // ------------------------------------------------------------------ values copied out at emission

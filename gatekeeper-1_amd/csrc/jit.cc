@@ -865,6 +865,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       for (uint32_t q = pc + 1; q < put && ok; ++q) {
         ins_regs(bank.code[q], rd, wr);
         wrs.insert(wr.begin(), wr.end());
+        // register memo entries (GKGPU_JIT_LMEMO) are the predicate's locals
+        const Ins& qi = bank.code[q];
+        if ((qi.op == OP_MEMO_GET || qi.op == OP_MEMO_PUT) && lslots.count(qi.y)) ok = false;
       }
       for (uint32_t r : wrs)
         if (r != in.a && (is_live(x, r) || r == in.b || r == in.c)) ok = false;
@@ -1034,18 +1037,45 @@ static int max_depth(const Program& p, const CodeBank& bank) {
   return (int)std::min<uint32_t>(m + 1, kMaxLoop);
 }
 
-struct StagePlan { bool params = false, dfa = false; };
+// LDS cache of the cross-lane memo (devrt.h GK_LDS_MEMO): entries per
+// wavefront for a program with pure-function memo sites, 0 = none.
+// GKGPU_JIT_LDSMEMO=0 disables it (A/B), =N sets the entries (a power of two).
+static int lds_memo_entries(const Gen& g) {
+  const char* v = getenv("GKGPU_JIT_LDSMEMO");
+  int n = v ? atoi(v) : 32;
+  if (n <= 0) return 0;
+  if (n > 256) n = 256;
+  while (n & (n - 1)) n &= n - 1;
+  return (g.pre.find("gm_get(") != std::string::npos || g.body.find("gm_get(") != std::string::npos) ? n : 0;
+}
+
+struct StagePlan { bool params = false, dfa = false; int memo = 0; };
 static StagePlan stage_plan(const Program& p, const Gen& g, int depth) {
   StagePlan sp;
   if (!lds_stage_on()) return sp;
   const char* w = getenv("GKGPU_JIT_WPE");
   const int wpe = w ? atoi(w) : (small_program(p) ? 3 : 2);
   const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
-  // lane heap words, lane scalars and (with the scalars) the loop watermarks
+  // lane heap words, lane scalars and (with the scalars) the loop watermarks;
+  // then, as they fit: the memo cache, the DFAs, the parameters
   uint32_t used = (uint32_t)lds_heap_words(p) * 8u * 256u + (lds_scalars() ? 9u * 4u * 256u + 4u * 256u * (uint32_t)depth : 0u);
+  // (the memo cache before the parameters when the program probes the memo at
+  // more sites than it reads parameters: K8sContainerLimits' canonify calls
+  // per container against its two parameter reads per lane)
+  auto count = [&](const char* w) {
+    size_t n = 0;
+    for (const std::string* t : {&g.pre, &g.body})
+      for (size_t at = 0; (at = t->find(w, at)) != std::string::npos; ++at) ++n;
+    return n;
+  };
+  const uint32_t mbytes = 4u * 32u * (uint32_t)lds_memo_entries(g);
+  const bool memo_first = mbytes && count("gm_get(") > count("vget_p(") + count("op_iter_next_p(");
+  auto memo = [&] { if (mbytes && used + mbytes <= limit) { sp.memo = lds_memo_entries(g); used += mbytes; } };
   const uint32_t pbytes = 4u * 64u * 16u, dbytes = 4u * 1024u + 4u * 17u * 4u;  // devrt.h LDS_PCAP / LDS_DFA_*
+  if (memo_first) memo();
   if (g.param_regex && used + dbytes <= limit) { sp.dfa = true; used += dbytes; }
   if (g.param_reads && used + pbytes <= limit) { sp.params = true; used += pbytes; }
+  if (!memo_first) memo();
   return sp;
 }
 
@@ -1064,7 +1094,7 @@ static std::string inline_hot_tag(const Program& p) {
 
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
   Gen g = generate(p, bank, st);
-  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix(p) + inline_hot_tag(p)));
+  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix(p) + inline_hot_tag(p) + "lm" + std::to_string(lds_memo_entries(g))));
 }
 
 std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
@@ -1090,6 +1120,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   const StagePlan sp = stage_plan(p, g, depth);
   if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
   if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
+  if (sp.memo) o << "#define GK_LDS_MEMO " << sp.memo << "\n";
   o << "#include \"devrt.h\"\n"
     << "namespace gk {\n"
     << g.pre

@@ -53,9 +53,13 @@ def test_parameter_reads_come_from_the_wave_lds_stage():
     parameters read the wave's LDS copy of the subtree (devrt.h stage_wave,
     vget_p / op_iter_next_p) when the kernel's LDS budget has room; a
     re_match with a computed pattern also stages the compressed DFAs
-    (GK_LDS_DFA).  GKGPU_LDS_STAGE=0 turns both off."""
-    lim = _dump("K8sContainerLimits")
-    assert "#define GK_LDS_PARAMS 1" in lim
+    (GK_LDS_DFA).  GKGPU_LDS_STAGE=0 turns both off.  K8sContainerLimits
+    probes the memo at more sites than it reads parameters, so its budget goes
+    to the memo cache first (GK_LDS_MEMO, jit.cc stage_plan); without the cache
+    the parameters take the room."""
+    assert "#define GK_LDS_MEMO 32" in _dump("K8sContainerLimits")
+    lim = _dump("K8sContainerLimits", [("GKGPU_JIT_LDSMEMO", "0")])
+    assert "#define GK_LDS_PARAMS 1" in lim and "GK_LDS_MEMO" not in lim
     assert "= vget_p(L, " in lim
     assert "#define GK_LDS_DFA 1" not in lim  # no computed re_match pattern
     lab = _dump("K8sRequiredLabels")
