@@ -65,6 +65,9 @@ namespace gk {
 #ifndef GK_VGET_UNROLL
 #define GK_VGET_UNROLL 0
 #endif
+#ifndef GK_VGET_REC
+#define GK_VGET_REC 1
+#endif
 #ifndef GK_HCAP
 #define GK_HCAP 128
 #endif
@@ -344,6 +347,8 @@ __device__ __forceinline__ void lane_error(PLane& L) {
   if (!L.fail) { L.fail = RF_ERROR; L.reason = 0; }
 }
 
+// the value of node idx whose record n the caller has already loaded (an
+// object scan reads whole member records: no second round trip)
 __device__ __forceinline__ uint64_t nodeval_of(const Node& n, uint32_t idx) {
   GK_TOUCH_NODE(idx);
   switch (n.type) {
@@ -784,15 +789,23 @@ __device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
         const Node* ch = gk_args.nodes + n.first;
         uint32_t i = 0;
         for (; i + 4 <= n.n; i += 4) {
-          uint32_t k0 = ch[i].key, k1 = ch[i + 1].key, k2 = ch[i + 2].key, k3 = ch[i + 3].key;
-          if (k0 == id) return nodeval(n.first + i);
-          if (k1 == id) return nodeval(n.first + i + 1);
-          if (k2 == id) return nodeval(n.first + i + 2);
-          if (k3 == id) return nodeval(n.first + i + 3);
+          const Node m0 = ch[i], m1 = ch[i + 1], m2 = ch[i + 2], m3 = ch[i + 3];
+          if (m0.key == id) return nodeval_of(m0, n.first + i);
+          if (m1.key == id) return nodeval_of(m1, n.first + i + 1);
+          if (m2.key == id) return nodeval_of(m2, n.first + i + 2);
+          if (m3.key == id) return nodeval_of(m3, n.first + i + 3);
         }
-        for (; i < n.n; ++i)
-          if (ch[i].key == id) return nodeval(n.first + i);
-#else
+        for (; i < n.n; ++i) {
+          const Node m = ch[i];
+          if (m.key == id) return nodeval_of(m, n.first + i);
+        }
+#elif GK_VGET_REC
+        // whole member records: the match's value needs no second load
+        for (uint32_t i = 0; i < n.n; ++i) {
+          const Node m = gk_args.nodes[n.first + i];
+          if (m.key == id) return nodeval_of(m, n.first + i);
+        }
+#else  // A/B (GKGPU_JIT_PRE=GK_VGET_REC=0): member keys, then the match's record
         for (uint32_t i = 0; i < n.n; ++i)
           if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
 #endif
