@@ -448,7 +448,12 @@ def from_cache_main(args):
             nm = json.loads(ns)["metadata"]["name"]
             drv.put_data("/external/%s/cluster/v1/Namespace/%s" % (TARGET, nm), ns)
         m = ident.match(js)
-        av, kind, name, ons = m.group(1), m.group(2), m.group(3), m.group(4)
+        if m:
+            av, kind, name, ons = m.group(1), m.group(2), m.group(3), m.group(4)
+        else:  # another member order: read the identity from the parsed object
+            o = json.loads(js)
+            md = o.get("metadata") or {}
+            av, kind, name, ons = o.get("apiVersion", ""), o.get("kind", ""), md.get("name", ""), md.get("namespace")
         gv = av.replace("/", "%2F")
         path = ("/external/%s/namespace/%s/%s/%s/%s" % (TARGET, ons, gv, kind, name) if ons
                 else "/external/%s/cluster/%s/%s/%s" % (TARGET, gv, kind, name))

@@ -25,6 +25,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
         cat "$OUT/c5_phases.txt"
         timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 > "$OUT/c5_batch.json" 2> "$OUT/c5_batch.err" || { echo C5_FAIL; tail "$OUT/c5_batch.err"; exit 1; }
         python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5', d['config']['latency_ms'], round(d['value']/1e6,2), 'M/s; cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']/1e6,2))" "$OUT/c5_batch.json" ;;
+    c5f) GKGPU_FUSED=1 timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 --cpu-sample 0 > "$OUT/c5f_batch.json" 2> "$OUT/c5f_batch.err" || { echo C5F_FAIL; tail "$OUT/c5f_batch.err"; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5F', d['config']['latency_ms'], round(d['value']/1e6,2), 'M/s', d['config']['kernel_ms_last_launch'])" "$OUT/c5f_batch.json" ;;
     cache) timeout -k 10 600 python -u bench.py --from-cache --steps 3 --warmup 1 > "$OUT/cache.json" 2> "$OUT/cache.err" || { echo CACHE_FAIL; tail "$OUT/cache.err"; exit 1; }
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('CACHE', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],1), 'ms', c['results_per_audit'], c['cache_builds'], c['first_audit_s'], c['steady_timing_ms'])" "$OUT/cache.json" ;;
   esac
