@@ -20,6 +20,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <immintrin.h>
+#include <map>
 #include <functional>
 #include <memory>
 #include <thread>
@@ -80,6 +82,7 @@ struct WorkPool {
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::pair<std::shared_ptr<PoolJob>, int>> q;  // (job, index)
+  std::atomic<int> pending{0};  // q.size(), readable without the lock
   int workers = 0;
   static void finish(PoolJob& j) {
     if (j.left.fetch_sub(1) == 1) {
@@ -89,12 +92,21 @@ struct WorkPool {
   }
   void worker() {
     for (;;) {
+      // spin a little before sleeping: a micro-batch's phases (parse, intern,
+      // relocate) and the next request come back to back, and waking a
+      // sleeping thread takes longer than a 256-request part's parse
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(200);
+      for (int k = 0; pending.load(std::memory_order_relaxed) == 0; ++k) {
+        _mm_pause();
+        if ((k & 63) == 63 && std::chrono::steady_clock::now() >= until) break;
+      }
       std::pair<std::shared_ptr<PoolJob>, int> t;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return !q.empty(); });
         t = q.front();
         q.pop_front();
+        pending.fetch_sub(1, std::memory_order_relaxed);
       }
       (*t.first->f)(t.second);
       finish(*t.first);
@@ -115,6 +127,7 @@ struct WorkPool {
         ++workers;
       }
       for (int i = 1; i < n; ++i) q.push_back({job, i});
+      pending.fetch_add(n - 1, std::memory_order_relaxed);
     }
     cv.notify_all();
     f(0);
@@ -127,6 +140,7 @@ struct WorkPool {
         if (q.empty()) break;
         t = q.front();
         q.pop_front();
+        pending.fetch_sub(1, std::memory_order_relaxed);
       }
       (*t.first->f)(t.second);
       finish(*t.first);
@@ -457,6 +471,65 @@ struct Part {
   uint64_t node_off = 0;             // global index of this part's node kFixedNodes
   std::vector<uint32_t> rbeg;        // per review: its first local node (device layout)
 };
+
+// Flattener parts are pooled: a new Part allocates its store's tables and
+// arenas, and for a webhook micro-batch (256 AdmissionReviews on 16 parts) the
+// page faults and mmap calls of those allocations serialized the parts on the
+// process's memory map (0.8 ms of setup, parsing that did not scale with
+// threads).  Parts come back reset, allocations kept; a batch's parts return
+// to the pool only if small (a 1M-Pod page's parts hold ~1 GB).
+void reset_part(Part& p) {
+  p.st.reset();
+  p.lo = p.hi = 0;
+  p.cols.clear();
+  p.nsglob.clear();
+  p.weight.clear();
+  p.res.clear();
+  p.ns_roots.clear();
+  p.count_paths = false;
+  p.paths = PathTab();
+  p.pcount.clear();
+  p.excluded = 0;
+  p.err.clear();
+  p.smap.clear();
+  p.nmap.clear();
+  p.node_off = 0;
+  p.rbeg.clear();
+}
+size_t part_bytes(const Part& p) {
+  return p.st.bytes() + p.smap.capacity() * 4 + p.nmap.capacity() * 4 + p.cols.capacity() * sizeof(ReviewCol);
+}
+struct PartPool {
+  std::mutex mu;
+  std::map<int, std::vector<std::vector<Part>>> free;
+};
+PartPool& part_pool() {
+  static PartPool* p = new PartPool();
+  return *p;
+}
+std::vector<Part> take_parts(int T) {
+  {
+    PartPool& pp = part_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    auto it = pp.free.find(T);
+    if (it != pp.free.end() && !it->second.empty()) {
+      std::vector<Part> v = std::move(it->second.back());
+      it->second.pop_back();
+      return v;
+    }
+  }
+  return std::vector<Part>(T);
+}
+void give_parts(std::vector<Part>& v) {
+  size_t bytes = 0;
+  for (auto& p : v) bytes += part_bytes(p);
+  if (v.empty() || bytes > (64u << 20)) return;
+  for (auto& p : v) reset_part(p);
+  PartPool& pp = part_pool();
+  std::lock_guard<std::mutex> g(pp.mu);
+  auto& l = pp.free[(int)v.size()];
+  if (l.size() < 8) l.push_back(std::move(v));
+}
 
 void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set<std::string>* ex, const Page& pg) {
   Store& st = p.st;
@@ -953,7 +1026,8 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
     std::vector<const Store*> src;
     for (auto& p : parts) src.push_back(&p.st);
     std::vector<std::vector<uint32_t>> maps;
-    gst.intern_parts(src, nwell, maps, T);
+    // (a micro-batch's few thousand strings: one thread, no pool round trips)
+    gst.intern_parts(src, nwell, maps, extra < 16384 ? 1 : T);
     for (size_t k = 0; k < parts.size(); ++k) parts[k].smap.swap(maps[k]);
     for (auto& p : parts) {
       const Store& ls = p.st;
@@ -1041,7 +1115,8 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
   int T = std::max(1, threads);
   // at least ~2k objects per thread: below that the merge costs more than it saves
   T = (int)std::min<size_t>((size_t)T, std::max<size_t>(1, n / 2048));
-  std::vector<Part> parts(T);
+  std::vector<Part> parts = take_parts(T);
+  struct Give { std::vector<Part>& v; ~Give() { give_parts(v); } } give{parts};
   for (int t = 0; t < T; ++t) {
     parts[t].lo = n * t / T;
     parts[t].hi = n * (t + 1) / T;
@@ -1065,20 +1140,31 @@ bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,
   // AdmissionReviews: 16 parts); the first input that is not JSON fails the call
   const size_t n = inputs.size();
   const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 16));
-  std::vector<Part> parts(T);
+  using Clock = std::chrono::steady_clock;
+  const auto t0 = Clock::now();
+  std::vector<Part> parts = take_parts(T);
+  struct Give { std::vector<Part>& v; ~Give() { give_parts(v); } } give{parts};
+  const auto t1 = Clock::now();
   for (int t = 0; t < T; ++t) {
     parts[t].lo = n * t / T;
     parts[t].hi = n * (t + 1) / T;
   }
+  std::vector<double> pt0(T), pt1(T);
   parallel_run(T, [&](int t) {
     Part& p = parts[t];
-    JDoc d;
+    pt0[t] = std::chrono::duration<double, std::milli>(Clock::now() - t1).count();
+    struct Stamp { double& x; Clock::time_point b; ~Stamp() { x = std::chrono::duration<double, std::milli>(Clock::now() - b).count(); } } stamp{pt1[t], t1};
+    std::string perr;
     for (size_t i = p.lo; i < p.hi; ++i) {
-      JsonReader rd(inputs[i].first, inputs[i].second, &d);
-      int root = rd.parse();
-      if (root < 0) { p.err = "invalid input JSON: " + d.err; return; }
-      int rv = d.nodes[root].type == NT_OBJ ? d.get(root, "review") : -1;
-      uint32_t rn = rv >= 0 ? p.st.add_doc(d, rv) : NO_ID;
+      // the input document straight into the part's arena; input.review is
+      // its "review" member (encoding/json: the last of duplicate keys)
+      Node top;
+      if (!p.st.parse_doc(inputs[i].first, inputs[i].second, &top, &perr)) {
+        p.err = "invalid input JSON: " + perr;
+        return;
+      }
+      const Node* rvn = member(p.st, top, p.st.s_review);
+      const uint32_t rn = rvn ? (uint32_t)(rvn - p.st.nodes().data()) : NO_ID;
       bool glob = false;
       p.cols.push_back(review_columns(p.st, gst, ns_cache, rn, &glob));
       p.nsglob.push_back(glob);
@@ -1088,9 +1174,16 @@ bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,
   });
   for (auto& p : parts)
     if (!p.err.empty()) { err = p.err; return false; }
+  const auto t2 = Clock::now();
   FlatResult out;
   if (!merge_parts(gst, smu, parts, base, dst, out, n, err)) return false;
   cols.swap(out.cols);
+  if (getenv("GKGPU_FLATTEN_TRACE") && atoi(getenv("GKGPU_FLATTEN_TRACE")) > 1)
+    for (int t = 0; t < T; ++t) fprintf(stderr, "  part %d: %.3f .. %.3f ms\n", t, pt0[t], pt1[t]);
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "flatten_reviews: %d parts: setup %.3f ms, parse %.3f ms, merge %.3f ms\n", T,
+            std::chrono::duration<double, std::milli>(t1 - t0).count(), std::chrono::duration<double, std::milli>(t2 - t1).count(),
+            std::chrono::duration<double, std::milli>(Clock::now() - t2).count());
   return true;
 }
 

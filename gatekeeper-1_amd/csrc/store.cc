@@ -246,6 +246,24 @@ std::string go_number_print(const char* s, size_t n) {
 Store::Store() {
   table_.assign(1 << 12, 0);
   num_table_.assign(1 << 10, 0);
+  init();
+}
+
+void Store::reset() {
+  pool_.clear();
+  strs_.clear();
+  sflags_.clear();
+  if (table_.size() > (1u << 16)) table_.assign(1 << 12, 0);
+  else std::fill(table_.begin(), table_.end(), 0);
+  nums_.clear();
+  if (num_table_.size() > (1u << 14)) num_table_.assign(1 << 10, 0);
+  else std::fill(num_table_.begin(), num_table_.end(), 0);
+  nodes_.resize(0);
+  if (!short_.empty()) std::fill(short_.begin(), short_.end(), ShortEnt{{0, 0, 0, 0}, ~0u, 0});
+  init();
+}
+
+void Store::init() {
   s_empty = intern("", 0);
   s_review = intern("review"); s_parameters = intern("parameters"); s_kind = intern("kind");
   s_group = intern("group"); s_version = intern("version"); s_name = intern("name");
@@ -325,7 +343,7 @@ static uint8_t str_flags_of(const char* p, size_t n) {
 }
 
 uint32_t Store::intern(const char* p, size_t n) {
-  if (n <= 32) {
+  if (n <= 32 && !short_.empty()) {  // (the cache is set up by parse_doc)
     // the string as four words (overlapping loads; with n they determine it)
     uint64_t w[4] = {0, 0, 0, 0};
     if (n > 16) { memcpy(&w[0], p, 8); memcpy(&w[1], p + 8, 8); memcpy(&w[2], p + n - 16, 8); memcpy(&w[3], p + n - 8, 8); }
@@ -340,7 +358,6 @@ uint32_t Store::intern(const char* p, size_t n) {
     }
     const uint64_t k = (w[0] * 0x9e3779b97f4a7c15ull) ^ (w[1] * 0xc2b2ae3d27d4eb4full) ^
                        ((w[2] ^ (w[3] << 1)) * 0x94d049bb133111ebull) ^ (n * 0x165667b19e3779f9ull);
-    if (short_.empty()) short_.assign(kShortCache, ShortEnt{{0, 0, 0, 0}, ~0u, 0});
     ShortEnt& e = short_[(k >> 40) & (kShortCache - 1)];
     if (e.len == n && e.w[0] == w[0] && e.w[1] == w[1] && e.w[2] == w[2] && e.w[3] == w[3]) return e.id;
     const uint32_t id = intern_slow(p, n, str_hash(p, n));
@@ -696,6 +713,7 @@ class DocParser {
 };
 
 bool Store::parse_doc(const char* p, size_t n, Node* root, std::string* err) {
+  if (short_.empty()) short_.assign(kShortCache, ShortEnt{{0, 0, 0, 0}, ~0u, 0});
   DocParser d(*this, p, n, err);
   return d.run(root);
 }

@@ -82,6 +82,9 @@ std::string go_number_print(const char* s, size_t n);
 class Store {
  public:
   Store();
+  // back to the state of a new Store (the well-known strings, the four fixed
+  // nodes), keeping the allocations: pooled flattener parts reuse their stores
+  void reset();
 
   // -- strings
   uint32_t intern(const char* p, size_t n);
@@ -150,6 +153,7 @@ class Store {
   std::vector<ShortEnt> short_;
   uint32_t intern_slow(const char* p, size_t n, uint64_t hv);
   friend class DocParser;
+  void init();
   void grow();
   void rehash(size_t sz);
   void grow_num();
