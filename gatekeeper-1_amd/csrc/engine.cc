@@ -31,6 +31,8 @@
 namespace gk {
 }
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
+extern "C" int gk_launch_compact(const gk::DevArgs* a, const gk::Viol* raw, const uint64_t* rfrec, uint32_t* tcnt,
+                                 unsigned long long* toff, hipStream_t stream);
 extern "C" int gk_launch_keys(const gk::DevArgs* args, hipStream_t stream);
 extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev);
 extern "C" size_t gk_devargs_size();
@@ -221,6 +223,9 @@ struct EvalCtx {
   DBuf d_mstr, d_mtop;  // memo-string arena + its cursor (V_GSTR)
   DBuf d_nodes, d_revs, d_out, d_bytes, d_counters, d_rflags, d_totals, d_rreason, d_prof, d_pchist, d_clist, d_gmemo,
       d_frec, d_hist, d_cut, d_ftot, d_cand, d_ncand, d_cerr, d_ebytes, d_lens, d_part;
+  // the predicate kernels' chunked tuples and argument words before
+  // compaction (devrt.h slot_reserve, kernels.hip gk_compact_*), tile counts
+  DBuf d_out_raw, d_frec_raw, d_ctcnt, d_ctoff;
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20, ebytes_cap = 16u << 20, cand_cap = 1 << 14;
   uint64_t eval_epoch = 0;   // bumps on every evaluation (output buffers reused)
   uint64_t perm_gen = 0;     // engine generation whose permanent nodes d_nodes holds below perm_nodes
@@ -247,7 +252,7 @@ struct EvalCtx {
     h_pin_cap = 0;
     for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
                     &d_clist, &d_gmemo, &d_mstr, &d_mtop, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
-                    &d_part})
+                    &d_part, &d_out_raw, &d_frec_raw, &d_ctcnt, &d_ctoff})
       b->free_();
     for (hipEvent_t x : events) hipEventDestroy(x);
     events.clear();
@@ -1555,6 +1560,8 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
   // sums of the size pass, final message bytes (+16: dword reads past the end)
   auto reserve_out = [&]() {
     return x->d_out.reserve(x->out_cap * sizeof(Viol)) && x->d_frec.reserve(x->out_cap * FMT_MAXARGS * 8) &&
+           x->d_out_raw.reserve(x->out_cap * sizeof(Viol)) && x->d_frec_raw.reserve(x->out_cap * FMT_MAXARGS * 8) &&
+           x->d_ctcnt.reserve((x->out_cap / 256 + 2) * 4) && x->d_ctoff.reserve((x->out_cap / 256 + 2) * 8) &&
            x->d_lens.reserve(x->out_cap * 4) && x->d_part.reserve((x->out_cap / FTILE + 2) * 8) &&
            x->d_ebytes.reserve(x->ebytes_cap + 16) && x->d_bytes.reserve(x->bytes_cap + 16);
   };
@@ -1651,7 +1658,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.lens = (uint32_t*)x->d_lens.p;
     a.part = (unsigned long long*)x->d_part.p;
     set_join_args(e, a);
-    while (x->events.size() < plan.size() + 4) {
+    while (x->events.size() < plan.size() + 5) {
       hipEvent_t ev1;
       if (hipEventCreate(&ev1) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
       x->events.push_back(ev1);
@@ -1662,6 +1669,9 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     for (size_t i = 0; i < plan.size(); ++i) {
       argv[i].clist = (const uint32_t*)x->d_clist.p + plan[i].off;
       argv[i].nclist = plan[i].n;
+      // chunked tuple slots go to the raw arrays; gk_compact packs them below
+      argv[i].out = (Viol*)x->d_out_raw.p;
+      argv[i].frec = (uint64_t*)x->d_frec_raw.p;
       const DevArgs& a = argv[i];
       int lr;
       if (plan[i].fn) {
@@ -1682,13 +1692,19 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       }
       hipEventRecord(ev[i + 1], x->stream);
       // cumulative (tuples, bytes) after this launch -> per-launch output counts
-      hipMemcpyAsync((char*)x->d_counters.p + 64 + 16 * i, x->d_counters.p, 16, hipMemcpyDeviceToDevice, x->stream);
+      // (tuples: counters[6], the waves' used slots; counters[0] counts holes too)
+      hipMemcpyAsync((char*)x->d_counters.p + 64 + 16 * i, (char*)x->d_counters.p + 48, 8, hipMemcpyDeviceToDevice, x->stream);
+      hipMemcpyAsync((char*)x->d_counters.p + 72 + 16 * i, (char*)x->d_counters.p + 8, 8, hipMemcpyDeviceToDevice, x->stream);
       if (lr != 0) {
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
     }
-    // size, spine and format passes over the tuples of every launch above
-    int flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 1]);
+    // the tuples of every launch above packed, then the size, spine and format passes
+    int flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
+                                (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream);
+    if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (compact): ") + hipGetErrorString((hipError_t)flr));
+    hipEventRecord(ev[plan.size() + 1], x->stream);
+    flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2]);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)flr));
     // one wait for the kernels and the small readbacks: counters, per-launch
     // counter snapshots, totals, and the per-review flags and reasons, queued
@@ -1725,7 +1741,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       if (!reserve_out()) return fail(e, GK_EDEVICE, "device allocation failed");
       a.bytes = (char*)x->d_bytes.p;
       a.bytes_cap = x->bytes_cap;
-      flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 1]);
+      flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2]);
       if (flr != 0 || hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "format pass failed");
       d2h(x, counters, x->d_counters.p, 32);
     }
@@ -1740,11 +1756,13 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
     }
     {
-      float k_size = 0, k_spine = 0, k_fmt = 0;
-      hipEventElapsedTime(&k_size, ev[plan.size()], ev[plan.size() + 1]);
-      hipEventElapsedTime(&k_spine, ev[plan.size() + 1], ev[plan.size() + 2]);
-      hipEventElapsedTime(&k_fmt, ev[plan.size() + 2], ev[plan.size() + 3]);
-      res->ms[2] += k_size + k_spine + k_fmt;
+      float k_cmp = 0, k_size = 0, k_spine = 0, k_fmt = 0;
+      hipEventElapsedTime(&k_cmp, ev[plan.size()], ev[plan.size() + 1]);
+      hipEventElapsedTime(&k_size, ev[plan.size() + 1], ev[plan.size() + 2]);
+      hipEventElapsedTime(&k_spine, ev[plan.size() + 2], ev[plan.size() + 3]);
+      hipEventElapsedTime(&k_fmt, ev[plan.size() + 3], ev[plan.size() + 4]);
+      res->ms[2] += k_cmp + k_size + k_spine + k_fmt;
+      res->launches.push_back({"gk_compact", (double)k_cmp, 0, counters[0], 0});
       res->launches.push_back({"gk_size_kernel", (double)k_size, 0, 0, 0});
       res->launches.push_back({"gk_scan_spine", (double)k_spine, 0, 0, 0});
       res->launches.push_back({"gk_format_kernel", (double)k_fmt, 0, 0, counters[3]});

@@ -287,6 +287,101 @@ __global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
   if (threadIdx.x == 0) gk_args.counters[3] = carry;
 }
 
+// ------------------------------------------------------------------ compaction
+// The predicate kernels write tuples into per-wave chunks of slots (devrt.h
+// slot_reserve); unused slots are holes (review = VIOL_HOLE).  These three
+// kernels pack the tuples of all launches, and their deferred-argument words,
+// into the dense arrays the size / format passes and the readback use:
+//   count   -- per tile of 256 raw slots, its tuples;
+//   scan    -- one block: exclusive prefix over the tiles; the dense count
+//              becomes counters[0] (counters[5] keeps the raw slot count);
+//   scatter -- each tuple to its dense slot, in raw order (a wave's tuples stay
+//              together, as they did on one counter).
+// Kernel arguments: DevArgs last (devrt.h gk_args finds it right before the
+// hidden arguments).  An overflowed evaluation (raw slots or staged bytes past capacity) is
+// re-run by the host with larger buffers: nothing is packed, counters[0]
+// keeps the raw count the host checks.
+constexpr uint32_t CTILE = 256;
+__device__ __forceinline__ bool compact_overflow(uint64_t raw) {
+  return raw > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap;
+}
+__device__ __forceinline__ uint32_t frec_words(const Viol& v) {
+  const uint32_t na = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
+  return na + ((v.pad & VF_DET_VAL) ? 1u : 0u);
+}
+
+__global__ void __launch_bounds__(256) gk_compact_count(const Viol* raw, uint32_t* tcnt, DevArgs) {
+  const uint64_t n = gk_args.counters[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) gk_args.counters[5] = n;
+  if (compact_overflow(n)) return;
+  const uint64_t ntile = (n + CTILE - 1) / CTILE;
+  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const uint64_t i = t * CTILE + threadIdx.x;
+    const bool real = i < n && raw[i].review != VIOL_HOLE;
+    const int c = __syncthreads_count(real);
+    if (threadIdx.x == 0) tcnt[t] = (uint32_t)c;
+  }
+}
+
+__global__ void __launch_bounds__(1024) gk_compact_scan(const uint32_t* tcnt, unsigned long long* toff, DevArgs) {
+  __shared__ unsigned long long wtot[16];
+  __syncthreads();  // (counters[5] is written by the previous kernel)
+  const uint64_t n = gk_args.counters[5];
+  if (compact_overflow(n)) return;
+  const uint64_t ntile = (n + CTILE - 1) / CTILE;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long carry = 0;
+  for (uint64_t b = 0; b < ntile; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const unsigned long long x = i < ntile ? tcnt[i] : 0ull;
+    unsigned long long incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    unsigned long long before = 0, all = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < w) before += wtot[k];
+      all += wtot[k];
+    }
+    if (i < ntile) toff[i] = carry + before + incl - x;
+    carry += all;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gk_args.counters[0] = carry;
+}
+
+__global__ void __launch_bounds__(256) gk_compact_scatter(const Viol* raw, const uint64_t* rfrec,
+                                                          const unsigned long long* toff, DevArgs) {
+  __shared__ uint32_t wc[4];
+  const uint64_t n = gk_args.counters[5];
+  if (compact_overflow(n)) return;
+  const uint64_t ntile = (n + CTILE - 1) / CTILE;
+  const uint64_t cap = gk_args.out_cap;
+  const uint32_t w = threadIdx.x >> 6;
+  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const uint64_t i = t * CTILE + threadIdx.x;
+    Viol v{};
+    bool real = false;
+    if (i < n) { v = raw[i]; real = v.review != VIOL_HOLE; }
+    const uint64_t m = __ballot(real);
+    if ((threadIdx.x & 63) == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint64_t before = toff[t];
+    for (uint32_t k = 0; k < w; ++k) before += wc[k];
+    if (real) {
+      const uint64_t d = before + gk_lanes_below(m);
+      gk_args.out[d] = v;
+      const uint32_t nw = frec_words(v);
+      for (uint32_t j = 0; j < nw && j < FMT_MAXARGS; ++j) gk_args.frec[(uint64_t)j * cap + d] = rfrec[(uint64_t)j * cap + i];
+    }
+    __syncthreads();
+  }
+}
+
 constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(DevArgs) {
@@ -397,6 +492,19 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   if (ev) hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[2], stream);
+  return (int)hipGetLastError();
+}
+
+// packs the predicate kernels' chunked tuples (raw, rfrec) into a->out /
+// a->frec; tcnt: one u32 per CTILE raw slots of capacity, toff: one u64 each
+extern "C" int gk_launch_compact(const gk::DevArgs* a, const gk::Viol* raw, const uint64_t* rfrec, uint32_t* tcnt,
+                                 unsigned long long* toff, hipStream_t stream) {
+  const uint64_t tiles = (a->out_cap + gk::CTILE - 1) / gk::CTILE;
+  const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
+  hipLaunchKernelGGL(gk::gk_compact_count, dim3(blocks), dim3(256), 0, stream, raw, tcnt, *a);
+  hipLaunchKernelGGL(gk::gk_compact_scan, dim3(1), dim3(1024), 0, stream, (const uint32_t*)tcnt, toff, *a);
+  hipLaunchKernelGGL(gk::gk_compact_scatter, dim3(blocks), dim3(256), 0, stream, raw, rfrec,
+                     (const unsigned long long*)toff, *a);
   return (int)hipGetLastError();
 }
 

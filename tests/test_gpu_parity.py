@@ -78,8 +78,10 @@ def test_config2_agilebank_pods():
     _assert_backend(drv, [t["spec"]["crd"]["spec"]["names"]["kind"] for t in ts])
     kernels = {k for k, _, _ in res.launches}
     # deferred messages sized and formatted by the size / format passes (kernels.hip)
-    assert {"gk_size_kernel", "gk_scan_spine", "gk_format_kernel"} <= kernels, res.launches
-    kernels -= {"gk_size_kernel", "gk_scan_spine", "gk_format_kernel"}
+    # (tuples from per-wave slot chunks packed first: gk_compact)
+    passes = {"gk_compact", "gk_size_kernel", "gk_scan_spine", "gk_format_kernel"}
+    assert passes <= kernels, res.launches
+    kernels -= passes
     if _BACKEND["jit"]:
         assert kernels and all(k.startswith("gk_t_") for k in kernels), res.launches
     else:
