@@ -20,6 +20,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C2T', round(d['value']/1e6,1), 'M/s stage_s', c['stage_s'], c['stage_ms'], 'prepare_s', c.get('prepare_s'), 'e2e', round(c['end_to_end_evals_per_s']/1e6,2))" "$OUT/c2t.json" ;;
     p4) ( bash profiles/run_profile.sh "${TAG}_c4" --config 4 ) > "$OUT/p4.log" 2>&1 || { echo P4_FAIL; tail "$OUT/p4.log"; exit 1; }
         tail -5 "$OUT/p4.log" ;;
+    p2) ( bash profiles/run_profile.sh "${TAG}" ) > "$OUT/p2.log" 2>&1 || { echo P2_FAIL; tail "$OUT/p2.log"; exit 1; }
+        tail -3 "$OUT/p2.log" ;;
     c4) bash tools/gpu_bench_ab.sh "$TAG/c4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
     c5) timeout -k 10 300 python -u tools/probe_c5_time.py 256 > "$OUT/c5_phases.txt" 2>&1 || { echo C5P_FAIL; tail "$OUT/c5_phases.txt"; exit 1; }
         cat "$OUT/c5_phases.txt"
