@@ -226,6 +226,12 @@ struct EvalCtx {
   // the predicate kernels' chunked tuples and argument words before
   // compaction (devrt.h slot_reserve, kernels.hip gk_compact_*), tile counts
   DBuf d_out_raw, d_frec_raw, d_ctcnt, d_ctoff;
+  // side streams for concurrent template launches (GKGPU_CONCURRENT), each
+  // with its own cross-lane memo table (memo sites are per program)
+  static constexpr int kSide = 3;
+  hipStream_t side[kSide] = {nullptr, nullptr, nullptr};
+  DBuf d_gmemo_side[kSide];
+  std::vector<hipEvent_t> lev;  // per launch: start, end (timing) + the join event
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20, ebytes_cap = 16u << 20, cand_cap = 1 << 14;
   uint64_t eval_epoch = 0;   // bumps on every evaluation (output buffers reused)
   uint64_t perm_gen = 0;     // engine generation whose permanent nodes d_nodes holds below perm_nodes
@@ -256,6 +262,13 @@ struct EvalCtx {
       b->free_();
     for (hipEvent_t x : events) hipEventDestroy(x);
     events.clear();
+    for (hipEvent_t x : lev) hipEventDestroy(x);
+    lev.clear();
+    for (int k = 0; k < kSide; ++k) {
+      d_gmemo_side[k].free_();
+      if (side[k]) hipStreamDestroy(side[k]);
+      side[k] = nullptr;
+    }
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -1573,6 +1586,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
   ensure_jit(e, true);
   struct Step { hipFunction_t fn; std::string name; uint32_t off, n; };
   std::vector<Step> plan;
+  std::vector<uint32_t> clist_host;  // constraint indices in launch order
   {
     std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
     const bool fused = e->fused.fn != nullptr;
@@ -1583,7 +1597,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       if (jit && fused) { fused_cons.push_back(c); continue; }
       groups[jit ? p : e->progs.size()].push_back(c);
     }
-    std::vector<uint32_t> clist;
+    std::vector<uint32_t>& clist = clist_host;
     if (!fused_cons.empty()) {
       plan.push_back({e->fused.fn, e->fused.name, 0, (uint32_t)fused_cons.size()});
       clist = fused_cons;
@@ -1665,8 +1679,32 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     const std::vector<hipEvent_t>& ev = x->events;
     hipEventRecord(ev[0], x->stream);
+    // GKGPU_CONCURRENT (A/B switch, default on): the template launches go
+    // round-robin to the context's stream and up to three side streams, each
+    // with its own memo table, and run side by side (a micro-batch's launches
+    // are latency-bound; a sweep's fill each other's tails); the compaction
+    // waits for all of them.  Per-launch timing then uses per-launch events.
+    int nstream = 1;
+    if (plan.size() > 1 && env_mode("GKGPU_CONCURRENT", 1, 1) != 0) {
+      nstream = (int)std::min<size_t>(plan.size(), 1 + EvalCtx::kSide);
+      for (int k = 0; k + 1 < nstream; ++k)
+        if (!x->side[k] && hipStreamCreateWithFlags(&x->side[k], hipStreamNonBlocking) != hipSuccess) { nstream = k + 1; break; }
+    }
+    while (x->lev.size() < 2 * plan.size() + 1) {
+      hipEvent_t ev1;
+      if (hipEventCreate(&ev1) != hipSuccess) return fail(e, GK_EDEVICE, "event creation failed");
+      x->lev.push_back(ev1);
+    }
+    const hipEvent_t ev_go = x->lev[2 * plan.size()];
+    if (nstream > 1) {
+      hipEventRecord(ev_go, x->stream);
+      for (int k = 0; k + 1 < nstream; ++k) hipStreamWaitEvent(x->side[k], ev_go, 0);
+    }
     std::vector<DevArgs> argv(plan.size(), a);  // live until the stream sync below
     for (size_t i = 0; i < plan.size(); ++i) {
+      const int si = nstream > 1 ? (int)(i % (size_t)nstream) : 0;
+      hipStream_t st = si == 0 ? x->stream : x->side[si - 1];
+      DBuf& gmemo = si == 0 ? x->d_gmemo : x->d_gmemo_side[si - 1];
       argv[i].clist = (const uint32_t*)x->d_clist.p + plan[i].off;
       argv[i].nclist = plan[i].n;
       // chunked tuple slots go to the raw arrays; gk_compact packs them below
@@ -1674,31 +1712,40 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       argv[i].frec = (uint64_t*)x->d_frec_raw.p;
       const DevArgs& a = argv[i];
       int lr;
+      hipEventRecord(x->lev[2 * i], st);
       if (plan[i].fn) {
         // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
         const bool gm_on = env_mode("GKGPU_GMEMO", 1, 1) != 0;  // A/B switch
-        if (gm_on && x->d_gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
-          argv[i].gmemo = (uint64_t*)x->d_gmemo.p;
+        if (gm_on && gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
+          argv[i].gmemo = (uint64_t*)gmemo.p;
           argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
-          hipMemsetAsync(x->d_gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, x->stream);
+          hipMemsetAsync(gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, st);
         }
         uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
         uint32_t blocks = (uint32_t)((threads + 255) / 256);
         // the arguments travel in the dispatch's kernarg segment (devrt.h gk_args)
         void* params[] = {(void*)&argv[i]};
-        lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, x->stream, params, nullptr);
+        lr = (int)hipModuleLaunchKernel(plan[i].fn, blocks, 1, 1, 256, 1, 1, 0, st, params, nullptr);
       } else {
-        lr = gk_launch_audit(&a, x->stream);
+        lr = gk_launch_audit(&a, st);
       }
-      hipEventRecord(ev[i + 1], x->stream);
+      hipEventRecord(x->lev[2 * i + 1], st);
       // cumulative (tuples, bytes) after this launch -> per-launch output counts
-      // (tuples: counters[6], the waves' used slots; counters[0] counts holes too)
-      hipMemcpyAsync((char*)x->d_counters.p + 64 + 16 * i, (char*)x->d_counters.p + 48, 8, hipMemcpyDeviceToDevice, x->stream);
-      hipMemcpyAsync((char*)x->d_counters.p + 72 + 16 * i, (char*)x->d_counters.p + 8, 8, hipMemcpyDeviceToDevice, x->stream);
+      // (tuples: counters[6], the waves' used slots; counters[0] counts holes
+      // too); concurrent launches: from the constraint totals instead (below)
+      if (nstream == 1) {
+        hipMemcpyAsync((char*)x->d_counters.p + 64 + 16 * i, (char*)x->d_counters.p + 48, 8, hipMemcpyDeviceToDevice, st);
+        hipMemcpyAsync((char*)x->d_counters.p + 72 + 16 * i, (char*)x->d_counters.p + 8, 8, hipMemcpyDeviceToDevice, st);
+      }
       if (lr != 0) {
         return fail(e, GK_EDEVICE, "kernel launch failed (" + plan[i].name + "): " + hipGetErrorString((hipError_t)lr));
       }
     }
+    for (int k = 0; k + 1 < nstream; ++k) {  // join the side streams
+      hipEventRecord(x->lev[2 * plan.size()], x->side[k]);
+      hipStreamWaitEvent(x->stream, x->lev[2 * plan.size()], 0);
+    }
+    hipEventRecord(ev[plan.size()], x->stream);
     // the tuples of every launch above packed, then the size, spine and format passes
     int flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
                                 (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream);
@@ -1748,12 +1795,25 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     res->launches.clear();
     std::vector<uint64_t> snap(2 * plan.size());
     memcpy(snap.data(), hp + o_snap, 16 * plan.size());
+    std::vector<uint64_t> ctot(ncons);
+    memcpy(ctot.data(), hp + o_tot, ncons * 8);
+    {
+      float all = 0;
+      hipEventElapsedTime(&all, ev[0], ev[plan.size()]);
+      res->ms[2] += all;  // predicate launches: wall time (they may overlap)
+    }
     for (size_t i = 0; i < plan.size(); ++i) {
       float kms = 0;
-      hipEventElapsedTime(&kms, ev[i], ev[i + 1]);
-      res->ms[2] += kms;
-      uint64_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
-      res->launches.push_back({plan[i].name, (double)kms, plan[i].n, snap[2 * i] - t0, snap[2 * i + 1] - b0});
+      hipEventElapsedTime(&kms, x->lev[2 * i], x->lev[2 * i + 1]);
+      uint64_t tup = 0, byt = 0;
+      if (nstream == 1) {
+        const uint64_t t0 = i ? snap[2 * i - 2] : 0, b0 = i ? snap[2 * i - 1] : 0;
+        tup = snap[2 * i] - t0;
+        byt = snap[2 * i + 1] - b0;
+      } else {  // the launch's constraints' clean emissions (bytes: not split per launch)
+        for (uint32_t k = 0; k < plan[i].n; ++k) tup += ctot[clist_host[plan[i].off + k]];
+      }
+      res->launches.push_back({plan[i].name, (double)kms, plan[i].n, tup, byt});
     }
     {
       float k_cmp = 0, k_size = 0, k_spine = 0, k_fmt = 0;
