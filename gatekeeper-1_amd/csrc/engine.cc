@@ -204,9 +204,12 @@ struct ConstraintEnt {
   bool kind_ok = true;
 };
 
+// a decoded row: message and details JSON are views into the evaluation's
+// downloaded output bytes (gk_results::rbytes, shared with the per-caller
+// results a coalesced launch is split into)
 struct ResultRow {
   uint32_t review, constraint, seq, rule;
-  std::string msg, details;
+  std::string_view msg, details;
 };
 
 // One evaluation's device state: its stream, its launch events and every
@@ -278,6 +281,7 @@ struct EvalCtx {
 
 struct gk_results {
   std::vector<gk::ResultRow> rows;
+  std::shared_ptr<const std::string> rbytes;  // the bytes rows view
   std::vector<uint32_t> status, reason;  // empty when no review was flagged (all zero)
   uint32_t nrev = 0;
   std::vector<uint64_t> totals;
@@ -1922,6 +1926,9 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       if (x.constraint != y.constraint) return x.constraint < y.constraint;
       return x.seq < y.seq;
     });
+    auto rb = std::make_shared<std::string>(std::move(bytes));
+    res->rbytes = rb;
+    const char* bp = rb->data();
     res->rows.reserve(vs.size());
     for (auto& v : vs) {
       if (res->status[v.review] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK)) continue;
@@ -1930,9 +1937,9 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       row.constraint = v.constraint;
       row.seq = v.seq;
       row.rule = v.rule;
-      row.msg.assign(bytes.data() + v.msg_off, v.msg_len);
-      row.details.assign(bytes.data() + v.msg_off + v.msg_len, v.det_len);
-      res->rows.push_back(std::move(row));
+      row.msg = std::string_view(bp + v.msg_off, v.msg_len);
+      row.details = std::string_view(bp + v.msg_off + v.msg_len, v.det_len);
+      res->rows.push_back(row);
     }
     for (auto& s : res->status) s &= (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK);
     mark_excluded();
@@ -2187,13 +2194,16 @@ static int eval_inputs(gk_engine* e, const std::vector<std::pair<const char*, si
 static gk_results* split_results(const gk_results& all, uint32_t k) {
   auto* r = new gk_results();
   r->nrev = 1;
+  r->rbytes = all.rbytes;
   r->totals.assign(all.totals.size(), 0);
-  for (const auto& row : all.rows)
-    if (row.review == k) {
-      r->rows.push_back(row);
-      r->rows.back().review = 0;
-      if (row.constraint < r->totals.size()) ++r->totals[row.constraint];
-    }
+  // rows are sorted by review (launch_and_collect): this caller's run
+  auto lo = std::lower_bound(all.rows.begin(), all.rows.end(), k,
+                             [](const ResultRow& row, uint32_t kk) { return row.review < kk; });
+  for (auto it = lo; it != all.rows.end() && it->review == k; ++it) {
+    r->rows.push_back(*it);
+    r->rows.back().review = 0;
+    if (it->constraint < r->totals.size()) ++r->totals[it->constraint];
+  }
   if (!all.status.empty()) {
     r->status.push_back(all.status[k]);
     r->reason.push_back(all.reason.empty() ? 0 : all.reason[k]);
