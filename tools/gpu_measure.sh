@@ -12,9 +12,8 @@ cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
 export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
 for what in "${@:-c2 c4 c5 cache}"; do
   case $what in
-    c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_JIT_LDSMEMO=0" \
-          "GKGPU_JIT_WPE=3 GKGPU_LDS_HEAP=16" "GKGPU_JIT_WPE=4 GKGPU_LDS_HEAP=8" "GKGPU_JIT_WPE=3 GKGPU_LDS_HEAP=8" \
-          "GKGPU_JIT_PRE=GK_VGET_REC=0" "GKGPU_JIT_PRE=GK_VGET_UNROLL=1" || exit 1 ;;
+    c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_CONCURRENT=0" \
+          "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16 GKGPU_CONCURRENT=0" || exit 1 ;;
     c2t) GKGPU_FLATTEN_TRACE=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/c2t.json" 2> "$OUT/c2t.err" || { echo C2T_FAIL; tail "$OUT/c2t.err"; exit 1; }
         grep -E "flatten|stage upload|intern" "$OUT/c2t.err" | tail -12
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C2T', round(d['value']/1e6,1), 'M/s stage_s', c['stage_s'], c['stage_ms'], 'prepare_s', c.get('prepare_s'), 'e2e', round(c['end_to_end_evals_per_s']/1e6,2))" "$OUT/c2t.json" ;;
@@ -22,7 +21,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
         tail -5 "$OUT/p4.log" ;;
     p2) ( bash profiles/run_profile.sh "${TAG}" ) > "$OUT/p2.log" 2>&1 || { echo P2_FAIL; tail "$OUT/p2.log"; exit 1; }
         tail -3 "$OUT/p2.log" ;;
-    c4) bash tools/gpu_bench_ab.sh "$TAG/c4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
+    c4) bash tools/gpu_bench_ab.sh "$TAG/c4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_CONCURRENT=0" \
+          "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16 GKGPU_CONCURRENT=0" || exit 1 ;;
     c5) timeout -k 10 300 python -u tools/probe_c5_time.py 256 > "$OUT/c5_phases.txt" 2>&1 || { echo C5P_FAIL; tail "$OUT/c5_phases.txt"; exit 1; }
         cat "$OUT/c5_phases.txt"
         timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 > "$OUT/c5_batch.json" 2> "$OUT/c5_batch.err" || { echo C5_FAIL; tail "$OUT/c5_batch.err"; exit 1; }
