@@ -1134,7 +1134,26 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
     << "    gk::" << name << "_pred(L, review, params, plo, pn);\n"
     << "  });\n"
     << "}\n";
-  return o.str();
+  std::string src = o.str();
+  // diagnostics (GPU probes of what a kernel's parts cost): GKGPU_JIT_PATCH =
+  // "from=>to||from2=>to2" replaces text in every generated kernel source
+  if (const char* pt = getenv("GKGPU_JIT_PATCH")) {
+    std::string spec = pt;
+    if (!spec.empty() && spec[0] == '@' && !read_file(spec.substr(1), spec)) spec.clear();  // @file: the spec in a file
+    for (size_t i = 0; i < spec.size();) {
+      size_t j = spec.find("||", i);
+      if (j == std::string::npos) j = spec.size();
+      const std::string item = spec.substr(i, j - i);
+      const size_t arrow = item.find("=>");
+      if (arrow != std::string::npos) {
+        const std::string from = item.substr(0, arrow), to = item.substr(arrow + 2);
+        for (size_t at = 0; !from.empty() && (at = src.find(from, at)) != std::string::npos; at += to.size())
+          src.replace(at, from.size(), to);
+      }
+      i = j + 2;
+    }
+  }
+  return src;
 }
 
 std::string jit_fused_source(const std::vector<const Program*>& progs, const std::vector<uint32_t>& ids,
