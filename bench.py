@@ -496,6 +496,8 @@ def from_cache_main(args):
             "first_audit_s": round(t_first, 3),
             "first_audit_timing_ms": [round(x, 2) for x in first["timing_ms"]],
             "steady_timing_ms": [round(x, 2) for x in last["timing_ms"]],
+            "first_launches": first.get("launches"),
+            "steady_launches": last.get("launches"),
             "timing_fields": "flatten, upload, kernels, download, decode (engine phases of one gk_query)",
             "sync_s": round(t_sync, 1),
         },

@@ -849,45 +849,28 @@ static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
 // region is compacted (maybe_compact).
 static void sync_inventory(gk_engine* e) {
   if (!e->uses_inventory || !e->inv_dirty || e->inv_node == NO_ID) return;
-  std::vector<std::pair<std::vector<std::string>, const std::string*>> ents;
-  for (auto& kv : e->inventory) {
-    auto p = split_path(kv.first);
+  // the synced objects under /external/<target>/, their paths split (URL
+  // unescaped) and ordered segment by segment -- the tree's member order
+  std::vector<std::pair<const std::string*, const std::string*>> kvs;
+  kvs.reserve(e->inventory.size());
+  for (auto& kv : e->inventory) kvs.push_back({&kv.first, &kv.second});
+  std::vector<std::vector<std::string>> segs(kvs.size());
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), kvs.size() / 4096));
+  parallel_run(T, [&](int t) {
+    for (size_t i = kvs.size() * t / T; i < kvs.size() * (t + 1) / T; ++i) segs[i] = split_path(*kvs[i].first);
+  });
+  std::vector<uint32_t> ents;
+  ents.reserve(kvs.size());
+  for (uint32_t i = 0; i < kvs.size(); ++i) {
+    const auto& p = segs[i];
     if (p.size() < 3 || p[0] != "external" || p[1] != TARGET) continue;
-    ents.push_back({std::vector<std::string>(p.begin() + 2, p.end()), &kv.second});
+    ents.push_back(i);
   }
-  std::sort(ents.begin(), ents.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-  std::string js;
-  auto quote = [&](const std::string& v) {
-    js.push_back('"');
-    for (unsigned char c : v) {
-      if (c == '"' || c == '\\') { js.push_back('\\'); js.push_back((char)c); }
-      else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); js += b; }
-      else js.push_back((char)c);
-    }
-    js.push_back('"');
-  };
-  // entries [lo, hi) share their first `depth` segments; a leaf at a segment
-  // shadows deeper paths under it (one value per path)
-  std::function<void(size_t, size_t, size_t)> emit = [&](size_t lo, size_t hi, size_t depth) {
-    js.push_back('{');
-    for (size_t i = lo; i < hi;) {
-      const std::string& seg = ents[i].first[depth];
-      size_t j = i;
-      while (j < hi && ents[j].first[depth] == seg) ++j;
-      if (i != lo) js.push_back(',');
-      quote(seg);
-      js.push_back(':');
-      if (ents[i].first.size() == depth + 1) js += *ents[i].second;
-      else emit(i, j, depth + 1);
-      i = j;
-    }
-    js.push_back('}');
-  };
-  emit(0, ents.size(), 0);
-  JDoc d;
-  JsonReader rd(js.data(), js.size(), &d);
-  int root = rd.parse();
-  if (root < 0) throw std::runtime_error("inventory tree: " + d.err);
+  // (segments 0 and 1 are equal for every entry: order by the rest)
+  std::sort(ents.begin(), ents.end(), [&](uint32_t a, uint32_t b) {
+    return std::lexicographical_compare(segs[a].begin() + 2, segs[a].end(), segs[b].begin() + 2, segs[b].end());
+  });
+  const size_t n = ents.size();
   reset_transient(e);
   if (e->inv_hi > e->inv_lo && e->inv_hi == e->perm_nodes) {
     // the previous tree is the region's tail: reuse its space
@@ -895,10 +878,52 @@ static void sync_inventory(gk_engine* e) {
     e->perm_nodes = e->inv_lo;
   }
   e->inv_lo = (uint32_t)e->st.nodes().size();
-  const uint32_t r = e->st.add_doc(d, root);
+  // every object parsed on the host threads into the permanent region
+  // (flatten_docs), then the tree of path segments above them
+  std::vector<std::string_view> docs(n);
+  for (size_t i = 0; i < n; ++i) docs[i] = *kvs[ents[i]].second;
+  NodeArena dst;
+  std::vector<uint32_t> roots;
+  std::string err;
+  if (!flatten_docs(e->st, e->smu, docs, e->inv_lo, dst, roots, err)) throw std::runtime_error("inventory tree: " + err);
+  {
+    NodeArena& N = e->st.nodes();
+    const size_t at = N.size();
+    N.resize(at + dst.size());
+    if (dst.size()) memcpy(N.data() + at, dst.data(), dst.size() * sizeof(Node));
+  }
+  // entries [lo, hi) share their first `depth` segments; a leaf at a segment
+  // shadows deeper paths under it (one value per path); an object of more than
+  // 0xffff members keeps the first 0xffff (flags bit 0), as parsed documents do
+  std::function<Node(size_t, size_t, size_t)> tree = [&](size_t lo, size_t hi, size_t depth) -> Node {
+    std::vector<std::pair<size_t, size_t>> groups;
+    for (size_t i = lo; i < hi;) {
+      const std::string& seg = segs[ents[i]][depth];
+      size_t j = i;
+      while (j < hi && segs[ents[j]][depth] == seg) ++j;
+      groups.push_back({i, j});
+      i = j;
+    }
+    Node o{};
+    o.type = NT_OBJ;
+    size_t cnt = groups.size();
+    if (cnt > 0xffff) { o.flags |= 1; cnt = 0xffff; }
+    const uint32_t first = (uint32_t)e->st.nodes().size();
+    e->st.nodes().resize(first + cnt);
+    for (size_t g = 0; g < cnt; ++g) {
+      const size_t i = groups[g].first;
+      const std::string& seg = segs[ents[i]][depth];
+      Node c = segs[ents[i]].size() == depth + 1 ? e->st.nodes()[roots[i]] : tree(i, groups[g].second, depth + 1);
+      c.key = e->st.intern(seg);
+      e->st.nodes()[first + g] = c;
+    }
+    o.first = cnt ? first : 0;
+    o.n = (uint16_t)cnt;
+    return o;
+  };
+  const Node t = tree(0, n, 2);
   e->inv_hi = (uint32_t)e->st.nodes().size();
   Node& slot = e->st.nodes()[e->inv_node];
-  const Node& t = e->st.nodes()[r];
   slot.type = t.type;
   slot.first = t.first;
   slot.n = t.n;
@@ -1403,18 +1428,32 @@ static void ensure_jit(gk_engine* e, bool load) {
 // tree, regex DFAs) and the device tables up to date with the last mutation.
 // Called with the exclusive lock held.
 static int prepare_locked(gk_engine* e, bool device) {
+  // GKGPU_PREPARE_TRACE: the time of each step on stderr
+  const bool tr = getenv("GKGPU_PREPARE_TRACE") != nullptr;
+  auto tp = Clock::now();
+  auto step = [&](const char* what) {
+    if (tr) fprintf(stderr, "prepare: %s %.1f ms\n", what, ms_since(tp));
+    tp = Clock::now();
+  };
   try {
     maybe_compact(e);
+    step("compact");
     rebuild_constraints(e);
+    step("constraints");
     rebuild_regex(e);
+    step("regex");
     rebuild_stage(e);
+    step("stage");
     plan_joins(e);
+    step("plan joins");
   } catch (const std::exception& ex) {
     return fail(e, GK_EPARSE, ex.what());
   }
   if (device && ensure_device(e)) {
     ensure_jit(e, true);
+    step("jit");
     if (!sync_tables(e)) return fail(e, GK_EDEVICE, "device upload failed");
+    step("tables");
     // without indexes every join site scans (same results): a failed build
     // (device memory, a key-pass launch) costs time, not correctness
     if (!build_joins(e)) {
@@ -1422,6 +1461,7 @@ static int prepare_locked(gk_engine* e, bool device) {
       fprintf(stderr, "gkgpu: inventory join indexes not built (%s); join sites scan\n",
               hipGetErrorString(hipGetLastError()));
     }
+    step("joins");
   }
   e->prepared_gen = e->gen;
   // the device side was brought up to date, or there is no device to use
@@ -1779,6 +1819,9 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     // [0] tuples, [1] staged bytes, [2] lanes that flagged their review (error/fallback), [3] output bytes
     uint64_t counters[4];
     memcpy(counters, hp, 32);
+    if (getenv("GKGPU_LAUNCH_TRACE"))
+      fprintf(stderr, "launch: attempt %d, %zu launches, slots %llu (cap %zu), staged bytes %llu (cap %zu)\n", attempt,
+              plan.size(), (unsigned long long)counters[0], x->out_cap, (unsigned long long)counters[1], x->ebytes_cap);
     if (counters[0] > x->out_cap || counters[1] > x->ebytes_cap) {
       x->out_cap = std::max<size_t>(x->out_cap * 2, counters[0] + 1024);
       x->ebytes_cap = std::max<size_t>(x->ebytes_cap * 2, (size_t)counters[1] + 65536);

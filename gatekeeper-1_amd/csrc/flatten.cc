@@ -1133,6 +1133,36 @@ bool flatten_page(Store& gst, std::mutex& smu, const NsCache& ns_cache, const st
   return merge_parts(gst, smu, parts, base, dst, out, n, err, order, perm, dl);
 }
 
+bool flatten_docs(Store& gst, std::mutex& smu, const std::vector<std::string_view>& docs, uint32_t base, NodeArena& dst,
+                  std::vector<uint32_t>& roots, std::string& err) {
+  const size_t n = docs.size();
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), n / 2048));
+  std::vector<Part> parts = take_parts(T);
+  struct Give { std::vector<Part>& v; ~Give() { give_parts(v); } } give{parts};
+  parallel_run(T, [&](int t) {
+    Part& p = parts[t];
+    p.lo = n * t / T;
+    p.hi = n * (t + 1) / T;
+    std::string perr;
+    for (size_t i = p.lo; i < p.hi; ++i) {
+      Node r;
+      if (!p.st.parse_doc(docs[i].data(), docs[i].size(), &r, &perr)) {
+        p.err = "invalid JSON at " + std::to_string(i) + ": " + perr;
+        return;
+      }
+      p.rbeg.push_back(p.st.add_node(r));  // (the part-local id of the placed root)
+    }
+  });
+  for (auto& p : parts)
+    if (!p.err.empty()) { err = p.err; return false; }
+  FlatResult out;
+  if (!merge_parts(gst, smu, parts, base, dst, out, 0, err)) return false;
+  roots.resize(n);
+  for (auto& p : parts)
+    for (size_t i = p.lo; i < p.hi; ++i) roots[i] = base + (uint32_t)p.node_off + p.rbeg[i - p.lo] - kFixedNodes;
+  return true;
+}
+
 bool flatten_reviews(Store& gst, std::mutex& smu, const NsCache& ns_cache,
                      const std::vector<std::pair<const char*, size_t>>& inputs, uint32_t base, NodeArena& dst,
                      std::vector<ReviewCol>& cols, std::string& err) {

@@ -146,6 +146,13 @@ bool flatten_reviews(Store& st, std::mutex& smu, const NsCache& ns_cache,
                      const std::vector<std::pair<const char*, size_t>>& inputs, uint32_t base, NodeArena& dst,
                      std::vector<ReviewCol>& cols, std::string& err);
 
+// Parses standalone JSON documents (the inventory's synced objects) on the
+// host threads into `dst` (node id base + k at dst[k], strings interned into
+// `st` under `smu`); roots[i] = the placed root node id of docs[i].  False +
+// err on malformed JSON (the index of the first bad document).
+bool flatten_docs(Store& st, std::mutex& smu, const std::vector<std::string_view>& docs, uint32_t base, NodeArena& dst,
+                  std::vector<uint32_t>& roots, std::string& err);
+
 int default_threads();
 
 // Runs f(0) .. f(n-1) in parallel on the engine's persistent host workers

@@ -586,7 +586,8 @@ class Driver:
             totals = [self._lib.gk_results_constraint_total(out, i) for i in range(nc)]
             ms = (C.c_double * 5)()
             self._lib.gk_results_timing(out, ms)
-            return {"results": n, "totals": totals, "timing_ms": list(ms)}
+            return {"results": n, "totals": totals, "timing_ms": list(ms),
+                    "launches": [(k.kernel, round(k.ms, 3), k.tuples) for k in _launches(self._lib, out)]}
         finally:
             self._lib.gk_results_free(out)
 
