@@ -1723,13 +1723,15 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     const std::vector<hipEvent_t>& ev = x->events;
     hipEventRecord(ev[0], x->stream);
-    // GKGPU_CONCURRENT (A/B switch, default on): the template launches go
-    // round-robin to the context's stream and up to three side streams, each
-    // with its own memo table, and run side by side (a micro-batch's launches
-    // are latency-bound; a sweep's fill each other's tails); the compaction
-    // waits for all of them.  Per-launch timing then uses per-launch events.
+    // GKGPU_CONCURRENT: the template launches go round-robin to the context's
+    // stream and up to three side streams, each with its own memo table, and
+    // run side by side; the compaction waits for all of them.  Per-launch
+    // timing uses per-launch events.  Default (2): micro-batches only (up to
+    // 65,536 reviews: latency-bound launches); a sweep's launches each fill
+    // the GPU and measured no faster side by side (profiles/r04/r04s_ab.txt).
     int nstream = 1;
-    if (plan.size() > 1 && env_mode("GKGPU_CONCURRENT", 1, 1) != 0) {
+    const int conc = env_mode("GKGPU_CONCURRENT", 2, 2);
+    if (plan.size() > 1 && (conc == 1 || (conc == 2 && nrev <= 65536))) {
       nstream = (int)std::min<size_t>(plan.size(), 1 + EvalCtx::kSide);
       for (int k = 0; k + 1 < nstream; ++k)
         if (!x->side[k] && hipStreamCreateWithFlags(&x->side[k], hipStreamNonBlocking) != hipSuccess) { nstream = k + 1; break; }

@@ -15,7 +15,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
     c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_CONCURRENT=0" \
           "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16 GKGPU_CONCURRENT=0" || exit 1 ;;
     rpv) bash tools/gpu_bench_ab.sh "$TAG/rpv" "--steps 10 --warmup 2" "" "GKGPU_JIT_PATCH=@tools/patches/rp_noemit.txt" \
-          "GKGPU_JIT_PATCH=@tools/patches/rp_nobody2.txt" || exit 1 ;;
+          "GKGPU_JIT_PATCH=@tools/patches/rp_nobody2.txt" "GKGPU_JIT_PATCH=@tools/patches/rp_contonly.txt" \
+          "GKGPU_JIT_PATCH=@tools/patches/rp_probeloop.txt" || exit 1 ;;
     c2t) GKGPU_FLATTEN_TRACE=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/c2t.json" 2> "$OUT/c2t.err" || { echo C2T_FAIL; tail "$OUT/c2t.err"; exit 1; }
         grep -E "flatten|stage upload|intern" "$OUT/c2t.err" | tail -12
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C2T', round(d['value']/1e6,1), 'M/s stage_s', c['stage_s'], c['stage_ms'], 'prepare_s', c.get('prepare_s'), 'e2e', round(c['end_to_end_evals_per_s']/1e6,2))" "$OUT/c2t.json" ;;
