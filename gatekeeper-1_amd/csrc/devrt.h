@@ -46,6 +46,14 @@ static_assert(sizeof(gk::DevArgs) % 8 == 0, "the hidden kernel arguments follow 
 #ifndef GK_TOUCH_STR
 #define GK_TOUCH_STR(s) ((void)0)
 #endif
+// heap word / lane-buffer byte writes (the accounting build counts where they
+// would land: LDS or the private segment)
+#ifndef GK_HEAP_WRITE
+#define GK_HEAP_WRITE(w) ((void)0)
+#endif
+#ifndef GK_BUF_WRITE
+#define GK_BUF_WRITE(n) ((void)0)
+#endif
 
 namespace gk {
 
@@ -229,7 +237,7 @@ __device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) {
 }
 #else
 __device__ __forceinline__ uint64_t hget(const PLane& L, uint32_t w) { return L.H[w]; }
-__device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) { L.H[w] = v; }
+__device__ __forceinline__ void hset(PLane& L, uint32_t w, uint64_t v) { GK_HEAP_WRITE(w); L.H[w] = v; }
 #endif
 
 // ------------------------------------------------------------------ LDS stage
@@ -858,7 +866,7 @@ struct Out {
   char* p;
   uint32_t n, cap;
   bool ovf;
-  __device__ __forceinline__ void put(char c) { if (n < cap) p[n++] = c; else ovf = true; }
+  __device__ __forceinline__ void put(char c) { if (n < cap) { GK_BUF_WRITE(1); p[n++] = c; } else ovf = true; }
 };
 struct Cnt {
   uint32_t n;

@@ -566,6 +566,8 @@ static void rebuild_modules(gk_engine* e) {
     auto m = rego::parse_module(kv.second);
     // the frameworks hooks + target library are served natively
     if (!m->pkg.empty() && m->pkg[0] == "hooks") continue;
+    // GKGPU_REGO_SETS (A/B switch, default on): set-algebra rewrite (rego.cc)
+    if (env_mode("GKGPU_REGO_SETS", 1, 1) != 0) rego::optimize_sets(*m);
     e->mods.add(m);
     parsed.push_back(m);
   }

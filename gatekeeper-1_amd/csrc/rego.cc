@@ -501,6 +501,151 @@ std::shared_ptr<Module> parse_module(const std::string& src) {
   return p.module();
 }
 
+// ------------------------------------------------------------------ set algebra
+// count(A - {k | T[k]}) == count(A)  <=>  no member a of A has T[a] truthy:
+// the comprehension collects exactly the keys k whose T[k] is defined and not
+// false (a scalar or missing T gives the empty set, and so does a lookup), and
+// |A - B| = |A| - |A & B|.  The rewrite never builds the two sets (heap lists
+// per lane in the template kernels: k8srequiredprobes' probe_field_empty,
+// demo/agilebank/templates/k8srequiredprobes_template.yaml:36-40).  A must be
+// a set, and defined: it is restricted to a rule of the module whose value is
+// a set comprehension (always defined).
+static bool is_var(const TermP& t, const std::string& name = "") {
+  return t && t->k == T_VAR && (name.empty() || t->s == name);
+}
+static bool is_call(const TermP& t, const char* op, size_t nargs) {
+  return t && t->k == T_CALL && t->op.size() == 1 && t->op[0] == op && t->items.size() == nargs;
+}
+static bool mentions(const TermP& t, const std::string& v);
+static bool mentions_body(const std::vector<ExprP>& body, const std::string& v) {
+  for (auto& e : body) {
+    for (auto& t : e->terms) if (mentions(t, v)) return true;
+    for (auto& w : e->withs) if (mentions(w.target, v) || mentions(w.value, v)) return true;
+  }
+  return false;
+}
+static bool mentions(const TermP& t, const std::string& v) {
+  if (!t) return false;
+  if (t->k == T_VAR && t->s == v) return true;
+  if (mentions(t->head, v) || mentions(t->key, v) || mentions(t->value, v)) return true;
+  for (auto& x : t->items) if (mentions(x, v)) return true;
+  return mentions_body(t->body, v);
+}
+static bool set_rule(const Module& m, const std::string& name) {
+  int n = 0;
+  bool ok = true;
+  for (auto& r : m.rules) {
+    if (r->name != name) continue;
+    ++n;
+    if (r->kind != Rule::COMPLETE || r->is_default || r->is_else || !r->args.empty()) { ok = false; continue; }
+    if (r->value && r->value->k == T_SETCOMPR && r->body.empty()) continue;
+    ok = ok && r->body.size() == 1 && r->body[0]->kind == Expr::ASSIGN && !r->body[0]->negated &&
+         r->body[0]->withs.empty() && r->body[0]->terms.size() == 2 && is_var(r->body[0]->terms[0]) &&
+         r->body[0]->terms[1]->k == T_SETCOMPR && is_var(r->value, r->body[0]->terms[0]->s);
+  }
+  return n == 1 && ok;
+}
+int optimize_sets(Module& m) {
+  int done = 0;
+  for (size_t ri = 0; ri < m.rules.size(); ++ri) {
+    Rule& r = *m.rules[ri];
+    auto& b = r.body;
+    for (size_t i = 0; i + 2 < b.size() + 0 && i < b.size(); ++i) {
+      // E1: v1 := {k | T[k]}
+      const ExprP e1 = b[i];
+      if (e1->kind != Expr::ASSIGN || e1->negated || !e1->withs.empty() || e1->terms.size() != 2 || !is_var(e1->terms[0]))
+        continue;
+      const TermP c = e1->terms[1];
+      if (c->k != T_SETCOMPR || !is_var(c->key) || c->body.size() != 1) continue;
+      const ExprP cb = c->body[0];
+      if (cb->kind != Expr::TERM || cb->negated || !cb->withs.empty() || cb->terms.size() != 1) continue;
+      const TermP ref = cb->terms[0];
+      const std::string k = c->key->s, v1 = e1->terms[0]->s;
+      if (ref->k != T_REF || ref->items.empty() || !is_var(ref->items.back(), k) || mentions(ref->head, k)) continue;
+      bool kin = false;
+      for (size_t q = 0; q + 1 < ref->items.size(); ++q) kin = kin || mentions(ref->items[q], k);
+      if (kin) continue;
+      // E2: v2 := A - v1, E3: count(v2) == count(A) (either side), later in the body
+      for (size_t j = i + 1; j < b.size(); ++j) {
+        const ExprP e2 = b[j];
+        if (e2->kind != Expr::ASSIGN || e2->negated || !e2->withs.empty() || e2->terms.size() != 2 || !is_var(e2->terms[0]))
+          continue;
+        const TermP mi = e2->terms[1];
+        if (!is_call(mi, "minus", 2) || !is_var(mi->items[1], v1) || !is_var(mi->items[0])) continue;
+        const std::string A = mi->items[0]->s, v2 = e2->terms[0]->s;
+        for (size_t l = j + 1; l < b.size(); ++l) {
+          const ExprP e3 = b[l];
+          if (e3->kind != Expr::TERM || e3->negated || !e3->withs.empty() || e3->terms.size() != 1) continue;
+          const TermP eq = e3->terms[0];
+          if (!is_call(eq, "equal", 2) || !is_call(eq->items[0], "count", 1) || !is_call(eq->items[1], "count", 1)) continue;
+          const TermP x0 = eq->items[0]->items[0], x1 = eq->items[1]->items[0];
+          if (!((is_var(x0, v2) && is_var(x1, A)) || (is_var(x0, A) && is_var(x1, v2)))) continue;
+          // v1 and v2 used nowhere else; A is the module's set rule, not shadowed
+          std::vector<ExprP> rest;
+          for (size_t q = 0; q < b.size(); ++q)
+            if (q != i && q != j && q != l) rest.push_back(b[q]);
+          bool shadow = false;
+          for (auto& a : r.args) shadow = shadow || mentions(a, A);
+          for (auto& q : b)
+            if ((q->kind == Expr::ASSIGN || q->kind == Expr::SOME) && !q->terms.empty() && mentions(q->terms[0], A)) shadow = true;
+          if (mentions_body(rest, v1) || mentions_body(rest, v2) || mentions(r.value, v1) || mentions(r.value, v2) ||
+              mentions(r.key, v1) || mentions(r.key, v2) || shadow || !set_rule(m, A))
+            continue;
+          TermP T;
+          if (ref->items.size() == 1) T = ref->head;
+          else {
+            T = mk(T_REF);
+            T->head = ref->head;
+            T->items.assign(ref->items.begin(), ref->items.end() - 1);
+          }
+          auto ne = std::make_shared<Expr>();
+          ne->kind = Expr::TERM;
+          ne->negated = true;
+          ne->line = e3->line;
+          ne->terms = {mk_call({"__gk_anyin"}, {mk_var(A), T})};
+          std::vector<ExprP> nb;
+          for (size_t q = 0; q < b.size(); ++q) {
+            if (q == i || q == j) continue;
+            nb.push_back(q == l ? ne : b[q]);
+          }
+          b.swap(nb);
+          ++done;
+          goto next_rule;
+        }
+      }
+    }
+  next_rule:;
+  }
+  if (done) {
+    bool have = false;
+    for (auto& r : m.rules) have = have || r->name == "__gk_anyin";
+    if (!have) {
+      // __gk_anyin(s, x) = true { y := s[w]; x[y] }
+      auto f = std::make_shared<Rule>();
+      f->kind = Rule::FUNC;
+      f->name = "__gk_anyin";
+      f->args = {mk_var("__gk_s"), mk_var("__gk_x")};
+      f->value = mk_scalar(S_TRUE, "true");
+      f->mod = &m;
+      auto it = mk(T_REF);
+      it->head = mk_var("__gk_s");
+      it->items = {mk_var("__gk_w")};
+      auto a1 = std::make_shared<Expr>();
+      a1->kind = Expr::ASSIGN;
+      a1->terms = {mk_var("__gk_y"), it};
+      auto lk = mk(T_REF);
+      lk->head = mk_var("__gk_x");
+      lk->items = {mk_var("__gk_y")};
+      auto a2 = std::make_shared<Expr>();
+      a2->kind = Expr::TERM;
+      a2->terms = {lk};
+      f->body = {a1, a2};
+      m.rules.push_back(f);
+    }
+  }
+  return done;
+}
+
 // ------------------------------------------------------------------ vars
 static void all_vars(const TermP& t, std::vector<std::string>& out);
 static void iter_vars(const TermP& t, std::vector<std::string>& out);

@@ -76,5 +76,13 @@ std::vector<ExprP> compile_body(const std::vector<ExprP>& body, const std::vecto
 // variables of a term (excluding comprehension-local ones)
 void term_vars(const TermP& t, std::vector<std::string>& out);
 
+// Set-algebra rewrite of a module's rule bodies (rego.cc optimize_sets):
+//   v1 := {k | T[k]}; v2 := A - v1; count(v2) == count(A)
+// with A a rule of the module whose value is a set comprehension, and v1, v2
+// used nowhere else, becomes `not __gk_anyin(A, T)`, the function
+// `__gk_anyin(s, x) = true { y := s[_]; x[y] }` added to the module.  Returns
+// the number of bodies rewritten.
+int optimize_sets(Module& m);
+
 }  // namespace rego
 }  // namespace gk

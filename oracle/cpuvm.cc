@@ -70,6 +70,15 @@ thread_local uint64_t* pc_hist = nullptr;  // executions per bytecode instructio
 }  // namespace gkcpu_touch
 #define GK_TOUCH_NODE(i) (gkcpu_touch::node_bits[(uint32_t)(i) >> 6] |= 1ull << ((uint32_t)(i) & 63))
 #define GK_TOUCH_STR(s) (gkcpu_touch::str_bits[(uint32_t)(s) >> 6] |= 1ull << ((uint32_t)(s) & 63))
+// lane-state writes by heap word index (bucket: <16, <32, <64, the rest) and
+// lane-buffer bytes: where a template kernel's lane state lands (LDS words vs
+// the private segment; gkcpu_scratch_stats)
+namespace gkcpu_touch {
+thread_local uint64_t heap_w[4] = {0, 0, 0, 0};
+thread_local uint64_t buf_b = 0;
+}  // namespace gkcpu_touch
+#define GK_HEAP_WRITE(w) (++gkcpu_touch::heap_w[(w) < 16 ? 0 : (w) < 32 ? 1 : (w) < 64 ? 2 : 3])
+#define GK_BUF_WRITE(n) (gkcpu_touch::buf_b += (n))
 #endif
 
 // the launch arguments devrt.h reads (the device reads its kernarg segment)
@@ -494,6 +503,18 @@ int gkcpu_referenced(const void* args, uint64_t n_nodes, uint64_t n_strings, uin
   for (auto& k : per) { viol += k.violations; flagged += k.flagged; }
   uint64_t o[5] = {nodes, strs, sbytes, viol, flagged};
   memcpy(out5, o, sizeof o);
+  return 0;
+}
+
+// the heap-word writes (by word index bucket) and lane-buffer bytes of the
+// last gkcpu_referenced call on this thread (threads = 1)
+int gkcpu_scratch_stats(uint64_t* out5, int reset) {
+  for (int i = 0; i < 4; ++i) out5[i] = gkcpu_touch::heap_w[i];
+  out5[4] = gkcpu_touch::buf_b;
+  if (reset) {
+    for (int i = 0; i < 4; ++i) gkcpu_touch::heap_w[i] = 0;
+    gkcpu_touch::buf_b = 0;
+  }
   return 0;
 }
 

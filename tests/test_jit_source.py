@@ -74,3 +74,10 @@ def test_lazy_sprintf_argument_count_is_an_immediate():
     src = _dump("K8sRequiredProbes")
     assert "lazy_sprintf_n(L," in src
     assert "lazy_sprintf(L," not in src
+
+
+def test_required_probes_builds_no_sets_after_the_rewrite():
+    """rego.cc optimize_sets: probe_field_empty's two sets and their difference
+    are gone from K8sRequiredProbes' kernel (GKGPU_REGO_SETS=0 keeps them)."""
+    assert "arith(L, 1u," not in _dump("K8sRequiredProbes")
+    assert "arith(L, 1u," in _dump("K8sRequiredProbes", [("GKGPU_REGO_SETS", "0")])

@@ -1,0 +1,65 @@
+"""The set-algebra rewrite of rule bodies (rego.cc optimize_sets,
+GKGPU_REGO_SETS): `v1 := {k | T[k]}; v2 := A - v1; count(v2) == count(A)` with
+A a set rule becomes `not __gk_anyin(A, T)` -- k8srequiredprobes'
+probe_field_empty (demo/agilebank/templates/k8srequiredprobes_template.yaml:36-40)
+no longer builds two sets per container and probe.  The CPU checker's result
+rows (oracle/cpuvm.cc gkcpu_sweep_digest) equal the oracle's with and without
+the rewrite, on config 2 Pods and on probe values of every shape (missing,
+scalar, empty object, false / non-false members, arrays with a numeric probe
+type)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CODE = r'''
+import copy, json, sys
+sys.path[:0] = [%r, %r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+from oracle import cpu_baseline
+from parity import oracle_for, oracle_review
+ts, cs = W.config2()
+ts = [t for t in ts if t["spec"]["crd"]["spec"]["names"]["kind"] == "K8sRequiredProbes"]
+cs = [c for c in cs if c["kind"] == "K8sRequiredProbes"]
+c2 = copy.deepcopy(cs[0])
+c2["metadata"]["name"] = "odd-probe-types"
+c2["spec"]["parameters"]["probeTypes"] = ["tcpSocket", 0, "exec"]
+cs = cs + [c2]
+pods, ns_of, ns_objs = W.gen_pods(300, seed=21, n_namespaces=10)
+nss = [ns_objs[n] for n in ns_of]
+shapes = [None, "x", {}, {"httpGet": False}, {"httpGet": {}}, {"exec": {"command": ["a"]}}, [True], [False, True],
+          {"tcpSocket": None}, 7]
+for i, s in enumerate(shapes):
+    ctr = {"name": "c%%d" %% i, "image": "openpolicyagent/opa:0.9.2"}
+    if s is not None:
+        ctr["livenessProbe"] = s
+        ctr["readinessProbe"] = s
+    pods.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "shape-%%d" %% i, "namespace": "default"},
+                 "spec": {"containers": [ctr]}})
+    nss.append({"metadata": {"name": "default"}})
+d = gkgpu.Driver(host_only=True); cl = Client(d)
+for t in ts: cl.add_template(t)
+for c in cs: cl.add_constraint(c)
+got = cpu_baseline.sweep_digest(d, d.stage_objects(pods, nss), threads=2)
+od = oracle_for(ts, cs)
+cidx = {kn: i for i, kn in enumerate(d.constraints())}
+rows = []
+for i, (o, n) in enumerate(zip(pods, nss)):
+    for kind, name, msg, det, _ea in oracle_review(od, augmented_review(o, n)):
+        rows.append((i, cidx[(kind, name)], msg, det))
+print(json.dumps([got[1], got[2], got[3], cpu_baseline.row_digest(rows), len(rows)]))
+''' % (os.path.join(ROOT, "gatekeeper-1_amd"), ROOT, os.path.join(ROOT, "tests"))
+
+
+def test_set_rewrite_keeps_required_probes_rows():
+    for on in ("1", "0"):
+        env = dict(os.environ, GKGPU_REGO_SETS=on)
+        out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-2000:]
+        v, fl, dg, wd, wn = json.loads(out.stdout.strip().splitlines()[-1])
+        assert fl == 0 and v == wn > 100, (on, v, wn)
+        assert dg == wd, (on, "row digests differ from the oracle's")
