@@ -14,6 +14,10 @@ for what in "${@:-c2 c4 c5 cache}"; do
   case $what in
     c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_CONCURRENT=0" \
           "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16" "GKGPU_JIT_WPE=2 GKGPU_LDS_HEAP=16 GKGPU_CONCURRENT=0" || exit 1 ;;
+    sets) bash tools/gpu_bench_ab.sh "$TAG/sets" "--steps 10 --warmup 2" "" "GKGPU_REGO_SETS=0" || exit 1
+          bash tools/gpu_bench_ab.sh "$TAG/sets4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
+    suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+          tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rpv) bash tools/gpu_bench_ab.sh "$TAG/rpv" "--steps 10 --warmup 2" "" "GKGPU_JIT_PATCH=@tools/patches/rp_noemit.txt" \
           "GKGPU_JIT_PATCH=@tools/patches/rp_nobody2.txt" "GKGPU_JIT_PATCH=@tools/patches/rp_contonly.txt" \
           "GKGPU_JIT_PATCH=@tools/patches/rp_probeloop.txt" || exit 1 ;;
