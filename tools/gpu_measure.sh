@@ -20,6 +20,9 @@ for what in "${@:-c2 c4 c5 cache}"; do
           bash tools/gpu_bench_ab.sh "$TAG/sets4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
+    rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
+          "GKGPU_JIT_PATCH=@tools/patches/rl_setsonly.txt" "GKGPU_JIT_PATCH=@tools/patches/rl_body1only.txt" \
+          "GKGPU_JIT_PATCH=@tools/patches/rl_noemit1.txt" || exit 1 ;;
     rpv) bash tools/gpu_bench_ab.sh "$TAG/rpv" "--steps 10 --warmup 2" "" "GKGPU_JIT_PATCH=@tools/patches/rp_noemit.txt" \
           "GKGPU_JIT_PATCH=@tools/patches/rp_nobody2.txt" "GKGPU_JIT_PATCH=@tools/patches/rp_contonly.txt" \
           "GKGPU_JIT_PATCH=@tools/patches/rp_probeloop.txt" || exit 1 ;;
