@@ -32,9 +32,9 @@ namespace gk {
 }
 extern "C" int gk_launch_audit(const gk::DevArgs* args, hipStream_t stream);
 extern "C" int gk_launch_compact(const gk::DevArgs* a, const gk::Viol* raw, const uint64_t* rfrec, uint32_t* tcnt,
-                                 unsigned long long* toff, hipStream_t stream);
+                                 unsigned long long* toff, hipStream_t stream, uint64_t hint);
 extern "C" int gk_launch_keys(const gk::DevArgs* args, hipStream_t stream);
-extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev);
+extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev, uint64_t hint);
 extern "C" size_t gk_devargs_size();
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
@@ -237,6 +237,7 @@ struct EvalCtx {
   std::vector<hipEvent_t> lev;  // per launch: start, end (timing) + the join event
   size_t out_cap = 1 << 20, bytes_cap = 64u << 20, ebytes_cap = 16u << 20, cand_cap = 1 << 14;
   uint64_t eval_epoch = 0;   // bumps on every evaluation (output buffers reused)
+  uint64_t last_tuples = 0;  // the last evaluation's tuple count (sizes the passes' grids)
   uint64_t perm_gen = 0;     // engine generation whose permanent nodes d_nodes holds below perm_nodes
   uint32_t perm_nodes = 0;
   void* perm_buf = nullptr;  // the d_nodes buffer that copy went to
@@ -1795,11 +1796,13 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     hipEventRecord(ev[plan.size()], x->stream);
     // the tuples of every launch above packed, then the size, spine and format passes
+    // pass grids sized for ~2x this context's last output (GKGPU_PASS_HINT=0: for the capacity)
+    const uint64_t pass_hint = env_mode("GKGPU_PASS_HINT", 1, 1) ? std::max<uint64_t>(2 * x->last_tuples, 65536) : 0;
     int flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
-                                (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream);
+                                (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream, pass_hint);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (compact): ") + hipGetErrorString((hipError_t)flr));
     hipEventRecord(ev[plan.size() + 1], x->stream);
-    flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2]);
+    flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2], pass_hint);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (format): ") + hipGetErrorString((hipError_t)flr));
     // one wait for the kernels and the small readbacks: counters, per-launch
     // counter snapshots, totals, and the per-review flags and reasons, queued
@@ -1839,7 +1842,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       if (!reserve_out()) return fail(e, GK_EDEVICE, "device allocation failed");
       a.bytes = (char*)x->d_bytes.p;
       a.bytes_cap = x->bytes_cap;
-      flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2]);
+      flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2], pass_hint);
       if (flr != 0 || hipStreamSynchronize(x->stream) != hipSuccess) return fail(e, GK_EDEVICE, "format pass failed");
       d2h(x, counters, x->d_counters.p, 32);
     }
@@ -1880,6 +1883,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     }
     auto t1 = Clock::now();
     res->dev_tuples = counters[0];
+    x->last_tuples = counters[0];
     res->dev_bytes = counters[3];
     res->failed_lanes = counters[2];
     res->epoch = ++x->eval_epoch;

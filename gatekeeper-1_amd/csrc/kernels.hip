@@ -483,8 +483,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
 // the size, spine and format passes after the predicate kernels of a call
 // (grids sized for the output capacity; the passes read the tuple count on the
 // device).  ev (optional, 3 events): recorded after size, spine and format.
-extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev) {
-  const uint64_t tiles = (a->out_cap + gk::FTILE - 1) / gk::FTILE;
+// (the passes loop over tiles with a grid stride: `hint`, an estimate of the
+// tuple count (the context's last evaluation), sizes the grid so a
+// micro-batch does not launch thousands of idle blocks; 0 = the capacity)
+extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev, uint64_t hint) {
+  const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::FTILE - 1) / gk::FTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
   hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[0], stream);
@@ -498,8 +501,8 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
 // packs the predicate kernels' chunked tuples (raw, rfrec) into a->out /
 // a->frec; tcnt: one u32 per CTILE raw slots of capacity, toff: one u64 each
 extern "C" int gk_launch_compact(const gk::DevArgs* a, const gk::Viol* raw, const uint64_t* rfrec, uint32_t* tcnt,
-                                 unsigned long long* toff, hipStream_t stream) {
-  const uint64_t tiles = (a->out_cap + gk::CTILE - 1) / gk::CTILE;
+                                 unsigned long long* toff, hipStream_t stream, uint64_t hint) {
+  const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::CTILE - 1) / gk::CTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
   hipLaunchKernelGGL(gk::gk_compact_count, dim3(blocks), dim3(256), 0, stream, raw, tcnt, *a);
   hipLaunchKernelGGL(gk::gk_compact_scan, dim3(1), dim3(1024), 0, stream, (const uint32_t*)tcnt, toff, *a);
