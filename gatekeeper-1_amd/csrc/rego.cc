@@ -616,7 +616,104 @@ int optimize_sets(Module& m) {
     }
   next_rule:;
   }
-  if (done) {
+  const bool anyin = done > 0;
+  // Second pattern: v1 := {k | T[k]}; v2 := A - v1 (v1 used nowhere else, A a
+  // set: a comprehension assigned earlier in the body or a set rule) becomes
+  // v2 := {e | e := A[i]; not T[e]} -- the members of A whose T[a] is
+  // undefined or false, the set A - {k | T[k]} without building the second
+  // set (k8srequiredlabels' `missing := required - provided`,
+  // demo/agilebank/templates/k8srequiredlabels_template.yaml:41-43).
+  int fresh = 0;
+  for (size_t ri = 0; ri < m.rules.size(); ++ri) {
+    Rule& r = *m.rules[ri];
+    auto& b = r.body;
+    for (size_t i = 0; i < b.size(); ++i) {
+      const ExprP e1 = b[i];
+      if (e1->kind != Expr::ASSIGN || e1->negated || !e1->withs.empty() || e1->terms.size() != 2 || !is_var(e1->terms[0]))
+        continue;
+      const TermP c = e1->terms[1];
+      if (c->k != T_SETCOMPR || !is_var(c->key) || c->body.size() != 1) continue;
+      const ExprP cb = c->body[0];
+      if (cb->kind != Expr::TERM || cb->negated || !cb->withs.empty() || cb->terms.size() != 1) continue;
+      const TermP ref = cb->terms[0];
+      const std::string k = c->key->s, v1 = e1->terms[0]->s;
+      if (ref->k != T_REF || ref->items.empty() || !is_var(ref->items.back(), k) || mentions(ref->head, k)) continue;
+      bool kin = false;
+      for (size_t q = 0; q + 1 < ref->items.size(); ++q) kin = kin || mentions(ref->items[q], k);
+      if (kin) continue;
+      bool hit = false;
+      for (size_t j = i + 1; j < b.size() && !hit; ++j) {
+        const ExprP e2 = b[j];
+        if (e2->kind != Expr::ASSIGN || e2->negated || !e2->withs.empty() || e2->terms.size() != 2 || !is_var(e2->terms[0]))
+          continue;
+        const TermP mi = e2->terms[1];
+        if (!is_call(mi, "minus", 2) || !is_var(mi->items[1], v1) || !is_var(mi->items[0])) continue;
+        const std::string A = mi->items[0]->s;
+        // A: assigned a set comprehension earlier in this body (and nowhere
+        // else), or the module's set rule (not shadowed)
+        int assigned = 0;
+        bool local_set = false;
+        for (size_t q = 0; q < b.size(); ++q) {
+          const ExprP& x = b[q];
+          if ((x->kind == Expr::ASSIGN || x->kind == Expr::UNIFY || x->kind == Expr::SOME) && !x->terms.empty() &&
+              mentions(x->terms[0], A)) {
+            ++assigned;
+            local_set = q < j && x->kind == Expr::ASSIGN && !x->negated && x->terms.size() == 2 && is_var(x->terms[0], A) &&
+                        x->terms[1]->k == T_SETCOMPR;
+          }
+        }
+        bool arg = false;
+        for (auto& a : r.args) arg = arg || mentions(a, A);
+        const bool set_ok = arg ? false : assigned == 1 ? local_set : assigned == 0 ? set_rule(m, A) : false;
+        std::vector<ExprP> rest;
+        for (size_t q = 0; q < b.size(); ++q)
+          if (q != i && q != j) rest.push_back(b[q]);
+        if (!set_ok || mentions_body(rest, v1) || mentions(r.value, v1) || mentions(r.key, v1)) continue;
+        const std::string e = "__gk_e" + std::to_string(fresh), ix = "__gk_i" + std::to_string(fresh);
+        ++fresh;
+        TermP T;
+        if (ref->items.size() == 1) T = ref->head;
+        else {
+          T = mk(T_REF);
+          T->head = ref->head;
+          T->items.assign(ref->items.begin(), ref->items.end() - 1);
+        }
+        auto it = mk(T_REF);
+        it->head = mk_var(A);
+        it->items = {mk_var(ix)};
+        auto x1 = std::make_shared<Expr>();
+        x1->kind = Expr::ASSIGN;
+        x1->terms = {mk_var(e), it};
+        auto lk = mk(T_REF);
+        lk->head = T;
+        lk->items = {mk_var(e)};
+        if (T->k == T_REF) {  // T[e] as one ref: T's path then e
+          lk->head = T->head;
+          lk->items = T->items;
+          lk->items.push_back(mk_var(e));
+        }
+        auto x2 = std::make_shared<Expr>();
+        x2->kind = Expr::TERM;
+        x2->negated = true;
+        x2->terms = {lk};
+        auto sc = mk(T_SETCOMPR);
+        sc->key = mk_var(e);
+        sc->body = {x1, x2};
+        auto ne = std::make_shared<Expr>(*e2);
+        ne->terms = {e2->terms[0], sc};
+        std::vector<ExprP> nb;
+        for (size_t q = 0; q < b.size(); ++q) {
+          if (q == i) continue;
+          nb.push_back(q == j ? ne : b[q]);
+        }
+        b.swap(nb);
+        ++done;
+        hit = true;
+      }
+      if (hit) i = (size_t)-1;  // rescan this body from the start (indices moved)
+    }
+  }
+  if (anyin) {
     bool have = false;
     for (auto& r : m.rules) have = have || r->name == "__gk_anyin";
     if (!have) {

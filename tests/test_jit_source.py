@@ -81,3 +81,10 @@ def test_required_probes_builds_no_sets_after_the_rewrite():
     are gone from K8sRequiredProbes' kernel (GKGPU_REGO_SETS=0 keeps them)."""
     assert "arith(L, 1u," not in _dump("K8sRequiredProbes")
     assert "arith(L, 1u," in _dump("K8sRequiredProbes", [("GKGPU_REGO_SETS", "0")])
+
+
+def test_required_labels_builds_no_provided_set():
+    """rego.cc optimize_sets (second pattern): k8srequiredlabels' `provided`
+    set is not built; `missing` iterates `required` with a lookup per key"""
+    on, off = _dump("K8sRequiredLabels"), _dump("K8sRequiredLabels", [("GKGPU_REGO_SETS", "0")])
+    assert "arith(L, 1u," not in on and "arith(L, 1u," in off

@@ -63,3 +63,53 @@ def test_set_rewrite_keeps_required_probes_rows():
         v, fl, dg, wd, wn = json.loads(out.stdout.strip().splitlines()[-1])
         assert fl == 0 and v == wn > 100, (on, v, wn)
         assert dg == wd, (on, "row digests differ from the oracle's")
+
+
+CODE_RL = r'''
+import json, sys
+sys.path[:0] = [%r, %r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+from oracle import cpu_baseline
+from parity import oracle_for, oracle_review
+ts, cs = W.config4()
+keep = ("K8sRequiredLabels",)
+ts = [t for t in ts if t["spec"]["crd"]["spec"]["names"]["kind"] in keep]
+cs = [c for c in cs if c["kind"] in keep]
+objs, nss = W.gen_config4_json(1500, seed=77)
+objs = [json.loads(o) for o in objs]
+nss = [json.loads(n) if n else None for n in nss]
+# label shapes: none, empty, a false / null / numeric value, every key present
+extra = [None, {}, {"owner": ""}, {"owner": "x", "app": "y", "team": "z", "env": "w"}]
+for i, lb in enumerate(extra):
+    md = {"name": "lbl-%%d" %% i, "namespace": "default"}
+    if lb is not None:
+        md["labels"] = lb
+    objs.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": md})
+    nss.append({"metadata": {"name": "default"}})
+d = gkgpu.Driver(host_only=True); cl = Client(d)
+for t in ts: cl.add_template(t)
+for c in cs: cl.add_constraint(c)
+got = cpu_baseline.sweep_digest(d, d.stage_objects(objs, nss), threads=2)
+od = oracle_for(ts, cs)
+cidx = {kn: i for i, kn in enumerate(d.constraints())}
+rows = []
+for i, (o, n) in enumerate(zip(objs, nss)):
+    for kind, name, msg, det, _ea in oracle_review(od, augmented_review(o, n)):
+        rows.append((i, cidx[(kind, name)], msg, det))
+print(json.dumps([got[1], got[2], got[3], cpu_baseline.row_digest(rows), len(rows)]))
+''' % (os.path.join(ROOT, "gatekeeper-1_amd"), ROOT, os.path.join(ROOT, "tests"))
+
+
+def test_set_rewrite_keeps_required_labels_rows():
+    """`missing := required - provided` with provided = {label | labels[label]}
+    becomes a comprehension over `required` with a negated lookup; rows (with
+    set-valued messages and details) equal the oracle's either way"""
+    for on in ("1", "0"):
+        env = dict(os.environ, GKGPU_REGO_SETS=on)
+        out = subprocess.run([sys.executable, "-c", CODE_RL], env=env, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-2000:]
+        v, fl, dg, wd, wn = json.loads(out.stdout.strip().splitlines()[-1])
+        assert fl == 0 and v == wn > 100, (on, v, wn)
+        assert dg == wd, (on, "row digests differ from the oracle's")
