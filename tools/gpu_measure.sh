@@ -17,7 +17,7 @@ for what in "${@:-c2 c4 c5 cache}"; do
     c5t) GKGPU_FLATTEN_TRACE=2 timeout -k 10 120 python -u tools/probe_c5_time.py 256 > "$OUT/c5t.txt" 2>&1 || { echo C5T_FAIL; tail "$OUT/c5t.txt"; exit 1; }
         grep -E "flatten_reviews|intern|relocate" "$OUT/c5t.txt" | tail -8; tail -3 "$OUT/c5t.txt" ;;
     sets) bash tools/gpu_bench_ab.sh "$TAG/sets" "--steps 10 --warmup 2" "" "GKGPU_REGO_SETS=0" || exit 1
-          bash tools/gpu_bench_ab.sh "$TAG/sets4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
+          bash tools/gpu_bench_ab.sh "$TAG/sets4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_REGO_SETS=0" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
