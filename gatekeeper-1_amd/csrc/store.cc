@@ -741,6 +741,22 @@ void Store::intern_parts(const std::vector<const Store*>& src, uint32_t first,
   struct Cand { uint64_t hv; uint32_t lid, gidx; };
   auto t0 = std::chrono::steady_clock::now();
   maps.assign(P, {});
+  {
+    // a micro-batch's few thousand strings: interned one by one (the sharded
+    // phases' fixed cost -- 256 shards x parts of candidate lists -- is larger)
+    size_t extra = 0;
+    for (const Store* ls : src) extra += ls->nstrings() > first ? ls->nstrings() - first : 0;
+    if (extra < 8192) {
+      for (size_t p = 0; p < P; ++p) {
+        const Store& ls = *src[p];
+        auto& m = maps[p];
+        m.resize(ls.nstrings());
+        for (uint32_t k = 0; k < first && k < ls.nstrings(); ++k) m[k] = k;
+        for (uint32_t k = first; k < ls.nstrings(); ++k) m[k] = intern(ls.str(k));
+      }
+      return;
+    }
+  }
   std::vector<std::vector<std::vector<Cand>>> cand(P, std::vector<std::vector<Cand>>(S));
   auto pfor = [&](size_t n, const std::function<void(size_t)>& f) {
     std::atomic<size_t> next{0};
