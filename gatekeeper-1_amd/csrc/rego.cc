@@ -545,9 +545,9 @@ static bool set_rule(const Module& m, const std::string& name) {
   }
   return n == 1 && ok;
 }
-int optimize_sets(Module& m) {
+int optimize_sets(Module& m, int mask) {
   int done = 0;
-  for (size_t ri = 0; ri < m.rules.size(); ++ri) {
+  for (size_t ri = 0; ri < m.rules.size() && (mask & 1); ++ri) {
     Rule& r = *m.rules[ri];
     auto& b = r.body;
     for (size_t i = 0; i + 2 < b.size() + 0 && i < b.size(); ++i) {
@@ -624,7 +624,7 @@ int optimize_sets(Module& m) {
   // set (k8srequiredlabels' `missing := required - provided`,
   // demo/agilebank/templates/k8srequiredlabels_template.yaml:41-43).
   int fresh = 0;
-  for (size_t ri = 0; ri < m.rules.size(); ++ri) {
+  for (size_t ri = 0; ri < m.rules.size() && (mask & 2); ++ri) {
     Rule& r = *m.rules[ri];
     auto& b = r.body;
     for (size_t i = 0; i < b.size(); ++i) {

@@ -80,9 +80,10 @@ void term_vars(const TermP& t, std::vector<std::string>& out);
 //   v1 := {k | T[k]}; v2 := A - v1; count(v2) == count(A)
 // with A a rule of the module whose value is a set comprehension, and v1, v2
 // used nowhere else, becomes `not __gk_anyin(A, T)`, the function
-// `__gk_anyin(s, x) = true { y := s[_]; x[y] }` added to the module.  Returns
-// the number of bodies rewritten.
-int optimize_sets(Module& m);
+// `__gk_anyin(s, x) = true { y := s[_]; x[y] }` added to the module (mask
+// bit 1); `v1 := {k | T[k]}; v2 := A - v1` becomes a comprehension over A
+// with a negated lookup (mask bit 2).  Returns the number of bodies rewritten.
+int optimize_sets(Module& m, int mask = 3);
 
 }  // namespace rego
 }  // namespace gk

@@ -1,5 +1,5 @@
 """The set-algebra rewrite of rule bodies (rego.cc optimize_sets,
-GKGPU_REGO_SETS): `v1 := {k | T[k]}; v2 := A - v1; count(v2) == count(A)` with
+GKGPU_REGO_SETS, a mask of two patterns): `v1 := {k | T[k]}; v2 := A - v1; count(v2) == count(A)` with
 A a set rule becomes `not __gk_anyin(A, T)` -- k8srequiredprobes'
 probe_field_empty (demo/agilebank/templates/k8srequiredprobes_template.yaml:36-40)
 no longer builds two sets per container and probe.  The CPU checker's result
@@ -56,7 +56,7 @@ print(json.dumps([got[1], got[2], got[3], cpu_baseline.row_digest(rows), len(row
 
 
 def test_set_rewrite_keeps_required_probes_rows():
-    for on in ("1", "0"):
+    for on in ("1", "2", "3", "0"):
         env = dict(os.environ, GKGPU_REGO_SETS=on)
         out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=600)
         assert out.returncode == 0, out.stderr[-2000:]
@@ -106,7 +106,7 @@ def test_set_rewrite_keeps_required_labels_rows():
     """`missing := required - provided` with provided = {label | labels[label]}
     becomes a comprehension over `required` with a negated lookup; rows (with
     set-valued messages and details) equal the oracle's either way"""
-    for on in ("1", "0"):
+    for on in ("1", "2", "3", "0"):
         env = dict(os.environ, GKGPU_REGO_SETS=on)
         out = subprocess.run([sys.executable, "-c", CODE_RL], env=env, capture_output=True, text=True, timeout=600)
         assert out.returncode == 0, out.stderr[-2000:]
