@@ -2031,6 +2031,9 @@ class Comp {
             for (int r : regs) varying |= r >= loop_var_lo_.back() && r < kVReg;
           static const bool memo_loopvar = getenv("GKGPU_MEMO_LOOPVAR") && atoi(getenv("GKGPU_MEMO_LOOPVAR")) != 0;
           bool skip = varying && !memo_loopvar && !pure_func(rules);
+          // the set rewrites' helpers (rego.cc optimize_sets) take a document
+          // collection as an argument: a memo key nobody else meets
+          skip = skip || name.rfind("__gk_", 0) == 0;
           int slot = nargs >= 1 && nargs <= 2 && !skip ? memo_slot(rules, stmt && !has_out) : -1;
           int Lhit = label();
           uint16_t k1 = nargs == 2 ? (uint16_t)regs[1] : NOREG;

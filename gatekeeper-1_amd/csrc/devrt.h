@@ -292,7 +292,8 @@ static_assert((GK_LDS_MEMO & (GK_LDS_MEMO - 1)) == 0, "GK_LDS_MEMO: a power of t
 __shared__ uint64_t gk_lds_memo[4][GK_LDS_MEMO][4];
 #endif
 #ifndef GK_HOST
-__shared__ unsigned long long gk_lds_chunk[4][3];  // per wave: tuple-slot chunk (slot_reserve)
+__shared__ unsigned long long gk_lds_chunk[4][6];  // per wave: tuple-slot chunk (slot_reserve), byte chunk (bytes_reserve)
+__shared__ uint32_t gk_lds_bscan[4];                // per wave: bytes_reserve's running sum
 #endif
 
 // copies this wave's stage (all 64 lanes, wave-uniform m); the wave's own
@@ -305,7 +306,8 @@ __device__ __forceinline__ void stage_wave(const MatchSpec& m, uint32_t lane) {
   for (uint32_t k = lane; k < GK_LDS_MEMO * 4u; k += 64) (&gk_lds_memo[wv][0][0])[k] = 0;
 #endif
 #ifndef GK_HOST
-  if (lane < 3) gk_lds_chunk[threadIdx.x >> 6][lane] = 0;  // no chunk yet (devrt.h slot_reserve)
+  if (lane < 6) gk_lds_chunk[threadIdx.x >> 6][lane] = 0;  // no chunks yet (devrt.h slot_reserve, bytes_reserve)
+  if (lane == 0) gk_lds_bscan[threadIdx.x >> 6] = 0;
 #endif
 #if GK_LDS_PARAMS
   const uint32_t pn = m.pn <= LDS_PCAP ? m.pn : 0;
@@ -1418,6 +1420,49 @@ __device__ __forceinline__ uint64_t wave_reserve_bytes(unsigned long long* ctr, 
   return (want && n) ? (uint64_t)atomicAdd(ctr, (unsigned long long)n) : 0;
 }
 
+// Staged bytes (ebytes) by per-wavefront chunks, as slot_reserve does for
+// tuples: the slow emission path (details, eager messages) otherwise takes one
+// same-address atomic on counters[1] per wave and site.  The lanes' byte
+// counts are numbered by an LDS atomic (any active-lane subset); the tail of a
+// chunk the next emission does not fit is left unused -- nothing reads
+// ebytes except through a tuple's offsets.  Chunk size: the wave's bytes so
+// far, BCHUNK_MIN .. BCHUNK_MAX.
+constexpr uint64_t BCHUNK_MIN = 512, BCHUNK_MAX = 16384;
+#ifndef GK_BCHUNK
+#define GK_BCHUNK 1  // A/B switch (GKGPU_JIT_PRE=GK_BCHUNK=0: one atomic per wave and site)
+#endif
+__device__ __forceinline__ uint64_t bytes_reserve(bool want, uint32_t n) {
+#if defined(GK_HOST) || !GK_BCHUNK
+  return wave_reserve_bytes(&gk_args.counters[1], want, n);
+#else
+  const uint32_t nn = want ? n : 0u;
+  if (!__ballot(nn != 0)) return 0;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t o = nn ? __hip_atomic_fetch_add(&gk_lds_bscan[wv], nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0u;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const uint64_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(&gk_lds_bscan[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+  unsigned long long* st = gk_lds_chunk[wv] + 3;
+  uint64_t base = st[0], left = st[1];
+  const uint64_t used = st[2];
+  if (tot > left) {
+    uint64_t take = used < BCHUNK_MIN ? BCHUNK_MIN : used > BCHUNK_MAX ? BCHUNK_MAX : used;
+    if (take < tot) take = tot;
+    uint64_t b = 0;
+    if (gk_lanes_below(__ballot(true)) == 0) b = (uint64_t)atomicAdd(&gk_args.counters[1], (unsigned long long)take);
+    base = rfl64(b);
+    left = take;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (gk_lanes_below(__ballot(true)) == 0) {
+    st[0] = base + tot;
+    st[1] = left - tot;
+    st[2] = used + tot;
+    gk_lds_bscan[wv] = 0;
+  }
+  return base + o;
+#endif
+}
+
 // the tuple order key of the lane's next emission; false = over the limits
 __device__ __forceinline__ bool next_seq(PLane& L, uint32_t& seq) {
   const uint32_t en = L.en, ord = L.ord;
@@ -1447,7 +1492,7 @@ __device__ __noinline__ void emit_eager(PLane& L, bool want, uint32_t rule, cons
   if (want) want = next_seq(L, seq);
   const bool detobj = det == nullptr;
   const uint32_t eb = want ? mlen + (detobj ? 0u : dlen) : 0u;
-  const uint64_t eoff = wave_reserve_bytes(&gk_args.counters[1], want, eb);
+  const uint64_t eoff = bytes_reserve(want, eb);
   const uint64_t slot = slot_reserve(want);
   if (!want) return;
   L.en = L.en + 1u;
@@ -2407,7 +2452,7 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
   const uint32_t sb = ok ? (defer ? 0u : ms.n) + (det ? dlen : 0u) : 0u;  // staged bytes
   const uint32_t words = ok ? gw + dw : 0u;                               // copied-out words (8-B aligned)
   const uint32_t eb = sb + (words ? 8u * words + 7u : 0u);
-  const uint64_t eoff = wave_reserve_bytes(&gk_args.counters[1], ok, eb);
+  const uint64_t eoff = bytes_reserve(ok, eb);
   const uint64_t slot = slot_reserve(ok);
   if (!ok) return false;
   L.en = L.en + 1u;

@@ -127,6 +127,17 @@ struct LOut {
   uint32_t pos;
   __device__ __forceinline__ void put(char c) { p[pos++] = (uint8_t)c; }
 };
+// LDS staging of one window [w0, w0 + n) of the output: the printer runs
+// whole, bytes outside the window are dropped (pos: output byte address)
+struct WOut {
+  uint8_t* p;
+  uint64_t w0, pos;
+  uint32_t n;
+  __device__ __forceinline__ void put(char c) {
+    const uint64_t r = pos++ - w0;
+    if (r < n) p[r] = (uint8_t)c;
+  }
+};
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 #pragma unroll
@@ -442,29 +453,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         else if (v.pad & VF_DET_VAL) { if (dl) put_json(L, o, det_word(v, i)); }
         else puts_(o, gk_args.ebytes + v.msg_off + (defer ? 0u : ml), dl);
       };
-      if (hi > lo && hi4 - lo4 <= FSTAGE) {
-        const uint32_t nw = (uint32_t)((hi4 - lo4) >> 2);
-        if (valid && len) {
-          LOut o{stb + (dst - lo4), 0};
-          body(o);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t q = lane; q < nw; q += 64) {
-          const uint64_t ad = lo4 + 4 * (uint64_t)q;
-          if (ad >= lo && ad + 4 <= hi) {
-            gw[(lo4 >> 2) + q] = st[q];
-          } else {
-            for (uint32_t b = 0; b < 4; ++b)
-              if (ad + b >= lo && ad + b < hi) gk_args.bytes[ad + b] = (char)stb[4 * q + b];
+      // the wave's bytes go through LDS in windows of FSTAGE: each lane prints
+      // into the windows its tuple overlaps (one, unless it straddles an edge
+      // or is longer than a window), then the wave writes the window back with
+      // coalesced dword stores (byte stores at the range's two edge dwords)
+      if (hi > lo) {
+        const bool one = hi4 - lo4 <= FSTAGE;
+        for (uint64_t w0 = lo4; w0 < hi4; w0 += FSTAGE) {  // wave-uniform
+          const uint64_t w1 = w0 + FSTAGE < hi4 ? w0 + FSTAGE : hi4;
+          if (valid && len && dst < w1 && dst + len > w0) {
+            if (one) {
+              LOut o{stb + (dst - lo4), 0};
+              body(o);
+            } else {
+              WOut o{stb, w0, dst, (uint32_t)(w1 - w0)};
+              body(o);
+            }
           }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const uint32_t nw = (uint32_t)((w1 - w0) >> 2);
+          for (uint32_t q = lane; q < nw; q += 64) {
+            const uint64_t ad = w0 + 4 * (uint64_t)q;
+            if (ad >= lo && ad + 4 <= hi) {
+              gw[(w0 >> 2) + q] = st[q];
+            } else {
+              for (uint32_t b = 0; b < 4; ++b)
+                if (ad + b >= lo && ad + b < hi) gk_args.bytes[ad + b] = (char)stb[4 * q + b];
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        __builtin_amdgcn_wave_barrier();
-      } else if (valid && len) {
-        GOut g{(uint8_t*)gk_args.bytes, dst, dst, 0, false};
-        body(g);
-        g.finish();
       }
       if (valid) {
         v.msg_off = dst;

@@ -18,6 +18,11 @@ for what in "${@:-c2 c4 c5 cache}"; do
         grep -E "flatten_reviews|intern|relocate" "$OUT/c5t.txt" | tail -8; tail -3 "$OUT/c5t.txt" ;;
     sets) bash tools/gpu_bench_ab.sh "$TAG/sets" "--steps 10 --warmup 2" "" "GKGPU_REGO_SETS=0" || exit 1
           bash tools/gpu_bench_ab.sh "$TAG/sets4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_REGO_SETS=0" || exit 1 ;;
+    bch) bash tools/gpu_bench_ab.sh "$TAG/bch" "--steps 10 --warmup 2" "" "GKGPU_JIT_PRE=GK_BCHUNK=0" "GKGPU_REGO_SETS=3" || exit 1
+         bash tools/gpu_bench_ab.sh "$TAG/bch4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PRE=GK_BCHUNK=0" "GKGPU_REGO_SETS=3" || exit 1 ;;
+    c5pmc) R=$PWD; ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_LDS \
+             -d "$R/$OUT/c5pmc" -o run -- python3 "$R/tools/probe_c5_time.py" 256 ) > "$OUT/c5pmc.log" 2>&1 || { echo C5PMC_FAIL; tail "$OUT/c5pmc.log"; exit 1; }
+           python3 tools/pmc_table.py "$OUT/c5pmc" | tee "$OUT/c5pmc.txt" ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
