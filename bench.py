@@ -42,6 +42,8 @@ def parse():
                          "the queueing")
     ap.add_argument("--clients", type=int, default=64, help="config 5 coalesced: concurrent client threads")
     ap.add_argument("--rate", type=float, default=20000.0, help="config 5 coalesced: offered requests/s (total)")
+    ap.add_argument("--loadgen", choices=("native", "python"), default="native",
+                    help="config 5 coalesced: client threads in C++ (libgkload.so) or Python")
     ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="resources of the staged batch timed on the native CPU baseline (oracle/cpuvm.cc; "
@@ -782,6 +784,8 @@ def webhook_coalesced_main(args, drv, templates, constraints, batches, world, ra
                                       "gk_results_export), queueing included",
                 "launches": launches,
                 "mean_requests_per_launch": served / max(1, launches),
+                "clients": "%s threads (%s)" % (args.clients, "native, gatekeeper-1_amd/csrc/loadgen.cc"
+                                                if args.loadgen == "native" else "Python"),
                 "parallelism": "replicas%d (independent webhook replicas, no collective)" % world,
             },
             "roofline": None,
@@ -841,6 +845,8 @@ def webhook_coalesced(args, drv, inputs, n_cons):
     import threading
     viol = 'hooks["admission.k8s.gatekeeper.sh"].violation'
     n = args.steps * args.batch  # requests
+    if args.loadgen == "native":
+        return webhook_coalesced_native(args, drv, inputs, viol, n)
     per = [n // args.clients + (1 if c < n % args.clients else 0) for c in range(args.clients)]
     gap = args.clients / args.rate  # each client's inter-arrival time
     lat = [[] for _ in range(args.clients)]
@@ -876,6 +882,28 @@ def webhook_coalesced(args, drv, inputs, n_cons):
     b1, r1 = drv.coalesce_stats()
     all_lat = sorted(x for l in lat for x in l)
     return all_lat, elapsed, n, b1 - b0, r1 - r0
+
+
+def webhook_coalesced_native(args, drv, inputs, viol, n):
+    """As webhook_coalesced, the clients being native threads of
+    libgkload.so (gatekeeper-1_amd/csrc/loadgen.cc), C-ABI callers of gk_query
+    + gk_results_export: Python client threads serialize on the interpreter
+    lock and their tail, not the engine's, dominated the latency."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(ROOT, "gatekeeper-1_amd", "gkgpu", "libgkload.so"))
+    lib.gkload_open_loop.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                     C.c_size_t, C.c_int, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    blobs = [b.encode() if isinstance(b, str) else b for b in inputs]
+    arr = (C.c_char_p * len(blobs))(*blobs)
+    lens = (C.c_size_t * len(blobs))(*[len(b) for b in blobs])
+    lat = (C.c_double * n)()
+    el = C.c_double()
+    b0, r0 = drv.coalesce_stats()
+    rc = lib.gkload_open_loop(drv._e, viol.encode(), arr, lens, len(blobs), n, args.clients, args.rate, lat, C.byref(el))
+    if rc:
+        raise RuntimeError("gkload_open_loop: gk status %d" % rc)
+    b1, r1 = drv.coalesce_stats()
+    return sorted(lat), el.value, n, b1 - b0, r1 - r0
 
 
 def webhook_cpu_baseline(templates, constraints, inputs):

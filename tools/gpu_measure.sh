@@ -23,6 +23,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
     c5pmc) R=$PWD; ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_LDS \
              -d "$R/$OUT/c5pmc" -o run -- python3 "$R/tools/probe_c5_time.py" 256 ) > "$OUT/c5pmc.log" 2>&1 || { echo C5PMC_FAIL; tail "$OUT/c5pmc.log"; exit 1; }
            python3 tools/pmc_table.py "$OUT/c5pmc" | tee "$OUT/c5pmc.txt" ;;
+    rememo) bash tools/gpu_bench_ab.sh "$TAG/rememo4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1
+            bash tools/gpu_bench_ab.sh "$TAG/rememo3" "--config 3 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
