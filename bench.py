@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--clients", type=int, default=64, help="config 5 coalesced: concurrent client threads")
     ap.add_argument("--rate", type=float, default=20000.0, help="config 5 coalesced: offered requests/s (total)")
     ap.add_argument("--loadgen", choices=("native", "python"), default="native",
-                    help="config 5 coalesced: client threads in C++ (libgkload.so) or Python")
+                    help="config 5: the timed calls from C++ (libgkload.so) or from Python")
     ap.add_argument("--pods", type=int, default=None, help="resources per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="resources of the staged batch timed on the native CPU baseline (oracle/cpuvm.cc; "
@@ -676,16 +676,40 @@ def webhook_main(args):
     lat = []
     n_results = n_flagged = 0
     blob_bytes = 0
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ts = time.perf_counter()
-        blob, st = drv.query_batch_export(batches[i % nb])
-        lat.append((time.perf_counter() - ts) * 1000.0)
-        blob_bytes += len(blob)
-        n_flagged += sum(1 for x in st if x & 3)
-    elapsed = time.perf_counter() - t0
+    if args.loadgen == "native":
+        # the same calls from C++ (gatekeeper-1_amd/csrc/loadgen.cc
+        # gkload_batch_loop): the request bytes as the webhook receives them,
+        # no Python marshalling inside the timed calls
+        import ctypes as C
+        lib = C.CDLL(os.path.join(ROOT, "gatekeeper-1_amd", "gkgpu", "libgkload.so"))
+        lib.gkload_batch_loop.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                          C.c_size_t, C.c_size_t, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        blobs = [(x if isinstance(x, str) else json.dumps(x)).encode() for b in batches for x in b]
+        arr = (C.c_char_p * len(blobs))(*blobs)
+        lens = (C.c_size_t * len(blobs))(*[len(b) for b in blobs])
+        lt = (C.c_double * args.steps)()
+        rows, nbytes, nfl = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        t0 = time.perf_counter()
+        rc = lib.gkload_batch_loop(drv._e, arr, lens, nb, args.batch, args.steps, lt, C.byref(rows), C.byref(nbytes),
+                                   C.byref(nfl))
+        elapsed = time.perf_counter() - t0
+        if rc:
+            raise RuntimeError("gkload_batch_loop: gk status %d" % rc)
+        lat = list(lt)
+        blob_bytes, n_flagged, n_results = nbytes.value, nfl.value, rows.value
+    else:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ts = time.perf_counter()
+            blob, st = drv.query_batch_export(batches[i % nb])
+            lat.append((time.perf_counter() - ts) * 1000.0)
+            blob_bytes += len(blob)
+            n_flagged += sum(1 for x in st if x & 3)
+        elapsed = time.perf_counter() - t0
     res = drv.query_batch(batches[(args.steps - 1) % nb])
-    n_results = len(res.results) * args.steps
+    if args.loadgen != "native":
+        n_results = len(res.results) * args.steps
     kernel_ms = [ln.ms for ln in res.launches]
     if dist is not None:
         import torch
@@ -728,7 +752,9 @@ def webhook_main(args):
                 "requests_per_s": args.steps * args.batch * world / elapsed,
                 "results_per_launch": n_results / args.steps,
                 "result_bytes_per_launch": blob_bytes / args.steps,
-                "timed": "gk_query_batch + gk_results_export (one bulk copy of the decoded rows) + status words",
+                "timed": "gk_query_batch + gk_results_export (one bulk copy of the decoded rows) + status words, "
+                         + ("called from C++ (gatekeeper-1_amd/csrc/loadgen.cc gkload_batch_loop)"
+                            if args.loadgen == "native" else "called from Python (ctypes)"),
                 "flagged_reviews": n_flagged,
                 "kernel_ms_last_launch": kernel_ms,
                 "parallelism": "replicas%d (independent webhook replicas, no collective)" % world,

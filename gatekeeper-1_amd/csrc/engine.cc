@@ -1971,14 +1971,35 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       res->ms[4] = ms_since(t2);
       return GK_OK;
     }
-    // deterministic order: review, autoreject first, constraint order, emission order
-    std::sort(vs.begin(), vs.end(), [](const Viol& x, const Viol& y) {
-      if (x.review != y.review) return x.review < y.review;
+    // deterministic order: review, autoreject first, constraint order, emission
+    // order -- a counting pass by review, then each review's few rows sorted
+    auto within = [](const Viol& x, const Viol& y) {
       bool ax = x.rule == RULE_AUTOREJECT, ay = y.rule == RULE_AUTOREJECT;
       if (ax != ay) return ax;
       if (x.constraint != y.constraint) return x.constraint < y.constraint;
       return x.seq < y.seq;
-    });
+    };
+    {
+      const size_t nr = res->status.size();
+      bool in_range = true;
+      for (auto& v : vs) in_range = in_range && v.review < nr;
+      if (in_range && nr && vs.size() > 64) {
+        std::vector<uint32_t> at(nr + 1, 0);
+        for (auto& v : vs) at[v.review + 1]++;
+        for (size_t r = 0; r < nr; ++r) at[r + 1] += at[r];
+        std::vector<Viol> sorted(vs.size());
+        std::vector<uint32_t> put(at.begin(), at.end() - 1);
+        for (auto& v : vs) sorted[put[v.review]++] = v;
+        for (size_t r = 0; r < nr; ++r)
+          if (at[r + 1] - at[r] > 1) std::sort(sorted.begin() + at[r], sorted.begin() + at[r + 1], within);
+        vs.swap(sorted);
+      } else {
+        std::sort(vs.begin(), vs.end(), [&](const Viol& x, const Viol& y) {
+          if (x.review != y.review) return x.review < y.review;
+          return within(x, y);
+        });
+      }
+    }
     auto rb = std::make_shared<std::string>(std::move(bytes));
     res->rbytes = rb;
     const char* bp = rb->data();

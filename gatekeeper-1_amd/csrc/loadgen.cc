@@ -90,3 +90,45 @@ extern "C" int gkload_open_loop(gk_engine* e, const char* path, const char* cons
   if (elapsed_s) *elapsed_s = last - t0;
   return err.load();
 }
+
+// Closed-loop micro-batches (bench.py --config 5): `steps` gk_query_batch
+// calls over the batches in turn (batch b = inputs[b * batch .. +batch)), each
+// followed by gk_results_export of every row into one caller buffer and the
+// per-review status words, as a native webhook replica reads them.  lat_ms:
+// per call; rows / bytes (optional): totals over the calls.
+extern "C" int gkload_batch_loop(gk_engine* e, const char* const* inputs, const size_t* lens, size_t n_batches,
+                                 size_t batch, size_t steps, double* lat_ms, uint64_t* rows, uint64_t* bytes,
+                                 uint64_t* flagged) {
+  if (!e || !inputs || !lens || !n_batches || !batch || !lat_ms) return GK_EINVAL;
+  std::vector<char> buf(1 << 20);
+  std::vector<uint32_t> st(batch);
+  uint64_t nrow = 0, nbytes = 0, nflag = 0;
+  for (size_t s = 0; s < steps; ++s) {
+    const size_t b = s % n_batches;
+    const double t0 = now_s();
+    gk_results* r = nullptr;
+    int rc = gk_query_batch(e, inputs + b * batch, lens + b * batch, batch, &r);
+    size_t need = 0;
+    if (rc == GK_OK) {
+      rc = gk_results_export(r, buf.data(), buf.size(), &need);
+      if (rc != GK_OK && need > buf.size()) {
+        buf.resize(need);
+        rc = gk_results_export(r, buf.data(), buf.size(), &need);
+      }
+    }
+    if (rc == GK_OK) rc = gk_results_copy_status(r, st.data(), nullptr);
+    const double t1 = now_s();
+    if (rc == GK_OK) {
+      nrow += gk_results_count(r);
+      for (uint32_t x : st) nflag += (x & 3) != 0;
+    }
+    if (r) gk_results_free(r);
+    if (rc != GK_OK) return rc;
+    lat_ms[s] = (t1 - t0) * 1e3;
+    nbytes += need;
+  }
+  if (rows) *rows = nrow;
+  if (bytes) *bytes = nbytes;
+  if (flagged) *flagged = nflag;
+  return GK_OK;
+}

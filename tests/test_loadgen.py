@@ -65,3 +65,35 @@ def test_loadgen_coalesced_calls_succeed():
     assert all(x >= 0 for x in lat) and el > 0
     assert r1 - r0 == 256 and b1 - b0 < 256
     d.close()
+
+
+def _batch_loop(drv, inputs, batch, steps):
+    lib = _lib()
+    lib.gkload_batch_loop.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                      C.c_size_t, C.c_size_t, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    blobs = [(x if isinstance(x, str) else json.dumps(x)).encode() for x in inputs]
+    arr = (C.c_char_p * len(blobs))(*blobs)
+    lens = (C.c_size_t * len(blobs))(*[len(b) for b in blobs])
+    lat = (C.c_double * steps)()
+    rows, nb, fl = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    rc = lib.gkload_batch_loop(drv._e, arr, lens, len(blobs) // batch, batch, steps, lat, C.byref(rows), C.byref(nb),
+                               C.byref(fl))
+    return rc, list(lat), rows.value, nb.value, fl.value
+
+
+def test_batch_loop_reports_failures():
+    d, ins = _driver(host_only=True)
+    rc, _lat, _r, _b, _f = _batch_loop(d, ins, 16, 2)
+    assert rc != 0
+    d.close()
+
+
+@pytest.mark.gpu
+def test_batch_loop_rows_equal_query_batch():
+    d, ins = _driver()
+    rc, lat, rows, nbytes, fl = _batch_loop(d, ins, 16, 4)
+    assert rc == 0 and all(x > 0 for x in lat) and fl == 0
+    want = len(d.query_batch(ins[:16]).results) + len(d.query_batch(ins[16:32]).results)
+    assert rows == 2 * want and nbytes > 0
+    d.close()
