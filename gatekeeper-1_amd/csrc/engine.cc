@@ -212,6 +212,50 @@ struct ResultRow {
   std::string_view msg, details;
 };
 
+// Pinned host blocks for decoded result bytes: the readback copies the
+// message bytes straight into a block the results then own (their rows view
+// it), and freeing the results returns it here.  Process-wide and never torn
+// down (a block may be released after its engine is gone; HIP may already be
+// unloading at exit).
+struct PinPool {
+  std::mutex mu;
+  std::vector<std::pair<size_t, char*>> free_;  // (capacity, block)
+};
+static PinPool& pin_pool() {
+  static PinPool* p = new PinPool();
+  return *p;
+}
+// a block of at least n bytes, owned by the returned handle; nullptr on failure
+static std::shared_ptr<const void> pinned_block(size_t n, char** out) {
+  PinPool& pp = pin_pool();
+  char* blk = nullptr;
+  size_t cap = 0;
+  {
+    std::lock_guard<std::mutex> g(pp.mu);
+    size_t best = pp.free_.size();
+    for (size_t i = 0; i < pp.free_.size(); ++i)
+      if (pp.free_[i].first >= n && pp.free_[i].first <= 4 * n + (1 << 16) &&
+          (best == pp.free_.size() || pp.free_[i].first < pp.free_[best].first))
+        best = i;
+    if (best < pp.free_.size()) {
+      cap = pp.free_[best].first;
+      blk = pp.free_[best].second;
+      pp.free_.erase(pp.free_.begin() + best);
+    }
+  }
+  if (!blk) {
+    cap = std::max<size_t>(n + (n >> 2), 1 << 16);
+    if (hipHostMalloc((void**)&blk, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+  }
+  *out = blk;
+  return std::shared_ptr<const void>(blk, [cap](const void* q) {
+    PinPool& pp = pin_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    if (pp.free_.size() < 16) pp.free_.emplace_back(cap, (char*)q);
+    else (void)hipHostFree((void*)q);
+  });
+}
+
 // One evaluation's device state: its stream, its launch events and every
 // buffer a call writes (review columns and documents of a query, output
 // tuples and bytes, flags, totals, sampling).  Concurrent evaluations
@@ -282,7 +326,7 @@ struct EvalCtx {
 
 struct gk_results {
   std::vector<gk::ResultRow> rows;
-  std::shared_ptr<const std::string> rbytes;  // the bytes rows view
+  std::shared_ptr<const void> rbytes;  // the bytes rows view (a std::string or a pinned block)
   std::vector<uint32_t> status, reason;  // empty when no review was flagged (all zero)
   uint32_t nrev = 0;
   std::vector<uint64_t> totals;
@@ -1932,26 +1976,32 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       return GK_OK;
     }
     std::vector<Viol> vs(counters[0]);
-    std::string bytes;
+    std::shared_ptr<const void> rb;  // the message bytes the rows view
+    const char* bp = nullptr;
     {
-      // tuples and (decoding) message bytes: two copies into the pinned
-      // buffer, one wait (a large output goes through pageable copies: no
-      // pinned buffer of its size is kept)
+      // tuples into the context's pinned buffer and (decoding) message bytes
+      // into a pinned block the results keep: two copies, one wait, no host
+      // copy of the bytes (a large output goes through pageable copies)
       const size_t tb = counters[0] * sizeof(Viol), bb = decode ? counters[3] : 0;
-      char* hq = tb + bb <= ((size_t)64 << 20) ? x->pin(tb + bb) : nullptr;
-      if (hq) {
+      char* hq = tb <= ((size_t)64 << 20) ? x->pin(tb) : nullptr;
+      char* hb = nullptr;
+      if (hq && bb && bb <= ((size_t)64 << 20)) rb = pinned_block(bb, &hb);
+      if (hq && (!bb || hb)) {
         bool cok = true;
         if (tb) cok = hipMemcpyAsync(hq, x->d_out.p, tb, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
-        if (bb && cok) cok = hipMemcpyAsync(hq + tb, x->d_bytes.p, bb, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
+        if (bb && cok) cok = hipMemcpyAsync(hb, x->d_bytes.p, bb, hipMemcpyDeviceToHost, x->stream) == hipSuccess;
         if (!cok || ((tb || bb) && hipStreamSynchronize(x->stream) != hipSuccess))
           return fail(e, GK_EDEVICE, "result download failed");
         if (tb) memcpy(vs.data(), hq, tb);
-        if (decode) bytes.assign(hq + tb, bb);
+        bp = hb;
       } else {
+        rb.reset();
         if (tb) d2h(x, vs.data(), x->d_out.p, tb);
         if (decode) {
-          bytes.assign(bb, '\0');
-          if (bb) d2h(x, &bytes[0], x->d_bytes.p, bb);
+          auto bytes = std::make_shared<std::string>(bb, '\0');
+          if (bb) d2h(x, &(*bytes)[0], x->d_bytes.p, bb);
+          bp = bytes->data();
+          rb = bytes;
         }
       }
     }
@@ -2000,9 +2050,8 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
         });
       }
     }
-    auto rb = std::make_shared<std::string>(std::move(bytes));
     res->rbytes = rb;
-    const char* bp = rb->data();
+    if (!bp) bp = "";
     res->rows.reserve(vs.size());
     for (auto& v : vs) {
       if (res->status[v.review] & (GK_REVIEW_ERROR | GK_REVIEW_FALLBACK)) continue;
