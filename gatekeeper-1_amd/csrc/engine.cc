@@ -2824,22 +2824,27 @@ static bool batch_upload_layout(gk_engine* e, gk_batch* b, const DevLayout& dl) 
   if (!docs || !nrev || b->cols.size() != nrev || dl.evalpos.size() != nrev || dl.root_d.size() != nrev ||
       dl.slot.size() != nrev)
     return batch_upload(e, b);
+  const auto t0 = Clock::now();
   if (!b->d_nodes.reserve((perm + docs + 1) * sizeof(Node))) return false;
   if (perm && (hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess ||
                hipStreamSynchronize(nullptr) != hipSuccess))
     return false;
+  const double ms_nodes = ms_since(t0);
   DBuf dD, dbeg, deval, droot, dslot;
   bool ok = dD.reserve(docs * sizeof(Node)) && dbeg.reserve(nrev * 4) && deval.reserve(nrev * 4) &&
             droot.reserve(nrev * 4) && dslot.reserve(nrev * 4);
+  const double ms_scratch = ms_since(t0);
   const size_t bytes = docs * sizeof(Node);
   const char* bm = getenv("GKGPU_BOUNCE_MIN");
   const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
   if (ok) ok = bytes >= bounce_min ? upload_bounce(dD.p, (const char*)b->arena.data(), bytes)
                                    : hipMemcpy(dD.p, b->arena.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
+  const double ms_up = ms_since(t0);
   ok = ok && hipMemcpy(dbeg.p, dl.beg.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(deval.p, dl.evalpos.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(droot.p, dl.root_d.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(dslot.p, dl.slot.data(), nrev * 4, hipMemcpyHostToDevice) == hipSuccess;
+  const double ms_small = ms_since(t0);
   hipStream_t st = nullptr;
   uint64_t nout = 0;
   if (ok) ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
@@ -2848,7 +2853,11 @@ static bool batch_upload_layout(gk_engine* e, gk_batch* b, const DevLayout& dl) 
                           (const uint32_t*)droot.p, (const uint32_t*)dslot.p, nrev, dl.nroots,
                           (Node*)b->d_nodes.p + perm, (ReviewCol*)b->d_revs.p, nrev, &nout, st) == 0;
   if (st) hipStreamDestroy(st);
+  const double ms_layout = ms_since(t0);
   for (DBuf* x : {&dD, &dbeg, &deval, &droot, &dslot}) x->free_();
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "upload layout: node buffer %.1f ms, scratch %.1f ms, upload %.1f ms, tables %.1f ms, layout %.1f ms, free %.1f ms\n",
+            ms_nodes, ms_scratch - ms_nodes, ms_up - ms_scratch, ms_small - ms_up, ms_layout - ms_small, ms_since(t0) - ms_layout);
   if (!ok) return false;
   b->d_nodes.used = (perm + docs) * sizeof(Node);
   b->device_layout = true;
