@@ -612,9 +612,10 @@ static void rebuild_modules(gk_engine* e) {
     // the frameworks hooks + target library are served natively
     if (!m->pkg.empty() && m->pkg[0] == "hooks") continue;
     // GKGPU_REGO_SETS: set-algebra rewrites (rego.cc), a mask of the two
-    // patterns; default 2 (the comprehension form: the __gk_anyin call form
-    // measured 0.07 ms slower on K8sRequiredProbes, profiles/r04/r04w_*)
-    if (const int sets = env_mode("GKGPU_REGO_SETS", 2, 3)) rego::optimize_sets(*m, sets);
+    // patterns, both on by default (profiles/r04/r04x_ab.txt: config 4
+    // 1,582 -> 1,656 M evals/s against the comprehension form alone, whose
+    // per-(container, probe) list made K8sRequiredProbes 1.86 -> 2.49 ms)
+    if (const int sets = env_mode("GKGPU_REGO_SETS", 3, 3)) rego::optimize_sets(*m, sets);
     e->mods.add(m);
     parsed.push_back(m);
   }

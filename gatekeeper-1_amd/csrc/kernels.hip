@@ -131,11 +131,11 @@ struct LOut {
 // whole, bytes outside the window are dropped (pos: output byte address)
 struct WOut {
   uint8_t* p;
-  uint64_t w0, pos;
+  int64_t rel;  // the next byte's offset from the window's start
   uint32_t n;
   __device__ __forceinline__ void put(char c) {
-    const uint64_t r = pos++ - w0;
-    if (r < n) p[r] = (uint8_t)c;
+    if ((uint64_t)rel < n) p[rel] = (uint8_t)c;
+    ++rel;
   }
 };
 
@@ -393,10 +393,13 @@ __global__ void __launch_bounds__(256) gk_compact_scatter(const Viol* raw, const
   }
 }
 
-constexpr uint32_t FSTAGE = 8192;  // LDS bytes per wavefront
+// LDS bytes per wavefront (dynamic shared memory, 4 waves per block): 8 KB
+// for a sweep's output (occupancy), 16 KB for a micro-batch's, whose messages
+// are long enough that 64 tuples overflow 8 KB (config 5: ~160 B per tuple)
+constexpr uint32_t FSTAGE = 8192, FSTAGE_SMALL = 16384;
+extern __shared__ uint32_t gk_fmt_stage[];
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(DevArgs) {
-  __shared__ uint32_t stage[4][FSTAGE / 4];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(uint32_t fstage, DevArgs) {
   __shared__ uint32_t wtot[4];
   const uint64_t n = ntuples();
   // an overflowed output buffer: the host grows it and runs the passes again
@@ -406,7 +409,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
     return;
   PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* st = stage[wv];
+  uint32_t* st = gk_fmt_stage + wv * (fstage / 4);
   uint8_t* stb = (uint8_t*)st;
   uint32_t* gw = (uint32_t*)gk_args.bytes;
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
@@ -458,15 +461,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       // or is longer than a window), then the wave writes the window back with
       // coalesced dword stores (byte stores at the range's two edge dwords)
       if (hi > lo) {
-        const bool one = hi4 - lo4 <= FSTAGE;
-        for (uint64_t w0 = lo4; w0 < hi4; w0 += FSTAGE) {  // wave-uniform
-          const uint64_t w1 = w0 + FSTAGE < hi4 ? w0 + FSTAGE : hi4;
+        const bool one = hi4 - lo4 <= fstage;
+        for (uint64_t w0 = lo4; w0 < hi4; w0 += fstage) {  // wave-uniform
+          const uint64_t w1 = w0 + fstage < hi4 ? w0 + fstage : hi4;
           if (valid && len && dst < w1 && dst + len > w0) {
             if (one) {
               LOut o{stb + (dst - lo4), 0};
               body(o);
             } else {
-              WOut o{stb, w0, dst, (uint32_t)(w1 - w0)};
+              WOut o{stb, (int64_t)(dst - w0), (uint32_t)(w1 - w0)};
               body(o);
             }
           }
@@ -515,7 +518,8 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
-  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 0, stream, *a);
+  const uint32_t fstage = hint && hint <= 65536 ? gk::FSTAGE_SMALL : gk::FSTAGE;
+  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
   if (ev) hipEventRecord(ev[2], stream);
   return (int)hipGetLastError();
 }

@@ -15,9 +15,7 @@ ROOT=$PWD
 OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 # template-kernel code objects: the tree's .jitcache plus new ones under gpurun_out/
-mkdir -p "$ROOT/gpurun_out/jitcache"
-cp -n "$ROOT"/.jitcache/*.co "$ROOT/gpurun_out/jitcache/" 2>/dev/null || true
-export GKGPU_JIT_CACHE=$ROOT/gpurun_out/jitcache
+if [ -z "$GKGPU_JIT_CACHE" ]; then mkdir -p /tmp/gkjit_cache; cp -n "$ROOT"/.jitcache/*.co /tmp/gkjit_cache/ 2>/dev/null || true; export GKGPU_JIT_CACHE=/tmp/gkjit_cache; fi
 cd /tmp && export TMPDIR=/tmp
 # GPU clocks around the run (box-to-box variance: compare only inside one call)
 rocm-smi --showclocks > "$OUT/clocks_before.txt" 2>&1 || true

@@ -8,9 +8,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; BARGS=$2; shift 2
 OUT=gpurun_out/$TAG
-mkdir -p "$OUT" gpurun_out/jitcache
-cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
-export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+mkdir -p "$OUT"
+# (gpu_measure.sh / gpu_final.sh set GKGPU_JIT_CACHE; standalone: seeded from .jitcache)
+if [ -z "$GKGPU_JIT_CACHE" ]; then mkdir -p /tmp/gkjit_cache; cp -n .jitcache/*.co /tmp/gkjit_cache/ 2>/dev/null || true; export GKGPU_JIT_CACHE=/tmp/gkjit_cache; fi
 i=0
 for s in "$@"; do
   i=$((i+1))

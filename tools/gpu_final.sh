@@ -8,9 +8,21 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; PART=$2
 OUT=gpurun_out/$TAG
-mkdir -p "$OUT" gpurun_out/jitcache
-cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
-export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+mkdir -p "$OUT"
+# template-kernel code objects: a cache outside gpurun_out/ seeded with the
+# tree's .jitcache (A/B variants compile many kernels; gpurun pulls back at
+# most 64 MiB), the new ones copied back to gpurun_out/jitcache_new at exit
+JC=${GKGPU_JIT_CACHE:-/tmp/gkjit_cache}
+mkdir -p "$JC"
+cp -n .jitcache/*.co "$JC/" 2>/dev/null || true
+export GKGPU_JIT_CACHE=$JC
+jit_pull() {
+  local new=() f sz=0
+  for f in "$JC"/*.co; do [ -e ".jitcache/$(basename "$f")" ] || { new+=("$f"); sz=$((sz + $(stat -c %s "$f"))); }; done
+  if [ ${#new[@]} -gt 0 ] && [ $sz -lt 40000000 ]; then mkdir -p gpurun_out/jitcache_new && cp -n "${new[@]}" gpurun_out/jitcache_new/; fi
+  echo "jit cache: ${#new[@]} new code objects, $sz bytes"
+}
+trap jit_pull EXIT
 if [ "$PART" = a ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; tail -3 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1

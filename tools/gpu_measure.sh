@@ -7,9 +7,21 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r04m}; shift
 OUT=gpurun_out/$TAG
-mkdir -p "$OUT" gpurun_out/jitcache
-cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
-export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+mkdir -p "$OUT"
+# template-kernel code objects: a cache outside gpurun_out/ seeded with the
+# tree's .jitcache (A/B variants compile many kernels; gpurun pulls back at
+# most 64 MiB), the new ones copied back to gpurun_out/jitcache_new at exit
+JC=${GKGPU_JIT_CACHE:-/tmp/gkjit_cache}
+mkdir -p "$JC"
+cp -n .jitcache/*.co "$JC/" 2>/dev/null || true
+export GKGPU_JIT_CACHE=$JC
+jit_pull() {
+  local new=() f sz=0
+  for f in "$JC"/*.co; do [ -e ".jitcache/$(basename "$f")" ] || { new+=("$f"); sz=$((sz + $(stat -c %s "$f"))); }; done
+  if [ ${#new[@]} -gt 0 ] && [ $sz -lt 40000000 ]; then mkdir -p gpurun_out/jitcache_new && cp -n "${new[@]}" gpurun_out/jitcache_new/; fi
+  echo "jit cache: ${#new[@]} new code objects, $sz bytes"
+}
+trap jit_pull EXIT
 for what in "${@:-c2 c4 c5 cache}"; do
   case $what in
     c2) bash tools/gpu_bench_ab.sh "$TAG/c2" "--steps 10 --warmup 2" "" "GKGPU_CONCURRENT=0" \
@@ -22,7 +34,7 @@ for what in "${@:-c2 c4 c5 cache}"; do
          bash tools/gpu_bench_ab.sh "$TAG/bch4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PRE=GK_BCHUNK=0" "GKGPU_REGO_SETS=3" || exit 1 ;;
     c5pmc) R=$PWD; ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_LDS \
              -d "$R/$OUT/c5pmc" -o run -- python3 "$R/tools/probe_c5_time.py" 256 ) > "$OUT/c5pmc.log" 2>&1 || { echo C5PMC_FAIL; tail "$OUT/c5pmc.log"; exit 1; }
-           python3 tools/pmc_table.py "$OUT/c5pmc" | tee "$OUT/c5pmc.txt" ;;
+           python3 tools/pmc_table.py "$OUT/c5pmc" | tee "$OUT/c5pmc.txt"; rm -rf "$OUT/c5pmc" ;;
     rememo) bash tools/gpu_bench_ab.sh "$TAG/rememo4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1
             bash tools/gpu_bench_ab.sh "$TAG/rememo3" "--config 3 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?

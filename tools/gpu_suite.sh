@@ -7,9 +7,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; PROF=$2; shift 2
 OUT=gpurun_out/$TAG
-mkdir -p "$OUT" gpurun_out/jitcache
-cp -n .jitcache/*.co gpurun_out/jitcache/ 2>/dev/null || true
-export GKGPU_JIT_CACHE=$PWD/gpurun_out/jitcache
+mkdir -p "$OUT"
+# (gpu_measure.sh / gpu_final.sh set GKGPU_JIT_CACHE; standalone: seeded from .jitcache)
+if [ -z "$GKGPU_JIT_CACHE" ]; then mkdir -p /tmp/gkjit_cache; cp -n .jitcache/*.co /tmp/gkjit_cache/ 2>/dev/null || true; export GKGPU_JIT_CACHE=/tmp/gkjit_cache; fi
 DESEL=()
 if [ $# -gt 0 ]; then
   timeout -k 10 600 python -u -m pytest "$@" -m gpu -v -s --timeout 300 --timeout-method thread > "$OUT/pytest_first.log" 2>&1

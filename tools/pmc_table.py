@@ -1,29 +1,25 @@
-"""Per-kernel averages of the counters of a rocprofv3 --pmc run (the
-*_counter_collection.csv files under a directory): one line per kernel with
-its dispatch count and each counter's mean per dispatch.
+"""Per-kernel means of the counters of a rocprofv3 --pmc run (the
+run_results.db under a directory, view counters_collection): one line per
+kernel with its dispatch count and each counter's mean per dispatch.
     python tools/pmc_table.py gpurun_out/<tag>/c5pmc"""
 import collections
-import csv
 import glob
 import os
+import sqlite3
 import sys
 
 
 def main(d):
-    acc = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                k = row.get("Kernel_Name", "?")
-                k = k if len(k) < 40 else k[:40]
-                disp[k].add((f, row.get("Dispatch_Id")))
-                acc[k][row.get("Counter_Name", "?")] += float(row.get("Counter_Value", 0) or 0)
-    names = sorted({c for v in acc.values() for c in v})
-    print("%-40s %6s " % ("kernel", "disp") + " ".join("%14s" % c for c in names))
-    for k in sorted(acc, key=lambda k: -len(disp[k])):
-        n = len(disp[k])
-        print("%-40s %6d " % (k, n) + " ".join("%14.0f" % (acc[k][c] / n) for c in names))
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+        c = sqlite3.connect(f)
+        for k, name, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
+            acc[k.split("(")[0].strip()[:40]][name].append(float(v))
+    names = sorted({n for v in acc.values() for n in v})
+    print("%-40s %6s " % ("kernel", "disp") + " ".join("%14s" % n[:14] for n in names))
+    for k in sorted(acc, key=lambda k: -max(len(x) for x in acc[k].values())):
+        n = max(len(x) for x in acc[k].values())
+        print("%-40s %6d " % (k, n) + " ".join("%14.0f" % (sum(acc[k][c]) / max(1, len(acc[k][c]))) for c in names))
 
 
 if __name__ == "__main__":
