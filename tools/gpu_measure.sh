@@ -37,6 +37,10 @@ for what in "${@:-c2 c4 c5 cache}"; do
            python3 tools/pmc_table.py "$OUT/c5pmc" | tee "$OUT/c5pmc.txt"; rm -rf "$OUT/c5pmc" ;;
     rememo) bash tools/gpu_bench_ab.sh "$TAG/rememo4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1
             bash tools/gpu_bench_ab.sh "$TAG/rememo3" "--config 3 --steps 5 --warmup 1" "" "GKGPU_RE_MEMO=0" || exit 1 ;;
+    c5c) for r in 20000 40000; do
+           timeout -k 10 300 python -u bench.py --config 5 --coalesce-us 300 --rate $r --steps 400 --cpu-sample 0 > "$OUT/c5c_$r.json" 2> "$OUT/c5c_$r.err" || { echo C5C_FAIL; tail "$OUT/c5c_$r.err"; exit 1; }
+           python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C5COAL', sys.argv[2], round(c['requests_per_s']), 'req/s', {k: round(v, 3) for k, v in c['latency_ms'].items()}, round(c['mean_requests_per_launch'], 1))" "$OUT/c5c_$r.json" $r
+         done ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
