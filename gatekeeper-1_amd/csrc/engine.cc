@@ -75,23 +75,45 @@ static int env_mode(const char* name, int def, int max) {
 // one while the DMA engine reads chunk k from the other.  A pageable
 // hipMemcpy of the same bytes runs at a fraction of the link rate.
 // GKGPU_PINNED_UPLOAD=0 keeps the plain hipMemcpy (A/B).
-static bool upload_bounce(void* dst, const char* src, size_t n) {
-  constexpr size_t CH = 64ull << 20;
-  static std::mutex mu;
-  static char* pin[2] = {nullptr, nullptr};
-  static hipStream_t st = nullptr;
-  static hipEvent_t ev[2] = {nullptr, nullptr};
-  static bool pending[2] = {false, false};  // a copy out of pin[b] may still be in flight
-  static int ok = -1;
-  std::lock_guard<std::mutex> g(mu);
-  if (ok < 0) {
-    ok = env_mode("GKGPU_PINNED_UPLOAD", 1, 1) != 0 && hipHostMalloc((void**)&pin[0], CH, hipHostMallocDefault) == hipSuccess &&
-         hipHostMalloc((void**)&pin[1], CH, hipHostMallocDefault) == hipSuccess &&
-         hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+// the pinned bounce buffers, their stream and events: set up once per process
+// (gk_engine_prepare does it ahead of the first staging: page-locking 128 MB
+// is not part of a sweep)
+struct Bounce {
+  static constexpr size_t CH = 64ull << 20;
+  std::mutex mu;
+  char* pin[2] = {nullptr, nullptr};
+  hipStream_t st = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};  // a copy out of pin[b] may still be in flight
+  int ok = -1;
+  bool init_locked() {
+    if (ok < 0)
+      ok = env_mode("GKGPU_PINNED_UPLOAD", 1, 1) != 0 && hipHostMalloc((void**)&pin[0], CH, hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&pin[1], CH, hipHostMallocDefault) == hipSuccess &&
+           hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+    return ok > 0;
   }
-  if (!ok) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess;
+};
+static Bounce& bounce() {
+  static Bounce* b = new Bounce();
+  return *b;
+}
+static void upload_bounce_init() {
+  Bounce& B = bounce();
+  std::lock_guard<std::mutex> g(B.mu);
+  B.init_locked();
+}
+static bool upload_bounce(void* dst, const char* src, size_t n) {
+  Bounce& B = bounce();
+  constexpr size_t CH = Bounce::CH;
+  char** pin = B.pin;
+  hipStream_t& st = B.st;
+  hipEvent_t* ev = B.ev;
+  bool* pending = B.pending;
+  std::lock_guard<std::mutex> g(B.mu);
+  if (!B.init_locked()) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess;
   const int T = std::max(1, std::min(16, default_threads()));
   const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
   // GKGPU_BOUNCE_CHUNK (tests): a smaller chunk, to exercise many chunks
@@ -3189,7 +3211,14 @@ int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double
 int gk_engine_prepare(gk_engine* e, int device) {
   if (!e) return GK_EINVAL;
   ReadLock rl;
-  return read_lock(e, rl, device != 0 && !e->host_only);
+  const int rc = read_lock(e, rl, device != 0 && !e->host_only);
+  if (rc == GK_OK && device != 0 && !e->host_only && e->dev_ok) {
+    // staging's process-wide resources: the pinned upload buffers and the
+    // host worker pool
+    upload_bounce_init();
+    parallel_run(default_threads(), [](int) {});
+  }
+  return rc;
 }
 
 int gk_template_backend(gk_engine* e, const char* kind, int* backend, const char** detail) {
