@@ -582,29 +582,14 @@ __device__ __forceinline__ uint32_t sample_bucket(uint32_t review, uint32_t nrev
   return (uint32_t)(((uint64_t)review * nb) / nrev);
 }
 
-// A wave's 64 consecutive tuples mostly fall in one or two (constraint,
-// bucket) cells (a wave's reviews are consecutive): the lanes of each distinct
-// cell add once, through their first lane, instead of 64 same-address atomics.
+// (one atomic per tuple: aggregating a wave's lanes per distinct cell with
+// ballots measured slower, profiles/r04/r04x_ab.txt gk_sample 0.38 -> 0.47 ms)
 __global__ void __launch_bounds__(256) gk_sample_hist(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
                                                       uint32_t nb, uint32_t* hist) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    bool want = false;
-    uint64_t cell = 0;
-    if (i < n) {
-      const Viol v = out[i];
-      want = !(rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK)));
-      cell = (uint64_t)v.constraint * nb + sample_bucket(v.review, nrev, nb);
-    }
-    uint64_t left = __ballot(want);
-    while (left) {
-      const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
-      const uint64_t lc = __shfl(cell, (int)lead, 64);
-      const uint64_t peers = __ballot(want && cell == lc) & left;
-      if ((threadIdx.x & 63) == lead) atomicAdd(&hist[lc], (uint32_t)__popcll(peers));
-      left &= ~peers;
-    }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Viol v = out[i];
+    if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
+    atomicAdd(&hist[(uint64_t)v.constraint * nb + sample_bucket(v.review, nrev, nb)], 1u);
   }
 }
 
