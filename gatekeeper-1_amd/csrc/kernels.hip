@@ -127,6 +127,8 @@ struct LOut {
   uint32_t pos;
   __device__ __forceinline__ void put(char c) { p[pos++] = (uint8_t)c; }
 };
+// LOut whose string sources are read in 16-B blocks (puts_wide below)
+struct LOutW : LOut {};
 // LDS staging of one window [w0, w0 + n) of the output: the printer runs
 // whole, bytes outside the window are dropped (pos: output byte address)
 struct WOut {
@@ -138,6 +140,26 @@ struct WOut {
     ++rel;
   }
 };
+
+// The format pass's byte sources (string pool, memo strings, staged bytes)
+// read in aligned 16-B blocks: the printers are chains of dependent loads,
+// and a dword at a time made a 60-byte message ~15 round trips.  An
+// aligned block that holds one byte of the string never leaves its page, so
+// reading the whole block is always in bounds.
+template <class O> __device__ __forceinline__ void puts_wide(O& o, const char* s, uint32_t n) {
+  if (!n) return;
+  const uint64_t a = (uint64_t)s, e = a + n;
+  uint32_t k = (uint32_t)(a & 15);
+  for (uint64_t b = a & ~(uint64_t)15; b < e; b += 16, k = 0) {
+    const uint4 q = *(const uint4*)b;
+    const uint32_t lim = b + 16 <= e ? 16u : (uint32_t)(e - b);
+    for (; k < lim; ++k) {
+      const uint32_t w = k < 8 ? (k < 4 ? q.x : q.y) : (k < 12 ? q.z : q.w);
+      o.put((char)(w >> (8 * (k & 3))));
+    }
+  }
+}
+__device__ __forceinline__ void puts_(LOutW& o, const char* s, uint32_t n) { puts_wide(o, s, n); }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 #pragma unroll
@@ -399,6 +421,7 @@ __global__ void __launch_bounds__(256) gk_compact_scatter(const Viol* raw, const
 constexpr uint32_t FSTAGE = 8192, FSTAGE_SMALL = 16384;
 extern __shared__ uint32_t gk_fmt_stage[];
 
+template <class LO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(uint32_t fstage, DevArgs) {
   __shared__ uint32_t wtot[4];
   const uint64_t n = ntuples();
@@ -466,7 +489,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
           const uint64_t w1 = w0 + fstage < hi4 ? w0 + fstage : hi4;
           if (valid && len && dst < w1 && dst + len > w0) {
             if (one) {
-              LOut o{stb + (dst - lo4), 0};
+              LO o;
+              o.p = stb + (dst - lo4);
+              o.pos = 0;
               body(o);
             } else {
               WOut o{stb, (int64_t)(dst - w0), (uint32_t)(w1 - w0)};
@@ -519,7 +544,10 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
   const uint32_t fstage = hint && hint <= 65536 ? gk::FSTAGE_SMALL : gk::FSTAGE;
-  hipLaunchKernelGGL(gk::gk_format_kernel, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
+  // GKGPU_FMT_WIDE (A/B switch, default on): 16-B source reads in the printers
+  static const bool wide = !getenv("GKGPU_FMT_WIDE") || atoi(getenv("GKGPU_FMT_WIDE")) != 0;
+  if (wide) hipLaunchKernelGGL(gk::gk_format_kernel<gk::LOutW>, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
+  else hipLaunchKernelGGL(gk::gk_format_kernel<gk::LOut>, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
   if (ev) hipEventRecord(ev[2], stream);
   return (int)hipGetLastError();
 }

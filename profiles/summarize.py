@@ -49,7 +49,7 @@ def traffic(d, bench):
     fetch = counter(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
     write = counter(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
     for k in fetch:
-        if k.endswith("gk_format_kernel"):
+        if k.endswith("gk_format_kernel") or "gk_format_kernel<" in k:
             kt[k] = "gk_format_kernel"
     cfg = bench["config"].get("workload", "config2").split(":")[0].replace("config", "") or "2"
     out = {"config": cfg, "pods": bench["config"]["resources_per_gpu"], "constraints": bench["config"]["constraints"],
