@@ -3208,6 +3208,46 @@ int gk_results_launch(const gk_results* r, size_t i, const char** kernel, double
   return GK_OK;
 }
 
+// Staging's device-side first use, ahead of the first staging: the device
+// layout's kernels (and rocPRIM's) are loaded by a two-node layout, and the
+// stream-ordered pool its temporaries come from keeps freed memory instead of
+// returning it after every staging.
+static void device_layout_warmup() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipMemPool_t pool = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    Node h[2] = {};
+    h[0].type = NT_OBJ;
+    h[0].n = 1;
+    h[0].first = 1;
+    h[0].val = 1;
+    h[1].type = NT_STR;
+    const uint32_t one[4] = {0, 0, 0, 0};  // beg, evalpos, root_d, slot of the one review
+    ReviewCol hc{};
+    hc.root = 0;
+    hc.labels = hc.old_labels = hc.ns_labels = NO_ID;
+    DBuf dD, dN, dv, dc;
+    hipStream_t st = nullptr;
+    uint64_t nout = 0;
+    if (dD.reserve(sizeof h) && dN.reserve(sizeof h) && dv.reserve(sizeof one) && dc.reserve(sizeof hc) &&
+        hipMemcpy(dD.p, h, sizeof h, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dv.p, one, sizeof one, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dc.p, &hc, sizeof hc, hipMemcpyHostToDevice) == hipSuccess &&
+        hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+      const uint32_t* v = (const uint32_t*)dv.p;
+      (void)gk_device_layout((const Node*)dD.p, 2, 0, v, v + 1, v + 2, v + 3, 1, 1, (Node*)dN.p, (ReviewCol*)dc.p, 1,
+                             &nout, st);
+    }
+    if (st) hipStreamDestroy(st);
+    for (DBuf* x : {&dD, &dN, &dv, &dc}) x->free_();
+  });
+}
+
 int gk_engine_prepare(gk_engine* e, int device) {
   if (!e) return GK_EINVAL;
   ReadLock rl;
@@ -3217,6 +3257,7 @@ int gk_engine_prepare(gk_engine* e, int device) {
     // host worker pool
     upload_bounce_init();
     parallel_run(default_threads(), [](int) {});
+    if (env_mode("GKGPU_DEVICE_LAYOUT", 1, 1) != 0) device_layout_warmup();
   }
   return rc;
 }
