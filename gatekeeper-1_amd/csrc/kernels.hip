@@ -543,7 +543,13 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
-  const uint32_t fstage = hint && hint <= 65536 ? gk::FSTAGE_SMALL : gk::FSTAGE;
+  uint32_t fstage = hint && hint <= 65536 ? gk::FSTAGE_SMALL : gk::FSTAGE;
+  // GKGPU_FMT_STAGE (tests): a smaller LDS window, so every wave's bytes go
+  // through several windows
+  if (const char* fs = getenv("GKGPU_FMT_STAGE")) {
+    const long v = atol(fs);
+    if (v >= 256 && v <= (long)gk::FSTAGE_SMALL) fstage = (uint32_t)v & ~3u;
+  }
   // GKGPU_FMT_WIDE (A/B switch, default on): 16-B source reads in the printers
   static const bool wide = !getenv("GKGPU_FMT_WIDE") || atoi(getenv("GKGPU_FMT_WIDE")) != 0;
   if (wide) hipLaunchKernelGGL(gk::gk_format_kernel<gk::LOutW>, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);

@@ -650,6 +650,30 @@ def test_config5_webhook_micro_batch():
     assert list(st) == list(res.status)
 
 
+def test_format_pass_lds_windows_keep_bytes(monkeypatch):
+    """The format pass stages each wavefront's output bytes in LDS windows
+    (kernels.hip gk_format_kernel); with a 256-B window every wave's range
+    spans many windows and tuples straddle window edges.  Rows equal the
+    default window's and the oracle's (config 5: ~160-B PSP messages)."""
+    ts, cs = W.config5(20)
+    drv = Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    ins = W.gen_admission_inputs(128, seed=7)
+    base = drv.query_batch(ins)
+    monkeypatch.setenv("GKGPU_FMT_STAGE", "256")
+    small = drv.query_batch(ins)
+    monkeypatch.delenv("GKGPU_FMT_STAGE")
+    assert len(base.results) > 128
+    assert [(x.review, x.msg, x.details_json) for x in small.results] == \
+        [(x.review, x.msg, x.details_json) for x in base.results]
+    rep = compare(oracle_for(ts, cs), [json.loads(s)["review"] for s in ins], small)
+    _assert_clean(rep)
+
+
 STR_BUILTINS = W._tmpl("K8sStrBuiltins", """package k8sstrbuiltins
 
 violation[{"msg": msg}] {
