@@ -1006,14 +1006,29 @@ static bool relocate_for_device(std::vector<Part>& parts, uint32_t base, NodeAre
   dl.evalpos.assign(n, 0);
   dl.slot.assign(n, NO_ID);
   dl.root_d.assign(n, NO_ID);
-  uint32_t live = 0;
-  for (size_t k = 0; k < perm.size(); ++k) {
-    const uint32_t b = perm[k];
-    dl.evalpos[b] = (uint32_t)k;
-    dl.root_d[b] = out.cols[b].root;
-    if (out.cols[b].root != NO_ID) dl.slot[b] = live++;
+  // evaluation positions and root slots (live roots numbered in evaluation
+  // order): a count per chunk of perm, a prefix, then the chunks in parallel
+  {
+    const size_t np = perm.size();
+    const int C = (int)std::max<size_t>(1, std::min<size_t>((size_t)T * 4, np / 16384));
+    std::vector<uint32_t> live_in(C + 1, 0);
+    parallel_run(C, [&](int c) {
+      uint32_t m = 0;
+      for (size_t k = np * c / C; k < np * (c + 1) / C; ++k) m += out.cols[perm[k]].root != NO_ID;
+      live_in[c + 1] = m;
+    });
+    for (int c = 0; c < C; ++c) live_in[c + 1] += live_in[c];
+    parallel_run(C, [&](int c) {
+      uint32_t live = live_in[c];
+      for (size_t k = np * c / C; k < np * (c + 1) / C; ++k) {
+        const uint32_t b = perm[k];
+        dl.evalpos[b] = (uint32_t)k;
+        dl.root_d[b] = out.cols[b].root;
+        if (out.cols[b].root != NO_ID) dl.slot[b] = live++;
+      }
+    });
+    dl.nroots = live_in[C];
   }
-  dl.nroots = live;
   out.excluded = 0;
   for (auto& p : parts) out.excluded += p.excluded;
   out.node_count = total;
