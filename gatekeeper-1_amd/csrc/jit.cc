@@ -994,9 +994,13 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // config 2 at 1M Pods, one call): K8sContainerLimits (64 registers) 4.70 ms
 // at 2 waves + 32 heap words, 5.87 at 3 + 16, 6.55 at 4 + 16; K8sRequiredProbes
 // (40 registers) 3.39 / 2.83 / 2.98.  So programs with at most 48 registers
-// get 3 waves and 16 LDS heap words (40 KB per block, three blocks per CU),
-// larger ones 2 waves and 32 words (72 KB, two blocks).  GKGPU_JIT_WPE and
-// GKGPU_LDS_HEAP override both choices (WPE 0 = the compiler's choice).
+// get 3 waves, larger ones 2.  Heap words: 16 for both since round 4 -- the
+// per-iteration heap marks keep the config-2 templates' lane heaps inside 16
+// words (CPU accounting build), and the 32 KB a 2-wave block no longer spends
+// on heap words goes to the LDS stage (parameters, memo cache): config 4's
+// K8sContainerLimits 7.8 -> 5.7 ms, config 2 unchanged (profiles/r04/
+// r04s_ab.txt).  GKGPU_JIT_WPE and GKGPU_LDS_HEAP override both choices (WPE
+// 0 = the compiler's choice).
 static bool small_program(const Program& p) { return p.nregs <= 48; }
 static std::string wpe_suffix(const Program& p) {
   const char* w = getenv("GKGPU_JIT_WPE");
@@ -1005,7 +1009,7 @@ static std::string wpe_suffix(const Program& p) {
 }
 static int lds_heap_words(const Program& p) {
   const char* v = getenv("GKGPU_LDS_HEAP");
-  int n = v ? atoi(v) : (small_program(p) ? 16 : 32);
+  int n = v ? atoi(v) : 16;
   return n < 0 ? 0 : (n > 64 ? 64 : n);
 }
 
