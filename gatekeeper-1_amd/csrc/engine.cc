@@ -2937,6 +2937,7 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   }
   b->ms_upload = ms_since(t1);
   b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
+  release_parts_async();
   *out = b.release();
   return GK_OK;
 }

@@ -503,12 +503,23 @@ size_t part_bytes(const Part& p) {
 struct PartPool {
   std::mutex mu;
   std::map<int, std::vector<std::vector<Part>>> free;
+  std::vector<std::vector<Part>> grave;  // large parts awaiting release
 };
 PartPool& part_pool() {
   static PartPool* p = new PartPool();
   return *p;
 }
+void release_parts_async() {
+  std::vector<std::vector<Part>> w;
+  {
+    PartPool& pp = part_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    w.swap(pp.grave);
+  }
+  if (!w.empty()) std::thread([w = std::move(w)]() mutable { w.clear(); }).detach();
+}
 std::vector<Part> take_parts(int T) {
+  release_parts_async();  // an earlier caller's, if it did not
   {
     PartPool& pp = part_pool();
     std::lock_guard<std::mutex> g(pp.mu);
@@ -536,8 +547,11 @@ void give_parts(std::vector<Part>& v) {
   if (v.empty()) return;
   if (bytes > (64u << 20)) {
     // a page's parts (~1.5 GB for 1M Pods): released off the caller's path
-    // (unmapping them took ~50 ms of a staging)
-    std::thread([w = std::move(v)]() mutable { w.clear(); }).detach();
+    // (unmapping them took ~50 ms of a staging), after its upload
+    // (release_parts_async: unmapping while the upload pins pages stalled both)
+    PartPool& pp = part_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    pp.grave.push_back(std::move(v));
     v.clear();
     return;
   }

@@ -136,6 +136,10 @@ struct DevLayout {
   std::vector<uint32_t> slot;     // per batch index: its root's index in the layout (NO_ID: excluded)
   uint32_t nroots = 0;            // live reviews
 };
+// large flattener parts kept since their flattening are released on a
+// background thread (callers that upload: after the upload)
+void release_parts_async();
+
 bool flatten_page(Store& st, std::mutex& smu, const NsCache& ns_cache, const std::set<std::string>* excluded_ns,
                   const Page& page, int threads, uint32_t base, NodeArena& dst, FlatResult& out, std::string& err,
                   const OrderFn* order = nullptr, std::vector<uint32_t>* perm = nullptr, DevLayout* dl = nullptr);

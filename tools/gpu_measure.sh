@@ -46,6 +46,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
            GKGPU_FMT_WIDE=$v timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 --cpu-sample 0 > "$OUT/c5w$v.json" 2> "$OUT/c5w$v.err" || { echo C5W_FAIL; tail "$OUT/c5w$v.err"; exit 1; }
            python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C5W', sys.argv[2], {k: round(v, 3) for k, v in c['latency_ms'].items()}, round(d['value']/1e6,2), 'M/s', [round(x, 3) for x in c['kernel_ms_last_launch']])" "$OUT/c5w$v.json" $v
          done ;;
+    heap) bash tools/gpu_bench_ab.sh "$TAG/heap" "--steps 10 --warmup 2" "" "GKGPU_LDS_HEAP=32" || exit 1
+          bash tools/gpu_bench_ab.sh "$TAG/heap4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_LDS_HEAP=32" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
