@@ -509,6 +509,7 @@ PartPool& part_pool() {
   static PartPool* p = new PartPool();
   return *p;
 }
+}  // namespace
 void release_parts_async() {
   std::vector<std::vector<Part>> w;
   {
@@ -518,6 +519,7 @@ void release_parts_async() {
   }
   if (!w.empty()) std::thread([w = std::move(w)]() mutable { w.clear(); }).detach();
 }
+namespace {
 std::vector<Part> take_parts(int T) {
   release_parts_async();  // an earlier caller's, if it did not
   {
