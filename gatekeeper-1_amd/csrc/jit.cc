@@ -999,7 +999,8 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // words (CPU accounting build), and the 32 KB a 2-wave block no longer spends
 // on heap words goes to the LDS stage (parameters, memo cache): config 4's
 // K8sContainerLimits 7.8 -> 5.7 ms, config 2 unchanged (profiles/r04/
-// r04s_ab.txt).  GKGPU_JIT_WPE and GKGPU_LDS_HEAP override both choices (WPE
+// r04s_ab.txt; all templates at 16 vs 32: config 4 1,774 vs 1,169 M evals/s,
+// r04zd_ab.txt).  GKGPU_JIT_WPE and GKGPU_LDS_HEAP override both choices (WPE
 // 0 = the compiler's choice).
 static bool small_program(const Program& p) { return p.nregs <= 48; }
 static std::string wpe_suffix(const Program& p) {
