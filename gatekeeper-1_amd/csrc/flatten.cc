@@ -1074,8 +1074,8 @@ static bool merge_parts(Store& gst, std::mutex& smu, std::vector<Part>& parts, u
     std::vector<const Store*> src;
     for (auto& p : parts) src.push_back(&p.st);
     std::vector<std::vector<uint32_t>> maps;
-    // (a micro-batch's few thousand strings: one thread, no pool round trips)
-    gst.intern_parts(src, nwell, maps, extra < 16384 ? 1 : T);
+    // (a micro-batch's few thousand strings: parallel lookups, serial inserts)
+    gst.intern_parts(src, nwell, maps, T);
     for (size_t k = 0; k < parts.size(); ++k) parts[k].smap.swap(maps[k]);
     for (auto& p : parts) {
       const Store& ls = p.st;

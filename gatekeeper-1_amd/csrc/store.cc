@@ -747,12 +747,26 @@ void Store::intern_parts(const std::vector<const Store*>& src, uint32_t first,
     size_t extra = 0;
     for (const Store* ls : src) extra += ls->nstrings() > first ? ls->nstrings() - first : 0;
     if (extra < 8192) {
-      for (size_t p = 0; p < P; ++p) {
+      // the parts look their strings up in parallel (the table is only read;
+      // the caller holds the store's lock), then the misses are interned in
+      // part order -- a webhook micro-batch's strings are mostly known
+      auto look = [&](size_t p) {
         const Store& ls = *src[p];
         auto& m = maps[p];
         m.resize(ls.nstrings());
         for (uint32_t k = 0; k < first && k < ls.nstrings(); ++k) m[k] = k;
-        for (uint32_t k = first; k < ls.nstrings(); ++k) m[k] = intern(ls.str(k));
+        for (uint32_t k = first; k < ls.nstrings(); ++k) {
+          std::string_view v = ls.str(k);
+          m[k] = find(v.data(), v.size());
+        }
+      };
+      if (threads > 1 && P > 1) parallel_run((int)P, [&](int p) { look((size_t)p); });
+      else for (size_t p = 0; p < P; ++p) look(p);
+      for (size_t p = 0; p < P; ++p) {
+        const Store& ls = *src[p];
+        auto& m = maps[p];
+        for (uint32_t k = first; k < ls.nstrings(); ++k)
+          if (m[k] == NO_ID) m[k] = intern(ls.str(k));
       }
       return;
     }
