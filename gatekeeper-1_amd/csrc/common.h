@@ -288,6 +288,8 @@ struct DevArgs {
   char* mstr;                 // memo-string arena of the evaluation (V_GSTR bytes; null: off)
   unsigned long long* mstr_top;  // its bump cursor (bytes used)
   uint64_t mstr_cap;
+  uint64_t gm_salt;           // per launch: mixed into memo hashes, so launches sharing a
+                              // memo table (one clear per evaluation) never read each other's entries
   uint64_t* frec;             // per output tuple, a deferred message's argument words, structure
                               // of arrays: word j of tuple i at frec[j * out_cap + i]
   char* ebytes;               // bytes that existed at emission (eager messages, details JSON)

@@ -2263,12 +2263,12 @@ __device__ __forceinline__ uint64_t gm_mix(uint64_t x) {
 #endif
 #if GK_GM_HASH_OLD  // diagnostics (GKGPU_JIT_PRE="GK_GM_HASH_OLD=1"): the round-2 mixers
 __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
-  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull));
+  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull + gk_args.gm_salt));
 }
 __device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
 #else
 __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
-  uint64_t h = (k0 ^ ((uint64_t)(site + 1) << 44)) * 0x9e3779b97f4a7c15ull;
+  uint64_t h = (k0 ^ ((uint64_t)(site + 1) << 44) ^ gk_args.gm_salt) * 0x9e3779b97f4a7c15ull;
   h ^= h >> 29;
   h += k1 * 0xbf58476d1ce4e5b9ull;
   return h ^ (h >> 32);

@@ -35,6 +35,7 @@ extern "C" int gk_launch_compact(const gk::DevArgs* a, const gk::Viol* raw, cons
                                  unsigned long long* toff, hipStream_t stream, uint64_t hint);
 extern "C" int gk_launch_keys(const gk::DevArgs* args, hipStream_t stream);
 extern "C" int gk_launch_format(const gk::DevArgs* args, hipStream_t stream, hipEvent_t* ev, uint64_t hint);
+extern "C" int gk_launch_zero(void* const* ptrs, const uint64_t* bytes, uint32_t n, hipStream_t stream);
 extern "C" size_t gk_devargs_size();
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
@@ -1729,10 +1730,8 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
   }
   res->ms[1] = ms_since(t0);
   for (int attempt = 0; attempt < 4; ++attempt) {
-    hipMemsetAsync(x->d_rflags.p, 0, nrev * 4, x->stream);
-    hipMemsetAsync(x->d_rreason.p, 0, nrev * 4, x->stream);
-    hipMemsetAsync(x->d_totals.p, 0, ncons * 8, x->stream);
-    hipMemsetAsync(x->d_counters.p, 0, 64 + 16 * plan.size(), x->stream);
+    // per-call state (flags, reasons, totals, counters, memo-string cursor, memo
+    // tables) is zeroed by one gk_zero dispatch below, once the streams are known
     bool prof = e->profile && x->d_prof.reserve(ncons * 32);
     if (prof) hipMemsetAsync(x->d_prof.p, 0, ncons * 32, x->stream);
     DevArgs a{};
@@ -1748,7 +1747,6 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     // the format pass after every template launch (GKGPU_MEMO_STRINGS=0: off, A/B)
     if (env_mode("GKGPU_GMEMO", 1, 1) != 0 && env_mode("GKGPU_MEMO_STRINGS", 1, 1) != 0 &&
         x->d_mstr.reserve(MSTR_BYTES) && x->d_mtop.reserve(8)) {
-      hipMemsetAsync(x->d_mtop.p, 0, 8, x->stream);
       a.mstr = (char*)x->d_mstr.p;
       a.mstr_top = (unsigned long long*)x->d_mtop.p;
       a.mstr_cap = MSTR_BYTES;
@@ -1814,6 +1812,27 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       x->lev.push_back(ev1);
     }
     const hipEvent_t ev_go = x->lev[2 * plan.size()];
+    {
+      // one dispatch zeroes the call's state and every used stream's memo table
+      // (launches sharing a table salt their memo hashes: DevArgs gm_salt)
+      const bool gm_on = env_mode("GKGPU_GMEMO", 1, 1) != 0;  // A/B switch
+      void* zp[12];
+      uint64_t zb[12];
+      uint32_t zn = 0;
+      auto zero = [&](void* p, uint64_t b) { if (p && b) { zp[zn] = p; zb[zn] = b; ++zn; } };
+      zero(x->d_rflags.p, (uint64_t)nrev * 4);
+      zero(x->d_rreason.p, (uint64_t)nrev * 4);
+      zero(x->d_totals.p, (uint64_t)ncons * 8);
+      zero(x->d_counters.p, 64 + 16 * (uint64_t)plan.size());
+      if (a.mstr_top) zero(x->d_mtop.p, 8);
+      bool any_fn = false;
+      for (auto& pl : plan) any_fn = any_fn || pl.fn;
+      for (int si = 0; si < nstream && gm_on && any_fn; ++si) {
+        DBuf& gm = si == 0 ? x->d_gmemo : x->d_gmemo_side[si - 1];
+        if (gm.reserve((size_t)GMEMO_ENTRIES * 32)) zero(gm.p, (uint64_t)GMEMO_ENTRIES * 32);
+      }
+      if (gk_launch_zero(zp, zb, zn, x->stream) != 0) return fail(e, GK_EDEVICE, "launch failed");
+    }
     if (nstream > 1) {
       hipEventRecord(ev_go, x->stream);
       for (int k = 0; k + 1 < nstream; ++k) hipStreamWaitEvent(x->side[k], ev_go, 0);
@@ -1834,10 +1853,10 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
       if (plan[i].fn) {
         // template kernel: a cleared cross-lane memo table (devrt.h gm_get)
         const bool gm_on = env_mode("GKGPU_GMEMO", 1, 1) != 0;  // A/B switch
-        if (gm_on && gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {
+        if (gm_on && gmemo.reserve((size_t)GMEMO_ENTRIES * 32)) {  // (zeroed above)
           argv[i].gmemo = (uint64_t*)gmemo.p;
           argv[i].gmemo_mask = GMEMO_ENTRIES - 1;
-          hipMemsetAsync(gmemo.p, 0, (size_t)GMEMO_ENTRIES * 32, st);
+          argv[i].gm_salt = (uint64_t)(i + 1) * 0xd6e8feb86659fd93ull;
         }
         uint64_t threads = (uint64_t)a.ntiles * a.nclist * 64;
         uint32_t blocks = (uint32_t)((threads + 255) / 256);

@@ -726,8 +726,47 @@ __global__ void __launch_bounds__(64) gk_clock_probe(unsigned long long* out, ui
 
 }  // namespace gk
 
+// Zeroes an evaluation's per-call device state in one dispatch: flags,
+// reasons, totals, counters, the memo-string cursor and the cross-lane memo
+// tables of every stream the launches use (round 3 issued one fill per buffer
+// and one per template launch: ~10 dispatches ahead of a micro-batch's work).
+namespace gk {
+struct ZeroList {
+  uint32_t* p[12];
+  uint64_t words[12];  // 4-byte words
+  uint32_t n;
+};
+__global__ void __launch_bounds__(256) gk_zero(ZeroList z) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t b = 0; b < z.n; ++b) {
+    uint32_t* q = z.p[b];
+    const uint64_t nw = z.words[b];
+    for (uint64_t i = t0; i < nw; i += stride) q[i] = 0u;
+  }
+}
+}  // namespace gk
+
 extern "C" int gk_launch_clock_probe(unsigned long long* out, uint32_t iters, hipStream_t stream) {
   hipLaunchKernelGGL(gk::gk_clock_probe, dim3(1), dim3(64), 0, stream, out, iters);
+  return (int)hipGetLastError();
+}
+
+// zero n buffers (bytes multiples of 4, at most 12) on the stream
+extern "C" int gk_launch_zero(void* const* ptrs, const uint64_t* bytes, uint32_t n, hipStream_t stream) {
+  if (n > 12) return (int)hipErrorInvalidValue;
+  gk::ZeroList z{};
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!ptrs[i] || !bytes[i]) continue;
+    z.p[z.n] = (uint32_t*)ptrs[i];
+    z.words[z.n] = bytes[i] / 4;
+    tot += bytes[i] / 4;
+    ++z.n;
+  }
+  if (!z.n) return 0;
+  const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tot + 1023) / 1024, 2048));
+  hipLaunchKernelGGL(gk::gk_zero, dim3(blocks), dim3(256), 0, stream, z);
   return (int)hipGetLastError();
 }
 

@@ -50,6 +50,8 @@ for what in "${@:-c2 c4 c5 cache}"; do
           bash tools/gpu_bench_ab.sh "$TAG/heap4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_LDS_HEAP=32" || exit 1 ;;
     fst) bash tools/gpu_bench_ab.sh "$TAG/fst" "--steps 10 --warmup 2" "" "GKGPU_FMT_STAGE=16384" || exit 1
          bash tools/gpu_bench_ab.sh "$TAG/fst4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FMT_STAGE=16384" || exit 1 ;;
+    c24) bash tools/gpu_bench_ab.sh "$TAG/c24" "--steps 10 --warmup 2" "" || exit 1
+         bash tools/gpu_bench_ab.sh "$TAG/c24_4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
     rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
