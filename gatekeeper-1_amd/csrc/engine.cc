@@ -194,7 +194,7 @@ struct DBuf {
     size_t from = append_only ? std::min(used, n) : 0;
     // GKGPU_BOUNCE_MIN (tests): the smallest copy that takes the bounce path
     const char* bm = getenv("GKGPU_BOUNCE_MIN");
-    const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+    const size_t bounce_min = bm ? (size_t)atoll(bm) : (16u << 20);
     if (n > from && n - from >= bounce_min) {
       if (!upload_bounce((char*)p + from, (const char*)src + from, n - from)) return false;
     } else if (n > from && hipMemcpy((char*)p + from, (const char*)src + from, n - from, hipMemcpyHostToDevice) != hipSuccess)
@@ -2842,7 +2842,7 @@ static bool batch_upload(gk_engine* e, gk_batch* b) {
   const size_t bytes = docs * sizeof(Node);
   char* dst = (char*)b->d_nodes.p + perm * sizeof(Node);
   const char* bm = getenv("GKGPU_BOUNCE_MIN");  // tests: the smallest copy that takes the bounce path
-  const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+  const size_t bounce_min = bm ? (size_t)atoll(bm) : (16u << 20);
   if (bytes >= bounce_min) {
     if (!upload_bounce(dst, (const char*)b->arena.data(), bytes)) return false;
   } else if (bytes && hipMemcpy(dst, b->arena.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
@@ -2878,7 +2878,7 @@ static bool batch_upload_layout(gk_engine* e, gk_batch* b, const DevLayout& dl) 
   const double ms_scratch = ms_since(t0);
   const size_t bytes = docs * sizeof(Node);
   const char* bm = getenv("GKGPU_BOUNCE_MIN");
-  const size_t bounce_min = bm ? (size_t)atoll(bm) : (256u << 20);
+  const size_t bounce_min = bm ? (size_t)atoll(bm) : (16u << 20);
   if (ok) ok = bytes >= bounce_min ? upload_bounce(dD.p, (const char*)b->arena.data(), bytes)
                                    : hipMemcpy(dD.p, b->arena.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
   const double ms_up = ms_since(t0);
