@@ -275,15 +275,11 @@ def main():
     # error/fallback flags.  The references are counted by running the same
     # programs over the same staged batch in the CPU build of the device
     # runtime with its accounting hooks on (oracle/cpuvm_touch.cc).
-    dom = max((k for k in launch_ms if k.startswith("gk_t_") or k.startswith("gk_f_") or k == "audit_kernel"),
+    dom = max((k for k in launch_ms if k.startswith("gk_t_") or k == "audit_kernel"),
               key=lambda k: sum(launch_ms[k]))
     k_avg_ms = sum(launch_ms[dom]) / len(launch_ms[dom])
     dl = [ln for ln in last.launches if ln.kernel == dom][0]
-    if dom.startswith("gk_f_"):
-        # GKGPU_FUSED=1: one kernel evaluates every template's constraints
-        ref = referenced_bytes(drv, batch, None, cons_ids, args.cpu_threads, every=True) if rank == 0 else None
-    else:
-        ref = referenced_bytes(drv, batch, kinds_of.get(dom), cons_ids, args.cpu_threads) if rank == 0 else None
+    ref = referenced_bytes(drv, batch, kinds_of.get(dom), cons_ids, args.cpu_threads) if rank == 0 else None
     if ref is not None:
         algo_bytes = 4 * ref["nodes"] + ref["string_bytes"] + 12 * nrev + 16 * dl.tuples + 4 * nrev
     else:

@@ -195,6 +195,8 @@ enum ReviewColFlags : uint32_t {
   RC_FALLBACK = 512,      // review shape outside the match fast path
   RC_REVIEW_DEF = 1024,   // input.review defined
   RC_EXCLUDED = 2048,     // namespace excluded for the audit process (excluder.go:82-86): not reviewed
+  RC_AUDIT = 4096,        // a hooks.audit review (matching_reviews_and_constraints, regolib src.go:45-62):
+                          // that rule never joins autoreject_review, so no "not cached" row
 };
 
 struct ReviewCol {

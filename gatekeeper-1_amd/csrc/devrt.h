@@ -2611,8 +2611,9 @@ __device__ __forceinline__ void audit_body(Run run) {
 #else
   const uint32_t plo = 0, pn = 0;
 #endif
-  // autoreject_review (target_template_source.go:12-25)
-  const bool autorej = live && !(rc.flags & RC_FALLBACK) && (m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) &&
+  // autoreject_review (target_template_source.go:12-25); hooks.violation only
+  // (regolib src.go:7-20): the hooks.audit rule (src.go:45-62) has no such join
+  const bool autorej = live && !(rc.flags & (RC_FALLBACK | RC_AUDIT)) && (m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) &&
                        rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) && !(rc.flags & RC_NS_CACHED) &&
                        !(rc.flags & RC_UNSTABLE_NS);
   if (__builtin_expect(gk_ballot(autorej) != 0, 0))

@@ -243,6 +243,10 @@ struct ResultRow {
 struct PinPool {
   std::mutex mu;
   std::vector<std::pair<size_t, char*>> free_;  // (capacity, block)
+  size_t bytes = 0;                              // pinned bytes kept in free_
+  // kept blocks: at most kKeepBytes in all, none above kKeepBlock (a burst of
+  // large decodes must not leave gigabytes of host memory pinned)
+  static constexpr size_t kKeepBytes = 256ull << 20, kKeepBlock = 96ull << 20;
 };
 static PinPool& pin_pool() {
   static PinPool* p = new PinPool();
@@ -263,6 +267,7 @@ static std::shared_ptr<const void> pinned_block(size_t n, char** out) {
     if (best < pp.free_.size()) {
       cap = pp.free_[best].first;
       blk = pp.free_[best].second;
+      pp.bytes -= cap;
       pp.free_.erase(pp.free_.begin() + best);
     }
   }
@@ -274,8 +279,12 @@ static std::shared_ptr<const void> pinned_block(size_t n, char** out) {
   return std::shared_ptr<const void>(blk, [cap](const void* q) {
     PinPool& pp = pin_pool();
     std::lock_guard<std::mutex> g(pp.mu);
-    if (pp.free_.size() < 16) pp.free_.emplace_back(cap, (char*)q);
-    else (void)hipHostFree((void*)q);
+    if (pp.free_.size() < 16 && cap <= PinPool::kKeepBlock && pp.bytes + cap <= PinPool::kKeepBytes) {
+      pp.free_.emplace_back(cap, (char*)q);
+      pp.bytes += cap;
+    } else {
+      (void)hipHostFree((void*)q);
+    }
   });
 }
 
@@ -459,10 +468,6 @@ struct gk_engine {
     hipFunction_t fn = nullptr;
   };
   std::vector<Jit> jits;
-  // GKGPU_FUSED=1 (A/B): one kernel for every template program (jit.cc
-  // jit_fused_source); its launch takes every constraint the per-template
-  // kernels would
-  Jit fused;
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
   bool host_only = false;    // opts {"host_only": true}: stage on the host only (CPU baseline / tests); no evaluation
   std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
@@ -615,8 +620,6 @@ static void rebuild_modules(gk_engine* e) {
   e->progs.clear();
   for (auto& j : e->jits) if (j.mod) hipModuleUnload(j.mod);
   e->jits.clear();
-  if (e->fused.mod) hipModuleUnload(e->fused.mod);
-  e->fused = gk_engine::Jit{};
   e->templates.clear();
   // drop the transient region before appending new permanent constant nodes
   reset_transient(e);
@@ -638,7 +641,10 @@ static void rebuild_modules(gk_engine* e) {
     // patterns, both on by default (profiles/r04/r04x_ab.txt: config 4
     // 1,582 -> 1,656 M evals/s against the comprehension form alone, whose
     // per-(container, probe) list made K8sRequiredProbes 1.86 -> 2.49 ms)
-    if (const int sets = env_mode("GKGPU_REGO_SETS", 3, 3)) rego::optimize_sets(*m, sets);
+    if (const int sets = env_mode("GKGPU_REGO_SETS", 3, 3)) {
+      const int n = rego::optimize_sets(*m, sets);
+      if (getenv("GKGPU_SETS_TRACE")) fprintf(stderr, "optimize_sets %s: %d rewrites\n", kv.first.c_str(), n);
+    }
     e->mods.add(m);
     parsed.push_back(m);
   }
@@ -712,12 +718,6 @@ static void rebuild_modules(gk_engine* e) {
       if (te.reason.empty()) te.reason = ex.what();
     }
     e->templates[kind] = te;
-  }
-  if (env_mode("GKGPU_FUSED", 0, 1) && e->progs.size() >= 2) {
-    std::vector<const Program*> ps;
-    std::vector<uint32_t> ids;
-    for (uint32_t i = 0; i < e->progs.size(); ++i) { ps.push_back(&e->progs[i]); ids.push_back(i); }
-    e->fused.src = jit_fused_source(ps, ids, e->bank, e->st, &e->fused.name);
   }
   e->perm_nodes = (uint32_t)e->st.nodes().size();
   e->module_nodes = e->st.nodes().size() - n_before;
@@ -1475,13 +1475,10 @@ static void ensure_jit(gk_engine* e, bool load) {
     if (j.state != 0) continue;
     th.emplace_back([&j] { j.state = jit_compile(j.src, j.code, j.log) ? 1 : -1; });
   }
-  if (!e->fused.src.empty() && e->fused.state == 0)
-    th.emplace_back([e] { e->fused.state = jit_compile(e->fused.src, e->fused.code, e->fused.log) ? 1 : -1; });
   for (auto& t : th) t.join();
   if (!load) return;
   std::vector<gk_engine::Jit*> all;
   for (auto& j : e->jits) all.push_back(&j);
-  if (!e->fused.src.empty()) all.push_back(&e->fused);
   for (auto* jp : all) {
     auto& j = *jp;
     if (j.state != 1 || j.fn) continue;
@@ -1706,19 +1703,12 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
   std::vector<uint32_t> clist_host;  // constraint indices in launch order
   {
     std::vector<std::vector<uint32_t>> groups(e->progs.size() + 1);
-    const bool fused = e->fused.fn != nullptr;
-    std::vector<uint32_t> fused_cons;
     for (uint32_t c = 0; c < ncons; ++c) {
       uint32_t p = e->corder[c]->spec.prog;
-      bool jit = p != NO_ID && p < e->jits.size() && (e->jits[p].fn || fused);
-      if (jit && fused) { fused_cons.push_back(c); continue; }
+      bool jit = p != NO_ID && p < e->jits.size() && e->jits[p].fn;
       groups[jit ? p : e->progs.size()].push_back(c);
     }
     std::vector<uint32_t>& clist = clist_host;
-    if (!fused_cons.empty()) {
-      plan.push_back({e->fused.fn, e->fused.name, 0, (uint32_t)fused_cons.size()});
-      clist = fused_cons;
-    }
     for (size_t g = 0; g < groups.size(); ++g) {
       if (groups[g].empty()) continue;
       bool vm = g == e->progs.size();
@@ -2421,32 +2411,32 @@ static int coalesced_query(gk_engine* e, const char* input, size_t len, gk_resul
     c.requests += batch.size();
     c.finished.notify_all();  // requests left in the queue elect the next leader
     lk.unlock();
-    std::vector<std::pair<const char*, size_t>> in;
-    in.reserve(batch.size());
-    for (auto* q : batch) in.push_back({q->input, q->len});
-    gk_results* all = nullptr;
-    const int rc = eval_inputs(e, in, &all);
-    std::unique_ptr<gk_results> hold(all);
-    for (uint32_t k = 0; k < batch.size(); ++k) {
-      CoalesceReq* q = batch[k];
-      q->rc = rc;
-      if (rc == GK_OK) q->out = split_results(*all, k);
-      else q->err = tl_err;
-    }
-    // A failed launch (one input that is not JSON, a device or arena failure)
-    // must not fail unrelated callers: each request of the batch is evaluated
-    // again on its own, so every caller gets the result an uncoalesced
-    // gk_query would have given it.
-    if (rc != GK_OK && batch.size() > 1) {
-      for (auto* q : batch) {
-        std::vector<std::pair<const char*, size_t>> one{{q->input, q->len}};
-        gk_results* r1 = nullptr;
-        q->rc = eval_inputs(e, one, &r1);
-        q->out = q->rc == GK_OK ? r1 : nullptr;
-        q->err = q->rc == GK_OK ? std::string() : tl_err;
-        if (q->rc != GK_OK) delete r1;
+    // A failed launch (an input that is not JSON, a device or arena failure)
+    // must not fail unrelated callers: the batch is bisected and each half
+    // evaluated again, so every caller gets the result an uncoalesced
+    // gk_query would have given it, at O(bad * log(batch)) extra launches
+    // instead of one launch per request.
+    std::function<void(size_t, size_t)> serve = [&](size_t lo, size_t hi) {
+      std::vector<std::pair<const char*, size_t>> in;
+      in.reserve(hi - lo);
+      for (size_t k = lo; k < hi; ++k) in.push_back({batch[k]->input, batch[k]->len});
+      gk_results* all = nullptr;
+      const int rc = eval_inputs(e, in, &all);
+      std::unique_ptr<gk_results> hold(all);
+      if (rc == GK_OK) {
+        for (size_t k = lo; k < hi; ++k) { batch[k]->rc = GK_OK; batch[k]->out = split_results(*all, (uint32_t)(k - lo)); }
+        return;
       }
-    }
+      if (hi - lo == 1) {
+        batch[lo]->rc = rc;
+        batch[lo]->err = tl_err;
+        return;
+      }
+      const size_t mid = lo + (hi - lo) / 2;
+      serve(lo, mid);
+      serve(mid, hi);
+    };
+    serve(0, batch.size());
     lk.lock();
     for (auto* q : batch) q->done = true;
     --c.inflight;

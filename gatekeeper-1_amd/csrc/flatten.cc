@@ -74,14 +74,20 @@ namespace {
 struct PoolJob {
   const std::function<void(int)>* f;
   int n;
+  std::atomic<int> next{1};  // next unclaimed index (the caller runs 0)
   std::atomic<int> left;
   std::mutex mu;
   std::condition_variable cv;
 };
+// Jobs, not indices, are queued: a thread claims the next index of the job
+// at the queue's front with one atomic.  The caller of run() helps only with
+// its OWN job's indices -- never another caller's task, so a caller holding a
+// lock across parallel_run (merge_parts' smu, the upload's Bounce::mu) cannot
+// be stalled by someone else's long part, nor re-enter a lock it holds.
 struct WorkPool {
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<std::pair<std::shared_ptr<PoolJob>, int>> q;  // (job, index)
+  std::deque<std::shared_ptr<PoolJob>> q;  // jobs with indices left to claim
   std::atomic<int> pending{0};  // q.size(), readable without the lock
   int workers = 0;
   static void finish(PoolJob& j) {
@@ -89,6 +95,11 @@ struct WorkPool {
       std::lock_guard<std::mutex> g(j.mu);
       j.cv.notify_all();
     }
+  }
+  void retire(const std::shared_ptr<PoolJob>& job) {  // every index claimed: off the queue
+    std::lock_guard<std::mutex> g(mu);
+    for (auto it = q.begin(); it != q.end(); ++it)
+      if (*it == job) { q.erase(it); pending.fetch_sub(1, std::memory_order_relaxed); break; }
   }
   void worker() {
     for (;;) {
@@ -100,16 +111,16 @@ struct WorkPool {
         _mm_pause();
         if ((k & 63) == 63 && std::chrono::steady_clock::now() >= until) break;
       }
-      std::pair<std::shared_ptr<PoolJob>, int> t;
+      std::shared_ptr<PoolJob> job;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return !q.empty(); });
-        t = q.front();
-        q.pop_front();
-        pending.fetch_sub(1, std::memory_order_relaxed);
+        job = q.front();
       }
-      (*t.first->f)(t.second);
-      finish(*t.first);
+      const int i = job->next.fetch_add(1);
+      if (i >= job->n) { retire(job); continue; }
+      (*job->f)(i);
+      finish(*job);
     }
   }
   void run(int n, const std::function<void(int)>& f) {
@@ -126,25 +137,17 @@ struct WorkPool {
         std::thread([this] { worker(); }).detach();
         ++workers;
       }
-      for (int i = 1; i < n; ++i) q.push_back({job, i});
-      pending.fetch_add(n - 1, std::memory_order_relaxed);
+      q.push_back(job);
+      pending.fetch_add(1, std::memory_order_relaxed);
     }
     cv.notify_all();
     f(0);
     finish(*job);
-    // help with whatever is queued (this job's indices or another caller's)
-    for (;;) {
-      std::pair<std::shared_ptr<PoolJob>, int> t;
-      {
-        std::lock_guard<std::mutex> g(mu);
-        if (q.empty()) break;
-        t = q.front();
-        q.pop_front();
-        pending.fetch_sub(1, std::memory_order_relaxed);
-      }
-      (*t.first->f)(t.second);
-      finish(*t.first);
+    for (int i; (i = job->next.fetch_add(1)) < n;) {  // help with this job only
+      f(i);
+      finish(*job);
     }
+    retire(job);
     std::unique_lock<std::mutex> lk(job->mu);
     job->cv.wait(lk, [&] { return job->left.load() == 0; });
   }
@@ -642,6 +645,7 @@ void run_part(Part& p, const Store& gst, const NsCache& ns_cache, const std::set
       const uint32_t root = build_cache_review(st, K, obj, pg.cache[i], &rid);
       bool glob = false;
       p.cols.push_back(review_columns(st, gst, ns_cache, root, &glob));
+      p.cols.back().flags |= RC_AUDIT;
       p.nsglob.push_back(glob);
       p.res.push_back(rid);
       if (p.count_paths) count_paths(root);

@@ -1161,61 +1161,6 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
   return src;
 }
 
-std::string jit_fused_source(const std::vector<const Program*>& progs, const std::vector<uint32_t>& ids,
-                             const CodeBank& bank, const Store& st, std::string* name) {
-  // the group's occupancy and LDS budget: the largest program's
-  const Program* big = progs[0];
-  for (auto* p : progs) if (!small_program(*p)) big = p;
-  std::vector<Gen> gs;
-  bool preads = false, pregex = false;
-  for (auto* p : progs) {
-    gs.push_back(generate(*p, bank, st));
-    preads = preads || gs.back().param_reads;
-    pregex = pregex || gs.back().param_regex;
-  }
-  Gen u;
-  u.param_reads = preads;
-  u.param_regex = pregex;
-  int depth = 1;
-  for (auto* q : progs) depth = std::max(depth, max_depth(*q, bank));
-  const StagePlan sp = stage_plan(*big, u, depth);
-  std::ostringstream body;
-  std::string key = wpe_suffix(*big) + inline_hot_tag(*big);
-  for (size_t i = 0; i < gs.size(); ++i) {
-    // the literal-regex helpers of each program under their own names
-    auto ren = [&](std::string t) {
-      const std::string from = "re_lit_", to = "re_lit_" + std::to_string(i) + "_";
-      for (size_t at = 0; (at = t.find(from, at)) != std::string::npos; at += to.size()) t.replace(at, from.size(), to);
-      return t;
-    };
-    body << ren(gs[i].pre) << "__device__ void pred_" << i
-         << "(PLane& L, uint64_t review, uint64_t params, uint32_t plo, uint32_t pn) {\n" << ren(gs[i].body) << "}\n";
-    key += gs[i].pre + gs[i].body + "|" + std::to_string(ids[i]);
-  }
-  *name = "gk_f_" + hex16(fnv1a(key));
-  std::ostringstream o;
-  o << "// generated by jit.cc: " << progs.size() << " template programs in one kernel\n";
-  if (!getenv("GKGPU_INLINE_HOT") || atoi(getenv("GKGPU_INLINE_HOT")) != 0) o << "#define GK_INLINE_HOT 1\n";
-  if (lds_heap_words(*big) > 0) o << "#define GK_LDS_HWORDS " << lds_heap_words(*big) << "\n";
-  if (lds_scalars()) o << "#define GK_LDS_SCALARS 1\n";
-  o << "#define GK_MAXDEPTH " << depth << "\n";
-  if (sp.params) o << "#define GK_LDS_PARAMS 1\n";
-  if (sp.dfa) o << "#define GK_LDS_DFA 1\n";
-  o << "#include \"devrt.h\"\n"
-    << "namespace gk {\n"
-    << (sp.params ? "" : "#define vget_p(L, c, k, lo, n) vget(L, c, k)\n"
-                         "#define op_iter_next_p(L, c, st, y, k, v, lo, n) op_iter_next(L, c, st, y, k, v)\n")
-    << body.str() << "}  // namespace gk\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(*big) << ") " << *name << "(gk::DevArgs) {\n"
-    << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t prog, uint32_t plo, uint32_t pn) {\n"
-    << "    switch (prog) {\n";
-  for (size_t i = 0; i < gs.size(); ++i)
-    o << "      case " << ids[i] << "u: gk::pred_" << i << "(L, review, params, plo, pn); break;\n";
-  o << "      default: gk::lane_fallback(L, gk::FB_UNSUPPORTED); break;\n"
-    << "    }\n  });\n}\n";
-  return o.str();
-}
-
 bool jit_compile(const std::string& src, std::string& code, std::string& log) {
   {
     std::lock_guard<std::mutex> g(g_mu);

@@ -27,12 +27,5 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log);
 // Kernel name for a source body: "gk_t_<16 hex digits of a content hash>".
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st);
 
-// One kernel for several templates (GKGPU_FUSED=1, A/B): each program's
-// predicate as its own device function, the wave's program chosen by a
-// switch on MatchSpec.prog (ids[i] is progs[i]'s index), so one launch
-// evaluates every constraint of a review tile in adjacent wavefronts.
-// Returns the source; *name receives the kernel's name.
-std::string jit_fused_source(const std::vector<const Program*>& progs, const std::vector<uint32_t>& ids,
-                             const CodeBank& bank, const Store& st, std::string* name);
 
 }  // namespace gk

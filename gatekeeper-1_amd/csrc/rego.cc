@@ -545,6 +545,40 @@ static bool set_rule(const Module& m, const std::string& name) {
   }
   return n == 1 && ok;
 }
+// the variables of t outside any comprehension it holds (a comprehension's
+// own variables are local to it)
+static void outer_vars(const TermP& t, std::set<std::string>& out) {
+  if (!t) return;
+  if (t->k == T_VAR) { out.insert(t->s); return; }
+  if (t->k == T_ARRCOMPR || t->k == T_SETCOMPR || t->k == T_OBJCOMPR) return;
+  outer_vars(t->head, out);
+  for (auto& x : t->items) outer_vars(x, out);
+}
+// T (the comprehension's collection, lifted out of it by a rewrite) may only
+// name variables bound before body position i -- a rule argument, a variable
+// of an earlier expression, `input` / `data` or a rule of the module.  A
+// variable local to the comprehension (a wildcard, an unbound name) would
+// otherwise be hoisted into the enclosing body and change what it means.
+static bool closed_before(const Module& m, const Rule& r, const std::vector<ExprP>& b, size_t i, const TermP& T,
+                          const std::string& k) {
+  std::set<std::string> need;
+  outer_vars(T, need);
+  if (mentions(T, k)) return false;
+  std::set<std::string> bound = {"input", "data"};
+  for (auto& a : r.args) outer_vars(a, bound);
+  for (size_t q = 0; q < i && q < b.size(); ++q)
+    for (auto& t : b[q]->terms) outer_vars(t, bound);
+  for (auto& x : m.rules) bound.insert(x->name);
+  for (auto& v : need)
+    if (v.rfind("$", 0) == 0 || !bound.count(v)) return false;
+  // T's selectors: constants or variables (a ref selector would be hoisted
+  // out of the comprehension by RewriteDynamicTerms)
+  if (T->k == T_REF)
+    for (auto& x : T->items)
+      if (x->k != T_SCALAR && x->k != T_VAR) return false;
+  return true;
+}
+
 int optimize_sets(Module& m, int mask) {
   int done = 0;
   for (size_t ri = 0; ri < m.rules.size() && (mask & 1); ++ri) {
@@ -598,6 +632,7 @@ int optimize_sets(Module& m, int mask) {
             T->head = ref->head;
             T->items.assign(ref->items.begin(), ref->items.end() - 1);
           }
+          if (!closed_before(m, r, b, i, T, k)) continue;
           auto ne = std::make_shared<Expr>();
           ne->kind = Expr::TERM;
           ne->negated = true;
@@ -669,8 +704,6 @@ int optimize_sets(Module& m, int mask) {
         for (size_t q = 0; q < b.size(); ++q)
           if (q != i && q != j) rest.push_back(b[q]);
         if (!set_ok || mentions_body(rest, v1) || mentions(r.value, v1) || mentions(r.key, v1)) continue;
-        const std::string e = "__gk_e" + std::to_string(fresh), ix = "__gk_i" + std::to_string(fresh);
-        ++fresh;
         TermP T;
         if (ref->items.size() == 1) T = ref->head;
         else {
@@ -678,6 +711,9 @@ int optimize_sets(Module& m, int mask) {
           T->head = ref->head;
           T->items.assign(ref->items.begin(), ref->items.end() - 1);
         }
+        if (!closed_before(m, r, b, i, T, k)) continue;
+        const std::string e = "__gk_e" + std::to_string(fresh), ix = "__gk_i" + std::to_string(fresh);
+        ++fresh;
         auto it = mk(T_REF);
         it->head = mk_var(A);
         it->items = {mk_var(ix)};
@@ -1003,7 +1039,14 @@ struct Rewriter {
         ne->terms = {dyn_in_term(e, e->terms[0], res), dyn_in_term(e, e->terms[1], res)};
       } else if (e->terms[0]->k == T_CALL) {
         auto c = std::make_shared<Term>(*e->terms[0]);
-        for (auto& a : c->items) a = dyn_one(e, a, res);
+        // optimize_sets' `not __gk_anyin(A, T)` stands for count(A - {k | T[k]})
+        // == count(A), where an undefined T is the empty set: T stays in the
+        // call (undefined there -> the call is undefined -> `not` holds)
+        // instead of being hoisted before the expression, where an undefined
+        // T would fail the body
+        const bool anyin = c->op.size() == 1 && c->op[0] == "__gk_anyin";
+        for (size_t ai = 0; ai < c->items.size(); ++ai)
+          if (!(anyin && ai == 1)) c->items[ai] = dyn_one(e, c->items[ai], res);
         ne->terms = {c};
       } else {
         ne->terms = {dyn_in_term(e, e->terms[0], res)};

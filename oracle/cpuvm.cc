@@ -231,7 +231,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
   if (rc.flags & RC_FALLBACK) {
     L.fail = RF_FALLBACK;
   } else {
-    if ((m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) &&
+    if (!(rc.flags & RC_AUDIT) && (m.flags & MF_HAS_NSSEL) && (rc.flags & RC_HAS_NS) && rc.ns != NO_ID && !(rc.flags & RC_NS_EMPTY) &&
         !(rc.flags & RC_NS_CACHED) && !(rc.flags & RC_UNSTABLE_NS))
       emit_eager(L, true, RULE_AUTOREJECT, "Namespace is not cached in OPA.", 31, nullptr, 2);
     int mr = match_constraint(m, rc);

@@ -140,3 +140,68 @@ def test_audit_from_cache_reuses_the_staged_batch():
     od.put_data(p, json.dumps(extra))
     assert eng_rows() == ref_rows()
     assert drv.audit_cache_stats()[0] == 2
+
+
+def _nssel_setup(n_pods, seed, host_only):
+    """config 2 plus a container-limits constraint with a namespaceSelector,
+    over Pods whose Namespaces are synced for only half of the namespaces.
+    hooks.audit (regolib src.go:45-62) joins only matching_reviews_and_constraints:
+    a Pod in an unsynced namespace fails matches_nsselector (get_ns has no
+    solution, target_template_source.go:300-307) and yields no row -- in
+    particular no autoreject "Namespace is not cached in OPA." row, which only
+    hooks.violation emits (src.go:7-20)."""
+    ts, cs = W.config2()
+    cs = cs + [W.constraint("K8sContainerLimits", "dev-limits",
+                            match={"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}],
+                                   "namespaceSelector": {"matchLabels": {"env": "dev"}}},
+                            parameters={"cpu": "100m", "memory": "512Mi"})]
+    pods, ns_of, ns_objs = W.gen_pods(n_pods, seed=seed, n_namespaces=12)
+    synced = sorted(ns_objs)[::2]
+    items = [(data_path(ns_objs[n]), ns_objs[n]) for n in synced] + [(data_path(o), o) for o in pods]
+    d = gkgpu.Driver(host_only=host_only)
+    cl = Client(d)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, cs)
+    for p, o in items:
+        d.put_data(p, o)
+        od.put_data(p, json.dumps(o))
+    return d, cl, od, cs, items, synced
+
+
+def test_cache_audit_has_no_autoreject_rows_for_unsynced_namespaces():
+    from oracle import cpu_baseline
+    d, cl, od, cs, items, synced = _nssel_setup(240, 41, True)
+    want = _oracle_rows(od)
+    assert not any(r["msg"] == "Namespace is not cached in OPA." for r in want)
+    assert any(r["constraint"].get("metadata").get("name") == "dev-limits" for r in want)
+    b = d.debug_stage_cache()
+    evals, viol, flagged, digest = cpu_baseline.sweep_digest(d, b, threads=4)
+    assert flagged == 0
+    assert viol == len(want), (viol, len(want))
+
+
+@pytest.mark.gpu
+def test_cache_audit_unsynced_namespace_under_namespace_selector():
+    """GPU: the from-cache audit's rows equal the oracle's hooks.audit rows
+    (no autoreject row) when half of the Pods' Namespaces are not synced."""
+    from oracle.driver import details_json
+    d, cl, od, cs, items, synced = _nssel_setup(1500, 42, False)
+    order = sorted(p for p, _ in items)
+    res = cl.audit()
+    assert not any(res.status), "no review may be flagged"
+    got = []
+    for r in res.results:
+        seg = order[r.review].split("/")
+        ns = seg[4] if seg[3] == "namespace" else ""
+        got.append((seg[-2], ns, seg[-1], r.constraint_kind, r.constraint_name, r.msg, r.details_json))
+    want = []
+    for r in _oracle_rows(od):
+        rv, c = r["review"], r["constraint"]
+        ns = rv.get("namespace")
+        want.append((rv.get("kind").get("kind"), ns if isinstance(ns, str) else "", rv.get("name"), c.get("kind"),
+                     c.get("metadata").get("name"), r["msg"], details_json(r["details"])))
+    assert not any(w[5] == "Namespace is not cached in OPA." for w in want)
+    assert sorted(got) == sorted(want)

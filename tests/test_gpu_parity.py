@@ -51,6 +51,8 @@ def _assert_backend(drv, kinds, guard=()):
 
 def _assert_clean(rep, max_fallback_frac=0.0):
     assert not rep.mismatches, rep.mismatches[:3]
+    # byte-exact: no test using _assert_clean reviews object-printing templates
+    assert rep.canonical_only == 0, rep
     assert rep.compared > 0
     total = rep.compared + rep.fallback + rep.errors
     assert rep.fallback <= max_fallback_frac * total, rep

@@ -85,6 +85,7 @@ def _run(cfg, n, gen, max_fallback_frac, inventory=(), oracle_factory=None):
     rep = compare(od, reviews, sub)
     print("config %d sample:" % cfg, rep, "heaviest lane emitted", int(counts.max()), flush=True)
     assert not rep.mismatches, rep.mismatches[:3]
+    assert rep.canonical_only == 0, rep  # byte-exact rows (no object-printing template here)
     assert rep.compared >= N_SAMPLE - 64 - 2 * flagged
     # self-consistency: the audit sweep's totals vs the decoded output's counts
     sweep = batch.eval_audit(limit=20)

@@ -113,3 +113,101 @@ def test_set_rewrite_keeps_required_labels_rows():
         v, fl, dg, wd, wn = json.loads(out.stdout.strip().splitlines()[-1])
         assert fl == 0 and v == wn > 100, (on, v, wn)
         assert dg == wd, (on, "row digests differ from the oracle's")
+
+
+# Bodies the rewrites must leave alone or keep exact: the comprehension's
+# collection names a variable local to it (a wildcard, a named index), which
+# the rewrite would hoist out of the comprehension; and the local-set form of
+# the second pattern (A assigned a comprehension earlier in the body).
+EDGE_REGO = """package k8sedgesets
+
+want = {x | x := input.parameters.keys[_]}
+
+violation[{"msg": msg}] {
+  have := {k | input.review.object.spec.containers[_].env[k]}
+  missing := want - have
+  count(missing) > 0
+  msg := sprintf("wildcard missing %v", [missing])
+}
+
+violation[{"msg": msg}] {
+  got := {k | input.review.object.spec.containers[i].env[k]}
+  miss := want - got
+  count(miss) == count(want)
+  msg := sprintf("named local: none of %v", [miss])
+}
+
+violation[{"msg": msg, "details": {"m": m2}}] {
+  req := {l | l := input.parameters.keys[_]}
+  prov := {k | input.review.object.metadata.labels[k]}
+  m2 := req - prov
+  count(m2) > 0
+  msg := sprintf("local set missing %v", [m2])
+}
+
+violation[{"msg": msg}] {
+  ann := {k | input.review.object.metadata.annotations[k]}
+  d := want - ann
+  count(d) == count(want)
+  msg := "no wanted annotation"
+}
+"""
+
+CODE_EDGE = r'''
+import json, random, sys
+sys.path[:0] = [%r, %r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client, augmented_review
+from oracle import cpu_baseline
+from parity import oracle_for, oracle_review
+ts = [W._tmpl("K8sEdgeSets", %r)]
+cs = [W.constraint("K8sEdgeSets", "edge", match={"kinds": [{"apiGroups": [""], "kinds": ["Pod"]}]},
+                   parameters={"keys": ["a", "b", "c"]})]
+rng = random.Random(5)
+vals = [True, False, None, 0, "", "x", {}, [1]]
+objs, nss = [], []
+for i in range(400):
+    ctrs = []
+    for j in range(rng.randint(0, 3)):
+        c = {"name": "c%%d" %% j}
+        if rng.random() < 0.8:
+            c["env"] = {k: rng.choice(vals) for k in rng.sample("abcdz", rng.randint(0, 4))}
+        ctrs.append(c)
+    md = {"name": "p%%d" %% i, "namespace": "default"}
+    if rng.random() < 0.8:
+        # label values are strings (the match stage's labelSelector columns)
+        md["labels"] = {k: rng.choice(["", "x"]) for k in rng.sample("abcz", rng.randint(0, 4))}
+    if rng.random() < 0.7:
+        md["annotations"] = {k: rng.choice(vals) for k in rng.sample("abcz", rng.randint(0, 3))}
+    objs.append({"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": {"containers": ctrs}})
+    nss.append({"metadata": {"name": "default"}})
+d = gkgpu.Driver(host_only=True); cl = Client(d)
+for t in ts: cl.add_template(t)
+for c in cs: cl.add_constraint(c)
+assert d.template_backend("K8sEdgeSets")[0] != 0, d.template_backend("K8sEdgeSets")
+got = cpu_baseline.sweep_digest(d, d.stage_objects(objs, nss), threads=2)
+od = oracle_for(ts, cs)
+cidx = {kn: i for i, kn in enumerate(d.constraints())}
+rows = []
+for i, (o, n) in enumerate(zip(objs, nss)):
+    for kind, name, msg, det, _ea in oracle_review(od, augmented_review(o, n)):
+        rows.append((i, cidx[(kind, name)], msg, det))
+print(json.dumps([got[1], got[2], got[3], cpu_baseline.row_digest(rows), len(rows)]))
+''' % (os.path.join(ROOT, "gatekeeper-1_amd"), ROOT, os.path.join(ROOT, "tests"), EDGE_REGO)
+
+
+def test_set_rewrite_refuses_comprehension_local_variables():
+    """rego.cc closed_before: of the four bodies only the two whose
+    collection is closed (metadata.labels, metadata.annotations) are
+    rewritten; the rows equal the oracle's with the rewrites on and off."""
+    for on in ("3", "0"):
+        env = dict(os.environ, GKGPU_REGO_SETS=on, GKGPU_SETS_TRACE="1")
+        out = subprocess.run([sys.executable, "-c", CODE_EDGE], env=env, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-2000:]
+        v, fl, dg, wd, wn = json.loads(out.stdout.strip().splitlines()[-1])
+        assert fl == 0 and v == wn > 50, (on, v, wn)
+        assert dg == wd, (on, "row digests differ from the oracle's")
+        if on == "3":
+            tr = [ln for ln in out.stderr.splitlines() if "optimize_sets" in ln and "K8sEdgeSets" in ln]
+            assert tr and tr[0].endswith(": 2 rewrites"), out.stderr[-1500:]

@@ -54,12 +54,6 @@ for what in "${@:-c2 c4 c5 cache}"; do
          bash tools/gpu_bench_ab.sh "$TAG/c24_4" "--config 4 --steps 5 --warmup 1" "" || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
-    rlv) bash tools/gpu_bench_ab.sh "$TAG/rlv" "--config 4 --steps 5 --warmup 1" "" "GKGPU_JIT_PATCH=@tools/patches/rl_nothing.txt" \
-          "GKGPU_JIT_PATCH=@tools/patches/rl_setsonly.txt" "GKGPU_JIT_PATCH=@tools/patches/rl_body1only.txt" \
-          "GKGPU_JIT_PATCH=@tools/patches/rl_noemit1.txt" || exit 1 ;;
-    rpv) bash tools/gpu_bench_ab.sh "$TAG/rpv" "--steps 10 --warmup 2" "" "GKGPU_JIT_PATCH=@tools/patches/rp_noemit.txt" \
-          "GKGPU_JIT_PATCH=@tools/patches/rp_nobody2.txt" "GKGPU_JIT_PATCH=@tools/patches/rp_contonly.txt" \
-          "GKGPU_JIT_PATCH=@tools/patches/rp_probeloop.txt" || exit 1 ;;
     c2t) GKGPU_FLATTEN_TRACE=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/c2t.json" 2> "$OUT/c2t.err" || { echo C2T_FAIL; tail "$OUT/c2t.err"; exit 1; }
         grep -E "flatten|stage upload|intern" "$OUT/c2t.err" | tail -12
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('C2T', round(d['value']/1e6,1), 'M/s stage_s', c['stage_s'], c['stage_ms'], 'prepare_s', c.get('prepare_s'), 'e2e', round(c['end_to_end_evals_per_s']/1e6,2))" "$OUT/c2t.json" ;;
@@ -73,8 +67,6 @@ for what in "${@:-c2 c4 c5 cache}"; do
         cat "$OUT/c5_phases.txt"
         timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 > "$OUT/c5_batch.json" 2> "$OUT/c5_batch.err" || { echo C5_FAIL; tail "$OUT/c5_batch.err"; exit 1; }
         python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5', d['config']['latency_ms'], round(d['value']/1e6,2), 'M/s; cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']/1e6,2))" "$OUT/c5_batch.json" ;;
-    c5f) GKGPU_FUSED=1 timeout -k 10 300 python -u bench.py --config 5 --steps 1000 --warmup 20 --cpu-sample 0 > "$OUT/c5f_batch.json" 2> "$OUT/c5f_batch.err" || { echo C5F_FAIL; tail "$OUT/c5f_batch.err"; exit 1; }
-        python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5F', d['config']['latency_ms'], round(d['value']/1e6,2), 'M/s', d['config']['kernel_ms_last_launch'])" "$OUT/c5f_batch.json" ;;
     cache) timeout -k 10 600 python -u bench.py --from-cache --steps 3 --warmup 1 > "$OUT/cache.json" 2> "$OUT/cache.err" || { echo CACHE_FAIL; tail "$OUT/cache.err"; exit 1; }
         python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('CACHE', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],1), 'ms', c['results_per_audit'], c['cache_builds'], c['first_audit_s'], c['steady_timing_ms'])" "$OUT/cache.json" ;;
   esac
