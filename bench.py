@@ -57,6 +57,13 @@ def parse():
                     help="audit from the cache: the config's objects (and their Namespaces) synced into the "
                          "inventory with PutData, a step = one Client.Audit (hooks.audit) over all of them, every "
                          "result row decoded on the host (--audit-from-cache, manager.go:195-197)")
+    ap.add_argument("--shard-leg", choices=("auto", "on", "off"), default="auto",
+                    help="also time config 4's one-GPU shard (1.25M mixed resources x 50 constraints, the north "
+                         "star's >=1M x 50 shape) in the same process and report it as `config4_shard` "
+                         "(auto: on for config 2 at one GPU)")
+    ap.add_argument("--cpu-e2e", choices=("on", "off"), default="on",
+                    help="CPU baseline end to end: the port also parses and flattens the same page on the leased "
+                         "cores before evaluating it (cpu_baseline.end_to_end)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch for this workload (rocprofv3 --pmc), if measured")
     return ap.parse_args()
@@ -332,6 +339,12 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample != 0:
         n_cpu = nrev if args.cpu_sample < 0 else min(args.cpu_sample, nrev)
         cpu = native_cpu_baseline(drv, batch, n_cpu, args.cpu_threads, last)
+        if args.cpu_e2e == "on" and n_cpu == nrev:
+            # like for like with end_to_end_evals_per_s: the port parses and
+            # flattens the same page on the same leased cores, then evaluates
+            cpu["end_to_end"] = native_cpu_end_to_end(templates, constraints, page,
+                                                      _inventory(args.config, cfg_gen, args.pods * world),
+                                                      args.cpu_threads)
         if args.oracle_sample > 0:
             sample = page.slice(0, min(args.oracle_sample, page.n))
             so = [sample.objs[int(sample.obj_offs[i]):int(sample.obj_offs[i + 1])].decode() for i in range(sample.n)]
@@ -410,10 +423,140 @@ def main():
             "kernels": kernels,
             "format_pass": fmt_roof,
             "cpu_baseline": cpu,
+            "config4_shard": None,
         }
+        if world == 1 and (args.shard_leg == "on" or (args.shard_leg == "auto" and args.config == "2")):
+            # the north star's shape (>=1M resources x 50 constraints): config
+            # 4's one-GPU shard, timed in this process after the headline's
+            # sweeps (its own engine; this one's device memory released first)
+            batch.free()
+            drv.close()
+            out["config4_shard"] = shard_leg("4", 5, 1, args.cpu_threads)
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def shard_leg(cfg, steps, warmup, cpu_threads):
+    """One configuration's one-GPU shard timed in the calling process (the
+    headline line's `config4_shard`): staged once, `steps` audit sweeps after
+    `warmup`, with its dominant kernel's roofline (SURVEY 8(d) algorithmic
+    bytes over its HIP-event time) and the counts that make it comparable
+    (fallback / error reviews, tuples)."""
+    import gkgpu
+    from gkgpu.client import Client
+    from gkgpu.page import Page
+    tfn, gen, n, desc = _configs()[cfg]
+    templates, constraints = tfn()
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    kinds_of = {}
+    for t in templates:
+        k = t["spec"]["crd"]["spec"]["names"]["kind"]
+        b, detail = drv.template_backend(k)
+        if b == 2:
+            kinds_of[detail] = k
+        elif b == 3 and "[guard kernel " in detail:
+            kinds_of[detail.split("[guard kernel ")[1].rstrip("]")] = k + " (guard)"
+    t0 = time.time()
+    objs, nss = gen(n, 0)
+    page = Page.from_lists(objs, nss)
+    del objs, nss
+    t_gen = time.time() - t0
+    drv.prepare()
+    t0 = time.time()
+    batch = drv.stage_page(page)
+    t_stage = time.time() - t0
+    nrev = batch.stats()[0]
+    for _ in range(warmup):
+        batch.eval_audit(limit=20)
+    launch_ms = {}
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(steps):
+        last = batch.eval_audit(limit=20)
+        for ln in last.launches:
+            launch_ms.setdefault(ln.kernel, []).append(ln.ms)
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / steps * 1000.0
+    n_cons = len(constraints)
+    dom = max((k for k in launch_ms if k.startswith("gk_t_") or k == "audit_kernel"), key=lambda k: sum(launch_ms[k]))
+    k_ms = sum(launch_ms[dom]) / len(launch_ms[dom])
+    dl = [ln for ln in last.launches if ln.kernel == dom][0]
+    ref = referenced_bytes(drv, batch, kinds_of.get(dom), drv.constraints(), cpu_threads)
+    algo = 4 * ref["nodes"] + ref["string_bytes"] + 12 * nrev + 16 * dl.tuples + 4 * nrev if ref else None
+    ach = algo / (k_ms / 1000.0) / 1e9 if algo else None
+    out = {
+        "workload": desc,
+        "resources": nrev,
+        "constraints": n_cons,
+        "value": nrev * n_cons / (ms / 1000.0),
+        "unit": "evals/s",
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms,
+        "timed_region_s": elapsed,
+        "stage_s": round(t_stage, 3),
+        "gen_s": round(t_gen, 3),
+        "end_to_end_evals_per_s": nrev * n_cons / (t_stage + ms / 1000.0),
+        "violations_per_step": last.device_tuples,
+        "fallback_reviews": last.n_fallbacks,
+        "error_reviews": last.n_errors,
+        "kernel_ms_per_step": sum(sum(v) / len(v) for v in launch_ms.values()),
+        "roofline": {"bound": "hbm", "kernel": dom, "template": kinds_of.get(dom), "kernel_ms_avg": k_ms,
+                     "algo_bytes_per_launch": algo, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": ach / HBM_PEAK_GBS if ach else None},
+        "kernels": {kinds_of.get(k, k): round(sum(v) / len(v), 4) for k, v in launch_ms.items()},
+    }
+    batch.free()
+    drv.close()
+    return out
+
+
+def native_cpu_end_to_end(templates, constraints, page, inventory, threads):
+    """cpu_baseline.end_to_end: the port (oracle/cpuvm.cc, NOT OPA) timed like
+    the GPU's end_to_end_evals_per_s -- the same page's JSON parsed and
+    flattened by the engine's parallel flattener on the leased cores (a
+    host-only engine), then every review x constraint evaluated on them."""
+    import gkgpu
+    from gkgpu.client import Client
+    from oracle import cpu_baseline as CB
+    hc = host_cpus()
+    threads = threads or hc["lease"]
+    d = gkgpu.Driver(host_only=True)
+    cl = Client(d)
+    for t in templates:
+        cl.add_template(t)
+    for c in constraints:
+        cl.add_constraint(c)
+    for path, obj in inventory:
+        d.put_data(path, obj)
+    d.template_backend(templates[0]["spec"]["crd"]["spec"]["names"]["kind"])  # compile before the clock
+    # the per-document layout: the path-grouped one exists for the GPU's
+    # coalesced wavefront reads and would only add host placement work here
+    saved = os.environ.get("GKGPU_PATH_LAYOUT")
+    os.environ["GKGPU_PATH_LAYOUT"] = "0"
+    try:
+        t0 = time.perf_counter()
+        b = d.stage_page(page)
+        stage_s = time.perf_counter() - t0
+    finally:
+        if saved is None:
+            os.environ.pop("GKGPU_PATH_LAYOUT", None)
+        else:
+            os.environ["GKGPU_PATH_LAYOUT"] = saved
+    secs, evals, viol, mbytes, flagged = CB.sweep(d, b, threads=threads)
+    b.free()
+    d.close()
+    return {"value": evals / (stage_s + secs), "unit": "evals/s", "cores": threads, "kind": "port",
+            "stage_seconds": stage_s, "eval_seconds": secs, "violations": viol, "flagged_pairs": flagged,
+            "sample": "the same %d resources x %d constraints: JSON parse + flatten (engine flattener, host-only) "
+                      "then oracle/cpuvm.cc evaluation, on %d threads; NOT OPA" % (evals // max(1, len(constraints)),
+                                                                                  len(constraints), threads)}
 
 
 def from_cache_main(args):

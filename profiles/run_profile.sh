@@ -20,13 +20,13 @@ cd /tmp && export TMPDIR=/tmp
 # GPU clocks around the run (box-to-box variance: compare only inside one call)
 rocm-smi --showclocks > "$OUT/clocks_before.txt" 2>&1 || true
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-sample 0 "${XA[@]}" > "$OUT/bench_trace.json"
+  python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-sample 0 --shard-leg off "${XA[@]}" > "$OUT/bench_trace.json"
 echo "trace done"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 "${XA[@]}" > "$OUT/bench_fetch.json"
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --shard-leg off "${XA[@]}" > "$OUT/bench_fetch.json"
 echo "fetch done"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 "${XA[@]}" > "$OUT/bench_write.json"
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --shard-leg off "${XA[@]}" > "$OUT/bench_write.json"
 echo "write done"
 python3 "$ROOT/profiles/summarize.py" --traffic-only "$OUT"
 # sample the clocks while the bench runs (killed by its PID afterwards)

@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-5 GPU calls: bash tools/gpu_r05.sh <tag> <step> [<step> ...]
+#   suite  the GPU test suite
+#   bench  the default bench line (config 2 + config4_shard + CPU end to end)
+#   early  GKGPU_FN_EARLY A/B on configs 2 and 4
+#   ab2 "<settings>..." / ab4: same-call A/Bs (settings in AB2 / AB4 env, ';'-separated)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+JC=${GKGPU_JIT_CACHE:-/tmp/gkjit_cache}
+mkdir -p "$JC"
+cp -n .jitcache/*.co "$JC/" 2>/dev/null || true
+export GKGPU_JIT_CACHE=$JC
+jit_pull() {
+  local new=() f sz=0
+  for f in "$JC"/*.co; do [ -e ".jitcache/$(basename "$f")" ] || { new+=("$f"); sz=$((sz + $(stat -c %s "$f"))); }; done
+  if [ ${#new[@]} -gt 0 ] && [ $sz -lt 40000000 ]; then mkdir -p gpurun_out/jitcache_new && cp -n "${new[@]}" gpurun_out/jitcache_new/; fi
+  echo "jit cache: ${#new[@]} new code objects, $sz bytes"
+}
+trap jit_pull EXIT
+for what in "$@"; do
+  case $what in
+    suite) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+           tail -4 "$OUT/pytest_gpu.log"; [ $rc = 0 ] || exit 1 ;;
+    bench) timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo BENCH_FAIL; tail "$OUT/bench.err"; exit 1; }
+           python - "$OUT/bench.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c = d["config"]
+print("BENCH", round(d["value"] / 1e6, 1), "M/s", round(d["ms_per_step"], 3), "ms; frac", d["roofline"]["frac"],
+      "e2e", round(c["end_to_end_evals_per_s"] / 1e6, 2), "stage", c["stage_s"])
+cb = d["cpu_baseline"] or {}
+print("CPU", cb.get("value"), "e2e", (cb.get("end_to_end") or {}).get("value"))
+s = d.get("config4_shard") or {}
+print("SHARD4", s.get("value"), s.get("ms_per_step"), s.get("fallback_reviews"), (s.get("roofline") or {}).get("frac"), s.get("kernels"))
+PY
+           ;;
+    early) bash tools/gpu_bench_ab.sh "$TAG/early2" "--steps 10 --warmup 2 --shard-leg off" "" "GKGPU_FN_EARLY=1" || exit 1
+           bash tools/gpu_bench_ab.sh "$TAG/early4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FN_EARLY=1" || exit 1 ;;
+    ab2) IFS=';' read -ra S <<< "$AB2"; bash tools/gpu_bench_ab.sh "$TAG/ab2" "--steps 10 --warmup 2 --shard-leg off" "${S[@]}" || exit 1 ;;
+    ab4) IFS=';' read -ra S <<< "$AB4"; bash tools/gpu_bench_ab.sh "$TAG/ab4" "--config 4 --steps 5 --warmup 1" "${S[@]}" || exit 1 ;;
+    p2) ( bash profiles/run_profile.sh "${TAG}" ) > "$OUT/p2.log" 2>&1 || { echo P2_FAIL; tail "$OUT/p2.log"; exit 1; }
+        tail -3 "$OUT/p2.log" ;;
+  esac
+done
