@@ -581,7 +581,7 @@ def from_cache_main(args):
         cl.add_constraint(c)
     objs, nss = cfg_gen(n, 0)
     t0 = time.time()
-    ident = re.compile(r'"apiVersion":"([^"]*)","kind":"([^"]*)","metadata":\{"name":"([^"]*)"(?:,"namespace":"([^"]*)")?')
+    ident = re.compile(r'\{"apiVersion":"([^"]*)","kind":"([^"]*)","metadata":\{"name":"([^"]*)"(?:,"namespace":"([^"]*)")?')
     seen_ns = set()
     for js, ns in zip(objs, nss):
         if ns is not None and id(ns) not in seen_ns:
@@ -601,16 +601,25 @@ def from_cache_main(args):
         drv.put_data(path, js)
     t_sync = time.time() - t0
     del objs, nss
+    # a step = one --audit-from-cache sweep as the audit manager consumes it
+    # (manager.go:195-207 then :462-508): Client.Audit over the synced
+    # inventory reduced on the device to exact totals + the first 20 results
+    # per constraint (gk_audit_cache_sample)
     t0 = time.perf_counter()
-    first = drv.audit_summary()
+    first = drv.audit_sample(limit=20)
     t_first = time.perf_counter() - t0
     for _ in range(args.warmup):
-        drv.audit_summary()
+        drv.audit_sample(limit=20)
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
-        last = drv.audit_summary()
+        last = drv.audit_sample(limit=20)
     elapsed = time.perf_counter() - t0
+    # for reference: the same audit with every result row decoded on the host
+    # (gk_query(hooks.audit), what Client.Audit returns)
+    t0 = time.perf_counter()
+    full = drv.audit_summary()
+    full_ms = (time.perf_counter() - t0) * 1000.0
     builds, reviews = drv.audit_cache_stats()
     n_cons = len(constraints)
     ms = elapsed / args.steps * 1000.0
@@ -631,15 +640,18 @@ def from_cache_main(args):
             "workload": cfg_desc + " -- audit from the cache (hooks.audit over the synced inventory)",
             "reviews": reviews,
             "constraints": n_cons,
-            "results_per_audit": last["results"],
-            "status_totals": sum(last["totals"]),
+            "results_per_audit": last.device_tuples,
+            "status_totals": sum(last.totals),
+            "samples": len(last.samples),
+            "flagged_reviews": len(last.flagged),
             "cache_builds": builds,
             "first_audit_s": round(t_first, 3),
-            "first_audit_timing_ms": [round(x, 2) for x in first["timing_ms"]],
-            "steady_timing_ms": [round(x, 2) for x in last["timing_ms"]],
-            "first_launches": first.get("launches"),
-            "steady_launches": last.get("launches"),
-            "timing_fields": "flatten, upload, kernels, download, decode (engine phases of one gk_query)",
+            "first_audit_timing_ms": [round(x, 2) for x in first.timing_ms],
+            "steady_timing_ms": [round(x, 2) for x in last.timing_ms],
+            "steady_launches": [(k.kernel, round(k.ms, 3), k.tuples) for k in last.launches],
+            "timing_fields": "flatten, upload, kernels, download, decode (engine phases of one call)",
+            "decode_all_rows_ms": round(full_ms, 2),
+            "decode_all_rows_results": full["results"],
             "sync_s": round(t_sync, 1),
         },
         "roofline": None,

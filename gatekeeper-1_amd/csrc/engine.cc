@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <atomic>
 #include <functional>
 #include <cstring>
 #include <map>
@@ -555,24 +556,26 @@ static void reset_transient(gk_engine* e) {
 namespace gk {
 
 // ------------------------------------------------------------------ path helpers
+static inline int hexval(char c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
 static std::vector<std::string> split_path(const std::string& p) {
   std::vector<std::string> out;
+  out.reserve(8);
   size_t i = 0;
   while (i < p.size()) {
     while (i < p.size() && p[i] == '/') ++i;
     size_t j = p.find('/', i);
     if (j == std::string::npos) j = p.size();
     if (j > i) {
-      std::string seg = p.substr(i, j - i);
       // storage.ParsePathEscaped: url.PathUnescape each segment
-      std::string u;
-      for (size_t k = 0; k < seg.size(); ++k) {
-        if (seg[k] == '%' && k + 2 < seg.size() + 0 && isxdigit((unsigned char)seg[k + 1]) && isxdigit((unsigned char)seg[k + 2])) {
-          u.push_back((char)std::stoi(seg.substr(k + 1, 2), nullptr, 16));
+      out.emplace_back();
+      std::string& u = out.back();
+      u.reserve(j - i);
+      for (size_t k = i; k < j; ++k) {
+        if (p[k] == '%' && k + 2 < j && isxdigit((unsigned char)p[k + 1]) && isxdigit((unsigned char)p[k + 2])) {
+          u.push_back((char)(hexval(p[k + 1]) * 16 + hexval(p[k + 2])));
           k += 2;
-        } else u.push_back(seg[k]);
+        } else u.push_back(p[k]);
       }
-      out.push_back(u);
     }
     i = j;
   }
@@ -922,6 +925,12 @@ static void compile_constraint(gk_engine* e, ConstraintEnt& c) {
 // region is compacted (maybe_compact).
 static void sync_inventory(gk_engine* e) {
   if (!e->uses_inventory || !e->inv_dirty || e->inv_node == NO_ID) return;
+  const bool tr = getenv("GKGPU_PREPARE_TRACE") != nullptr;
+  auto tp = Clock::now();
+  auto step = [&](const char* what) {
+    if (tr) fprintf(stderr, "inventory: %s %.1f ms\n", what, ms_since(tp));
+    tp = Clock::now();
+  };
   // the synced objects under /external/<target>/, their paths split (URL
   // unescaped) and ordered segment by segment -- the tree's member order
   std::vector<std::pair<const std::string*, const std::string*>> kvs;
@@ -940,9 +949,24 @@ static void sync_inventory(gk_engine* e) {
     ents.push_back(i);
   }
   // (segments 0 and 1 are equal for every entry: order by the rest)
-  std::sort(ents.begin(), ents.end(), [&](uint32_t a, uint32_t b) {
+  step("split");
+  auto seg_less = [&](uint32_t a, uint32_t b) {
     return std::lexicographical_compare(segs[a].begin() + 2, segs[a].end(), segs[b].begin() + 2, segs[b].end());
-  });
+  };
+  // the map's raw-path order is usually the segment order already (it is not
+  // when an escape or a segment that prefixes another reorders them): check
+  // in parallel, sort only if needed
+  std::atomic<bool> sorted{true};
+  if (ents.size() > 1) {
+    const int TS = (int)std::max<size_t>(1, std::min<size_t>((size_t)default_threads(), ents.size() / 4096));
+    parallel_run(TS, [&](int t) {
+      const size_t m = ents.size() - 1;
+      for (size_t i = m * t / TS; i < m * (t + 1) / TS && sorted.load(std::memory_order_relaxed); ++i)
+        if (seg_less(ents[i + 1], ents[i])) sorted = false;
+    });
+  }
+  if (!sorted) std::stable_sort(ents.begin(), ents.end(), seg_less);
+  step("sort");
   const size_t n = ents.size();
   reset_transient(e);
   if (e->inv_hi > e->inv_lo && e->inv_hi == e->perm_nodes) {
@@ -959,6 +983,7 @@ static void sync_inventory(gk_engine* e) {
   std::vector<uint32_t> roots;
   std::string err;
   if (!flatten_docs(e->st, e->smu, docs, e->inv_lo, dst, roots, err)) throw std::runtime_error("inventory tree: " + err);
+  step("flatten");
   {
     NodeArena& N = e->st.nodes();
     const size_t at = N.size();
@@ -995,6 +1020,7 @@ static void sync_inventory(gk_engine* e) {
     return o;
   };
   const Node t = tree(0, n, 2);
+  step("tree");
   e->inv_hi = (uint32_t)e->st.nodes().size();
   Node& slot = e->st.nodes()[e->inv_node];
   slot.type = t.type;
@@ -2527,25 +2553,30 @@ static void build_cache_page(gk_engine* e, CachePage& c) {
 }
 
 static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out);
+// the staged batch of the current engine state's inventory (built on first
+// use after a mutation; shared lock held by the caller)
+static int cache_batch_locked(gk_engine* e, std::shared_ptr<gk_batch>* out) {
+  std::lock_guard<std::mutex> g(e->cache_mu);
+  if (!e->cache_batch || e->cache_batch->gen != e->gen) {
+    e->cache_batch.reset();
+    CachePage cp;
+    build_cache_page(e, cp);
+    gk_batch* nb = nullptr;
+    const int rc = stage_page_locked(e, cp.pg, &nb);
+    if (rc != GK_OK) return rc;
+    e->cache_batch = std::shared_ptr<gk_batch>(nb, gk_batch_free);
+    ++e->cache_builds;
+  }
+  *out = e->cache_batch;
+  return GK_OK;
+}
 static int audit_from_cache(gk_engine* e, gk_results** out) {
   ReadLock rl;
   int rc = read_lock(e, rl, !e->host_only);
   if (rc != GK_OK) return rc;
   std::shared_ptr<gk_batch> b;
-  {
-    std::lock_guard<std::mutex> g(e->cache_mu);
-    if (!e->cache_batch || e->cache_batch->gen != e->gen) {
-      e->cache_batch.reset();
-      CachePage cp;
-      build_cache_page(e, cp);
-      gk_batch* nb = nullptr;
-      rc = stage_page_locked(e, cp.pg, &nb);
-      if (rc != GK_OK) return rc;
-      e->cache_batch = std::shared_ptr<gk_batch>(nb, gk_batch_free);
-      ++e->cache_builds;
-    }
-    b = e->cache_batch;
-  }
+  rc = cache_batch_locked(e, &b);
+  if (rc != GK_OK) return rc;
   if (!e->dev_ok || !b->d_nodes.p) return fail(e, GK_EDEVICE, "no HIP device available");
   CtxLease lease(e);
   TablePtrs tp;
@@ -3018,11 +3049,29 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
 // first `limit` results per constraint in evaluation order (batch index,
 // autoreject first, emission order), selected on the device (kernels.hip
 // gk_sample_*) so only O(constraints x limit) records reach the host.
+static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out);
 int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out) {
   if (!e || !b || !out) return GK_EINVAL;
   ReadLock rl;
   int rc = read_lock(e, rl, true);
   if (rc != GK_OK) return rc;
+  return batch_eval_audit_locked(e, b, limit, out);
+}
+
+int gk_audit_cache_sample(gk_engine* e, uint32_t limit, gk_results** out) {
+  if (!e || !out) return GK_EINVAL;
+  if (e->host_only) return fail(e, GK_EDEVICE, "host-only engine");
+  ReadLock rl;
+  int rc = read_lock(e, rl, true);
+  if (rc != GK_OK) return rc;
+  std::shared_ptr<gk_batch> b;
+  rc = cache_batch_locked(e, &b);
+  if (rc != GK_OK) return rc;
+  return batch_eval_audit_locked(e, b.get(), limit, out);
+}
+
+static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out) {
+  int rc = GK_OK;
   if (b->gen != e->gen) return fail(e, GK_EINVAL, "engine state changed since the batch was staged");
   if (!e->dev_ok || !b->d_nodes.p) return fail(e, GK_EDEVICE, "no HIP device available");
   CtxLease lease(e);

@@ -32,7 +32,7 @@ EXPORTS = [
     "gk_excluder_add", "gk_excluder_clear", "gk_excluder_is_excluded", "gk_results_excluded",
     "gk_batch_eval_audit", "gk_results_sample_count", "gk_results_sample_get", "gk_results_constraint_action",
     "gk_results_export", "gk_results_samples_export", "gk_results_generation", "gk_coalesce_stats",
-    "gk_template_joins", "gk_join_stats", "gk_engine_prepare",
+    "gk_template_joins", "gk_join_stats", "gk_engine_prepare", "gk_audit_cache_sample",
 ]
 
 
@@ -574,6 +574,17 @@ class Driver:
         self._lib.gk_audit_cache_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         self._check(self._lib.gk_audit_cache_stats(self._e, C.byref(b), C.byref(r)))
         return b.value, r.value
+
+    def audit_sample(self, limit: int = 20) -> AuditSweep:
+        """--audit-from-cache as the audit manager consumes it
+        (gk_audit_cache_sample): Client.Audit over the synced inventory's
+        staged batch, reduced on the device to exact per-constraint totals and
+        the first `limit` results per constraint (manager.go:195-207,
+        :462-508); review indexes are inventory path order"""
+        out = C.c_void_p()
+        self._lib.gk_audit_cache_sample.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
+        self._check(self._lib.gk_audit_cache_sample(self._e, limit, C.byref(out)))
+        return _collect_audit(self._lib, out)
 
     def audit_summary(self):
         """Client.Audit (hooks.audit) without materializing Python rows: the

@@ -167,6 +167,15 @@ int gk_batch_stats(const gk_batch* b, uint64_t* reviews, uint64_t* nodes, uint64
  * GK_SAMPLE_MSG bytes (the status truncates at 256, manager.go:622-631). */
 #define GK_SAMPLE_MSG 256
 int gk_batch_eval_audit(gk_engine* e, gk_batch* b, uint32_t limit, gk_results** out);
+/* --audit-from-cache as the audit manager consumes it: Client.Audit
+ * (hooks.audit, client.go:805-833) over the synced inventory's staged batch
+ * (built as gk_query(hooks.audit) builds it, reused until a mutation), with
+ * the sweep reduced on the device as gk_batch_eval_audit does -- exact
+ * per-constraint totals and the first `limit` results per constraint
+ * (manager.go:195-207 then addAuditResponsesToUpdateLists :462-508) -- so no
+ * result row is decoded on the host.  Reviews are numbered in inventory path
+ * order (gk_results_sample_* review indexes). */
+int gk_audit_cache_sample(gk_engine* e, uint32_t limit, gk_results** out);
 typedef struct {
   uint32_t review, constraint;
   uint16_t seq, rule;          /* rule 0xffff = autoreject */

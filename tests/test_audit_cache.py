@@ -205,3 +205,51 @@ def test_cache_audit_unsynced_namespace_under_namespace_selector():
                      c.get("metadata").get("name"), r["msg"], details_json(r["details"])))
     assert not any(w[5] == "Namespace is not cached in OPA." for w in want)
     assert sorted(got) == sorted(want)
+
+
+@pytest.mark.gpu
+def test_audit_cache_sample_totals_and_first_results():
+    """gk_audit_cache_sample: the from-cache audit reduced on the device as
+    the audit manager consumes it (manager.go:195-207, :462-508) -- exact
+    per-constraint totals and the first 20 results per constraint in
+    inventory order -- equal the oracle's hooks.audit rows counted and cut the
+    same way; the staged batch is shared with gk_query(hooks.audit)."""
+    import collections
+    ts, cs = W.config2()
+    items = _inventory(1500, 33)
+    items = [(p, o) for p, o in items if not p.endswith("/null-pod")]  # no CPU-driver review
+    drv = gkgpu.Driver()
+    cl = Client(drv)
+    for t in ts:
+        cl.add_template(t)
+    for c in cs:
+        cl.add_constraint(c)
+    od = oracle_for(ts, cs)
+    for p, o in items:
+        drv.put_data(p, o)
+        od.put_data(p, json.dumps(o))
+    order = sorted(p for p, _ in items if "%2Fb%2F" not in p)
+    idx = {}
+    for i, p in enumerate(order):
+        seg = p.split("/")
+        idx[(seg[-2], seg[4] if seg[3] == "namespace" else "", seg[-1])] = i
+    cons = drv.constraints()
+    cidx = {kn: i for i, kn in enumerate(cons)}
+    per = collections.defaultdict(list)  # constraint -> [(review, k, msg)] in evaluation order
+    for k, r in enumerate(_oracle_rows(od)):
+        rv, c = r["review"], r["constraint"]
+        ns = rv.get("namespace")
+        key = (rv.get("kind").get("kind"), ns if isinstance(ns, str) else "", rv.get("name"))
+        per[cidx[(c.get("kind"), c.get("metadata").get("name"))]].append((idx[key], k, r["msg"]))
+    sw = drv.audit_sample(limit=20)
+    assert not sw.flagged and sw.n_errors == 0 and sw.n_fallbacks == 0
+    assert sw.totals == [len(per[c]) for c in range(len(cons))]
+    got = collections.defaultdict(list)
+    for s in sw.samples:
+        got[s.constraint].append((s.review, s.msg.decode("utf-8", "surrogateescape")))
+    for c in range(len(cons)):
+        want = [(rv, m[:256]) for rv, _k, m in sorted(per[c])[:20]]
+        assert got[c] == want, (cons[c], got[c][:3], want[:3])
+    # one staged batch for both entry points
+    assert drv.audit_summary()["results"] == sum(sw.totals)
+    assert drv.audit_cache_stats()[0] == 1

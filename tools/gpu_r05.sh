@@ -40,6 +40,20 @@ PY
            bash tools/gpu_bench_ab.sh "$TAG/early4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FN_EARLY=1" || exit 1 ;;
     ab2) IFS=';' read -ra S <<< "$AB2"; bash tools/gpu_bench_ab.sh "$TAG/ab2" "--steps 10 --warmup 2 --shard-leg off" "${S[@]}" || exit 1 ;;
     ab4) IFS=';' read -ra S <<< "$AB4"; bash tools/gpu_bench_ab.sh "$TAG/ab4" "--config 4 --steps 5 --warmup 1" "${S[@]}" || exit 1 ;;
+    cache) timeout -k 10 600 python -u bench.py --from-cache --steps 5 --warmup 1 > "$OUT/cache.json" 2> "$OUT/cache.err" || { echo CACHE_FAIL; tail "$OUT/cache.err"; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print('CACHE', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],2), 'ms', c['results_per_audit'], c['first_audit_s'], c['steady_timing_ms'], 'decode-all', c['decode_all_rows_ms'])" "$OUT/cache.json" ;;
+    sq) # SQ / TCP / TA counters of a short config-2 bench, one rocprofv3 pass per set
+        R=$PWD; i=0
+        for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+                   "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA" \
+                   "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_FLAT_READ_WAVEFRONTS_sum TA_FLAT_WRITE_WAVEFRONTS_sum" \
+                   ${SQ_EXTRA:+"$SQ_EXTRA"}; do
+          i=$((i+1))
+          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $set -d "$R/$OUT/sq$i" -o run -- \
+              python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --shard-leg off $SQ_ARGS ) > "$OUT/sq$i.log" 2>&1; rc=$?
+          if [ $rc != 0 ]; then echo "SQ pass $i rc $rc"; tail -3 "$OUT/sq$i.log"; case $rc in 124|134|137|139) exit 1;; esac; continue; fi
+          python3 tools/pmc_table.py "$OUT/sq$i" | tee "$OUT/sq$i.txt"; rm -rf "$OUT/sq$i"
+        done ;;
     p2) ( bash profiles/run_profile.sh "${TAG}" ) > "$OUT/p2.log" 2>&1 || { echo P2_FAIL; tail "$OUT/p2.log"; exit 1; }
         tail -3 "$OUT/p2.log" ;;
   esac
