@@ -312,6 +312,13 @@ struct DevArgs {
   uint64_t jparams;           // the constraint's parameters value
   uint32_t jpc, jstride;
   uint64_t jrow0;
+  // the format table with its literal segments resolved (engine.cc
+  // sync_tables): same offsets as `fmt`; a literal segment is
+  // (0 | len << 8, byte offset in fmtb) instead of (0, string id), so the
+  // size / format passes print literals without the string table (null: off)
+  const uint32_t* fmtr;
+  const char* fmtb;           // the literals' bytes, padded to a dword
+  uint32_t nfmt, nfmtb;       // words of fmtr, bytes of fmtb
 };
 // join sites per template program (compiler.cc join_site)
 constexpr uint32_t JMAX_SITES = 4;

@@ -73,6 +73,9 @@ namespace gk {
 #ifndef GK_VGET_UNROLL
 #define GK_VGET_UNROLL 0
 #endif
+#ifndef GK_VGET_BATCH
+#define GK_VGET_BATCH 0
+#endif
 #ifndef GK_VGET_REC
 #define GK_VGET_REC 1
 #endif
@@ -799,7 +802,27 @@ __device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
       uint32_t kt = vtag(key);
       if (n.type == NT_OBJ && kt == V_STR) {
         uint32_t id = (uint32_t)vpay(key);
-#if GK_VGET_UNROLL
+#if GK_VGET_BATCH
+        // the keys of the first 8 members in one round trip (dword loads at a
+        // 16-B stride, predicated on the run length only, so they issue
+        // together), then the matching record: two round trips wherever the
+        // member sits instead of one per member scanned
+        {
+          const Node* ch = gk_args.nodes + n.first;
+          const uint32_t m = n.n < 8u ? (uint32_t)n.n : 8u;
+          uint32_t k[8];
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) k[j] = j < m ? ch[j].key : NO_ID;
+          uint32_t hit = 8;
+#pragma unroll
+          for (uint32_t j = 8; j-- > 0;) hit = (j < m && k[j] == id) ? j : hit;
+          if (hit < 8) return nodeval(n.first + hit);
+          for (uint32_t i = 8; i < n.n; ++i) {
+            const Node mm = ch[i];
+            if (mm.key == id) return nodeval_of(mm, n.first + i);
+          }
+        }
+#elif GK_VGET_UNROLL
         // four member keys per round trip: the loads are independent, so the
         // lane waits once per four members instead of once per member
         const Node* ch = gk_args.nodes + n.first;

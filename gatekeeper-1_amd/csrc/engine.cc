@@ -42,6 +42,7 @@ extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflag
                                 uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
                                 unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
                                 unsigned int* ncand, int select_only, hipStream_t stream);
+extern "C" uint32_t gk_sample_fine(uint32_t nrev);
 extern "C" int gk_launch_clock_probe(unsigned long long* out, uint32_t iters, hipStream_t stream);
 extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflags, const uint8_t* cerr,
                                 gk::Viol* dst, unsigned long long* count, hipStream_t stream);
@@ -508,7 +509,8 @@ struct gk_engine {
   std::vector<uint32_t> dfa_c, stage;
   // device mirrors of the permanent tables (written under the exclusive lock,
   // except the append-only string / number tables: under smu, graveyard kept)
-  gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_cons, d_mwords, d_progoff, d_dfa_keys,
+  uint32_t nfmtr = 0, nfmtb = 0;  // resolved format table (sync_tables; 0: not built)
+  gk::DBuf d_nodes, d_strs, d_pool, d_sflags, d_nums, d_code, d_K, d_fmt, d_fmtr, d_fmtb, d_cons, d_mwords, d_progoff, d_dfa_keys,
       d_dfa_meta, d_dfa_words, d_stage, d_dfa_c;
   // gk_debug_host_args: host copies of the per-call tables (diagnostics / CPU baseline)
   std::vector<gk::MatchSpec> dbg_cons;
@@ -1264,6 +1266,43 @@ static bool sync_tables(gk_engine* e) {
   std::vector<uint32_t> fmt = e->bank.fmt;
   if (fmt.empty()) fmt.push_back(0);
   ok &= up(e->d_fmt, fmt, false);
+  {
+    // the format table with literal segments resolved to (0 | len << 8,
+    // offset in the literal bytes): the size / format passes keep it in LDS
+    // and print literals without the string table and pool (DevArgs.fmtr)
+    std::vector<uint32_t> fr(fmt.size(), 0);
+    std::string fb;
+    bool okr = true;
+    for (size_t off = 0; okr && off + 2 <= e->bank.fmt.size();) {
+      const uint32_t nseg = e->bank.fmt[off];
+      if (off + 2 + 2 * (size_t)nseg > e->bank.fmt.size()) { okr = false; break; }
+      fr[off] = nseg;
+      fr[off + 1] = e->bank.fmt[off + 1];
+      for (uint32_t sg = 0; sg < nseg; ++sg) {
+        const uint32_t kind = e->bank.fmt[off + 2 + 2 * sg], a = e->bank.fmt[off + 3 + 2 * sg];
+        if (kind == 0) {
+          const std::string_view lit = e->st.str(a);
+          if (lit.size() >= (1u << 24)) { okr = false; break; }
+          fr[off + 2 + 2 * sg] = (uint32_t)lit.size() << 8;
+          fr[off + 3 + 2 * sg] = (uint32_t)fb.size();
+          fb.append(lit.data(), lit.size());
+        } else {
+          fr[off + 2 + 2 * sg] = kind;
+          fr[off + 3 + 2 * sg] = a;
+        }
+      }
+      off += 2 + 2 * (size_t)nseg;
+    }
+    e->nfmtr = 0;
+    e->nfmtb = 0;
+    if (okr && !e->bank.fmt.empty()) {
+      std::vector<uint32_t> fbw((fb.size() + 3) / 4 + 1, 0);
+      memcpy(fbw.data(), fb.data(), fb.size());
+      ok &= up(e->d_fmtr, fr, false) && up(e->d_fmtb, fbw, false);
+      e->nfmtr = (uint32_t)fr.size();
+      e->nfmtb = (uint32_t)fb.size();
+    }
+  }
   std::vector<MatchSpec> cons;
   for (auto* c : e->corder) cons.push_back(c->spec);
   if (cons.empty()) cons.push_back(MatchSpec{});
@@ -1774,6 +1813,12 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.code = (const Ins*)e->d_code.p;
     a.K = (const uint64_t*)e->d_K.p;
     a.fmt = (const uint32_t*)e->d_fmt.p;
+    if (e->nfmtr && env_mode("GKGPU_FMT_RESOLVED", 1, 1)) {  // A/B switch (default on)
+      a.fmtr = (const uint32_t*)e->d_fmtr.p;
+      a.fmtb = (const char*)e->d_fmtb.p;
+      a.nfmt = e->nfmtr;
+      a.nfmtb = e->nfmtb;
+    }
     a.cons = (const MatchSpec*)e->d_cons.p;
     a.mwords = (const uint32_t*)e->d_mwords.p;
     a.prog_off = (const uint32_t*)e->d_progoff.p;
@@ -2179,7 +2224,7 @@ void gk_engine_destroy(gk_engine* e) {
   e->cache_batch.reset();
   for (auto& x : e->ctxs) x->release_all();
   for (DBuf* b : {&e->d_nodes, &e->d_strs, &e->d_pool, &e->d_sflags, &e->d_nums, &e->d_code, &e->d_K, &e->d_fmt,
-                  &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
+                  &e->d_fmtr, &e->d_fmtb, &e->d_cons, &e->d_mwords, &e->d_progoff, &e->d_dfa_keys, &e->d_dfa_meta, &e->d_dfa_words,
                   &e->d_stage, &e->d_dfa_c})
     b->free_();
   for (void* p : e->graveyard) hipFree(p);
@@ -3090,11 +3135,11 @@ static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk
     *out = resp.release();
     return GK_OK;
   }
-  const uint32_t nb = std::min<uint32_t>(8192, nrev);
+  const uint32_t nb = gk_sample_fine(nrev);
   bool any_err = false;
   std::vector<uint8_t> cerr(ncons, 0);
   for (uint32_t c = 0; c < ncons; ++c) { cerr[c] = e->corder[c]->ea_error; any_err |= cerr[c] != 0; }
-  bool ok = x->d_hist.reserve((size_t)ncons * nb * 4) && x->d_cut.reserve(ncons * 4) && x->d_ftot.reserve(ncons * 8) &&
+  bool ok = x->d_hist.reserve((size_t)ncons * (nb + 256) * 4) && x->d_cut.reserve(ncons * 8) && x->d_ftot.reserve(ncons * 8) &&
             x->d_ncand.reserve(16) && x->d_cand.reserve(x->cand_cap * sizeof(SampleRec)) &&
             (!any_err || up(x->d_cerr, cerr, false));
   if (!ok) return fail(e, GK_EDEVICE, "device allocation failed");

@@ -213,12 +213,114 @@ __device__ __forceinline__ uint64_t ntuples() {
   return n < gk_args.out_cap ? n : gk_args.out_cap;
 }
 
+// ---- the resolved format table in LDS (DevArgs.fmtr / fmtb, engine.cc
+// sync_tables).  The size and format passes print most messages from their
+// format's literals and argument strings; with the table staged per block,
+// a literal costs no global round trip (before: the format word, the string
+// entry, then the pool bytes -- three dependent loads per segment), and the
+// argument strings' entries are loaded together up front.
+constexpr uint32_t FMTR_LDS = 1024, FMTB_LDS = 4096;
+struct FmtLds {
+  uint32_t r[FMTR_LDS];
+  uint32_t b[FMTB_LDS / 4];
+};
+__shared__ FmtLds gk_fmt_lds;
+// every thread of the block calls it; true when the table is staged
+__device__ __forceinline__ bool fmt_stage() {
+  const bool on = gk_args.fmtr && gk_args.nfmt <= FMTR_LDS && gk_args.nfmtb <= FMTB_LDS;  // block-uniform
+  if (on) {
+    for (uint32_t k = threadIdx.x; k < gk_args.nfmt; k += blockDim.x) gk_fmt_lds.r[k] = gk_args.fmtr[k];
+    const uint32_t nb = (gk_args.nfmtb + 3) / 4;
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) gk_fmt_lds.b[k] = ((const uint32_t*)gk_args.fmtb)[k];
+  }
+  __syncthreads();
+  return on;
+}
+// argument j of a tuple held in registers (an unrolled select: a dynamic index
+// into a local array would put it in the private segment)
+template <class T> __device__ __forceinline__ T sel_arg(const T (&a)[FMT_MAXARGS], uint32_t j) {
+  T r = a[0];
+#pragma unroll
+  for (uint32_t k = 1; k < FMT_MAXARGS; ++k) r = j == k ? a[k] : r;
+  return r;
+}
+// A deferred message whose sprintf arguments are interned strings (verbs v /
+// s) or ints not printed in g-form (verbs v / d): the resolved table's
+// segments, the strings' entries loaded once.  false: another printer.
+__device__ __forceinline__ bool plain_args(const uint32_t* f, const uint64_t (&a)[FMT_MAXARGS], StrEnt (&se)[FMT_MAXARGS],
+                                           uint32_t na) {
+#pragma unroll
+  for (uint32_t j = 0; j < FMT_MAXARGS; ++j) {
+    se[j] = StrEnt{};
+    if (j < na && vtag(a[j]) == V_STR) se[j] = gk_args.strs[(uint32_t)vpay(a[j])];
+  }
+  const uint32_t nseg = f[0];
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t w0 = f[2 + 2 * s], w1 = f[3 + 2 * s];
+    if ((w0 & 0xff) == 0) continue;
+    const uint32_t verb = w1 >> 16, j = w1 & 0xffff;
+    if (j >= na) return false;
+    const uint64_t v = sel_arg(a, j);
+    if (vtag(v) == V_STR) { if (verb == 'd') return false; continue; }
+    if (vtag(v) == V_INT && !intv_gform(v) && verb != 's') continue;
+    return false;
+  }
+  return true;
+}
+__device__ __forceinline__ uint32_t size_plain_r(const uint32_t* f, const uint64_t (&a)[FMT_MAXARGS],
+                                                 const StrEnt (&se)[FMT_MAXARGS]) {
+  const uint32_t nseg = f[0];
+  Cnt o{0, false};
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t w0 = f[2 + 2 * s], w1 = f[3 + 2 * s];
+    if ((w0 & 0xff) == 0) { o.n += w0 >> 8; continue; }
+    const uint32_t j = w1 & 0xffff;
+    const uint64_t v = sel_arg(a, j);
+    if (vtag(v) == V_STR) o.n += sel_arg(se, j).len;
+    else put_int(o, intof(v));
+  }
+  return o.n;
+}
+template <class O>
+__device__ __forceinline__ void print_plain_r(O& o, const uint32_t* f, const uint64_t (&a)[FMT_MAXARGS],
+                                              const StrEnt (&se)[FMT_MAXARGS]) {
+  const uint32_t nseg = f[0];
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t w0 = f[2 + 2 * s], w1 = f[3 + 2 * s];
+    if ((w0 & 0xff) == 0) {
+      // the literal's bytes from LDS, a dword at a time
+      const uint32_t off = w1, n = w0 >> 8;
+      uint32_t q = off >> 2, sh = off & 3, cur = gk_fmt_lds.b[q];
+      for (uint32_t k = 0; k < n; ++k) {
+        o.put((char)(cur >> (8 * sh)));
+        if (++sh == 4 && k + 1 < n) { sh = 0; cur = gk_fmt_lds.b[++q]; }
+      }
+      continue;
+    }
+    const uint32_t j = w1 & 0xffff;
+    const uint64_t v = sel_arg(a, j);
+    if (vtag(v) == V_STR) {
+      const StrEnt e = sel_arg(se, j);
+      puts_(o, (const char*)gk_args.pool + e.off, e.len);
+    } else {
+      put_int(o, intof(v));
+    }
+  }
+}
+
 // a deferred tuple's printed message length; false = not printable here
-__device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint64_t i, uint32_t& len) {
+__device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint64_t i, uint32_t& len, bool fl) {
   const uint32_t fidx = v.msg_len & 0xffffffu, na = v.msg_len >> 24;
   uint64_t a[FMT_MAXARGS];
 #pragma unroll
   for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
+  if (fl) {
+    StrEnt se[FMT_MAXARGS];
+    if (plain_args(gk_fmt_lds.r + fidx, a, se, na)) {
+      len = size_plain_r(gk_fmt_lds.r + fidx, a, se);
+      return true;
+    }
+  }
   if (size_plain(fidx, a, len)) return true;
   Cnt cn{0, false};
   if (!fmt_run(L, cn, fidx, [&](uint32_t j) { return a[j]; })) return false;
@@ -253,6 +355,7 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
   PLane& L = *(PLane*)&gk_pass_lane;
   const uint64_t n = ntuples();
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  const bool fl = blockIdx.x < ntile ? fmt_stage() : false;  // block-uniform
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
     unsigned long long s = 0;
     for (uint32_t k = 0; k < FTILE; k += 256) {
@@ -261,7 +364,7 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
       const Viol v = gk_args.out[i];
       uint32_t ml = v.msg_len, dl = det_bytes(v);
       bool printable = true;
-      if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml);
+      if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml, fl);
       if (v.pad & VF_DET_VAL) {
         Cnt cn{0, false};
         printable = put_json(L, cn, det_word(v, i)) && printable;
@@ -436,6 +539,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
   uint8_t* stb = (uint8_t*)st;
   uint32_t* gw = (uint32_t*)gk_args.bytes;
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  const bool fl = blockIdx.x < ntile ? fmt_stage() : false;  // block-uniform
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {  // block-uniform
     uint64_t run = gk_args.part[t];
     for (uint32_t k = 0; k < FTILE; k += 256) {
@@ -472,8 +576,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       const uint64_t lo = __shfl(dst, 0, 64);
       const uint64_t hi = __shfl(dst + len, 63, 64);
       const uint64_t lo4 = lo & ~(uint64_t)3, hi4 = (hi + 3) & ~(uint64_t)3;
+      // the resolved-table printer for plain arguments (string entries loaded
+      // before the window loop)
+      StrEnt se[FMT_MAXARGS];
+      const bool plain = fl && defer && len && plain_args(gk_fmt_lds.r + (v.msg_len & 0xffffffu), a, se, na);
       auto body = [&](auto& o) {
-        if (defer) fmt_run(L, o, v.msg_len & 0xffffffu, [&](uint32_t j) { return a[j]; });
+        if (plain) print_plain_r(o, gk_fmt_lds.r + (v.msg_len & 0xffffffu), a, se);
+        else if (defer) fmt_run(L, o, v.msg_len & 0xffffffu, [&](uint32_t j) { return sel_arg(a, j); });
         else puts_(o, gk_args.ebytes + v.msg_off, ml);
         if (v.pad & VF_DET_OBJ) { o.put('{'); o.put('}'); }
         else if (v.pad & VF_DET_VAL) { if (dl) put_json(L, o, det_word(v, i)); }
@@ -612,56 +721,118 @@ __global__ void __launch_bounds__(256) gk_mark_ea_error(const Viol* out, uint64_
   }
 }
 
-__device__ __forceinline__ uint32_t sample_bucket(uint32_t review, uint32_t nrev, uint32_t nb) {
-  return (uint32_t)(((uint64_t)review * nb) / nrev);
+// Two levels of review buckets per constraint, so that almost no tuple
+// costs a global atomic (round 4: one per tuple into 8,192 buckets, 0.38 ms
+// of a config-2 sweep):
+//   h1     -- SB1 coarse buckets, counted in LDS per block and added to the
+//             global counts once per block and bin;
+//   c1     -- one wavefront per constraint: the coarse bucket where the running
+//             count reaches `limit` (cut1), the count before it, the exact total;
+//   h2     -- only the tuples in their constraint's cut1 bucket: one bin per
+//             review of that bucket;
+//   c2     -- the first review of the bucket where the running count reaches
+//             `limit` (cut2);
+//   select -- the tuples of reviews before that one, and of it (ties), copied
+//             out with their message's first GK_SAMPLE_MSG bytes.
+constexpr uint32_t SB1 = 256;
+__device__ __forceinline__ uint32_t coarse_of(uint32_t review, uint32_t nrev) {
+  return (uint32_t)(((uint64_t)review * SB1) / nrev);
 }
-
-// (one atomic per tuple: aggregating a wave's lanes per distinct cell with
-// ballots measured slower, profiles/r04/r04x_ab.txt gk_sample 0.38 -> 0.47 ms)
-__global__ void __launch_bounds__(256) gk_sample_hist(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
-                                                      uint32_t nb, uint32_t* hist) {
+// the first review of coarse bucket b (review r is in b iff
+// b * nrev <= r * SB1 < (b + 1) * nrev)
+__device__ __forceinline__ uint32_t coarse_lo(uint32_t b, uint32_t nrev) {
+  return (uint32_t)(((uint64_t)b * nrev + SB1 - 1) / SB1);
+}
+extern __shared__ uint32_t gk_sample_lds[];
+__global__ void __launch_bounds__(256) gk_sample_h1(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
+                                                    uint32_t ncons, int lds, uint32_t* h1) {
+  const uint32_t nbin = ncons * SB1;
+  if (lds) {
+    for (uint32_t k = threadIdx.x; k < nbin; k += blockDim.x) gk_sample_lds[k] = 0;
+    __syncthreads();
+  }
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Viol v = out[i];
     if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
-    atomicAdd(&hist[(uint64_t)v.constraint * nb + sample_bucket(v.review, nrev, nb)], 1u);
+    const uint32_t bin = v.constraint * SB1 + coarse_of(v.review, nrev);
+    if (lds) atomicAdd(&gk_sample_lds[bin], 1u);
+    else atomicAdd(&h1[bin], 1u);
+  }
+  if (lds) {
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nbin; k += blockDim.x)
+      if (gk_sample_lds[k]) atomicAdd(&h1[k], gk_sample_lds[k]);
   }
 }
 
-__global__ void __launch_bounds__(64) gk_sample_cut(const uint32_t* hist, uint32_t nb, uint32_t limit, uint32_t* cut,
-                                                    unsigned long long* ftot) {
-  const uint32_t c = blockIdx.x, lane = threadIdx.x;
-  const uint32_t* h = hist + (uint64_t)c * nb;
-  uint64_t run = 0;
+// one wavefront per constraint: the first of `nb` counts (after `before`)
+// where the running count reaches `limit`; nb - 1 when it never does
+__device__ __forceinline__ uint32_t first_reaching(const uint32_t* h, uint32_t nb, uint64_t before, uint32_t limit,
+                                                   uint64_t* total) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t run = before;
   uint32_t cb = 0xffffffffu;
   for (uint32_t base = 0; base < nb; base += 64) {
-    uint32_t x = base + lane < nb ? h[base + lane] : 0u;
+    const uint32_t x = base + lane < nb ? h[base + lane] : 0u;
     uint32_t incl = x;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      uint32_t y = __shfl_up(incl, d, 64);
+      const uint32_t y = __shfl_up(incl, d, 64);
       if (lane >= (uint32_t)d) incl += y;
     }
-    uint32_t tot = __shfl(incl, 63, 64);
+    const uint32_t tot = __shfl(incl, 63, 64);
     if (cb == 0xffffffffu && run + tot >= limit) {
-      // first lane whose inclusive count reaches the limit
-      unsigned long long m = __ballot(run + incl >= limit);
+      const unsigned long long m = __ballot(run + incl >= limit);
       cb = base + (uint32_t)__ffsll((long long)m) - 1;
     }
     run += tot;
   }
-  if (lane == 0) {
-    cut[c] = cb == 0xffffffffu ? nb - 1 : cb;
-    ftot[c] = run;
+  *total = run;
+  return cb == 0xffffffffu ? nb - 1 : cb;
+}
+// cut[2c] = coarse cut, cut[2c + 1] = the count before it (then c2's fine cut)
+__global__ void __launch_bounds__(64) gk_sample_c1(const uint32_t* h1, uint32_t limit, uint32_t* cut,
+                                                   unsigned long long* ftot) {
+  const uint32_t c = blockIdx.x;
+  const uint32_t* h = h1 + (uint64_t)c * SB1;
+  uint64_t total = 0;
+  const uint32_t cb = first_reaching(h, SB1, 0, limit, &total);
+  uint32_t before = 0;
+  for (uint32_t k = threadIdx.x; k < cb; k += 64) before += h[k];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) before += __shfl_xor(before, d, 64);
+  if (threadIdx.x == 0) {
+    cut[2 * c] = cb;
+    cut[2 * c + 1] = before;
+    ftot[c] = total;
   }
+}
+__global__ void __launch_bounds__(256) gk_sample_h2(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
+                                                    uint32_t nf, const uint32_t* cut, uint32_t* h2) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Viol v = out[i];
+    const uint32_t b = coarse_of(v.review, nrev);
+    if (b != cut[2 * v.constraint]) continue;
+    if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
+    atomicAdd(&h2[(uint64_t)v.constraint * nf + (v.review - coarse_lo(b, nrev))], 1u);
+  }
+}
+__global__ void __launch_bounds__(64) gk_sample_c2(const uint32_t* h2, uint32_t nf, uint32_t limit, uint32_t* cut) {
+  const uint32_t c = blockIdx.x;
+  uint64_t total = 0;
+  const uint32_t f = first_reaching(h2 + (uint64_t)c * nf, nf, cut[2 * c + 1], limit, &total);
+  __syncthreads();
+  if (threadIdx.x == 0) cut[2 * c + 1] = f;
 }
 
 __global__ void __launch_bounds__(256) gk_sample_select(const Viol* out, uint64_t n, const uint32_t* rflags, uint32_t nrev,
-                                                        uint32_t nb, const uint32_t* cut, const char* bytes,
-                                                        SampleRec* cand, uint32_t cap, unsigned int* ncand) {
+                                                        const uint32_t* cut, const char* bytes, SampleRec* cand,
+                                                        uint32_t cap, unsigned int* ncand) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const Viol v = out[i];
+    const uint32_t b = coarse_of(v.review, nrev), cb = cut[2 * v.constraint];
+    if (b > cb || (b == cb && v.review - coarse_lo(b, nrev) > cut[2 * v.constraint + 1])) continue;
     if (rflags && (rflags[v.review] & (RF_ERROR | RF_FALLBACK))) continue;
-    if (sample_bucket(v.review, nrev, nb) > cut[v.constraint]) continue;
     uint32_t slot = atomicAdd(ncand, 1u);
     if (slot >= cap) continue;  // the host grows the buffer and runs this pass again
     SampleRec& r = cand[slot];
@@ -781,19 +952,33 @@ extern "C" int gk_launch_filter(const gk::Viol* out, uint64_t n, uint32_t* rflag
 }
 
 extern "C" int gk_launch_sample(const gk::Viol* out, uint64_t n, uint32_t* rflags, uint32_t nrev, const uint8_t* cerr,
-                                uint32_t ncons, uint32_t nb, uint32_t limit, uint32_t* hist, uint32_t* cut,
+                                uint32_t ncons, uint32_t nf, uint32_t limit, uint32_t* hist, uint32_t* cut,
                                 unsigned long long* ftot, const char* bytes, gk::SampleRec* cand, uint32_t cap,
                                 unsigned int* ncand, int select_only, hipStream_t stream) {
+  // hist: ncons * SB1 coarse counts, then ncons * nf fine counts
+  // (nf = gk_sample_fine(nrev)); cut: 2 words per constraint
   uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
   if (blocks == 0) blocks = 1;
   if (!select_only) {
     if (cerr) hipLaunchKernelGGL(gk::gk_mark_ea_error, dim3(blocks), dim3(256), 0, stream, out, n, cerr, rflags);
-    (void)hipMemsetAsync(hist, 0, (size_t)ncons * nb * 4, stream);
-    hipLaunchKernelGGL(gk::gk_sample_hist, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev, nb, hist);
-    hipLaunchKernelGGL(gk::gk_sample_cut, dim3(ncons), dim3(64), 0, stream, (const uint32_t*)hist, nb, limit, cut, ftot);
+    uint32_t* h1 = hist;
+    uint32_t* h2 = hist + (size_t)ncons * gk::SB1;
+    (void)hipMemsetAsync(hist, 0, (size_t)ncons * (gk::SB1 + nf) * 4, stream);
+    const size_t lds = (size_t)ncons * gk::SB1 * 4;
+    const bool use_lds = lds <= 65536;
+    // fewer, longer-running blocks for the LDS histogram: each flushes its bins once
+    const uint32_t hb = use_lds ? std::min<uint32_t>(blocks, 512) : blocks;
+    hipLaunchKernelGGL(gk::gk_sample_h1, dim3(hb), dim3(256), use_lds ? lds : 0, stream, out, n, (const uint32_t*)rflags,
+                       nrev, ncons, use_lds ? 1 : 0, h1);
+    hipLaunchKernelGGL(gk::gk_sample_c1, dim3(ncons), dim3(64), 0, stream, (const uint32_t*)h1, limit, cut, ftot);
+    hipLaunchKernelGGL(gk::gk_sample_h2, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev, nf,
+                       (const uint32_t*)cut, h2);
+    hipLaunchKernelGGL(gk::gk_sample_c2, dim3(ncons), dim3(64), 0, stream, (const uint32_t*)h2, nf, limit, cut);
   }
   (void)hipMemsetAsync(ncand, 0, 4, stream);
-  hipLaunchKernelGGL(gk::gk_sample_select, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev, nb,
+  hipLaunchKernelGGL(gk::gk_sample_select, dim3(blocks), dim3(256), 0, stream, out, n, (const uint32_t*)rflags, nrev,
                      (const uint32_t*)cut, bytes, cand, cap, ncand);
   return (int)hipGetLastError();
 }
+// fine bins per constraint for nrev reviews (the reviews of one coarse bucket)
+extern "C" uint32_t gk_sample_fine(uint32_t nrev) { return nrev / gk::SB1 + 2; }
