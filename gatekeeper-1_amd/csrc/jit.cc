@@ -159,7 +159,11 @@ FmtFlow fmt_flow(const Program& p, const CodeBank& bank) {
 // (or forced from a deferred sprintf), and all facts die at OP_ITER_NEXT, where
 // the lane heap of the previous iteration is reclaimed.
 struct LookFlow {
-  struct Fact { uint16_t base; uint32_t kidx; uint16_t res; };
+  // kidx: a constant's index, or DYN | key register (a lookup with a computed
+  // key, e.g. RequiredProbes' ctr[probe]); res: the register holding the
+  // result, or NOREG when it is in the shadow local of the lookup at pc spc
+  static constexpr uint32_t DYN = 0x80000000u;
+  struct Fact { uint16_t base; uint32_t kidx; uint16_t res; uint32_t spc = 0; };
   struct State {
     bool top = true;                     // not reached yet (identity of the meet)
     std::vector<Fact> facts;             // sorted by (base, kidx)
@@ -172,6 +176,13 @@ struct LookFlow {
     for (const Fact& f : in[k].facts) if (f.base == base && f.kidx == kidx) return f.res;
     return -1;
   }
+  // the pc whose shadow local holds R[base][R[key]] on entry to k, or -1
+  int find_dyn(uint32_t k, uint16_t base, uint16_t key) const {
+    if (k >= in.size() || in[k].top) return -1;
+    for (const Fact& f : in[k].facts)
+      if (f.base == base && f.kidx == (DYN | key) && f.res == 0xffff) return (int)f.spc;
+    return -1;
+  }
   int konst(uint32_t k, uint16_t r) const {
     if (k >= in.size() || in[k].top) return -1;
     auto it = in[k].konst.find(r);
@@ -179,12 +190,97 @@ struct LookFlow {
   }
 };
 
+// Document-derived registers (must-analysis): on entry to each instruction,
+// the registers that hold, on every path, a value read out of the review or
+// the parameters -- a document node or a scalar, never a lane-heap value --
+// so a lookup on them stays valid when a loop reclaims its heap (look_flow).
+FmtFlow doc_flow(const Program& p, const CodeBank& bank) {
+  const uint32_t b0 = p.code_off, n = p.code_len;
+  FmtFlow F;
+  F.nw = (p.nregs + 64) / 64;
+  F.in.assign(n, std::vector<uint64_t>(F.nw, ~0ull));  // unreached: TOP
+  F.reached.assign(n, 0);
+  auto has = [&](const std::vector<uint64_t>& s, uint32_t r) { return r < 64 * F.nw && ((s[r >> 6] >> (r & 63)) & 1); };
+  auto put = [&](std::vector<uint64_t>& s, uint32_t r, bool v) {
+    if (r >= 64 * F.nw) return;
+    if (v) s[r >> 6] |= 1ull << (r & 63);
+    else s[r >> 6] &= ~(1ull << (r & 63));
+  };
+  std::vector<uint32_t> work;
+  auto flow = [&](uint32_t to, const std::vector<uint64_t>& s) {
+    if (to < b0 || to >= b0 + n) return;
+    uint32_t k = to - b0;
+    bool ch = !F.reached[k];
+    F.reached[k] = 1;
+    for (uint32_t w = 0; w < F.nw; ++w) {
+      uint64_t nv = F.in[k][w] & s[w];
+      if (nv != F.in[k][w]) { F.in[k][w] = nv; ch = true; }
+    }
+    if (ch) work.push_back(k);
+  };
+  if (n) {
+    F.reached[0] = 1;
+    std::fill(F.in[0].begin(), F.in[0].end(), 0ull);  // entry: nothing is known
+    work.push_back(0);
+  }
+  while (!work.empty()) {
+    uint32_t k = work.back();
+    work.pop_back();
+    const Ins& in = bank.code[b0 + k];
+    std::vector<uint64_t> s = F.in[k];
+    const uint32_t next = b0 + k + 1;
+    switch (in.op) {
+      case OP_END: case OP_FAIL_FALLBACK: continue;
+      case OP_JMP: flow(in.x, s); continue;
+      case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: flow(in.x, s); flow(next, s); continue;
+      case OP_ITER_NEXT: {
+        flow(in.x, s);
+        const bool dv = has(s, in.a);
+        if (in.b != 0xffff) put(s, in.b, dv);  // an object's key (interned string) or an array index
+        if (in.c != 0xffff) put(s, in.c, dv);
+        flow(next, s);
+        continue;
+      }
+      case OP_JPROBE:
+        put(s, in.a, false);
+        put(s, in.a + 1u, false);
+        flow(in.x, s);
+        flow(next, s);
+        continue;
+      case OP_JNEXT:
+        flow(in.x, s);
+        put(s, in.b, false);
+        flow(next, s);
+        continue;
+      case OP_MEMO_GET: {
+        std::vector<uint64_t> t = s;
+        put(t, in.a, false);
+        flow(in.x, t);
+        flow(next, s);
+        continue;
+      }
+      case OP_LOADREV: case OP_LOADPARAM: put(s, in.a, true); break;
+      case OP_MOV: case OP_GET: case OP_GETK: put(s, in.a, has(s, in.b)); break;
+      case OP_ITER_INIT: put(s, in.a, has(s, in.b)); put(s, in.a + 1u, false); break;
+      case OP_EMIT: case OP_MEMO_PUT: case OP_ORD: break;
+      default: put(s, in.a, false); break;
+    }
+    flow(next, s);
+  }
+  return F;
+}
+
+static bool dyn_cse_on() {
+  const char* v = getenv("GKGPU_JIT_DYNCSE");  // A/B switch, default on
+  return !v || atoi(v) != 0;
+}
+
 static bool lookflow_on() {
   const char* v = getenv("GKGPU_JIT_CSE");  // A/B switch, default on
   return !v || atoi(v) != 0;
 }
 
-LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
+LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F, const FmtFlow& DF) {
   const uint32_t b0 = p.code_off, n = p.code_len;
   LookFlow LF;
   LF.in.assign(n, LookFlow::State{});
@@ -193,9 +289,16 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
   auto kill = [](State& s, uint32_t r) {
     if (r == 0xffff) return;
     s.facts.erase(std::remove_if(s.facts.begin(), s.facts.end(),
-                                 [&](const LookFlow::Fact& f) { return f.base == r || f.res == r; }),
+                                 [&](const LookFlow::Fact& f) {
+                                   return f.base == r || f.res == r || f.kidx == (LookFlow::DYN | r);
+                                 }),
                   s.facts.end());
     s.konst.erase((uint16_t)r);
+  };
+  auto keep_docs = [&](State& s, uint32_t k) {
+    s.facts.erase(std::remove_if(s.facts.begin(), s.facts.end(),
+                                 [&](const LookFlow::Fact& f) { return !(DF.reached[k] && DF.has(k, f.base)); }),
+                  s.facts.end());
   };
   auto add = [](State& s, uint16_t base, uint32_t kidx, uint16_t res) {
     if (base == res) return;
@@ -215,7 +318,7 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
     std::vector<LookFlow::Fact> nf;
     for (const auto& f : d.facts)
       for (const auto& g : s.facts)
-        if (f.base == g.base && f.kidx == g.kidx && f.res == g.res) { nf.push_back(f); break; }
+        if (f.base == g.base && f.kidx == g.kidx && f.res == g.res && f.spc == g.spc) { nf.push_back(f); break; }
     std::map<uint16_t, uint32_t> nk;
     for (const auto& kv : d.konst) {
       auto it = s.konst.find(kv.first);
@@ -240,7 +343,10 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
       case OP_JMP: flow(in.x, s); continue;
       case OP_JUNDEF: case OP_JFALSE: case OP_JTRUE: flow(in.x, s); flow(next, s); continue;
       case OP_ITER_NEXT: {
-        s.facts.clear();
+        // the previous iteration's heap is reclaimed: a fact survives only if
+        // its base holds a document (or parameters) value on every path, so
+        // that the looked-up value is no heap value either (doc_flow)
+        keep_docs(s, k);
         flow(in.x, s);
         kill(s, in.b);
         kill(s, in.c);
@@ -255,7 +361,7 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         continue;
       case OP_JNEXT:
         // like OP_ITER_NEXT: the previous iteration's heap is reclaimed here
-        s.facts.clear();
+        keep_docs(s, k);
         flow(in.x, s);
         kill(s, in.b);
         flow(next, s);
@@ -281,6 +387,18 @@ LookFlow look_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         const int kc = it == s.konst.end() ? -1 : (int)it->second;
         kill(s, in.a);
         if (kc >= 0 && in.a != in.c) add(s, in.b, (uint32_t)kc, in.a);
+        else if (kc < 0 && in.a != in.b && in.a != in.c && dyn_cse_on() && DF.reached[k] && DF.has(k, in.b)) {
+          // computed key: the result in this site's shadow local
+          s.facts.erase(std::remove_if(s.facts.begin(), s.facts.end(),
+                                       [&](const LookFlow::Fact& f) {
+                                         return f.base == in.b && f.kidx == (LookFlow::DYN | in.c);
+                                       }),
+                        s.facts.end());
+          s.facts.push_back({in.b, LookFlow::DYN | in.c, 0xffff, b0 + k});
+          std::sort(s.facts.begin(), s.facts.end(), [](const LookFlow::Fact& x, const LookFlow::Fact& y) {
+            return x.base != y.base ? x.base < y.base : x.kidx < y.kidx;
+          });
+        }
         break;
       }
       case OP_ITER_INIT: kill(s, in.a); kill(s, in.a + 1u); break;
@@ -541,7 +659,16 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   const char* lm = getenv("GKGPU_JIT_LMEMO");
   if (!lm || atoi(lm) == 0) for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
   FmtFlow F = fmt_flow(p, bank);
-  LookFlow LK = look_flow(p, bank, F);
+  FmtFlow DF = doc_flow(p, bank);
+  LookFlow LK = look_flow(p, bank, F, DF);
+  // computed-key lookups whose result a later lookup reuses: their shadow locals
+  std::set<uint32_t> shadowed;
+  for (uint32_t pc = b0; pc < b1; ++pc) {
+    const Ins& in = bank.code[pc];
+    if (in.op != OP_GET || LK.konst(pc - b0, in.c) >= 0) continue;
+    const int spc = LK.find_dyn(pc - b0, in.b, in.c);
+    if (spc >= 0 && (uint32_t)spc != pc) shadowed.insert((uint32_t)spc);
+  }
   FmtFlow PF = param_flow(p, bank);
   const bool pstage = lds_stage_on();
   Gen g;
@@ -573,6 +700,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r) << (init ? " = 0" : "");
   if (!p.nregs) o << "unused_";
   o << ";\n";
+  for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)
   for (uint32_t m : lslots) {
     o << "  uint64_t mk0_" << m << ", mk1_" << m << ", mv_" << m << "; bool mok_" << m << " = false;\n";
@@ -630,10 +758,13 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       case OP_GET: {
         const int kc = LK.konst(k, in.c);
         const int have = kc >= 0 ? LK.find(k, in.b, (uint32_t)kc) : -1;
+        const int dyn = kc < 0 ? LK.find_dyn(k, in.b, in.c) : -1;
         if (have == (int)in.a) o << "/* " << a << " holds " << b << "[" << c << "] */";
         else if (have >= 0) o << a << " = " << R((uint32_t)have) << ";  // = vget(L, " << b << ", " << c << ")";
+        else if (dyn >= 0 && (uint32_t)dyn != pc) o << a << " = dk" << dyn << ";  // = vget(L, " << b << ", " << c << ")";
         else if (pstage && PF.has(k, in.b)) { o << a << " = vget_p(L, " << b << ", " << c << ", plo, pn);"; g.param_reads = true; }
         else o << a << " = vget(L, " << b << ", " << c << ");";
+        if (shadowed.count(pc)) o << " dk" << pc << " = " << a << ";";
         break;
       }
       case OP_GETK: {

@@ -43,9 +43,23 @@ def test_lookup_cse_reuses_prologue_lookups_in_inlined_calls():
     reused = on.count("// = vget(")
     assert reused >= 8, reused
     assert off.count("// = vget(") == 0
-    # every lookup is either still a call or a copy
+    # every lookup is either still a call, a copy, or already in its register
     calls = lambda src: src.count("= vget(L,") + src.count("= vget_p(L,")  # noqa: E731
-    assert calls(on) == calls(off)
+    assert calls(on) + on.count(" holds ") == calls(off) + off.count(" holds ")
+
+
+def test_computed_key_lookup_reuses_its_shadow():
+    """jit.cc look_flow computed-key facts: K8sRequiredProbes reads
+    ctr[probe] in probe_is_missing's first body and again in
+    probe_field_empty; the second read copies the first's shadow local (the
+    result register itself is reused in between).  GKGPU_JIT_DYNCSE=0: both
+    scan the container."""
+    on = _dump("K8sRequiredProbes")
+    off = _dump("K8sRequiredProbes", [("GKGPU_JIT_DYNCSE", "0")])
+    import re
+    assert re.search(r"uint64_t dk\d+;", on)
+    assert re.search(r"= dk\d+;  // = vget\(L, ", on)
+    assert "dk" not in off.split("_pred(")[1]
 
 
 def test_parameter_reads_come_from_the_wave_lds_stage():
