@@ -208,8 +208,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // The tuple count is read on the device (counters[0]): the passes follow the
 // predicate kernels on the stream with no host round trip.
 
+// the slots the passes read: the dense tuples, or with fused compaction
+// (DevArgs.dout) the predicate kernels' raw slots (counters[5], set by the
+// host before the size pass; the spine turns counters[0] into the dense count)
+__device__ __forceinline__ uint64_t raw_slots() { return gk_args.dout ? gk_args.counters[5] : gk_args.counters[0]; }
 __device__ __forceinline__ uint64_t ntuples() {
-  const uint64_t n = gk_args.counters[0];
+  const uint64_t n = raw_slots();
   return n < gk_args.out_cap ? n : gk_args.out_cap;
 }
 
@@ -346,22 +350,31 @@ __device__ __forceinline__ uint64_t det_word(const Viol& v, uint64_t i) {
 // segment on every lane, and the dispatch paid for it (~1 ms fixed per call).
 __device__ Lane gk_pass_lane;
 
+template <bool FR>
 __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
   __shared__ unsigned long long wsum[4];
+  __shared__ uint32_t wreal[4];
   // an overflowed evaluation is re-run whole by the host: an emission that
   // found its slot but not its staged bytes left that slot unwritten, so the
   // tuples must not be read (the format pass returns here too)
-  if (gk_args.counters[0] > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;
+  if (raw_slots() > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;
   PLane& L = *(PLane*)&gk_pass_lane;
   const uint64_t n = ntuples();
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
-  const bool fl = blockIdx.x < ntile ? fmt_stage() : false;  // block-uniform
+  bool fl = false;  // block-uniform
+  if (FR) fl = blockIdx.x < ntile ? fmt_stage() : false;
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
     unsigned long long s = 0;
+    uint32_t nreal = 0;
     for (uint32_t k = 0; k < FTILE; k += 256) {
       const uint64_t i = t * FTILE + k + threadIdx.x;
       if (i >= n) break;
       const Viol v = gk_args.out[i];
+      if (v.review == VIOL_HOLE) {  // (raw slots only) an unused slot: no bytes
+        gk_args.lens[i] = 0;
+        continue;
+      }
+      ++nreal;
       uint32_t ml = v.msg_len, dl = det_bytes(v);
       bool printable = true;
       if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml, fl);
@@ -386,23 +399,28 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
       s += len;
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    for (int d = 32; d >= 1; d >>= 1) {
+      s += __shfl_xor(s, d, 64);
+      nreal += (uint32_t)__shfl_xor((int)nreal, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) { wsum[threadIdx.x >> 6] = s; wreal[threadIdx.x >> 6] = nreal; }
     __syncthreads();
-    if (threadIdx.x == 0) gk_args.part[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (threadIdx.x == 0) {
+      gk_args.part[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      if (gk_args.tcnt) gk_args.tcnt[t] = wreal[0] + wreal[1] + wreal[2] + wreal[3];
+    }
     __syncthreads();
   }
 }
 
-__global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
-  __shared__ unsigned long long wtot[16];
-  const uint64_t n = ntuples();
-  const uint64_t ntile = (n + FTILE - 1) / FTILE;
+// one block: exclusive prefix of `v` over `ntile` entries in place; the total
+template <class T, class S>
+__device__ __forceinline__ unsigned long long spine_scan(T* v, S* out, uint64_t ntile, unsigned long long* wtot) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long carry = 0;
   for (uint64_t b = 0; b < ntile; b += 1024) {
     const uint64_t i = b + threadIdx.x;
-    const unsigned long long x = i < ntile ? gk_args.part[i] : 0ull;
+    const unsigned long long x = i < ntile ? (unsigned long long)v[i] : 0ull;
     unsigned long long incl = x;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -416,11 +434,24 @@ __global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
       if (k < w) before += wtot[k];
       all += wtot[k];
     }
-    if (i < ntile) gk_args.part[i] = carry + before + incl - x;
+    if (i < ntile) out[i] = (S)(carry + before + incl - x);
     carry += all;
     __syncthreads();
   }
-  if (threadIdx.x == 0) gk_args.counters[3] = carry;
+  return carry;
+}
+__global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
+  __shared__ unsigned long long wtot[16];
+  if (raw_slots() > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;  // re-run by the host
+  const uint64_t n = ntuples();
+  const uint64_t ntile = (n + FTILE - 1) / FTILE;
+  const unsigned long long bytes = spine_scan(gk_args.part, gk_args.part, ntile, wtot);
+  if (gk_args.dout) {
+    // fused compaction: the tiles' dense offsets and the dense tuple count
+    const unsigned long long dense = spine_scan(gk_args.tcnt, gk_args.toff, ntile, wtot);
+    if (threadIdx.x == 0) gk_args.counters[0] = dense;
+  }
+  if (threadIdx.x == 0) gk_args.counters[3] = bytes;
 }
 
 // ------------------------------------------------------------------ compaction
@@ -526,14 +557,14 @@ extern __shared__ uint32_t gk_fmt_stage[];
 
 template <class LO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(uint32_t fstage, DevArgs) {
-  __shared__ uint32_t wtot[4];
+  __shared__ uint32_t wtot[4], wreal[4];
   const uint64_t n = ntuples();
   // an overflowed output buffer: the host grows it and runs the passes again
   // (the tuples stay as the predicate kernels wrote them)
-  if (gk_args.counters[3] > gk_args.bytes_cap || gk_args.counters[0] > gk_args.out_cap ||
+  if (gk_args.counters[3] > gk_args.bytes_cap || raw_slots() > gk_args.out_cap ||
       gk_args.counters[1] > gk_args.ebytes_cap)
     return;
-  PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel
+  PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel<>
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* st = gk_fmt_stage + wv * (fstage / 4);
   uint8_t* stb = (uint8_t*)st;
@@ -542,12 +573,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
   const bool fl = blockIdx.x < ntile ? fmt_stage() : false;  // block-uniform
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {  // block-uniform
     uint64_t run = gk_args.part[t];
+    uint64_t drun = gk_args.dout ? gk_args.toff[t] : 0;  // fused compaction: the tile's dense offset
     for (uint32_t k = 0; k < FTILE; k += 256) {
       const uint64_t tb = t * FTILE + k;
       if (tb >= n) break;  // block-uniform
       const uint64_t i = tb + threadIdx.x;
-      const bool valid = i < n;
+      Viol v{};
+      if (i < n) v = gk_args.out[i];
+      // a hole (raw slots only) prints nothing and has no dense place
+      const bool valid = i < n && v.review != VIOL_HOLE;
       const uint32_t len = valid ? gk_args.lens[i] : 0u;
+      const unsigned long long rm = __ballot(valid);
+      if (lane == 0) wreal[wv] = (uint32_t)__popcll(rm);
       // block-level exclusive prefix of len
       uint32_t incl = len;
 #pragma unroll
@@ -557,14 +594,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       }
       if (lane == 63) wtot[wv] = incl;
       __syncthreads();
-      uint64_t wbase = run;
-      for (uint32_t q = 0; q < wv; ++q) wbase += wtot[q];
+      uint64_t wbase = run, dbase = drun;
+      for (uint32_t q = 0; q < wv; ++q) { wbase += wtot[q]; dbase += wreal[q]; }
       const uint64_t all = (uint64_t)wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      const uint64_t dall = (uint64_t)wreal[0] + wreal[1] + wreal[2] + wreal[3];
       __syncthreads();
       run += all;
+      drun += dall;
       const uint64_t dst = wbase + incl - len;
-      Viol v{};
-      if (valid) v = gk_args.out[i];
+      const uint64_t dpos = dbase + gk_lanes_below(rm);
       const bool defer = valid && (v.pad & VF_DEFER);
       const uint32_t dl = valid ? det_bytes(v) : 0u;
       const uint32_t ml = len - dl;
@@ -630,7 +668,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         v.msg_len = ml;
         v.det_len = dl;
         v.pad = 0;
-        gk_args.out[i] = v;
+        if (gk_args.dout) gk_args.dout[dpos] = v;
+        else gk_args.out[i] = v;
       }
     }
   }
@@ -648,7 +687,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
 extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev, uint64_t hint) {
   const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::FTILE - 1) / gk::FTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
-  hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
+  // the resolved-format size pass (GKGPU_SIZE_RESOLVED, A/B): literal lengths
+  // from the LDS table; else the string table's
+  static const bool size_fr = !getenv("GKGPU_SIZE_RESOLVED") || atoi(getenv("GKGPU_SIZE_RESOLVED")) != 0;
+  if (size_fr && a->fmtr) hipLaunchKernelGGL(gk::gk_size_kernel<true>, dim3(blocks), dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL(gk::gk_size_kernel<false>, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
