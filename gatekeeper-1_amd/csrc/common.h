@@ -319,15 +319,6 @@ struct DevArgs {
   const uint32_t* fmtr;
   const char* fmtb;           // the literals' bytes, padded to a dword
   uint32_t nfmt, nfmtb;       // words of fmtr, bytes of fmtb
-  // compaction fused into the passes (engine.cc, GKGPU_FUSED_COMPACT): the
-  // size / spine / format passes read the predicate kernels' raw slots
-  // (`out`, `frec`, holes included; counters[5] = their count), the size pass
-  // counts each FTILE tile's tuples (tcnt), the spine turns the counts into
-  // dense offsets (toff, counters[0] = the dense count) and the format pass
-  // writes every finished tuple to its dense place in `dout`.  null: in place.
-  Viol* dout;
-  uint32_t* tcnt;
-  unsigned long long* toff;
 };
 // join sites per template program (compiler.cc join_site)
 constexpr uint32_t JMAX_SITES = 4;

@@ -1947,23 +1947,8 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     // the tuples of every launch above packed, then the size, spine and format passes
     // pass grids sized for ~2x this context's last output (GKGPU_PASS_HINT=0: for the capacity)
     const uint64_t pass_hint = env_mode("GKGPU_PASS_HINT", 1, 1) ? std::max<uint64_t>(2 * x->last_tuples, 65536) : 0;
-    // GKGPU_FUSED_COMPACT (A/B switch, default on): the passes read the raw
-    // slots and the format pass writes each tuple to its dense place, instead
-    // of three compaction kernels packing them first
-    const bool fused = env_mode("GKGPU_FUSED_COMPACT", 1, 1) != 0;
-    int flr = 0;
-    if (fused) {
-      a.out = (Viol*)x->d_out_raw.p;
-      a.frec = (uint64_t*)x->d_frec_raw.p;
-      a.dout = (Viol*)x->d_out.p;
-      a.tcnt = (uint32_t*)x->d_ctcnt.p;
-      a.toff = (unsigned long long*)x->d_ctoff.p;
-      // counters[5] = the raw slot count the passes read (the spine sets counters[0] to the dense count)
-      flr = (int)hipMemcpyAsync((char*)x->d_counters.p + 40, x->d_counters.p, 8, hipMemcpyDeviceToDevice, x->stream);
-    } else {
-      flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
-                              (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream, pass_hint);
-    }
+    int flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
+                                (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream, pass_hint);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (compact): ") + hipGetErrorString((hipError_t)flr));
     hipEventRecord(ev[plan.size() + 1], x->stream);
     flr = gk_launch_format(&a, x->stream, &x->events[plan.size() + 2], pass_hint);

@@ -208,12 +208,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // The tuple count is read on the device (counters[0]): the passes follow the
 // predicate kernels on the stream with no host round trip.
 
-// the slots the passes read: the dense tuples, or with fused compaction
-// (DevArgs.dout) the predicate kernels' raw slots (counters[5], set by the
-// host before the size pass; the spine turns counters[0] into the dense count)
-__device__ __forceinline__ uint64_t raw_slots() { return gk_args.dout ? gk_args.counters[5] : gk_args.counters[0]; }
 __device__ __forceinline__ uint64_t ntuples() {
-  const uint64_t n = raw_slots();
+  const uint64_t n = gk_args.counters[0];
   return n < gk_args.out_cap ? n : gk_args.out_cap;
 }
 
@@ -271,20 +267,6 @@ __device__ __forceinline__ bool plain_args(const uint32_t* f, const uint64_t (&a
   }
   return true;
 }
-__device__ __forceinline__ uint32_t size_plain_r(const uint32_t* f, const uint64_t (&a)[FMT_MAXARGS],
-                                                 const StrEnt (&se)[FMT_MAXARGS]) {
-  const uint32_t nseg = f[0];
-  Cnt o{0, false};
-  for (uint32_t s = 0; s < nseg; ++s) {
-    const uint32_t w0 = f[2 + 2 * s], w1 = f[3 + 2 * s];
-    if ((w0 & 0xff) == 0) { o.n += w0 >> 8; continue; }
-    const uint32_t j = w1 & 0xffff;
-    const uint64_t v = sel_arg(a, j);
-    if (vtag(v) == V_STR) o.n += sel_arg(se, j).len;
-    else put_int(o, intof(v));
-  }
-  return o.n;
-}
 template <class O>
 __device__ __forceinline__ void print_plain_r(O& o, const uint32_t* f, const uint64_t (&a)[FMT_MAXARGS],
                                               const StrEnt (&se)[FMT_MAXARGS]) {
@@ -313,18 +295,13 @@ __device__ __forceinline__ void print_plain_r(O& o, const uint32_t* f, const uin
 }
 
 // a deferred tuple's printed message length; false = not printable here
-__device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint64_t i, uint32_t& len, bool fl) {
+// (the string table's lengths: the resolved table staged in LDS measured
+// slower here, 0.20 -> 0.27 ms per config-2 sweep, profiles/r05/)
+__device__ __forceinline__ bool size_deferred_msg(PLane& L, const Viol& v, uint64_t i, uint32_t& len) {
   const uint32_t fidx = v.msg_len & 0xffffffu, na = v.msg_len >> 24;
   uint64_t a[FMT_MAXARGS];
 #pragma unroll
   for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
-  if (fl) {
-    StrEnt se[FMT_MAXARGS];
-    if (plain_args(gk_fmt_lds.r + fidx, a, se, na)) {
-      len = size_plain_r(gk_fmt_lds.r + fidx, a, se);
-      return true;
-    }
-  }
   if (size_plain(fidx, a, len)) return true;
   Cnt cn{0, false};
   if (!fmt_run(L, cn, fidx, [&](uint32_t j) { return a[j]; })) return false;
@@ -350,34 +327,24 @@ __device__ __forceinline__ uint64_t det_word(const Viol& v, uint64_t i) {
 // segment on every lane, and the dispatch paid for it (~1 ms fixed per call).
 __device__ Lane gk_pass_lane;
 
-template <bool FR>
 __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
   __shared__ unsigned long long wsum[4];
-  __shared__ uint32_t wreal[4];
   // an overflowed evaluation is re-run whole by the host: an emission that
   // found its slot but not its staged bytes left that slot unwritten, so the
   // tuples must not be read (the format pass returns here too)
-  if (raw_slots() > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;
+  if (gk_args.counters[0] > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;
   PLane& L = *(PLane*)&gk_pass_lane;
   const uint64_t n = ntuples();
   const uint64_t ntile = (n + FTILE - 1) / FTILE;
-  bool fl = false;  // block-uniform
-  if (FR) fl = blockIdx.x < ntile ? fmt_stage() : false;
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
     unsigned long long s = 0;
-    uint32_t nreal = 0;
     for (uint32_t k = 0; k < FTILE; k += 256) {
       const uint64_t i = t * FTILE + k + threadIdx.x;
       if (i >= n) break;
       const Viol v = gk_args.out[i];
-      if (v.review == VIOL_HOLE) {  // (raw slots only) an unused slot: no bytes
-        gk_args.lens[i] = 0;
-        continue;
-      }
-      ++nreal;
       uint32_t ml = v.msg_len, dl = det_bytes(v);
       bool printable = true;
-      if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml, fl);
+      if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml);
       if (v.pad & VF_DET_VAL) {
         Cnt cn{0, false};
         printable = put_json(L, cn, det_word(v, i)) && printable;
@@ -399,28 +366,23 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
       s += len;
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      s += __shfl_xor(s, d, 64);
-      nreal += (uint32_t)__shfl_xor((int)nreal, d, 64);
-    }
-    if ((threadIdx.x & 63) == 0) { wsum[threadIdx.x >> 6] = s; wreal[threadIdx.x >> 6] = nreal; }
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      gk_args.part[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-      if (gk_args.tcnt) gk_args.tcnt[t] = wreal[0] + wreal[1] + wreal[2] + wreal[3];
-    }
+    if (threadIdx.x == 0) gk_args.part[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }
 }
 
-// one block: exclusive prefix of `v` over `ntile` entries in place; the total
-template <class T, class S>
-__device__ __forceinline__ unsigned long long spine_scan(T* v, S* out, uint64_t ntile, unsigned long long* wtot) {
+__global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
+  __shared__ unsigned long long wtot[16];
+  const uint64_t n = ntuples();
+  const uint64_t ntile = (n + FTILE - 1) / FTILE;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long carry = 0;
   for (uint64_t b = 0; b < ntile; b += 1024) {
     const uint64_t i = b + threadIdx.x;
-    const unsigned long long x = i < ntile ? (unsigned long long)v[i] : 0ull;
+    const unsigned long long x = i < ntile ? gk_args.part[i] : 0ull;
     unsigned long long incl = x;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -434,24 +396,11 @@ __device__ __forceinline__ unsigned long long spine_scan(T* v, S* out, uint64_t 
       if (k < w) before += wtot[k];
       all += wtot[k];
     }
-    if (i < ntile) out[i] = (S)(carry + before + incl - x);
+    if (i < ntile) gk_args.part[i] = carry + before + incl - x;
     carry += all;
     __syncthreads();
   }
-  return carry;
-}
-__global__ void __launch_bounds__(1024) gk_scan_spine(DevArgs) {
-  __shared__ unsigned long long wtot[16];
-  if (raw_slots() > gk_args.out_cap || gk_args.counters[1] > gk_args.ebytes_cap) return;  // re-run by the host
-  const uint64_t n = ntuples();
-  const uint64_t ntile = (n + FTILE - 1) / FTILE;
-  const unsigned long long bytes = spine_scan(gk_args.part, gk_args.part, ntile, wtot);
-  if (gk_args.dout) {
-    // fused compaction: the tiles' dense offsets and the dense tuple count
-    const unsigned long long dense = spine_scan(gk_args.tcnt, gk_args.toff, ntile, wtot);
-    if (threadIdx.x == 0) gk_args.counters[0] = dense;
-  }
-  if (threadIdx.x == 0) gk_args.counters[3] = bytes;
+  if (threadIdx.x == 0) gk_args.counters[3] = carry;
 }
 
 // ------------------------------------------------------------------ compaction
@@ -557,14 +506,14 @@ extern __shared__ uint32_t gk_fmt_stage[];
 
 template <class LO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gk_format_kernel(uint32_t fstage, DevArgs) {
-  __shared__ uint32_t wtot[4], wreal[4];
+  __shared__ uint32_t wtot[4];
   const uint64_t n = ntuples();
   // an overflowed output buffer: the host grows it and runs the passes again
   // (the tuples stay as the predicate kernels wrote them)
-  if (gk_args.counters[3] > gk_args.bytes_cap || raw_slots() > gk_args.out_cap ||
+  if (gk_args.counters[3] > gk_args.bytes_cap || gk_args.counters[0] > gk_args.out_cap ||
       gk_args.counters[1] > gk_args.ebytes_cap)
     return;
-  PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel<>
+  PLane& L = *(PLane*)&gk_pass_lane;  // see gk_size_kernel
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* st = gk_fmt_stage + wv * (fstage / 4);
   uint8_t* stb = (uint8_t*)st;
@@ -573,18 +522,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
   const bool fl = blockIdx.x < ntile ? fmt_stage() : false;  // block-uniform
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {  // block-uniform
     uint64_t run = gk_args.part[t];
-    uint64_t drun = gk_args.dout ? gk_args.toff[t] : 0;  // fused compaction: the tile's dense offset
     for (uint32_t k = 0; k < FTILE; k += 256) {
       const uint64_t tb = t * FTILE + k;
       if (tb >= n) break;  // block-uniform
       const uint64_t i = tb + threadIdx.x;
-      Viol v{};
-      if (i < n) v = gk_args.out[i];
-      // a hole (raw slots only) prints nothing and has no dense place
-      const bool valid = i < n && v.review != VIOL_HOLE;
+      const bool valid = i < n;
       const uint32_t len = valid ? gk_args.lens[i] : 0u;
-      const unsigned long long rm = __ballot(valid);
-      if (lane == 0) wreal[wv] = (uint32_t)__popcll(rm);
       // block-level exclusive prefix of len
       uint32_t incl = len;
 #pragma unroll
@@ -594,15 +537,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       }
       if (lane == 63) wtot[wv] = incl;
       __syncthreads();
-      uint64_t wbase = run, dbase = drun;
-      for (uint32_t q = 0; q < wv; ++q) { wbase += wtot[q]; dbase += wreal[q]; }
+      uint64_t wbase = run;
+      for (uint32_t q = 0; q < wv; ++q) wbase += wtot[q];
       const uint64_t all = (uint64_t)wtot[0] + wtot[1] + wtot[2] + wtot[3];
-      const uint64_t dall = (uint64_t)wreal[0] + wreal[1] + wreal[2] + wreal[3];
       __syncthreads();
       run += all;
-      drun += dall;
       const uint64_t dst = wbase + incl - len;
-      const uint64_t dpos = dbase + gk_lanes_below(rm);
+      Viol v{};
+      if (valid) v = gk_args.out[i];
       const bool defer = valid && (v.pad & VF_DEFER);
       const uint32_t dl = valid ? det_bytes(v) : 0u;
       const uint32_t ml = len - dl;
@@ -668,8 +610,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         v.msg_len = ml;
         v.det_len = dl;
         v.pad = 0;
-        if (gk_args.dout) gk_args.dout[dpos] = v;
-        else gk_args.out[i] = v;
+        gk_args.out[i] = v;
       }
     }
   }
@@ -687,11 +628,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
 extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev, uint64_t hint) {
   const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::FTILE - 1) / gk::FTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
-  // the resolved-format size pass (GKGPU_SIZE_RESOLVED, A/B): literal lengths
-  // from the LDS table; else the string table's
-  static const bool size_fr = !getenv("GKGPU_SIZE_RESOLVED") || atoi(getenv("GKGPU_SIZE_RESOLVED")) != 0;
-  if (size_fr && a->fmtr) hipLaunchKernelGGL(gk::gk_size_kernel<true>, dim3(blocks), dim3(256), 0, stream, *a);
-  else hipLaunchKernelGGL(gk::gk_size_kernel<false>, dim3(blocks), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
   if (ev) hipEventRecord(ev[1], stream);
