@@ -1399,6 +1399,13 @@ __device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, bool w
 // wave in LDS: next slot, slots left, slots used so far.
 constexpr uint32_t VIOL_HOLE = 0xffffffffu;
 constexpr uint64_t CHUNK_MIN = 64, CHUNK_MAX = 1024;
+// a new chunk takes the wave's slots so far divided by GK_CHUNK_DIV (clamped):
+// 1 doubles (a wave's last chunk leaves up to half its slots as holes, which
+// the wave writes and the compaction reads); larger divisors trade holes for
+// a few more atomics
+#ifndef GK_CHUNK_DIV
+#define GK_CHUNK_DIV 1
+#endif
 #ifndef GK_HOST
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
@@ -1425,7 +1432,8 @@ __device__ __forceinline__ uint64_t slot_reserve(bool want) {
   const uint64_t used = st[2];
   if (n > left) {
     mark_holes(base, left);
-    uint64_t take = used < CHUNK_MIN ? CHUNK_MIN : used > CHUNK_MAX ? CHUNK_MAX : used;
+    const uint64_t want = used / GK_CHUNK_DIV;
+    uint64_t take = want < CHUNK_MIN ? CHUNK_MIN : want > CHUNK_MAX ? CHUNK_MAX : want;
     if (take < n) take = n;
     uint64_t b = 0;
     if (gk_lanes_below(__ballot(true)) == 0) b = (uint64_t)atomicAdd(&gk_args.counters[0], (unsigned long long)take);
