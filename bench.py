@@ -392,6 +392,11 @@ def main():
                 "dist_backend": (os.environ.get("GKGPU_DIST_BACKEND", "nccl") if dist is not None else None),
                 "stage_s": round(t_stage, 3),
                 "stage_s_max_over_ranks": round(t_stage_max, 3),
+                # host -> device bytes of the staged batch (16-B document nodes
+                # + 48-B review columns; the shared string table is uploaded
+                # separately and grows only by the page's new strings)
+                "upload_bytes": batch.device_bytes(),
+                "upload_bytes_per_resource": round(batch.device_bytes() / max(1, nrev), 1),
                 "stage_ms": {"parse": round(stage_ms[0], 1), "flatten": round(stage_ms[1], 1),
                              "upload": round(stage_ms[2], 1)},
                 "gen_s": round(t_gen, 3),
