@@ -1399,12 +1399,13 @@ __device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, bool w
 // wave in LDS: next slot, slots left, slots used so far.
 constexpr uint32_t VIOL_HOLE = 0xffffffffu;
 constexpr uint64_t CHUNK_MIN = 64, CHUNK_MAX = 1024;
-// a new chunk takes the wave's slots so far divided by GK_CHUNK_DIV (clamped):
+// a new chunk takes the wave's slots so far divided by GK_CHUNK_DIV (clamped;
+// 4 since round 5: compaction 0.33 -> 0.31 ms, profiles/r05/r05g_chunk_ab.txt):
 // 1 doubles (a wave's last chunk leaves up to half its slots as holes, which
 // the wave writes and the compaction reads); larger divisors trade holes for
 // a few more atomics
 #ifndef GK_CHUNK_DIV
-#define GK_CHUNK_DIV 1
+#define GK_CHUNK_DIV 4
 #endif
 #ifndef GK_HOST
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
