@@ -1133,10 +1133,20 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // r04s_ab.txt; all templates at 16 vs 32: config 4 1,774 vs 1,169 M evals/s,
 // r04zd_ab.txt).  GKGPU_JIT_WPE and GKGPU_LDS_HEAP override both choices (WPE
 // 0 = the compiler's choice).
+// Round 5 (profiles/r05/r05h_wpe_ab.txt, r05i_wpe_ab.txt): 4 waves for small
+// programs without regular expressions -- K8sRequiredProbes 1.55 -> 1.45 ms
+// (config 2) and 4.29 -> 4.11 ms (config 4), K8sAllowedRepos 0.195 -> 0.179 /
+// 4.12 -> 4.04 ms -- while the regex templates (their DFAs staged in LDS) and
+// K8sContainerLimits lose at 4.
 static bool small_program(const Program& p) { return p.nregs <= 48; }
-static std::string wpe_suffix(const Program& p) {
+static int wpe_of(const Program& p) {
   const char* w = getenv("GKGPU_JIT_WPE");
-  int n = w ? atoi(w) : (small_program(p) ? 3 : 2);
+  if (w) return atoi(w);
+  if (!small_program(p)) return 2;
+  return p.uses_regex ? 3 : 4;
+}
+static std::string wpe_suffix(const Program& p) {
+  const int n = wpe_of(p);
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 static int lds_heap_words(const Program& p) {
@@ -1189,8 +1199,7 @@ struct StagePlan { bool params = false, dfa = false; int memo = 0; };
 static StagePlan stage_plan(const Program& p, const Gen& g, int depth) {
   StagePlan sp;
   if (!lds_stage_on()) return sp;
-  const char* w = getenv("GKGPU_JIT_WPE");
-  const int wpe = w ? atoi(w) : (small_program(p) ? 3 : 2);
+  const int wpe = wpe_of(p);
   const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
   // lane heap words, lane scalars and (with the scalars) the loop watermarks;
   // then, as they fit: the memo cache, the DFAs, the parameters
