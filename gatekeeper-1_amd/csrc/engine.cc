@@ -3431,14 +3431,16 @@ int gk_results_copy_device_output(gk_engine* e, const gk_results* r, void* tuple
     int lr = gk_launch_filter((const Viol*)x->d_out.p, r->dev_tuples, (uint32_t*)x->d_rflags.p,
                               any_err ? (const uint8_t*)x->d_cerr.p : nullptr, (Viol*)tuples_dst,
                               (unsigned long long*)x->d_ncand.p, x->stream);
-    if (lr != 0 || hipMemcpyAsync(&kept, x->d_ncand.p, 8, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
-        hipStreamSynchronize(x->stream) != hipSuccess)
-      return fail(e, GK_EDEVICE, "device copy failed");
+    if (lr != 0) return fail(e, GK_EDEVICE, std::string("device copy failed (filter launch): ") + hipGetErrorString((hipError_t)lr));
+    hipError_t ce = hipMemcpyAsync(&kept, x->d_ncand.p, 8, hipMemcpyDeviceToHost, x->stream);
+    if (ce == hipSuccess) ce = hipStreamSynchronize(x->stream);
+    if (ce != hipSuccess) return fail(e, GK_EDEVICE, std::string("device copy failed (filter): ") + hipGetErrorString(ce));
   }
-  if (bytes_dst && r->dev_bytes &&
-      (hipMemcpyAsync(bytes_dst, x->d_bytes.p, r->dev_bytes, hipMemcpyDeviceToDevice, x->stream) != hipSuccess ||
-       hipStreamSynchronize(x->stream) != hipSuccess))
-    return fail(e, GK_EDEVICE, "device copy failed");
+  if (bytes_dst && r->dev_bytes) {
+    hipError_t ce = hipMemcpyAsync(bytes_dst, x->d_bytes.p, r->dev_bytes, hipMemcpyDeviceToDevice, x->stream);
+    if (ce == hipSuccess) ce = hipStreamSynchronize(x->stream);
+    if (ce != hipSuccess) return fail(e, GK_EDEVICE, std::string("device copy failed (bytes): ") + hipGetErrorString(ce));
+  }
   if (n_tuples) *n_tuples = kept;
   return GK_OK;
 }

@@ -40,6 +40,8 @@ PY
            tail -4 "$OUT/pytest_parity.log"; [ $rc = 0 ] || exit 1 ;;
     audit) timeout -k 10 900 python -u -m pytest tests/test_audit_cache.py tests/test_audit_writer.py tests/test_parallel_gpu.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_audit.log" 2>&1; rc=$?
            tail -4 "$OUT/pytest_audit.log"; [ $rc = 0 ] || exit 1 ;;
+    scale4) timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -q -k config4 --timeout 300 --timeout-method thread > "$OUT/pytest_scale4.log" 2>&1; rc=$?
+           tail -4 "$OUT/pytest_scale4.log"; grep -E "^E " "$OUT/pytest_scale4.log" | head -5; [ $rc = 0 ] || exit 1 ;;
     early) bash tools/gpu_bench_ab.sh "$TAG/early2" "--steps 10 --warmup 2 --shard-leg off" "" "GKGPU_FN_EARLY=1" || exit 1
            bash tools/gpu_bench_ab.sh "$TAG/early4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FN_EARLY=1" || exit 1 ;;
     ab2) IFS=';' read -ra S <<< "$AB2"; bash tools/gpu_bench_ab.sh "$TAG/ab2" "--steps 10 --warmup 2 --shard-leg off" "${S[@]}" || exit 1 ;;
