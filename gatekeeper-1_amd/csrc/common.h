@@ -319,10 +319,6 @@ struct DevArgs {
   const uint32_t* fmtr;
   const char* fmtb;           // the literals' bytes, padded to a dword
   uint32_t nfmt, nfmtb;       // words of fmtr, bytes of fmtb
-  // message dedup of a sweep (kernels.hip md_owner): open-addressing table of
-  // (key hash << 32 | owner tuple + 1), cleared per evaluation; null: off
-  unsigned long long* mdtab;
-  uint32_t mdmask;            // slots - 1 (a power of two)
 };
 // join sites per template program (compiler.cc join_site)
 constexpr uint32_t JMAX_SITES = 4;
@@ -348,11 +344,7 @@ constexpr uint32_t FMT_MAXARGS = 6;
 // deferred message's details (unless VF_DET_*) are at ebytes[msg_off, +det_len)
 //   VF_NOPRINT set by the size pass: the message or details cannot be printed
 //              on the GPU (the review goes to the CPU); the tuple gets no bytes
-//   VF_DUP     set by the size pass (message dedup, DevArgs.mdtab): the tuple's
-//              message and details equal those of tuple msg_off (its format,
-//              plain argument words and `{}` details); it gets no bytes of its
-//              own, and gk_fixup_dups points it at that tuple's bytes
-constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2, VF_DET_VAL = 4, VF_NOPRINT = 8, VF_DUP = 16;
+constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2, VF_DET_VAL = 4, VF_NOPRINT = 8;
 // the size / format passes work in tiles of FTILE consecutive tuples
 constexpr uint32_t FTILE = 256;  // one block pass: a small output still spreads over many blocks
 

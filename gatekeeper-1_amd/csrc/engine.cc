@@ -307,7 +307,6 @@ struct EvalCtx {
   // the predicate kernels' chunked tuples and argument words before
   // compaction (devrt.h slot_reserve, kernels.hip gk_compact_*), tile counts
   DBuf d_out_raw, d_frec_raw, d_ctcnt, d_ctoff;
-  DBuf d_mdtab;  // message dedup table of the size pass (kernels.hip md_owner)
   // side streams for concurrent template launches (GKGPU_CONCURRENT), each
   // with its own cross-lane memo table (memo sites are per program)
   static constexpr int kSide = 3;
@@ -341,7 +340,7 @@ struct EvalCtx {
     h_pin_cap = 0;
     for (DBuf* b : {&d_nodes, &d_revs, &d_out, &d_bytes, &d_counters, &d_rflags, &d_totals, &d_rreason, &d_prof, &d_pchist,
                     &d_clist, &d_gmemo, &d_mstr, &d_mtop, &d_frec, &d_hist, &d_cut, &d_ftot, &d_cand, &d_ncand, &d_cerr, &d_ebytes, &d_lens,
-                    &d_part, &d_out_raw, &d_frec_raw, &d_ctcnt, &d_ctoff, &d_mdtab})
+                    &d_part, &d_out_raw, &d_frec_raw, &d_ctcnt, &d_ctoff})
       b->free_();
     for (hipEvent_t x : events) hipEventDestroy(x);
     events.clear();
@@ -1948,16 +1947,6 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     // the tuples of every launch above packed, then the size, spine and format passes
     // pass grids sized for ~2x this context's last output (GKGPU_PASS_HINT=0: for the capacity)
     const uint64_t pass_hint = env_mode("GKGPU_PASS_HINT", 1, 1) ? std::max<uint64_t>(2 * x->last_tuples, 65536) : 0;
-    // message dedup for large outputs (GKGPU_MSG_DEDUP, A/B switch, default
-    // on; kernels.hip md_owner): a table of about twice the last output's tuples
-    if (nrev >= 4096 && env_mode("GKGPU_MSG_DEDUP", 1, 1) != 0) {
-      uint64_t slots = 1u << 20;
-      while (slots < 2 * x->last_tuples && slots < (1u << 24)) slots <<= 1;
-      if (x->d_mdtab.reserve(slots * 8)) {
-        a.mdtab = (unsigned long long*)x->d_mdtab.p;
-        a.mdmask = (uint32_t)(slots - 1);
-      }
-    }
     int flr = gk_launch_compact(&a, (const Viol*)x->d_out_raw.p, (const uint64_t*)x->d_frec_raw.p,
                                 (uint32_t*)x->d_ctcnt.p, (unsigned long long*)x->d_ctoff.p, x->stream, pass_hint);
     if (flr != 0) return fail(e, GK_EDEVICE, std::string("kernel launch failed (compact): ") + hipGetErrorString((hipError_t)flr));

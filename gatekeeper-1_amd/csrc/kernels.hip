@@ -294,61 +294,6 @@ __device__ __forceinline__ void print_plain_r(O& o, const uint32_t* f, const uin
   }
 }
 
-// ---- message dedup.  A sweep's messages repeat: the same format over the
-// same argument words (K8sContainerLimits: a few container names x a few
-// limit strings) -- round 4 printed all 6.9M of config 2's messages, 460 MB.
-// The size pass keys each deferred message whose arguments are plain scalars
-// (interned strings, ints: equal words print equal bytes) and whose details
-// are the hook default `{}`; the first tuple of a key owns it and is printed,
-// the others are marked VF_DUP with the owner's index and get no bytes;
-// gk_fixup_dups then gives them the owner's (msg_off, msg_len, det_len).
-// A key whose probes run out (a full neighbourhood) is printed as before.
-constexpr uint32_t MD_PROBES = 32;
-__device__ __forceinline__ uint64_t md_hash(uint32_t fidx, const uint64_t (&a)[FMT_MAXARGS], uint32_t na) {
-  uint64_t h = 0x9e3779b97f4a7c15ull ^ ((uint64_t)fidx << 8) ^ na;
-#pragma unroll
-  for (uint32_t j = 0; j < FMT_MAXARGS; ++j) {
-    if (j >= na) break;
-    h ^= a[j] + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
-    h *= 0xff51afd7ed558ccdull;
-  }
-  h ^= h >> 33;
-  return h;
-}
-// the tuple whose bytes tuple i shares (i itself: i prints its own)
-__device__ __forceinline__ uint32_t md_owner(uint64_t i, const Viol& v, const uint64_t (&a)[FMT_MAXARGS], uint32_t na) {
-  const uint32_t fidx = v.msg_len & 0xffffffu;
-  const uint64_t h = md_hash(fidx, a, na);
-  const uint64_t me = (h & 0xffffffff00000000ull) | (uint64_t)(uint32_t)(i + 1);
-  uint32_t slot = (uint32_t)h & gk_args.mdmask;
-  for (uint32_t p = 0; p < MD_PROBES; ++p, slot = (slot + 1) & gk_args.mdmask) {
-    // a plain load first: the few hot keys of a sweep are met by millions of
-    // tuples, and a compare-and-swap on their slots would serialize them
-    unsigned long long cur = __hip_atomic_load(&gk_args.mdtab[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == 0) {
-      cur = atomicCAS(&gk_args.mdtab[slot], 0ull, (unsigned long long)me);
-      if (cur == 0) return (uint32_t)i;
-    }
-    if ((cur >> 32) != (h >> 32)) continue;
-    const uint32_t o = (uint32_t)cur - 1;
-    const Viol ov = gk_args.out[o];
-    if ((ov.msg_len & 0xffffffu) != fidx || (ov.msg_len >> 24) != na || !(ov.pad & VF_DET_OBJ)) continue;
-    bool same = true;
-#pragma unroll
-    for (uint32_t j = 0; j < FMT_MAXARGS; ++j)
-      if (j < na && gk_args.frec[(uint64_t)j * gk_args.out_cap + o] != a[j]) same = false;
-    if (same) return o;
-  }
-  return (uint32_t)i;
-}
-__device__ __forceinline__ bool md_keyable(const Viol& v, const uint64_t (&a)[FMT_MAXARGS], uint32_t na) {
-  if (!gk_args.mdtab || !(v.pad & VF_DEFER) || !(v.pad & VF_DET_OBJ) || (v.pad & VF_DET_VAL)) return false;
-#pragma unroll
-  for (uint32_t j = 0; j < FMT_MAXARGS; ++j)
-    if (j < na && vtag(a[j]) != V_STR && vtag(a[j]) != V_INT) return false;
-  return true;
-}
-
 // a deferred tuple's printed message length; false = not printable here
 // (the string table's lengths: the resolved table staged in LDS measured
 // slower here, 0.20 -> 0.27 ms per config-2 sweep, profiles/r05/)
@@ -396,31 +341,10 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
     for (uint32_t k = 0; k < FTILE; k += 256) {
       const uint64_t i = t * FTILE + k + threadIdx.x;
       if (i >= n) break;
-      Viol v = gk_args.out[i];
-      if (v.pad & VF_DUP) {  // a mark of an overflowed earlier run of the passes
-        v.pad &= ~VF_DUP;
-        v.msg_off = 0;
-        gk_args.out[i].pad = v.pad;
-        gk_args.out[i].msg_off = 0;
-      }
+      const Viol v = gk_args.out[i];
       uint32_t ml = v.msg_len, dl = det_bytes(v);
       bool printable = true;
       if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml);
-      if (printable && gk_args.mdtab && (v.pad & VF_DEFER)) {
-        const uint32_t na = v.msg_len >> 24;
-        uint64_t a[FMT_MAXARGS];
-#pragma unroll
-        for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
-        if (md_keyable(v, a, na)) {
-          const uint32_t o = md_owner(i, v, a, na);
-          if (o != (uint32_t)i) {
-            gk_args.out[i].pad = v.pad | VF_DUP;
-            gk_args.out[i].msg_off = o;
-            gk_args.lens[i] = 0;
-            continue;
-          }
-        }
-      }
       if (v.pad & VF_DET_VAL) {
         Cnt cn{0, false};
         printable = put_json(L, cn, det_word(v, i)) && printable;
@@ -621,9 +545,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       const uint64_t dst = wbase + incl - len;
       Viol v{};
       if (valid) v = gk_args.out[i];
-      const bool dup = valid && (v.pad & VF_DUP);  // shares another tuple's bytes (gk_fixup_dups)
-      const bool defer = valid && !dup && (v.pad & VF_DEFER);
-      const uint32_t dl = valid && !dup ? det_bytes(v) : 0u;
+      const bool defer = valid && (v.pad & VF_DEFER);
+      const uint32_t dl = valid ? det_bytes(v) : 0u;
       const uint32_t ml = len - dl;
       uint64_t a[FMT_MAXARGS];
       const uint32_t na = defer ? (v.msg_len >> 24) : 0u;
@@ -682,7 +605,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
       }
-      if (valid && !dup) {
+      if (valid) {
         v.msg_off = dst;
         v.msg_len = ml;
         v.det_len = dl;
@@ -690,26 +613,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         gk_args.out[i] = v;
       }
     }
-  }
-}
-
-// after the format pass: each VF_DUP tuple takes its owner's final bytes
-// (the owner was formatted by some block of the format pass)
-__global__ void __launch_bounds__(256) gk_fixup_dups(DevArgs) {
-  if (gk_args.counters[3] > gk_args.bytes_cap || gk_args.counters[0] > gk_args.out_cap ||
-      gk_args.counters[1] > gk_args.ebytes_cap)
-    return;
-  const uint64_t n = ntuples();
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t pad = gk_args.out[i].pad;
-    if (!(pad & VF_DUP)) continue;
-    Viol v = gk_args.out[i];
-    const Viol o = gk_args.out[v.msg_off];
-    v.msg_off = o.msg_off;
-    v.msg_len = o.msg_len;
-    v.det_len = o.det_len;
-    v.pad = 0;
-    gk_args.out[i] = v;
   }
 }
 
@@ -725,7 +628,6 @@ __global__ void __launch_bounds__(256) gk_fixup_dups(DevArgs) {
 extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev, uint64_t hint) {
   const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::FTILE - 1) / gk::FTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
-  if (a->mdtab) (void)hipMemsetAsync(a->mdtab, 0, ((size_t)a->mdmask + 1) * 8, stream);  // a fresh dedup table
   hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
@@ -741,8 +643,6 @@ extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEve
   static const bool wide = !getenv("GKGPU_FMT_WIDE") || atoi(getenv("GKGPU_FMT_WIDE")) != 0;
   if (wide) hipLaunchKernelGGL(gk::gk_format_kernel<gk::LOutW>, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
   else hipLaunchKernelGGL(gk::gk_format_kernel<gk::LOut>, dim3(blocks), dim3(256), 4 * fstage, stream, fstage, *a);
-  // message dedup: the duplicates take their owners' bytes (timed with the format pass)
-  if (a->mdtab) hipLaunchKernelGGL(gk::gk_fixup_dups, dim3(std::min<uint32_t>(blocks * 4, 8192)), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[2], stream);
   return (int)hipGetLastError();
 }
