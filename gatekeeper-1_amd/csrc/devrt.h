@@ -2559,6 +2559,40 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
   return op_emit_slow(L, m, d, depth, rule);
 }
 
+// op_emit for a deferred message whose argument registers the JIT knows
+// (jit.cc emit_flow): the same record, the argument words taken from the
+// registers instead of the lane heap's list
+template <uint32_t N>
+__device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
+                                             const uint64_t (&args)[N]) {
+#if GK_EMIT_FAST
+  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX &&
+              L.ord < EM_MAXORD;
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
+  if (fast) {
+    const uint32_t seq = ((uint32_t)L.ord << 8) | (uint32_t)L.en;
+    const uint64_t slot = slot_reserve(true);
+    L.en = L.en + 1u;
+    if (slot >= gk_args.out_cap) { slot_overflow(L); return true; }
+    Viol v;
+    v.review = L.rv;
+    v.constraint = L.cn;
+    v.seq = (uint16_t)seq;
+    v.rule = (uint16_t)rule;
+    v.msg_len = fmt_fidx(m) | (N << 24);
+    v.msg_off = 0;
+    v.det_len = 2;
+    v.pad = VF_DEFER | VF_DET_OBJ;
+    gk_args.out[slot] = v;
+#pragma unroll
+    for (uint32_t i = 0; i < N; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = args[i];
+    return true;
+  }
+#endif
+  return op_emit(L, m, d, depth, rule);
+}
+
 // Printed length of a deferred message whose arguments are plain scalars:
 // put_fmt_arg restricted to interned strings and ints, on a counter (the size
 // pass's fast path; fmt_run on a counter serves every other record).

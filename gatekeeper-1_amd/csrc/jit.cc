@@ -190,6 +190,182 @@ struct LookFlow {
   }
 };
 
+// Emissions whose message is a deferred sprintf of an argument list built
+// right before it (forward must-analysis): `L := [x0, .., xn-1]` (LIST_NEW of
+// an array, n LIST_ADDs), `F := sprintf(fmt, L)` (lazy), then EMIT(F).  On
+// entry to each instruction, the registers F known to hold such a value with
+// the argument registers still unchanged.  The emission then takes the
+// arguments from those registers (devrt.h op_emit_args) instead of reading
+// the list back out of the lane heap -- K8sContainerLimits' eight bodies per
+// container build their lists past the 16 LDS heap words, so the read-back
+// went to the private segment.
+void ins_regs(const Ins& in, std::vector<uint32_t>& rd, std::vector<uint32_t>& wr);
+void ins_succ(const Ins& in, uint32_t pc, std::vector<uint32_t>& out);
+struct EmitFlow {
+  struct LFact { uint16_t list; uint16_t n; uint16_t args[FMT_MAXARGS]; };
+  // mu: on some paths F holds undefined instead (a function's result that
+  // one path leaves unset); the emission then checks the tag first
+  // site: the sprintf's pc; its argument registers are copied there into
+  // shadow locals (es<site>_i), so later reuse of those registers is harmless
+  struct FFact { uint16_t f, list, n; uint16_t args[FMT_MAXARGS]; bool mu = false; uint32_t site = 0; };
+  struct State {
+    bool top = true;
+    std::vector<LFact> lists;
+    std::vector<FFact> fmts;
+    std::vector<uint16_t> undef;  // registers known to hold undefined (sorted)
+  };
+  std::vector<State> in;
+  const FFact* find(uint32_t k, uint16_t f) const {
+    if (k >= in.size() || in[k].top) return nullptr;
+    for (const FFact& x : in[k].fmts) if (x.f == f) return &x;
+    return nullptr;
+  }
+};
+static bool emitflow_on() {
+  const char* v = getenv("GKGPU_JIT_EMITARGS");  // A/B switch, default on
+  return !v || atoi(v) != 0;
+}
+static bool same_lfact(const EmitFlow::LFact& a, const EmitFlow::LFact& b) {
+  if (a.list != b.list || a.n != b.n) return false;
+  for (uint16_t i = 0; i < a.n; ++i) if (a.args[i] != b.args[i]) return false;
+  return true;
+}
+static bool same_ffact(const EmitFlow::FFact& a, const EmitFlow::FFact& b) {
+  return a.f == b.f && a.site == b.site && a.n == b.n && a.mu == b.mu;
+}
+EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
+  const uint32_t b0 = p.code_off, n = p.code_len;
+  EmitFlow EF;
+  EF.in.assign(n, EmitFlow::State{});
+  if (!emitflow_on()) return EF;
+  using State = EmitFlow::State;
+  auto mentions_l = [](const EmitFlow::LFact& x, uint32_t r) {
+    if (x.list == r) return true;
+    for (uint16_t i = 0; i < x.n; ++i) if (x.args[i] == r) return true;
+    return false;
+  };
+  auto mentions_f = [](const EmitFlow::FFact& x, uint32_t r) { return x.f == r; };
+  auto kill = [&](State& s, uint32_t r) {
+    if (r == 0xffff) return;
+    s.undef.erase(std::remove(s.undef.begin(), s.undef.end(), (uint16_t)r), s.undef.end());
+    s.lists.erase(std::remove_if(s.lists.begin(), s.lists.end(), [&](const EmitFlow::LFact& x) { return mentions_l(x, r); }),
+                  s.lists.end());
+    s.fmts.erase(std::remove_if(s.fmts.begin(), s.fmts.end(), [&](const EmitFlow::FFact& x) { return mentions_f(x, r); }),
+                 s.fmts.end());
+  };
+  std::vector<uint32_t> work;
+  auto flow = [&](uint32_t to, const State& s) {
+    if (to < b0 || to >= b0 + n) return;
+    State& d = EF.in[to - b0];
+    if (d.top) { d = s; d.top = false; work.push_back(to - b0); return; }
+    std::vector<EmitFlow::LFact> nl;
+    for (const auto& x : d.lists)
+      for (const auto& y : s.lists) if (same_lfact(x, y)) { nl.push_back(x); break; }
+    auto has_undef = [](const State& t, uint16_t r) { return std::binary_search(t.undef.begin(), t.undef.end(), r); };
+    auto same_but_mu = [](EmitFlow::FFact a, EmitFlow::FFact b) { a.mu = b.mu = false; return same_ffact(a, b); };
+    std::vector<EmitFlow::FFact> nf;
+    for (const auto& x : d.fmts) {
+      bool kept = false;
+      for (const auto& y : s.fmts)
+        if (same_but_mu(x, y)) { EmitFlow::FFact z = x; z.mu = x.mu || y.mu; nf.push_back(z); kept = true; break; }
+      if (!kept && has_undef(s, x.f)) { EmitFlow::FFact z = x; z.mu = true; nf.push_back(z); }
+    }
+    for (const auto& y : s.fmts) {
+      bool there = false;
+      for (const auto& x : d.fmts) there = there || x.f == y.f;
+      if (!there && has_undef(d, y.f)) { EmitFlow::FFact z = y; z.mu = true; nf.push_back(z); }
+    }
+    std::vector<uint16_t> nu;
+    std::set_intersection(d.undef.begin(), d.undef.end(), s.undef.begin(), s.undef.end(), std::back_inserter(nu));
+    bool fchanged = nf.size() != d.fmts.size();
+    for (size_t i = 0; !fchanged && i < nf.size(); ++i) fchanged = !same_ffact(nf[i], d.fmts[i]);
+    if (nl.size() != d.lists.size() || fchanged || nu.size() != d.undef.size()) {
+      d.lists.swap(nl);
+      d.fmts.swap(nf);
+      d.undef.swap(nu);
+      work.push_back(to - b0);
+    }
+  };
+  if (n) { EF.in[0].top = false; work.push_back(0); }
+  std::vector<uint32_t> rd, wr, succ;
+  while (!work.empty()) {
+    const uint32_t k = work.back();
+    work.pop_back();
+    const Ins& in = bank.code[b0 + k];
+    State s = EF.in[k];
+    for (uint32_t r : fmt_reads(in)) if (F.has(k, r)) kill(s, r);  // forced here: the register changes
+    switch (in.op) {
+      case OP_ITER_NEXT: case OP_JNEXT:
+        // the previous iteration's heap is reclaimed: no fact crosses
+        s.lists.clear();
+        s.fmts.clear();
+        break;
+      case OP_LIST_NEW:
+        kill(s, in.a);
+        if (in.y == LK_ARR) s.lists.push_back({in.a, 0, {}});
+        break;
+      case OP_LOADK:
+        kill(s, in.a);
+        if (in.x < bank.consts.size() && bank.consts[in.x] == 0) {  // undefined
+          s.undef.insert(std::lower_bound(s.undef.begin(), s.undef.end(), (uint16_t)in.a), (uint16_t)in.a);
+        }
+        break;
+      case OP_LIST_ADD: {
+        // the list grows: sprintf values over it no longer describe it
+        s.fmts.erase(std::remove_if(s.fmts.begin(), s.fmts.end(),
+                                    [&](const EmitFlow::FFact& x) { return x.f == in.a || x.list == in.a; }),
+                     s.fmts.end());
+        EmitFlow::LFact* lf = nullptr;
+        for (auto& x : s.lists) if (x.list == in.a) lf = &x;
+        bool ok = lf && in.b != 0xffff && in.b != in.a && lf->n < FMT_MAXARGS;
+        if (ok) lf->args[lf->n++] = in.b;
+        s.lists.erase(std::remove_if(s.lists.begin(), s.lists.end(),
+                                     [&](const EmitFlow::LFact& x) { return (x.list == in.a && !ok) || (x.list != in.a && mentions_l(x, in.a)); }),
+                      s.lists.end());
+        break;
+      }
+      case OP_SPRINTF: {
+        const EmitFlow::LFact* lf = nullptr;
+        for (const auto& x : s.lists) if (x.list == in.b) lf = &x;
+        EmitFlow::FFact ff{};
+        const bool ok = lazy_fmt(in) && lf && in.a != in.b && in.x + 1 < bank.fmt.size() && lf->n == bank.fmt[in.x + 1];
+        if (ok) {
+          ff.f = in.a;
+          ff.list = in.b;
+          ff.n = lf->n;
+          ff.site = b0 + k;
+          for (uint16_t i = 0; i < lf->n; ++i) ff.args[i] = lf->args[i];
+        }
+        kill(s, in.a);
+        if (ok) s.fmts.push_back(ff);
+        break;
+      }
+      case OP_MOV: case OP_YIELD: {
+        // a copy (a yield assigns, or errs on a conflicting value): the
+        // destination describes the same sprintf
+        const EmitFlow::FFact* src = nullptr;
+        for (const auto& x : s.fmts) if (x.f == in.b) src = &x;
+        EmitFlow::FFact cp{};
+        const bool ok = src && in.a != in.b && in.a != src->list;
+        if (ok) cp = *src;
+        kill(s, in.a);
+        if (ok) {
+          cp.f = in.a;
+          s.fmts.push_back(cp);
+        }
+        break;
+      }
+      default:
+        ins_regs(in, rd, wr);
+        for (uint32_t r : wr) kill(s, r);
+        break;
+    }
+    ins_succ(in, b0 + k, succ);
+    for (uint32_t t : succ) flow(t, s);
+  }
+  return EF;
+}
+
 // Document-derived registers (must-analysis): on entry to each instruction,
 // the registers that hold, on every path, a value read out of the review or
 // the parameters -- a document node or a scalar, never a lane-heap value --
@@ -661,6 +837,15 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   FmtFlow F = fmt_flow(p, bank);
   FmtFlow DF = doc_flow(p, bank);
   LookFlow LK = look_flow(p, bank, F, DF);
+  EmitFlow EFL = emit_flow(p, bank, F);
+  // sprintf sites whose arguments a fused emission reads: their shadow locals
+  std::map<uint32_t, std::vector<uint16_t>> esites;  // site pc -> argument registers there
+  for (uint32_t pc = b0; pc < b1; ++pc) {
+    const Ins& in = bank.code[pc];
+    if (in.op != OP_EMIT || in.b != 0xffff) continue;
+    if (const EmitFlow::FFact* ff = EFL.find(pc - b0, in.a))
+      if (ff->n > 0) esites[ff->site] = std::vector<uint16_t>(ff->args, ff->args + ff->n);
+  }
   // computed-key lookups whose result a later lookup reuses: their shadow locals
   std::set<uint32_t> shadowed;
   for (uint32_t pc = b0; pc < b1; ++pc) {
@@ -701,6 +886,8 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   if (!p.nregs) o << "unused_";
   o << ";\n";
   for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << ";\n";
+  for (const auto& es : esites)
+    for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)
   for (uint32_t m : lslots) {
     o << "  uint64_t mk0_" << m << ", mk1_" << m << ", mv_" << m << "; bool mok_" << m << " = false;\n";
@@ -848,17 +1035,34 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         }
         break;
       }
-      case OP_SPRINTF:
+      case OP_SPRINTF: {
+        // (a fused emission's shadow copies of the arguments, before the write)
+        auto es = esites.find(pc);
+        if (es != esites.end())
+          for (size_t i = 0; i < es->second.size(); ++i) o << "es" << pc << "_" << i << " = " << R(es->second[i]) << "; ";
         if (lazy_fmt(in) && in.x + 1 < bank.fmt.size())  // argument count as an immediate (no table load)
           o << a << " = lazy_sprintf_n(L, " << in.x << "u, " << b << ", " << bank.fmt[in.x + 1] << "u);";
         else
           o << a << " = " << (lazy_fmt(in) ? "lazy_sprintf" : "do_sprintf") << "(L, " << in.x << "u, " << b << ");";
         break;
+      }
       case OP_LEN_EQ: o << a << " = op_len_eq(L, " << b << ", " << y << ");"; break;
-      case OP_EMIT:
-        o << "if (!op_emit(L, " << a << ", " << (in.b == 0xffff ? std::string(UND) : b) << ", " << in.c << "u, " << y
-          << ")) " << RET;
+      case OP_EMIT: {
+        const EmitFlow::FFact* ff = in.b == 0xffff ? EFL.find(k, in.a) : nullptr;
+        if (ff && ff->n > 0) {
+          // (mu: the argument registers are read only where the message is the sprintf)
+          if (ff->mu) o << "if (vtag(" << a << ") == V_FMT) ";
+          o << "{ const uint64_t ea_[" << ff->n << "] = {";
+          for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << "es" << ff->site << "_" << i;
+          o << "}; if (!op_emit_args(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
+          if (ff->mu)
+            o << " else if (!op_emit(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ")) " << RET;
+        } else {
+          o << "if (!op_emit(L, " << a << ", " << (in.b == 0xffff ? std::string(UND) : b) << ", " << in.c << "u, " << y
+            << ")) " << RET;
+        }
         break;
+      }
       case OP_MEMO_GET: {
         // two entries per slot (most recent first): call sites of one function
         // with alternating arguments (canonify_mem(x) vs canonify_mem(max)) hit
