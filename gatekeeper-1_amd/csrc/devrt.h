@@ -2589,8 +2589,32 @@ __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, u
     for (uint32_t i = 0; i < N; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = args[i];
     return true;
   }
-#endif
+  // the list holds these same arguments: op_emit's fast path would fail too
+  return op_emit_slow(L, m, d, depth, rule);
+#else
   return op_emit(L, m, d, depth, rule);
+#endif
+}
+
+// op_emit_args for a sprintf whose argument list the JIT did not build
+// (jit.cc dce_sites): the value carries the format only, so the slow path
+// builds the list from the arguments first (the same LIST_ADDs the program
+// would have run)
+template <uint32_t N>
+__device__ __forceinline__ bool op_emit_args_build(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
+                                                   const uint64_t (&args)[N], const uint32_t (&ys)[N]) {
+  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX &&
+              L.ord < EM_MAXORD;
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
+  if (fast) return op_emit_args(L, m, d, depth, rule, args);
+  if (vtag(m) != V_FMT) return op_emit(L, m, d, depth, rule);
+  uint64_t l = list_new(L, LK_ARR, 4);
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i)
+    if (!op_list_add(L, l, args[i], ys[i])) return false;
+  const uint64_t m2 = lazy_sprintf_n(L, fmt_fidx(m), l, N);
+  return op_emit(L, m2, d, depth, rule);
 }
 
 // Printed length of a deferred message whose arguments are plain scalars:

@@ -202,12 +202,19 @@ struct LookFlow {
 void ins_regs(const Ins& in, std::vector<uint32_t>& rd, std::vector<uint32_t>& wr);
 void ins_succ(const Ins& in, uint32_t pc, std::vector<uint32_t>& out);
 struct EmitFlow {
-  struct LFact { uint16_t list; uint16_t n; uint16_t args[FMT_MAXARGS]; };
+  struct LFact { uint16_t list; uint16_t n; uint16_t args[FMT_MAXARGS]; uint32_t newpc = 0; uint32_t ys[FMT_MAXARGS] = {}; };
   // mu: on some paths F holds undefined instead (a function's result that
   // one path leaves unset); the emission then checks the tag first
   // site: the sprintf's pc; its argument registers are copied there into
   // shadow locals (es<site>_i), so later reuse of those registers is harmless
-  struct FFact { uint16_t f, list, n; uint16_t args[FMT_MAXARGS]; bool mu = false; uint32_t site = 0; };
+  struct FFact {
+    uint16_t f, list, n;
+    uint16_t args[FMT_MAXARGS];
+    bool mu = false;
+    uint32_t site = 0;
+    uint32_t newpc = 0;              // the list's LIST_NEW
+    uint32_t ys[FMT_MAXARGS] = {};   // its LIST_ADDs' y operands
+  };
   struct State {
     bool top = true;
     std::vector<LFact> lists;
@@ -226,7 +233,7 @@ static bool emitflow_on() {
   return !v || atoi(v) != 0;
 }
 static bool same_lfact(const EmitFlow::LFact& a, const EmitFlow::LFact& b) {
-  if (a.list != b.list || a.n != b.n) return false;
+  if (a.list != b.list || a.n != b.n || a.newpc != b.newpc) return false;
   for (uint16_t i = 0; i < a.n; ++i) if (a.args[i] != b.args[i]) return false;
   return true;
 }
@@ -300,10 +307,16 @@ EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         s.lists.clear();
         s.fmts.clear();
         break;
-      case OP_LIST_NEW:
+      case OP_LIST_NEW: {
         kill(s, in.a);
-        if (in.y == LK_ARR) s.lists.push_back({in.a, 0, {}});
+        if (in.y == LK_ARR) {
+          EmitFlow::LFact lf{};
+          lf.list = in.a;
+          lf.newpc = b0 + k;
+          s.lists.push_back(lf);
+        }
         break;
+      }
       case OP_LOADK:
         kill(s, in.a);
         if (in.x < bank.consts.size() && bank.consts[in.x] == 0) {  // undefined
@@ -318,7 +331,7 @@ EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         EmitFlow::LFact* lf = nullptr;
         for (auto& x : s.lists) if (x.list == in.a) lf = &x;
         bool ok = lf && in.b != 0xffff && in.b != in.a && lf->n < FMT_MAXARGS;
-        if (ok) lf->args[lf->n++] = in.b;
+        if (ok) { lf->ys[lf->n] = in.y; lf->args[lf->n++] = in.b; }
         s.lists.erase(std::remove_if(s.lists.begin(), s.lists.end(),
                                      [&](const EmitFlow::LFact& x) { return (x.list == in.a && !ok) || (x.list != in.a && mentions_l(x, in.a)); }),
                       s.lists.end());
@@ -334,7 +347,8 @@ EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
           ff.list = in.b;
           ff.n = lf->n;
           ff.site = b0 + k;
-          for (uint16_t i = 0; i < lf->n; ++i) ff.args[i] = lf->args[i];
+          ff.newpc = lf->newpc;
+          for (uint16_t i = 0; i < lf->n; ++i) { ff.args[i] = lf->args[i]; ff.ys[i] = lf->ys[i]; }
         }
         kill(s, in.a);
         if (ok) s.fmts.push_back(ff);
@@ -357,6 +371,9 @@ EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
       }
       default:
         ins_regs(in, rd, wr);
+        for (uint32_t r : rd)
+          s.lists.erase(std::remove_if(s.lists.begin(), s.lists.end(), [&](const EmitFlow::LFact& x) { return x.list == r; }),
+                        s.lists.end());
         for (uint32_t r : wr) kill(s, r);
         break;
     }
@@ -840,11 +857,79 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   EmitFlow EFL = emit_flow(p, bank, F);
   // sprintf sites whose arguments a fused emission reads: their shadow locals
   std::map<uint32_t, std::vector<uint16_t>> esites;  // site pc -> argument registers there
+  std::map<uint32_t, EmitFlow::FFact> efacts;  // site pc -> its fact (list, LIST_NEW pc, add operands)
   for (uint32_t pc = b0; pc < b1; ++pc) {
     const Ins& in = bank.code[pc];
     if (in.op != OP_EMIT || in.b != 0xffff) continue;
     if (const EmitFlow::FFact* ff = EFL.find(pc - b0, in.a))
-      if (ff->n > 0) esites[ff->site] = std::vector<uint16_t>(ff->args, ff->args + ff->n);
+      if (ff->n > 0) { esites[ff->site] = std::vector<uint16_t>(ff->args, ff->args + ff->n); efacts[ff->site] = *ff; }
+  }
+  // Sites whose list exists only for the emission (GKGPU_JIT_EMITDCE, default
+  // on): every read of a value that may be a deferred sprintf is a copy, a
+  // definedness test or a fused emission; the list is built in straight-line
+  // code right before the sprintf and dead after it.  Then the list is not
+  // built at all -- the sprintf value carries its format only -- and the
+  // emission's slow path (arguments that are not plain scalars) builds it
+  // from the shadow copies (devrt.h op_emit_args_build).
+  std::set<uint32_t> dce_sites, dce_pcs;
+  {
+    const char* dv = getenv("GKGPU_JIT_EMITDCE");
+    bool prog_ok = (!dv || atoi(dv) != 0) && !efacts.empty();
+    std::vector<uint32_t> rd, wr;
+    for (uint32_t pc = b0; prog_ok && pc < b1; ++pc) {
+      const Ins& in = bank.code[pc];
+      const uint32_t k = pc - b0;
+      if (!F.reached[k]) continue;
+      for (uint32_t r : fmt_reads(in)) if (F.has(k, r)) prog_ok = false;
+      ins_regs(in, rd, wr);
+      for (uint32_t r : rd) {
+        if (!F.has(k, r)) continue;
+        const bool fused = in.op == OP_EMIT && in.b == 0xffff && r == in.a && EFL.find(k, in.a) && EFL.find(k, in.a)->n > 0;
+        // (not a yield: op_yield forces a V_FMT to compare it with a defined output)
+        if (!(in.op == OP_MOV || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || fused))
+          prog_ok = false;
+      }
+    }
+    // liveness (backward may-analysis) for "the list is dead after the sprintf"
+    const uint32_t nw = (p.nregs + 64) / 64;
+    std::vector<std::vector<uint64_t>> live(prog_ok ? p.code_len : 0, std::vector<uint64_t>(nw, 0));
+    std::vector<uint32_t> sc;
+    for (bool changed = prog_ok; changed;) {
+      changed = false;
+      for (uint32_t k = p.code_len; k-- > 0;) {
+        const uint32_t pc = b0 + k;
+        std::vector<uint64_t> out(nw, 0);
+        ins_succ(bank.code[pc], pc, sc);
+        for (uint32_t t : sc)
+          if (t >= b0 && t < b1) for (uint32_t w = 0; w < nw; ++w) out[w] |= live[t - b0][w];
+        ins_regs(bank.code[pc], rd, wr);
+        for (uint32_t r : wr) if (r < 64 * nw) out[r >> 6] &= ~(1ull << (r & 63));
+        for (uint32_t r : rd) if (r < 64 * nw) out[r >> 6] |= 1ull << (r & 63);
+        if (out != live[k]) { live[k] = out; changed = true; }
+      }
+    }
+    for (const auto& ef : efacts) {
+      if (!prog_ok) break;
+      const EmitFlow::FFact& ff = ef.second;
+      const uint32_t S = ff.site, N = ff.newpc, Lr = ff.list;
+      bool ok = N >= b0 && N < S && S + 1 < b1 && Lr < 64 * nw;
+      // dead after the sprintf
+      if (ok) ok = !((live[S + 1 - b0][Lr >> 6] >> (Lr & 63)) & 1);
+      // straight-line: no jump into (N, S], no jump out of [N, S)
+      std::vector<uint32_t> adds;
+      for (uint32_t pc = N; ok && pc <= S; ++pc) {
+        if (pc > N && labels.count(pc)) ok = false;
+        const Ins& in = bank.code[pc];
+        if (pc < S && jump_op(in.op)) ok = false;
+        if (pc > N && pc < S && in.op == OP_LIST_ADD && in.a == Lr) adds.push_back(pc);
+        if (pc > N && pc < S && in.op == OP_LIST_NEW && in.a == Lr) ok = false;
+      }
+      if (ok && adds.size() != ff.n) ok = false;
+      if (!ok) continue;
+      dce_sites.insert(S);
+      dce_pcs.insert(N);
+      for (uint32_t a : adds) dce_pcs.insert(a);
+    }
   }
   // computed-key lookups whose result a later lookup reuses: their shadow locals
   std::set<uint32_t> shadowed;
@@ -980,8 +1065,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         break;
       case OP_CMP: o << "if (!op_cmp(L, " << y << ", " << b << ", " << c << ", " << a << ")) " << RET; break;
       case OP_ARITH: o << a << " = arith(L, " << y << ", " << b << ", " << c << ");"; break;
-      case OP_LIST_NEW: o << a << " = list_new(L, " << y << ", 4);"; break;
-      case OP_LIST_ADD: o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) " << RET; break;
+      case OP_LIST_NEW:
+        if (dce_pcs.count(pc)) o << "/* " << a << ": the argument list of a fused emission */";
+        else o << a << " = list_new(L, " << y << ", 4);";
+        break;
+      case OP_LIST_ADD:
+        if (dce_pcs.count(pc)) o << "/* " << a << " += " << b << " */";
+        else o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) " << RET;
+        break;
       case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) " << RET; break;
       case OP_YIELD: o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) " << RET; break;
       case OP_CALL: {
@@ -1040,7 +1131,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         auto es = esites.find(pc);
         if (es != esites.end())
           for (size_t i = 0; i < es->second.size(); ++i) o << "es" << pc << "_" << i << " = " << R(es->second[i]) << "; ";
-        if (lazy_fmt(in) && in.x + 1 < bank.fmt.size())  // argument count as an immediate (no table load)
+        if (dce_sites.count(pc))  // the format alone: the fused emission has the arguments
+          o << a << " = mkv(V_FMT, (uint64_t)" << in.x << "u << 32);";
+        else if (lazy_fmt(in) && in.x + 1 < bank.fmt.size())  // argument count as an immediate (no table load)
           o << a << " = lazy_sprintf_n(L, " << in.x << "u, " << b << ", " << bank.fmt[in.x + 1] << "u);";
         else
           o << a << " = " << (lazy_fmt(in) ? "lazy_sprintf" : "do_sprintf") << "(L, " << in.x << "u, " << b << ");";
@@ -1054,7 +1147,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           if (ff->mu) o << "if (vtag(" << a << ") == V_FMT) ";
           o << "{ const uint64_t ea_[" << ff->n << "] = {";
           for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << "es" << ff->site << "_" << i;
-          o << "}; if (!op_emit_args(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
+          if (dce_sites.count(ff->site)) {
+            o << "}; const uint32_t ey_[" << ff->n << "] = {";
+            for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << ff->ys[i] << "u";
+            o << "}; if (!op_emit_args_build(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_, ey_)) " << RET
+              << " }";
+          } else {
+            o << "}; if (!op_emit_args(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
+          }
           if (ff->mu)
             o << " else if (!op_emit(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ")) " << RET;
         } else {

@@ -102,3 +102,17 @@ def test_required_labels_builds_no_provided_set():
     set is not built; `missing` iterates `required` with a lookup per key"""
     on, off = _dump("K8sRequiredLabels"), _dump("K8sRequiredLabels", [("GKGPU_REGO_SETS", "0")])
     assert "arith(L, 1u," not in on and "arith(L, 1u," in off
+
+
+def test_fused_emission_builds_no_argument_list():
+    """jit.cc dce_sites: K8sContainerLimits' violation messages are sprintfs
+    whose argument lists exist only for the emission; the fused emission takes
+    the arguments from the shadow copies and the list is not built
+    (op_emit_args_build rebuilds it only on the slow path).
+    GKGPU_JIT_EMITDCE=0 keeps the lists."""
+    on = _dump("K8sContainerLimits")
+    off = _dump("K8sContainerLimits", [("GKGPU_JIT_EMITDCE", "0")])
+    assert "op_emit_args_build(L," in on
+    assert "list_new(L," not in on
+    assert "op_emit_args_build(L," not in off
+    assert "list_new(L," in off and "op_emit_args(L," in off
