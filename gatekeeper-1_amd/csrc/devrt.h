@@ -2523,7 +2523,24 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
 #ifndef GK_EMIT_FAST
 #define GK_EMIT_FAST 1
 #endif
-__device__ __forceinline__ bool plain_scalar(uint64_t v) { return vtag(v) == V_STR || vtag(v) == V_INT; }
+// GK_EMIT_WIDE (GKGPU_JIT_PRE=GK_EMIT_WIDE=1, off): every heap-free argument
+// (numbers, booleans, nodes) on the fast path, not only interned strings and
+// ints.  Off: with it on, K8sContainerLimits lost its "memory limit ... is
+// higher" rows on the GPU (tests/test_audit_cache.py namespace-selector
+// case): a loop-carried register of the predicate (the lazily loaded
+// parameter) held a foreign value at the next body, and the loss came and
+// went with unrelated code changes (a printf after each emission hid it).
+// Left off until that is understood (tools/diag_rows.py reproduces it).
+#ifndef GK_EMIT_WIDE
+#define GK_EMIT_WIDE 0
+#endif
+__device__ __forceinline__ bool plain_scalar(uint64_t v) {
+#if GK_EMIT_WIDE
+  return memo_stable(v) && vtag(v) != V_UNDEF;
+#else
+  return vtag(v) == V_STR || vtag(v) == V_INT;
+#endif
+}
 __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
 #if GK_EMIT_FAST
   bool fast = false;
@@ -2596,6 +2613,18 @@ __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, u
 #endif
 }
 
+// (out of line: the argument list is built only where an argument is not a
+// plain scalar)
+__device__ __noinline__ bool op_emit_build_slow(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
+                                                const uint64_t* args, const uint32_t* ys, uint32_t n) {
+  uint64_t l = list_new(L, LK_ARR, 4);
+  for (uint32_t i = 0; i < n; ++i)
+    if (!op_list_add(L, l, args[i], ys[i])) return false;
+  const uint64_t m2 = lazy_sprintf_n(L, fmt_fidx(m), l, n);
+  if (L.fail) return false;
+  return op_emit_slow(L, m2, d, depth, rule);
+}
+
 // op_emit_args for a sprintf whose argument list the JIT did not build
 // (jit.cc dce_sites): the value carries the format only, so the slow path
 // builds the list from the arguments first (the same LIST_ADDs the program
@@ -2608,13 +2637,8 @@ __device__ __forceinline__ bool op_emit_args_build(PLane& L, uint64_t m, uint64_
 #pragma unroll
   for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
   if (fast) return op_emit_args(L, m, d, depth, rule, args);
-  if (vtag(m) != V_FMT) return op_emit(L, m, d, depth, rule);
-  uint64_t l = list_new(L, LK_ARR, 4);
-#pragma unroll
-  for (uint32_t i = 0; i < N; ++i)
-    if (!op_list_add(L, l, args[i], ys[i])) return false;
-  const uint64_t m2 = lazy_sprintf_n(L, fmt_fidx(m), l, N);
-  return op_emit(L, m2, d, depth, rule);
+  if (vtag(m) != V_FMT) return op_emit_slow(L, m, d, depth, rule);
+  return op_emit_build_slow(L, m, d, depth, rule, args, ys, N);
 }
 
 // Printed length of a deferred message whose arguments are plain scalars:

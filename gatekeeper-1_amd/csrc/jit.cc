@@ -970,14 +970,17 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r) << (init ? " = 0" : "");
   if (!p.nregs) o << "unused_";
   o << ";\n";
-  for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << ";\n";
+  // The shadow and memo locals below start at 0: they are read only behind
+  // their valid flags, but a read of an uninitialised local is undefined
+  // behaviour, which the optimiser may exploit across the whole predicate
+  for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << " = 0;\n";
   for (const auto& es : esites)
-    for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << ";\n";
+    for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << " = 0;\n";
   // memo slots are locals too: (key0, key1, value, valid)
   for (uint32_t m : lslots) {
-    o << "  uint64_t mk0_" << m << ", mk1_" << m << ", mv_" << m << "; bool mok_" << m << " = false;\n";
+    o << "  uint64_t mk0_" << m << " = 0, mk1_" << m << " = 0, mv_" << m << " = 0; bool mok_" << m << " = false;\n";
     if (memo2.count(m))
-      o << "  uint64_t mkb0_" << m << ", mkb1_" << m << ", mvb_" << m << "; bool mokb_" << m << " = false;\n";
+      o << "  uint64_t mkb0_" << m << " = 0, mkb1_" << m << " = 0, mvb_" << m << " = 0; bool mokb_" << m << " = false;\n";
   }
   // Param-keyed register memo (GKGPU_JIT_PMEMO, default on): a pure call whose
   // arguments are derived from the constraint's parameters (jit.cc
@@ -1339,7 +1342,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       if (psite.erase(q)) put_site.erase(bank.code[q].x - 1);
     }
   for (uint32_t ps : psite)
-    o << "  uint64_t psk0_" << ps << ", psk1_" << ps << ", psv_" << ps << "; bool psok_" << ps << " = false;\n";
+    o << "  uint64_t psk0_" << ps << " = 0, psk1_" << ps << " = 0, psv_" << ps << " = 0; bool psok_" << ps << " = false;\n";
   std::ostringstream fo;  // the outlined functions (before the predicate)
   for (auto& kv : outl) {
     const uint32_t g0 = kv.first, put = kv.second;
