@@ -222,6 +222,10 @@ struct EmitFlow {
     std::vector<uint16_t> undef;  // registers known to hold undefined (sorted)
   };
   std::vector<State> in;
+  // r holds undefined on entry to instruction k, on every path
+  bool undef_at(uint32_t k, uint16_t r) const {
+    return k < in.size() && !in[k].top && std::binary_search(in[k].undef.begin(), in[k].undef.end(), r);
+  }
   const FFact* find(uint32_t k, uint16_t f) const {
     if (k >= in.size() || in[k].top) return nullptr;
     for (const FFact& x : in[k].fmts) if (x.f == f) return &x;
@@ -306,6 +310,8 @@ EmitFlow emit_flow(const Program& p, const CodeBank& bank, const FmtFlow& F) {
         // the previous iteration's heap is reclaimed: no fact crosses
         s.lists.clear();
         s.fmts.clear();
+        ins_regs(in, rd, wr);
+        for (uint32_t r : wr) kill(s, r);
         break;
       case OP_LIST_NEW: {
         kill(s, in.a);
@@ -885,8 +891,10 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       for (uint32_t r : rd) {
         if (!F.has(k, r)) continue;
         const bool fused = in.op == OP_EMIT && in.b == 0xffff && r == in.a && EFL.find(k, in.a) && EFL.find(k, in.a)->n > 0;
-        // (not a yield: op_yield forces a V_FMT to compare it with a defined output)
-        if (!(in.op == OP_MOV || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || fused))
+        // (a yield only into an output known to be undefined: op_yield forces
+        // a V_FMT to compare it with a defined one)
+        const bool copy = in.op == OP_MOV || (in.op == OP_YIELD && r == in.b && r != in.a && EFL.undef_at(k, in.a));
+        if (!(copy || in.op == OP_JUNDEF || in.op == OP_JFALSE || in.op == OP_JTRUE || fused))
           prog_ok = false;
       }
     }
@@ -1077,7 +1085,12 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         else o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) " << RET;
         break;
       case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) " << RET; break;
-      case OP_YIELD: o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) " << RET; break;
+      case OP_YIELD:
+        if (EFL.undef_at(k, in.a) && in.a != in.b)  // into an output known to be undefined: a copy (no conflict check)
+          o << a << " = " << b << ";" << (in.y ? " if (heap_val(" + a + ")) pin_escape(L, " + y + ");" : std::string());
+        else
+          o << "if (!op_yield(L, " << a << ", " << b << ", " << y << ")) " << RET;
+        break;
       case OP_CALL: {
         // builtins are called directly with register operands (no argument
         // array, no dispatch on the builtin id)

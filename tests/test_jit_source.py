@@ -57,7 +57,7 @@ def test_computed_key_lookup_reuses_its_shadow():
     on = _dump("K8sRequiredProbes")
     off = _dump("K8sRequiredProbes", [("GKGPU_JIT_DYNCSE", "0")])
     import re
-    assert re.search(r"uint64_t dk\d+;", on)
+    assert re.search(r"uint64_t dk\d+ = 0;", on)
     assert re.search(r"= dk\d+;  // = vget\(L, ", on)
     assert "dk" not in off.split("_pred(")[1]
 
@@ -85,7 +85,8 @@ def test_parameter_reads_come_from_the_wave_lds_stage():
 
 
 def test_lazy_sprintf_argument_count_is_an_immediate():
-    src = _dump("K8sRequiredProbes")
+    # (with the list built: the fused emission otherwise drops it, below)
+    src = _dump("K8sRequiredProbes", [("GKGPU_JIT_EMITDCE", "0")])
     assert "lazy_sprintf_n(L," in src
     assert "lazy_sprintf(L," not in src
 
@@ -116,3 +117,13 @@ def test_fused_emission_builds_no_argument_list():
     assert "list_new(L," not in on
     assert "op_emit_args_build(L," not in off
     assert "list_new(L," in off and "op_emit_args(L," in off
+
+
+def test_yield_into_an_undefined_output_is_a_copy():
+    """jit.cc: a yield whose output register holds undefined on every path
+    (EmitFlow.undef_at) is a plain copy -- no conflict check, so a deferred
+    sprintf passes through it unforced and K8sRequiredProbes' message list is
+    dropped too (jit.cc dce_sites)."""
+    src = _dump("K8sRequiredProbes")
+    assert "op_emit_args_build(L," in src
+    assert "list_new(L, 2u" not in src
