@@ -30,8 +30,15 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
-const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-w"};
-constexpr int kNOpts = 4;
+// -amdgpu-prealloc-sgpr-spill-vgprs: the lanes of the VGPRs that hold spilled
+// SGPRs are allocated up front.  Without it this toolchain (ROCm 7.2) miscompiled
+// large template kernels: a loop-carried register of K8sContainerLimits'
+// predicate was overwritten with values of uniform (scalar) bookkeeping, and
+// an inventory-join kernel faulted or flagged reviews; which code shape
+// triggered it came and went with unrelated edits.  -O1 and this option
+// each cleared both cases; the option keeps -O3 (profiles/r05/r05ag_sgpr_spill.txt).
+const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs"};
+constexpr int kNOpts = 6;
 
 std::string hex16(uint64_t v) {
   char b[17];
@@ -1629,8 +1636,16 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
   }
   int ver_major = 0, ver_minor = 0;
   hiprtcVersion(&ver_major, &ver_minor);
-  std::string key = hex16(fnv1a(src, fnv1a(std::string(gk_rt_common_h) + gk_rt_devrt_h +
-                                           std::to_string(ver_major) + "." + std::to_string(ver_minor))));
+  // GKGPU_JIT_OPTS (diagnostics): extra hipRTC options, space-separated
+  std::vector<std::string> xopt;
+  if (const char* xo = getenv("GKGPU_JIT_OPTS")) {
+    std::istringstream is(xo);
+    for (std::string t; is >> t;) xopt.push_back(t);
+  }
+  std::string xkey;
+  for (const auto& t : xopt) xkey += " " + t;
+  std::string key = hex16(fnv1a(src + xkey, fnv1a(std::string(gk_rt_common_h) + gk_rt_devrt_h +
+                                                  std::to_string(ver_major) + "." + std::to_string(ver_minor))));
   std::string dir = cache_dir();
   std::string fname = key + ".co";
   if (!dir.empty() && read_file(dir + "/" + fname, code)) {
@@ -1652,7 +1667,9 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
     log = "hiprtcCreateProgram failed";
     return false;
   }
-  hiprtcResult r = hiprtcCompileProgram(prog, kNOpts, kOpts);
+  std::vector<const char*> opts(kOpts, kOpts + kNOpts);
+  for (const auto& t : xopt) opts.push_back(t.c_str());
+  hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);
   log.assign(ls, '\0');

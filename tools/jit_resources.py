@@ -54,7 +54,7 @@ def resources(path):
     src = open(path).read()
     name = re.search(r"__global__ void __launch_bounds__\([^)]*\) (gk_t_[0-9a-f]+)\(", src)
     out = path + ".o"
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "--cuda-device-only",
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs", "--cuda-device-only",
                         "-c", "-I" + CSRC, "-Rpass-analysis=kernel-resource-usage", path, "-o", out],
                        capture_output=True, text=True, timeout=900)
     lines = [ln.split("remark: ")[-1] for ln in r.stderr.splitlines() if "remark:" in ln]
