@@ -2523,16 +2523,14 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
 #ifndef GK_EMIT_FAST
 #define GK_EMIT_FAST 1
 #endif
-// GK_EMIT_WIDE (GKGPU_JIT_PRE=GK_EMIT_WIDE=1, off): every heap-free argument
-// (numbers, booleans, nodes) on the fast path, not only interned strings and
-// ints.  Off: with it on, K8sContainerLimits lost its "memory limit ... is
-// higher" rows on the GPU (tests/test_audit_cache.py namespace-selector
-// case): a loop-carried register of the predicate (the lazily loaded
-// parameter) held a foreign value at the next body, and the loss came and
-// went with unrelated code changes (a printf after each emission hid it).
-// Left off until that is understood (tools/diag_rows.py reproduces it).
+// GK_EMIT_WIDE (GKGPU_JIT_PRE=GK_EMIT_WIDE=0 turns it off): every heap-free
+// argument (numbers, booleans, document and parameter nodes such as
+// k8sallowedrepos' input.parameters.repos) on the fast path, not only
+// interned strings and ints.  It first lost rows on the GPU -- a compiler
+// miscompile, cleared by -amdgpu-prealloc-sgpr-spill-vgprs (jit.cc kOpts);
+// profiles/r05/r05ah_prealloc_wide_ab.txt: config 4 1,995 -> 2,038 M evals/s.
 #ifndef GK_EMIT_WIDE
-#define GK_EMIT_WIDE 0
+#define GK_EMIT_WIDE 1
 #endif
 __device__ __forceinline__ bool plain_scalar(uint64_t v) {
 #if GK_EMIT_WIDE
