@@ -2611,13 +2611,24 @@ __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, u
 #endif
 }
 
-// (out of line: the argument list is built only where an argument is not a
-// plain scalar)
+// (out of line: the argument list is built only where an argument is not
+// heap-free.  Arguments by value and the LIST_ADD escape ranges packed 16
+// bits each: an array passed by address would be stored to the private
+// segment at every emission, fast path included -- 0.4 GB of writes per
+// K8sContainerLimits launch, profiles/r05/)
+__device__ __forceinline__ uint64_t sel6(uint32_t i, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3, uint64_t a4,
+                                         uint64_t a5) {
+  return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : i == 4 ? a4 : a5;
+}
+// an escape range (pin_escape: lo | hi << 8) packed in 10 bits as lo | hi << 5
+__device__ __forceinline__ uint32_t esc_unpack(uint32_t p) { return (p & 0x1fu) | (((p >> 5) & 0x1fu) << 8); }
 __device__ __noinline__ bool op_emit_build_slow(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
-                                                const uint64_t* args, const uint32_t* ys, uint32_t n) {
+                                                uint32_t n, uint64_t ys, uint64_t a0, uint64_t a1, uint64_t a2,
+                                                uint64_t a3, uint64_t a4, uint64_t a5) {
   uint64_t l = list_new(L, LK_ARR, 4);
   for (uint32_t i = 0; i < n; ++i)
-    if (!op_list_add(L, l, args[i], ys[i])) return false;
+    if (!op_list_add(L, l, sel6(i, a0, a1, a2, a3, a4, a5), esc_unpack((uint32_t)(ys >> (10 * i)) & 0x3ffu)))
+      return false;
   const uint64_t m2 = lazy_sprintf_n(L, fmt_fidx(m), l, n);
   if (L.fail) return false;
   return op_emit_slow(L, m2, d, depth, rule);
@@ -2626,17 +2637,20 @@ __device__ __noinline__ bool op_emit_build_slow(PLane& L, uint64_t m, uint64_t d
 // op_emit_args for a sprintf whose argument list the JIT did not build
 // (jit.cc dce_sites): the value carries the format only, so the slow path
 // builds the list from the arguments first (the same LIST_ADDs the program
-// would have run)
+// would have run; ys: their escape ranges, 10 bits each)
 template <uint32_t N>
 __device__ __forceinline__ bool op_emit_args_build(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
-                                                   const uint64_t (&args)[N], const uint32_t (&ys)[N]) {
+                                                   const uint64_t (&args)[N], uint64_t ys) {
+  static_assert(N <= 6, "fused emissions take up to six arguments");
   bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX &&
               L.ord < EM_MAXORD;
 #pragma unroll
   for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
   if (fast) return op_emit_args(L, m, d, depth, rule, args);
   if (vtag(m) != V_FMT) return op_emit_slow(L, m, d, depth, rule);
-  return op_emit_build_slow(L, m, d, depth, rule, args, ys, N);
+  return op_emit_build_slow(L, m, d, depth, rule, N, ys, args[0], N > 1 ? args[N > 1 ? 1 : 0] : 0,
+                            N > 2 ? args[N > 2 ? 2 : 0] : 0, N > 3 ? args[N > 3 ? 3 : 0] : 0,
+                            N > 4 ? args[N > 4 ? 4 : 0] : 0, N > 5 ? args[N > 5 ? 5 : 0] : 0);
 }
 
 // Printed length of a deferred message whose arguments are plain scalars:

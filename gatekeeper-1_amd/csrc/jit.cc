@@ -940,6 +940,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (pc > N && pc < S && in.op == OP_LIST_NEW && in.a == Lr) ok = false;
       }
       if (ok && adds.size() != ff.n) ok = false;
+      // escape ranges packed 10 bits each (devrt.h esc_unpack), six arguments at most
+      for (uint16_t i = 0; ok && i < ff.n; ++i) ok = (ff.ys[i] & 0xffu) < 32 && (ff.ys[i] >> 8) < 32;
+      if (ff.n > 6) ok = false;
       if (!ok) continue;
       dce_sites.insert(S);
       dce_pcs.insert(N);
@@ -1171,10 +1174,11 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           o << "{ const uint64_t ea_[" << ff->n << "] = {";
           for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << "es" << ff->site << "_" << i;
           if (dce_sites.count(ff->site)) {
-            o << "}; const uint32_t ey_[" << ff->n << "] = {";
-            for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << ff->ys[i] << "u";
-            o << "}; if (!op_emit_args_build(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_, ey_)) " << RET
-              << " }";
+            uint64_t yp = 0;
+            for (uint16_t i = 0; i < ff->n; ++i)
+              yp |= (uint64_t)((ff->ys[i] & 0x1fu) | (((ff->ys[i] >> 8) & 0x1fu) << 5)) << (10 * i);
+            o << "}; if (!op_emit_args_build(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_, " << yp
+              << "ull)) " << RET << " }";
           } else {
             o << "}; if (!op_emit_args(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
           }

@@ -1,12 +1,12 @@
 """Kernel resource usage of the template kernels (jit.cc) without a GPU.
 
-Dumps the hipRTC source of every template kernel of a configuration
-(GKGPU_JIT_DUMP_ONLY: the generator runs, hipRTC does not) and compiles each
-with hipcc for gfx950 with -Rpass-analysis=kernel-resource-usage, which prints
-the VGPR/SGPR counts, spills, the private-segment (scratch) bytes per lane,
-LDS bytes and occupancy the code object will have on the device.
+Compiles every template kernel of a configuration with hipRTC, exactly as the
+engine does (jit.cc kOpts, gfx950), into a scratch code-object cache, and
+reads each code object's metadata notes (llvm-readelf --notes): VGPRs, AGPRs,
+SGPRs, their spill counts, the private-segment (scratch) bytes per lane, LDS
+bytes per block, and the waves per SIMD the VGPR count allows.
 
-    python tools/jit_resources.py [--config 2] [--out profiles/r03_jit_resources.txt]
+    python tools/jit_resources.py [--config 2] [--out profiles/r05/r05_jit_resources_c2.txt]
 """
 import argparse
 import glob
@@ -17,11 +17,12 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "gatekeeper-1_amd", "csrc")
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+FIELDS = (".vgpr_count", ".agpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count",
+          ".private_segment_fixed_size", ".group_segment_fixed_size", ".uses_dynamic_stack")
 
 
-def dump_sources(config):
-    d = tempfile.mkdtemp(prefix="gkjit_res")
+def compile_kernels(config, cache):
     code = r'''
 import sys
 sys.path[:0] = [%r, %r]
@@ -29,37 +30,39 @@ import gkgpu
 from gkgpu import workloads as W
 from gkgpu.client import Client
 ts, cs = getattr(W, "config%d")()
-import os
+d = gkgpu.Driver(host_only=True)
+cl = Client(d)
 for t in ts:
-    # one engine per template: its kernel source alone in its own directory
+    cl.add_template(t)
+for t in ts:
     k = t["spec"]["crd"]["spec"]["names"]["kind"]
-    os.makedirs(os.path.join(%r, k), exist_ok=True)
-    os.environ["GKGPU_JIT_DUMP"] = os.path.join(%r, k)
-    d = gkgpu.Driver()
-    Client(d).add_template(t)
-    print(k, d.template_backend(k))
-''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), config, d, d)
-    env = dict(os.environ, GKGPU_JIT_CACHE="0", GKGPU_JIT_DUMP=d, GKGPU_JIT_DUMP_ONLY="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
+    print(k, *d.template_backend(k))
+''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), config)
+    env = dict(os.environ, GKGPU_JIT_CACHE=cache)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=1800)
     if r.returncode != 0:
         raise SystemExit(r.stderr[-3000:])
-    files = [(os.path.basename(os.path.dirname(f)), f) for f in sorted(glob.glob(os.path.join(d, "*", "*.hip")))]
-    return files, r.stdout
+    out = {}
+    for ln in r.stdout.splitlines():
+        p = ln.split()
+        if len(p) == 3:
+            out[p[2]] = (p[0], p[1])
+    return out
 
 
-FIELDS = ("VGPRs:", "AGPRs:", "SGPRs:", "ScratchSize", "Occupancy", "LDS Size", "VGPRs Spill", "SGPRs Spill")
-
-
-def resources(path):
-    src = open(path).read()
-    name = re.search(r"__global__ void __launch_bounds__\([^)]*\) (gk_t_[0-9a-f]+)\(", src)
-    out = path + ".o"
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs", "--cuda-device-only",
-                        "-c", "-I" + CSRC, "-Rpass-analysis=kernel-resource-usage", path, "-o", out],
-                       capture_output=True, text=True, timeout=900)
-    lines = [ln.split("remark: ")[-1] for ln in r.stderr.splitlines() if "remark:" in ln]
-    keep = [ln for ln in lines if any(f in ln for f in FIELDS)]
-    return (name.group(1) if name else os.path.basename(path)), r.returncode, keep
+def notes(path):
+    r = subprocess.run([READELF, "--notes", path], capture_output=True, text=True)
+    kernels, cur = {}, None
+    for ln in r.stdout.splitlines():
+        m = re.search(r"\.name:\s+(\S+)", ln)
+        if m and m.group(1).startswith("gk_t_"):
+            cur = kernels.setdefault(m.group(1), {})
+            continue
+        for f in FIELDS:
+            m = re.search(re.escape(f) + r":\s+(\S+)", ln)
+            if m and cur is not None:
+                cur[f[1:]] = m.group(1)
+    return kernels
 
 
 def main():
@@ -67,12 +70,24 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    files, backends = dump_sources(a.config)
-    rep = ["config %d template kernels (hipcc gfx950 -O3, kernel-resource-usage)" % a.config, backends.strip(), ""]
-    for kind, f in files:
-        name, rc, keep = resources(f)
-        rep.append("%s %s (rc %d)" % (kind, name, rc))
-        rep.extend("  " + k for k in keep)
+    cache = tempfile.mkdtemp(prefix="gkjit_res")
+    names = compile_kernels(a.config, cache)
+    found = {}
+    for co in glob.glob(os.path.join(cache, "*.co")):
+        found.update(notes(co))
+    rep = ["config %d template kernels: hipRTC code objects (jit.cc kOpts, gfx950), metadata notes" % a.config, ""]
+    for name, (kind, backend) in names.items():
+        k = found.get(name)
+        rep.append("%s %s (backend %s)" % (kind, name, backend))
+        if not k:
+            rep.append("  no code object (bytecode VM)")
+            continue
+        regs = int(k.get("vgpr_count", 0)) + int(k.get("agpr_count", 0))
+        waves = min(8, 512 // max(8, (regs + 7) // 8 * 8)) if regs else 8
+        for f in FIELDS:
+            if f[1:] in k:
+                rep.append("  %s: %s" % (f[1:], k[f[1:]]))
+        rep.append("  waves per SIMD (VGPR-bound): %d" % waves)
     text = "\n".join(rep) + "\n"
     print(text)
     if a.out:
