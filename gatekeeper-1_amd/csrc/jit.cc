@@ -991,9 +991,11 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   // The shadow and memo locals below start at 0: they are read only behind
   // their valid flags, but a read of an uninitialised local is undefined
   // behaviour, which the optimiser may exploit across the whole predicate
-  for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << " = 0;\n";
+  const char* z0 = getenv("GKGPU_JIT_ZERO");  // A/B: 0 = shadows uninitialised
+  const std::string Z = (z0 && atoi(z0) == 0) ? "" : " = 0";
+  for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << Z << ";\n";
   for (const auto& es : esites)
-    for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << " = 0;\n";
+    for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << Z << ";\n";
   // memo slots are locals too: (key0, key1, value, valid)
   for (uint32_t m : lslots) {
     o << "  uint64_t mk0_" << m << " = 0, mk1_" << m << " = 0, mv_" << m << " = 0; bool mok_" << m << " = false;\n";
