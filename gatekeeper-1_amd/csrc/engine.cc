@@ -322,6 +322,7 @@ struct EvalCtx {
   NodeArena arena;           // host documents of the current query (node id perm_nodes + k)
   // pinned host staging for the readback: several device-to-host copies are
   // queued back to back and waited for once (a pageable copy syncs each time)
+  unsigned int last_ncand = 0;  // sample candidates of the context's last audit (gk_batch_eval_audit)
   char* h_pin = nullptr;
   size_t h_pin_cap = 0;
   char* pin(size_t n) {
@@ -3147,6 +3148,12 @@ static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk
   hipEvent_t ev0 = x->events[0], ev1 = x->events[1];
   hipEventRecord(ev0, x->stream);
   unsigned int ncand = 0;
+  // one wait per pass: the candidate count, the totals and the first K
+  // candidates (K from the last audit's count) come back in one batch of
+  // async copies into the context's pinned buffer
+  const size_t o_tot = 16, o_cand = o_tot + (size_t)ncons * 8;
+  size_t kcand = 0;
+  char* hp = nullptr;
   for (int pass = 0; pass < 3; ++pass) {
     // no lane failed and no enforcementAction error: every review counts, and
     // the sampling passes skip the per-tuple review-flag reads
@@ -3158,9 +3165,16 @@ static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk
                               (unsigned int*)x->d_ncand.p, pass > 0, x->stream);
     if (lr != 0) return fail(e, GK_EDEVICE, std::string("sample launch failed: ") + hipGetErrorString((hipError_t)lr));
     if (pass == 0) hipEventRecord(ev1, x->stream);
-    if (hipMemcpyAsync(&ncand, x->d_ncand.p, 4, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+    kcand = std::min<size_t>(x->cand_cap, std::max<size_t>(2 * (size_t)x->last_ncand, 256));
+    hp = x->pin(o_cand + kcand * sizeof(SampleRec));
+    if (!hp) return fail(e, GK_EDEVICE, "pinned host allocation failed");
+    if (hipMemcpyAsync(hp, x->d_ncand.p, 4, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipMemcpyAsync(hp + o_tot, x->d_ftot.p, (size_t)ncons * 8, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipMemcpyAsync(hp + o_cand, x->d_cand.p, kcand * sizeof(SampleRec), hipMemcpyDeviceToHost, x->stream) !=
+            hipSuccess ||
         hipStreamSynchronize(x->stream) != hipSuccess)
       return fail(e, GK_EDEVICE, "sample pass failed");
+    memcpy(&ncand, hp, 4);
     if (ncand <= x->cand_cap) break;
     x->cand_cap = std::max<size_t>(x->cand_cap * 2, (size_t)ncand + 1024);
     if (!x->d_cand.reserve(x->cand_cap * sizeof(SampleRec))) return fail(e, GK_EDEVICE, "device allocation failed");
@@ -3168,9 +3182,13 @@ static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk
   float kms = 0;
   hipEventElapsedTime(&kms, ev0, ev1);
   res->launches.push_back({"gk_sample", (double)kms, ncons, 0, 0});
+  if (ncand > x->cand_cap) return fail(e, GK_EDEVICE, "sample candidates past capacity");
+  x->last_ncand = ncand;
   std::vector<uint64_t> ftot(ncons);
   std::vector<SampleRec> cand(ncand);
-  if (!d2h(x, ftot.data(), x->d_ftot.p, ncons * 8) || !d2h(x, cand.data(), x->d_cand.p, (size_t)ncand * sizeof(SampleRec)))
+  memcpy(ftot.data(), hp + o_tot, (size_t)ncons * 8);
+  if (ncand <= kcand) memcpy(cand.data(), hp + o_cand, (size_t)ncand * sizeof(SampleRec));
+  else if (!d2h(x, cand.data(), x->d_cand.p, (size_t)ncand * sizeof(SampleRec)))  // more than the last audit's
     return fail(e, GK_EDEVICE, "sample copy failed");
   for (uint32_t c = 0; c < ncons; ++c) res->totals[c] = ftot[c];
   std::sort(cand.begin(), cand.end(), [](const SampleRec& x, const SampleRec& y) {
