@@ -344,7 +344,10 @@ constexpr uint32_t FMT_MAXARGS = 6;
 // deferred message's details (unless VF_DET_*) are at ebytes[msg_off, +det_len)
 //   VF_NOPRINT set by the size pass: the message or details cannot be printed
 //              on the GPU (the review goes to the CPU); the tuple gets no bytes
-constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2, VF_DET_VAL = 4, VF_NOPRINT = 8;
+//   VF_DET_KV  (with VF_DEFER) the details are a one-member object {k: v}: k
+//              and v are the two frec words after the message's arguments
+//              (k8sallowedlabelregex's {"label": key}); printed like VF_DET_VAL
+constexpr uint32_t VF_DEFER = 1, VF_DET_OBJ = 2, VF_DET_VAL = 4, VF_NOPRINT = 8, VF_DET_KV = 16;
 // the size / format passes work in tiles of FTILE consecutive tuples
 constexpr uint32_t FTILE = 256;  // one block pass: a small output still spreads over many blocks
 

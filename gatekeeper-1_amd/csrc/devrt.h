@@ -2539,16 +2539,40 @@ __device__ __forceinline__ bool plain_scalar(uint64_t v) {
   return vtag(v) == V_STR || vtag(v) == V_INT;
 #endif
 }
+// Details the fast path carries: none (the hook default), or a one-member
+// object whose key is an interned string and whose value is heap-free
+// (VF_DET_KV: two frec words, no staged bytes, no out-of-line call)
+#ifndef GK_DET_KV
+#define GK_DET_KV 1  // A/B: GKGPU_JIT_PRE=GK_DET_KV=0
+#endif
+__device__ __forceinline__ bool det_fast(PLane& L, uint64_t d, bool& kv, uint64_t& dk, uint64_t& dv) {
+  kv = false;
+  if (vtag(d) == V_UNDEF) return true;
+  if (!GK_DET_KV) return false;
+  if (tclass(d) != 8 || coll_len(L, d) != 1) return false;
+  coll_at(L, d, 0, dk, dv);
+  kv = vtag(dk) == V_STR && plain_scalar(dv);
+  return kv;
+}
+__device__ __forceinline__ void det_fast_put(Viol& v, bool kv, uint64_t slot, uint32_t n, uint64_t dk, uint64_t dv) {
+  v.det_len = kv ? 0u : 2u;
+  v.pad = VF_DEFER | (kv ? VF_DET_KV : VF_DET_OBJ);
+  if (kv) {
+    gk_args.frec[(uint64_t)n * gk_args.out_cap + slot] = dk;
+    gk_args.frec[(uint64_t)(n + 1) * gk_args.out_cap + slot] = dv;
+  }
+}
+
 __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule) {
 #if GK_EMIT_FAST
-  bool fast = false;
+  bool fast = false, kv = false;
   uint32_t n = 0, seq = 0;
-  uint64_t args = 0;
-  if (vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX && L.ord < EM_MAXORD) {
+  uint64_t args = 0, dk = 0, dv = 0;
+  if (vtag(m) == V_FMT && !L.fail && L.en < EM_MAXIDX && L.ord < EM_MAXORD && det_fast(L, d, kv, dk, dv)) {
     args = fmt_args(m);
     if (vtag(args) == V_LIST) {
       n = list_len(L, args);
-      fast = n <= FMT_MAXARGS;
+      fast = n + (kv ? 2u : 0u) <= FMT_MAXARGS;
       for (uint32_t i = 0; i < n && fast; ++i) fast = plain_scalar(list_at(L, args, i));
     }
   }
@@ -2564,8 +2588,7 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
     v.rule = (uint16_t)rule;
     v.msg_len = fmt_fidx(m) | (n << 24);
     v.msg_off = 0;
-    v.det_len = 2;
-    v.pad = VF_DEFER | VF_DET_OBJ;
+    det_fast_put(v, kv, slot, n, dk, dv);
     gk_args.out[slot] = v;
     for (uint32_t i = 0; i < n; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = list_at(L, args, i);
     return true;
@@ -2581,8 +2604,10 @@ template <uint32_t N>
 __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
                                              const uint64_t (&args)[N]) {
 #if GK_EMIT_FAST
-  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX &&
-              L.ord < EM_MAXORD;
+  bool kv = false;
+  uint64_t dk = 0, dv = 0;
+  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && !L.fail && L.en < EM_MAXIDX && L.ord < EM_MAXORD &&
+              det_fast(L, d, kv, dk, dv) && N + (kv ? 2u : 0u) <= FMT_MAXARGS;
 #pragma unroll
   for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
   if (fast) {
@@ -2597,8 +2622,7 @@ __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, u
     v.rule = (uint16_t)rule;
     v.msg_len = fmt_fidx(m) | (N << 24);
     v.msg_off = 0;
-    v.det_len = 2;
-    v.pad = VF_DEFER | VF_DET_OBJ;
+    det_fast_put(v, kv, slot, N, dk, dv);
     gk_args.out[slot] = v;
 #pragma unroll
     for (uint32_t i = 0; i < N; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = args[i];
@@ -2642,8 +2666,10 @@ template <uint32_t N>
 __device__ __forceinline__ bool op_emit_args_build(PLane& L, uint64_t m, uint64_t d, uint32_t depth, uint32_t rule,
                                                    const uint64_t (&args)[N], uint64_t ys) {
   static_assert(N <= 6, "fused emissions take up to six arguments");
-  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && vtag(d) == V_UNDEF && !L.fail && L.en < EM_MAXIDX &&
-              L.ord < EM_MAXORD;
+  bool kv = false;
+  uint64_t dk = 0, dv = 0;
+  bool fast = N <= FMT_MAXARGS && vtag(m) == V_FMT && !L.fail && L.en < EM_MAXIDX && L.ord < EM_MAXORD &&
+              det_fast(L, d, kv, dk, dv) && N + (kv ? 2u : 0u) <= FMT_MAXARGS;
 #pragma unroll
   for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
   if (fast) return op_emit_args(L, m, d, depth, rule, args);

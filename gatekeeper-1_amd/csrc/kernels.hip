@@ -319,6 +319,22 @@ __device__ __forceinline__ uint64_t det_word(const Viol& v, uint64_t i) {
   const uint32_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
   return gk_args.frec[(uint64_t)di * gk_args.out_cap + i];
 }
+// Details printed from frec words: VF_DET_VAL the JSON of one value, VF_DET_KV
+// {k: v} as encoding/json prints a one-key map (k an interned string).  One
+// put_json site for both: a second inlined copy of the printer pushed the
+// format pass past its registers (spills).
+template <class O>
+__device__ __forceinline__ bool put_det_words(PLane& L, O& o, uint32_t pad, uint64_t k, uint64_t val) {
+  const bool kv = (pad & VF_DET_KV) != 0;
+  if (kv) {
+    put(o, '{');
+    if (!put_json_str(o, sview(L, k))) return false;
+    put(o, ':');
+  }
+  if (!put_json(L, o, val)) return false;
+  if (kv) put(o, '}');
+  return true;
+}
 
 // The lane the size / format passes hand to the printers.  Deferred arguments
 // are heap-free values, so nothing reads it; a failing print only sets its
@@ -345,9 +361,13 @@ __global__ void __launch_bounds__(256) gk_size_kernel(DevArgs) {
       uint32_t ml = v.msg_len, dl = det_bytes(v);
       bool printable = true;
       if (v.pad & VF_DEFER) printable = size_deferred_msg(L, v, i, ml);
-      if (v.pad & VF_DET_VAL) {
+      if (v.pad & (VF_DET_VAL | VF_DET_KV)) {
+        const uint64_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
+        const bool kv = (v.pad & VF_DET_KV) != 0;
+        const uint64_t k = kv ? gk_args.frec[di * gk_args.out_cap + i] : 0ull;
+        const uint64_t val = gk_args.frec[(di + (kv ? 1u : 0u)) * gk_args.out_cap + i];
         Cnt cn{0, false};
-        printable = put_json(L, cn, det_word(v, i)) && printable;
+        printable = put_det_words(L, cn, v.pad, k, val) && printable;
         dl = cn.n;
         gk_args.out[i].det_len = dl;  // the format pass's det_bytes
       }
@@ -423,7 +443,7 @@ __device__ __forceinline__ bool compact_overflow(uint64_t raw) {
 }
 __device__ __forceinline__ uint32_t frec_words(const Viol& v) {
   const uint32_t na = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
-  return na + ((v.pad & VF_DET_VAL) ? 1u : 0u);
+  return na + ((v.pad & VF_DET_VAL) ? 1u : (v.pad & VF_DET_KV) ? 2u : 0u);
 }
 
 __global__ void __launch_bounds__(256) gk_compact_count(const Viol* raw, uint32_t* tcnt, DevArgs) {
@@ -550,8 +570,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
       const uint32_t ml = len - dl;
       uint64_t a[FMT_MAXARGS];
       const uint32_t na = defer ? (v.msg_len >> 24) : 0u;
+      const uint32_t nw = na + ((valid && (v.pad & VF_DET_KV)) ? 2u : 0u);  // (the details' key and value)
 #pragma unroll
-      for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < na ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
+      for (uint32_t j = 0; j < FMT_MAXARGS; ++j) a[j] = j < nw ? gk_args.frec[(uint64_t)j * gk_args.out_cap + i] : 0;
       // the wave's range [lo, hi): consecutive tuples, consecutive bytes
       const uint64_t lo = __shfl(dst, 0, 64);
       const uint64_t hi = __shfl(dst + len, 63, 64);
@@ -565,7 +586,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         else if (defer) fmt_run(L, o, v.msg_len & 0xffffffu, [&](uint32_t j) { return sel_arg(a, j); });
         else puts_(o, gk_args.ebytes + v.msg_off, ml);
         if (v.pad & VF_DET_OBJ) { o.put('{'); o.put('}'); }
-        else if (v.pad & VF_DET_VAL) { if (dl) put_json(L, o, det_word(v, i)); }
+        else if (v.pad & (VF_DET_VAL | VF_DET_KV)) {
+          if (dl)
+            put_det_words(L, o, v.pad, sel_arg(a, na),
+                          (v.pad & VF_DET_KV) ? sel_arg(a, na + 1) : det_word(v, i));
+        }
         else puts_(o, gk_args.ebytes + v.msg_off + (defer ? 0u : ml), dl);
       };
       // the wave's bytes go through LDS in windows of FSTAGE: each lane prints

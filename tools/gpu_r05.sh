@@ -40,12 +40,15 @@ PY
            tail -4 "$OUT/pytest_parity.log"; [ $rc = 0 ] || exit 1 ;;
     audit) timeout -k 10 900 python -u -m pytest tests/test_audit_cache.py tests/test_audit_writer.py tests/test_parallel_gpu.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_audit.log" 2>&1; rc=$?
            tail -4 "$OUT/pytest_audit.log"; [ $rc = 0 ] || exit 1 ;;
+    scale) timeout -k 10 900 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -q --timeout 400 --timeout-method thread > "$OUT/pytest_scale.log" 2>&1; rc=$?
+           tail -4 "$OUT/pytest_scale.log"; [ $rc = 0 ] || exit 1 ;;
     scale4) timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -q -k config4 --timeout 300 --timeout-method thread > "$OUT/pytest_scale4.log" 2>&1; rc=$?
            tail -4 "$OUT/pytest_scale4.log"; grep -E "^E " "$OUT/pytest_scale4.log" | head -5; [ $rc = 0 ] || exit 1 ;;
     early) bash tools/gpu_bench_ab.sh "$TAG/early2" "--steps 10 --warmup 2 --shard-leg off" "" "GKGPU_FN_EARLY=1" || exit 1
            bash tools/gpu_bench_ab.sh "$TAG/early4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FN_EARLY=1" || exit 1 ;;
     ab2) IFS=';' read -ra S <<< "$AB2"; bash tools/gpu_bench_ab.sh "$TAG/ab2" "--steps 10 --warmup 2 --shard-leg off" "${S[@]}" || exit 1 ;;
     ab4) IFS=';' read -ra S <<< "$AB4"; bash tools/gpu_bench_ab.sh "$TAG/ab4" "--config 4 --steps 5 --warmup 1" "${S[@]}" || exit 1 ;;
+    ab3) IFS=';' read -ra S <<< "$AB3"; bash tools/gpu_bench_ab.sh "$TAG/ab3" "--config 3 --steps 5 --warmup 1 --shard-leg off" "${S[@]}" || exit 1 ;;
     quick) timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --shard-leg off --cpu-sample 0 > "$OUT/quick.json" 2> "$OUT/quick.err" || { echo QUICK_FAIL; tail "$OUT/quick.err"; exit 1; }
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c=d['config']; print('QUICK', round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],3), 'ms kernels', round(c['kernel_ms_per_step'],3))" "$OUT/quick.json" ;;
     cache) timeout -k 10 600 python -u bench.py --from-cache --steps 5 --warmup 1 > "$OUT/cache.json" 2> "$OUT/cache.err" || { echo CACHE_FAIL; tail "$OUT/cache.err"; exit 1; }
