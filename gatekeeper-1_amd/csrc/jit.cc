@@ -873,7 +873,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   std::map<uint32_t, EmitFlow::FFact> efacts;  // site pc -> its fact (list, LIST_NEW pc, add operands)
   for (uint32_t pc = b0; pc < b1; ++pc) {
     const Ins& in = bank.code[pc];
-    if (in.op != OP_EMIT || in.b != 0xffff) continue;
+    if (in.op != OP_EMIT || in.b == in.a) continue;
     if (const EmitFlow::FFact* ff = EFL.find(pc - b0, in.a))
       if (ff->n > 0) { esites[ff->site] = std::vector<uint16_t>(ff->args, ff->args + ff->n); efacts[ff->site] = *ff; }
   }
@@ -897,7 +897,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       ins_regs(in, rd, wr);
       for (uint32_t r : rd) {
         if (!F.has(k, r)) continue;
-        const bool fused = in.op == OP_EMIT && in.b == 0xffff && r == in.a && EFL.find(k, in.a) && EFL.find(k, in.a)->n > 0;
+        const bool fused = in.op == OP_EMIT && in.b != in.a && r == in.a && EFL.find(k, in.a) && EFL.find(k, in.a)->n > 0;
         // (a yield only into an output known to be undefined: op_yield forces
         // a V_FMT to compare it with a defined one)
         const bool copy = in.op == OP_MOV || (in.op == OP_YIELD && r == in.b && r != in.a && EFL.undef_at(k, in.a));
@@ -1169,7 +1169,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       }
       case OP_LEN_EQ: o << a << " = op_len_eq(L, " << b << ", " << y << ");"; break;
       case OP_EMIT: {
-        const EmitFlow::FFact* ff = in.b == 0xffff ? EFL.find(k, in.a) : nullptr;
+        // (with details: a register the fast path reads for a one-member object, devrt.h det_fast)
+        const EmitFlow::FFact* ff = in.b != in.a ? EFL.find(k, in.a) : nullptr;
+        const std::string D = in.b == 0xffff ? std::string(UND) : b;
         if (ff && ff->n > 0) {
           // (mu: the argument registers are read only where the message is the sprintf)
           if (ff->mu) o << "if (vtag(" << a << ") == V_FMT) ";
@@ -1179,13 +1181,13 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
             uint64_t yp = 0;
             for (uint16_t i = 0; i < ff->n; ++i)
               yp |= (uint64_t)((ff->ys[i] & 0x1fu) | (((ff->ys[i] >> 8) & 0x1fu) << 5)) << (10 * i);
-            o << "}; if (!op_emit_args_build(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_, " << yp
+            o << "}; if (!op_emit_args_build(L, " << a << ", " << D << ", " << in.c << "u, " << y << ", ea_, " << yp
               << "ull)) " << RET << " }";
           } else {
-            o << "}; if (!op_emit_args(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
+            o << "}; if (!op_emit_args(L, " << a << ", " << D << ", " << in.c << "u, " << y << ", ea_)) " << RET << " }";
           }
           if (ff->mu)
-            o << " else if (!op_emit(L, " << a << ", " << UND << ", " << in.c << "u, " << y << ")) " << RET;
+            o << " else if (!op_emit(L, " << a << ", " << D << ", " << in.c << "u, " << y << ")) " << RET;
         } else {
           o << "if (!op_emit(L, " << a << ", " << (in.b == 0xffff ? std::string(UND) : b) << ", " << in.c << "u, " << y
             << ")) " << RET;
