@@ -2597,6 +2597,28 @@ __device__ __forceinline__ bool op_emit(PLane& L, uint64_t m, uint64_t d, uint32
   return op_emit_slow(L, m, d, depth, rule);
 }
 
+// the fast path's record: the tuple and its argument (and details) words
+template <uint32_t N>
+__device__ __forceinline__ bool emit_fast_write(PLane& L, uint64_t m, uint32_t rule, const uint64_t (&args)[N], bool kv,
+                                                uint64_t dk, uint64_t dv) {
+  const uint32_t seq = ((uint32_t)L.ord << 8) | (uint32_t)L.en;
+  const uint64_t slot = slot_reserve(true);
+  L.en = L.en + 1u;
+  if (slot >= gk_args.out_cap) { slot_overflow(L); return true; }
+  Viol v;
+  v.review = L.rv;
+  v.constraint = L.cn;
+  v.seq = (uint16_t)seq;
+  v.rule = (uint16_t)rule;
+  v.msg_len = fmt_fidx(m) | (N << 24);
+  v.msg_off = 0;
+  det_fast_put(v, kv, slot, N, dk, dv);
+  gk_args.out[slot] = v;
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = args[i];
+  return true;
+}
+
 // op_emit for a deferred message whose argument registers the JIT knows
 // (jit.cc emit_flow): the same record, the argument words taken from the
 // registers instead of the lane heap's list
@@ -2610,24 +2632,7 @@ __device__ __forceinline__ bool op_emit_args(PLane& L, uint64_t m, uint64_t d, u
               det_fast(L, d, kv, dk, dv) && N + (kv ? 2u : 0u) <= FMT_MAXARGS;
 #pragma unroll
   for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
-  if (fast) {
-    const uint32_t seq = ((uint32_t)L.ord << 8) | (uint32_t)L.en;
-    const uint64_t slot = slot_reserve(true);
-    L.en = L.en + 1u;
-    if (slot >= gk_args.out_cap) { slot_overflow(L); return true; }
-    Viol v;
-    v.review = L.rv;
-    v.constraint = L.cn;
-    v.seq = (uint16_t)seq;
-    v.rule = (uint16_t)rule;
-    v.msg_len = fmt_fidx(m) | (N << 24);
-    v.msg_off = 0;
-    det_fast_put(v, kv, slot, N, dk, dv);
-    gk_args.out[slot] = v;
-#pragma unroll
-    for (uint32_t i = 0; i < N; ++i) gk_args.frec[(uint64_t)i * gk_args.out_cap + slot] = args[i];
-    return true;
-  }
+  if (fast) return emit_fast_write(L, m, rule, args, kv, dk, dv);
   // the list holds these same arguments: op_emit's fast path would fail too
   return op_emit_slow(L, m, d, depth, rule);
 #else
@@ -2677,6 +2682,25 @@ __device__ __forceinline__ bool op_emit_args_build(PLane& L, uint64_t m, uint64_
   return op_emit_build_slow(L, m, d, depth, rule, N, ys, args[0], N > 1 ? args[N > 1 ? 1 : 0] : 0,
                             N > 2 ? args[N > 2 ? 2 : 0] : 0, N > 3 ? args[N > 3 ? 3 : 0] : 0,
                             N > 4 ? args[N > 4 ? 4 : 0] : 0, N > 5 ? args[N > 5 ? 5 : 0] : 0);
+}
+
+// A fused emission whose details are the one-member object literal {k: v}
+// built right before it (jit.cc kv_sites): the object is not built unless the
+// fast path fails -- then exactly as the program would have (list_new +
+// op_obj_put, escape range yput) before the general path.  BUILD: the message's
+// argument list was not built either (op_emit_args_build).
+template <bool BUILD, uint32_t N>
+__device__ __forceinline__ bool op_emit_args_kvd(PLane& L, uint64_t m, uint64_t k, uint64_t v, uint32_t yput,
+                                                 uint32_t depth, uint32_t rule, const uint64_t (&args)[N], uint64_t ys) {
+  bool fast = GK_DET_KV && N + 2 <= FMT_MAXARGS && vtag(m) == V_FMT && !L.fail && L.en < EM_MAXIDX &&
+              L.ord < EM_MAXORD && vtag(k) == V_STR && plain_scalar(v);
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) fast = fast && plain_scalar(args[i]);
+  if (fast) return emit_fast_write(L, m, rule, args, true, k, v);
+  uint64_t d = list_new(L, LK_OBJ, 4);
+  if (!op_obj_put(L, d, k, v, yput)) return false;
+  if (BUILD) return op_emit_args_build(L, m, d, depth, rule, args, ys);
+  return op_emit_args(L, m, d, depth, rule, args);
 }
 
 // Printed length of a deferred message whose arguments are plain scalars:

@@ -885,6 +885,10 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   // emission's slow path (arguments that are not plain scalars) builds it
   // from the shadow copies (devrt.h op_emit_args_build).
   std::set<uint32_t> dce_sites, dce_pcs;
+  // fused emissions whose details register is the one-member object literal
+  // built by the two instructions right before the emission: emit pc -> its
+  // OBJ_PUT pc (devrt.h op_emit_args_kvd; the LIST_NEW goes into dce_pcs)
+  std::map<uint32_t, uint32_t> kv_sites;
   {
     const char* dv = getenv("GKGPU_JIT_EMITDCE");
     bool prog_ok = (!dv || atoi(dv) != 0) && !efacts.empty();
@@ -947,6 +951,23 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       dce_sites.insert(S);
       dce_pcs.insert(N);
       for (uint32_t a : adds) dce_pcs.insert(a);
+    }
+    const char* kvv = getenv("GKGPU_JIT_KVDCE");  // A/B switch, default on
+    const bool kv_on = !kvv || atoi(kvv) != 0;
+    for (uint32_t E = b0 + 2; prog_ok && kv_on && E + 1 < b1; ++E) {
+      const Ins& em = bank.code[E];
+      if (em.op != OP_EMIT || em.b == 0xffff || em.b == em.a) continue;
+      const EmitFlow::FFact* ff = EFL.find(E - b0, em.a);
+      if (!ff || ff->n == 0 || ff->mu || ff->n + 2 > 6) continue;
+      const Ins& put = bank.code[E - 1];
+      const Ins& nw0 = bank.code[E - 2];
+      const uint32_t Dr = em.b;
+      if (put.op != OP_OBJ_PUT || put.a != Dr || put.b == Dr || put.c == Dr || nw0.op != OP_LIST_NEW || nw0.a != Dr ||
+          nw0.y != LK_OBJ || labels.count(E - 1) || labels.count(E) || Dr >= 64 * nw)
+        continue;
+      if ((live[E + 1 - b0][Dr >> 6] >> (Dr & 63)) & 1) continue;  // the object is read after the emission
+      kv_sites[E] = E - 1;
+      dce_pcs.insert(E - 2);
     }
   }
   // computed-key lookups whose result a later lookup reuses: their shadow locals
@@ -1096,7 +1117,10 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (dce_pcs.count(pc)) o << "/* " << a << " += " << b << " */";
         else o << "if (!op_list_add(L, " << a << ", " << b << ", " << y << ")) " << RET;
         break;
-      case OP_OBJ_PUT: o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) " << RET; break;
+      case OP_OBJ_PUT:
+        if (kv_sites.count(pc + 1) && kv_sites.at(pc + 1) == pc) o << "/* " << a << "[" << b << "] = " << c << " (the emission's details) */";
+        else o << "if (!op_obj_put(L, " << a << ", " << b << ", " << c << ", " << y << ")) " << RET;
+        break;
       case OP_YIELD:
         if (EFL.undef_at(k, in.a) && in.a != in.b)  // into an output known to be undefined: a copy (no conflict check)
           o << a << " = " << b << ";" << (in.y ? " if (heap_val(" + a + ")) pin_escape(L, " + y + ");" : std::string());
@@ -1177,10 +1201,15 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           if (ff->mu) o << "if (vtag(" << a << ") == V_FMT) ";
           o << "{ const uint64_t ea_[" << ff->n << "] = {";
           for (uint16_t i = 0; i < ff->n; ++i) o << (i ? ", " : "") << "es" << ff->site << "_" << i;
-          if (dce_sites.count(ff->site)) {
-            uint64_t yp = 0;
-            for (uint16_t i = 0; i < ff->n; ++i)
-              yp |= (uint64_t)((ff->ys[i] & 0x1fu) | (((ff->ys[i] >> 8) & 0x1fu) << 5)) << (10 * i);
+          uint64_t yp = 0;
+          for (uint16_t i = 0; dce_sites.count(ff->site) && i < ff->n; ++i)
+            yp |= (uint64_t)((ff->ys[i] & 0x1fu) | (((ff->ys[i] >> 8) & 0x1fu) << 5)) << (10 * i);
+          if (kv_sites.count(pc)) {
+            const Ins& put = bank.code[kv_sites.at(pc)];
+            o << "}; if (!op_emit_args_kvd<" << (dce_sites.count(ff->site) ? "true" : "false") << ">(L, " << a << ", "
+              << R(put.b) << ", " << R(put.c) << ", " << put.y << "u, " << in.c << "u, " << y << ", ea_, " << yp << "ull)) "
+              << RET << " }";
+          } else if (dce_sites.count(ff->site)) {
             o << "}; if (!op_emit_args_build(L, " << a << ", " << D << ", " << in.c << "u, " << y << ", ea_, " << yp
               << "ull)) " << RET << " }";
           } else {

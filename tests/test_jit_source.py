@@ -127,3 +127,38 @@ def test_yield_into_an_undefined_output_is_a_copy():
     src = _dump("K8sRequiredProbes")
     assert "op_emit_args_build(L," in src
     assert "list_new(L, 2u" not in src
+
+
+def _dump_c3(kind, env_extra=()):
+    d = tempfile.mkdtemp(prefix="gkjit_test")
+    code = r'''
+import sys
+sys.path[:0] = [%r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client
+ts, cs = W.config3()
+d = gkgpu.Driver()
+cl = Client(d)
+for t in ts:
+    if t["spec"]["crd"]["spec"]["names"]["kind"] == %r:
+        cl.add_template(t)
+print(d.template_backend(%r))
+''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), kind, kind)
+    env = dict(os.environ, GKGPU_JIT_CACHE="0", GKGPU_JIT_DUMP=d, GKGPU_JIT_DUMP_ONLY="1", **dict(env_extra))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    files = glob.glob(os.path.join(d, "*.hip"))
+    assert len(files) == 1, files
+    return open(files[0]).read()
+
+
+def test_details_object_of_a_fused_emission_is_not_built():
+    """jit.cc kv_sites: k8sallowedlabelregex's {"label": key} details object
+    is built right before its emission and read nowhere else; the emission
+    takes the key and value registers (devrt.h op_emit_args_kvd) and builds
+    the object only on its slow path.  GKGPU_JIT_KVDCE=0 keeps it."""
+    on = _dump_c3("K8sAllowedLabelRegex")
+    off = _dump_c3("K8sAllowedLabelRegex", [("GKGPU_JIT_KVDCE", "0")])
+    assert "op_emit_args_kvd<true>(L," in on and "op_obj_put(L," not in on.split("_pred(")[1]
+    assert "op_emit_args_kvd" not in off.split("_pred(")[1] and "op_obj_put(L," in off
