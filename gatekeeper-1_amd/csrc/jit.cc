@@ -1501,7 +1501,10 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // programs without regular expressions -- K8sRequiredProbes 1.55 -> 1.45 ms
 // (config 2) and 4.29 -> 4.11 ms (config 4), K8sAllowedRepos 0.195 -> 0.179 /
 // 4.12 -> 4.04 ms -- while the regex templates (their DFAs staged in LDS) and
-// K8sContainerLimits lose at 4.
+// K8sContainerLimits lose at 4.  Re-checked at the end of round 5, after the
+// emission changes (profiles/r05/r05ay_wpe_recheck_ab.txt): every template at 3
+// or at 2 is slower on config 2 (1,000 -> 938 / 898 M evals/s), and the regex
+// templates at 2 or 4 on config 3 (1,030 -> 762 / 749 M).
 static bool small_program(const Program& p) { return p.nregs <= 48; }
 static int wpe_of(const Program& p) {
   const char* w = getenv("GKGPU_JIT_WPE");
