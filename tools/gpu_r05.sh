@@ -48,6 +48,7 @@ PY
            bash tools/gpu_bench_ab.sh "$TAG/early4" "--config 4 --steps 5 --warmup 1" "" "GKGPU_FN_EARLY=1" || exit 1 ;;
     ab2) IFS=';' read -ra S <<< "$AB2"; bash tools/gpu_bench_ab.sh "$TAG/ab2" "--steps 10 --warmup 2 --shard-leg off" "${S[@]}" || exit 1 ;;
     ab4) IFS=';' read -ra S <<< "$AB4"; bash tools/gpu_bench_ab.sh "$TAG/ab4" "--config 4 --steps 5 --warmup 1" "${S[@]}" || exit 1 ;;
+    ab6) IFS=';' read -ra S <<< "$AB6"; bash tools/gpu_bench_ab.sh "$TAG/ab6" "--config 6 --steps 5 --warmup 1 --shard-leg off" "${S[@]}" || exit 1 ;;
     ab3) IFS=';' read -ra S <<< "$AB3"; bash tools/gpu_bench_ab.sh "$TAG/ab3" "--config 3 --steps 5 --warmup 1 --shard-leg off" "${S[@]}" || exit 1 ;;
     quick) timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --shard-leg off --cpu-sample 0 > "$OUT/quick.json" 2> "$OUT/quick.err" || { echo QUICK_FAIL; tail "$OUT/quick.err"; exit 1; }
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c=d['config']; print('QUICK', round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],3), 'ms kernels', round(c['kernel_ms_per_step'],3))" "$OUT/quick.json" ;;
