@@ -1420,6 +1420,21 @@ __device__ __forceinline__ void mark_holes(uint64_t from, uint64_t k) {
     if (from + j < gk_args.out_cap) gk_args.out[from + j].review = VIOL_HOLE;
 }
 #endif
+#ifndef GK_HOST
+// The wave's chunk state is shared by its lanes, and divergent lane subsets
+// update it at different emission sites.  Plain loads and stores of it are a
+// data race to the compiler, which may then forward a lane's own earlier store
+// to a later load (a phi over the emission sites its own path took) instead of
+// reloading what another subset wrote: stale chunk state hands out slots twice
+// and marks live tuples as holes.  Every access is a wave-scope atomic, which
+// the compiler neither forwards nor caches, and is read back uniformly.
+__device__ __forceinline__ uint64_t chunk_ld(unsigned long long* p) {
+  return rfl64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+}
+__device__ __forceinline__ void chunk_st(unsigned long long* p, uint64_t v) {
+  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+#endif
 // a slot for each lane with `want` (every active lane calls it)
 __device__ __forceinline__ uint64_t slot_reserve(bool want) {
 #ifdef GK_HOST
@@ -1429,8 +1444,8 @@ __device__ __forceinline__ uint64_t slot_reserve(bool want) {
   if (!m) return 0;
   const uint64_t n = (uint64_t)__popcll(m);
   unsigned long long* st = gk_lds_chunk[threadIdx.x >> 6];
-  uint64_t base = st[0], left = st[1];
-  const uint64_t used = st[2];
+  uint64_t base = chunk_ld(&st[0]), left = chunk_ld(&st[1]);
+  const uint64_t used = chunk_ld(&st[2]);
   if (n > left) {
     mark_holes(base, left);
     const uint64_t want = used / GK_CHUNK_DIV;
@@ -1442,9 +1457,9 @@ __device__ __forceinline__ uint64_t slot_reserve(bool want) {
     left = take;
   }
   const uint64_t slot = base + gk_lanes_below(m);
-  st[0] = base + n;
-  st[1] = left - n;
-  st[2] = used + n;
+  chunk_st(&st[0], base + n);
+  chunk_st(&st[1], left - n);
+  chunk_st(&st[2], used + n);
   return slot;
 #endif
 }
@@ -1474,8 +1489,8 @@ __device__ __forceinline__ uint64_t bytes_reserve(bool want, uint32_t n) {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const uint64_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(&gk_lds_bscan[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
   unsigned long long* st = gk_lds_chunk[wv] + 3;
-  uint64_t base = st[0], left = st[1];
-  const uint64_t used = st[2];
+  uint64_t base = chunk_ld(&st[0]), left = chunk_ld(&st[1]);
+  const uint64_t used = chunk_ld(&st[2]);
   if (tot > left) {
     uint64_t take = used < BCHUNK_MIN ? BCHUNK_MIN : used > BCHUNK_MAX ? BCHUNK_MAX : used;
     if (take < tot) take = tot;
@@ -1486,11 +1501,12 @@ __device__ __forceinline__ uint64_t bytes_reserve(bool want, uint32_t n) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (gk_lanes_below(__ballot(true)) == 0) {
-    st[0] = base + tot;
-    st[1] = left - tot;
-    st[2] = used + tot;
-    gk_lds_bscan[wv] = 0;
+    chunk_st(&st[0], base + tot);
+    chunk_st(&st[1], left - tot);
+    chunk_st(&st[2], used + tot);
+    __hip_atomic_store(&gk_lds_bscan[wv], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   return base + o;
 #endif
 }
@@ -2818,7 +2834,7 @@ __device__ __forceinline__ void audit_body(Run run) {
     // the wave's unused slots become holes; its slot count for the per-launch
     // tuple statistics (counters[6])
     unsigned long long* st = gk_lds_chunk[threadIdx.x >> 6];
-    const uint64_t base = st[0], left = st[1], used = st[2];
+    const uint64_t base = chunk_ld(&st[0]), left = chunk_ld(&st[1]), used = chunk_ld(&st[2]);
     mark_holes(base, left);
     if (lane == 0 && used) atomicAdd(&gk_args.counters[6], (unsigned long long)used);
   }

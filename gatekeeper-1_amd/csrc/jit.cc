@@ -39,6 +39,12 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
 // each cleared both cases; the option keeps -O3 (profiles/r05/r05ag_sgpr_spill.txt).
 const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs"};
 constexpr int kNOpts = 6;
+// GKGPU_JIT_PREALLOC=0 (diagnostic): without the spill preallocation
+std::vector<const char*> base_opts() {
+  const char* e = getenv("GKGPU_JIT_PREALLOC");
+  const bool pre = !(e && e[0] == '0');
+  return std::vector<const char*>(kOpts, kOpts + (pre ? kNOpts : kNOpts - 2));
+}
 
 std::string hex16(uint64_t v) {
   char b[17];
@@ -1682,8 +1688,12 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
     std::istringstream is(xo);
     for (std::string t; is >> t;) xopt.push_back(t);
   }
+  // the key covers every option the code object is compiled with (the base
+  // options too: a changed base option must not reuse code built without it)
+  std::vector<const char*> opts = base_opts();
+  for (const auto& t : xopt) opts.push_back(t.c_str());
   std::string xkey;
-  for (const auto& t : xopt) xkey += " " + t;
+  for (const char* t : opts) xkey += std::string(" ") + t;
   std::string key = hex16(fnv1a(src + xkey, fnv1a(std::string(gk_rt_common_h) + gk_rt_devrt_h +
                                                   std::to_string(ver_major) + "." + std::to_string(ver_minor))));
   std::string dir = cache_dir();
@@ -1707,8 +1717,6 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
     log = "hiprtcCreateProgram failed";
     return false;
   }
-  std::vector<const char*> opts(kOpts, kOpts + kNOpts);
-  for (const auto& t : xopt) opts.push_back(t.c_str());
   hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);

@@ -3,8 +3,12 @@
 // regexp.Compile + unanchored MatchString over the UTF-8 text.
 //   * `^` / `\A` = beginning of text, `$` / `\z` = end of text (no (?m));
 //   * `.` = any character except '\n' (any with (?s)); classes \d \w \s ASCII;
-//   * (?i) ASCII case folding; lazy quantifiers behave like greedy for a
-//     match/no-match answer.
+//   * `\s` = [\t\n\f\r ] (Go's Perl class: no \v, regexp/syntax perl_groups.go);
+//   * (?i) is Go's simple case folding (regexp/syntax appendFoldedClass): the
+//     ASCII letters pair up, and a set holding k/K also matches U+212A (KELVIN
+//     SIGN) and one holding s/S U+017F (LATIN SMALL LETTER LONG S) -- the only
+//     non-ASCII members of ASCII letters' fold orbits -- as their UTF-8 byte
+//     sequences; lazy quantifiers behave like greedy for a match/no-match answer.
 // Constructs whose behaviour depends on UTF-8 decoding (`.`, negated classes,
 // \D \W \S) mark the DFA "utf8-sensitive": the kernel serves texts with bytes
 // >= 0x80 through the CPU fallback.  \b, Unicode classes, (?m), (?U) and
@@ -124,6 +128,29 @@ struct Parser {
     }
     return s;
   }
+  // a (folded) byte set as a node: under (?i) a set with k or s also matches
+  // the UTF-8 of U+212A (E2 84 AA) / U+017F (C5 BF), Go's fold orbits of those
+  // letters (unicode.SimpleFold); negated sets stay single bytes (they are
+  // utf8-sensitive, so non-ASCII subjects take the CPU fallback)
+  AstP lit(const CSet& s) {
+    auto a = mk(Ast::LIT);
+    a->set = s;
+    if (!icase || !(s['k'] || s['s'])) return a;
+    auto alt = mk(Ast::ALT);
+    alt->kids.push_back(a);
+    auto seq = [&](std::initializer_list<int> bytes) {
+      auto c = mk(Ast::CAT);
+      for (int b : bytes) {
+        auto l = mk(Ast::LIT);
+        l->set[b] = true;
+        c->kids.push_back(l);
+      }
+      alt->kids.push_back(c);
+    };
+    if (s['k']) seq({0xE2, 0x84, 0xAA});
+    if (s['s']) seq({0xC5, 0xBF});
+    return alt;
+  }
   static CSet cls_digit() { CSet s; for (int c = '0'; c <= '9'; ++c) s[c] = true; return s; }
   static CSet cls_word() {
     CSet s = cls_digit();
@@ -131,7 +158,7 @@ struct Parser {
     s['_'] = true;
     return s;
   }
-  static CSet cls_space() { CSet s; for (char c : std::string("\t\n\f\r ")) s[(unsigned char)c] = true; s['\v'] = true; return s; }
+  static CSet cls_space() { CSet s; for (char c : std::string("\t\n\f\r ")) s[(unsigned char)c] = true; return s; }
   static CSet ascii_neg(const CSet& s) {
     CSet r;
     for (int c = 0; c < 128; ++c) r[c] = !s[c];
@@ -261,11 +288,8 @@ struct Parser {
       if (i < p.size() && p[i] == 'z') { ++i; return mk(Ast::EOL); }
       CSet s;
       int ch = -1;
-      auto a = mk(Ast::LIT);
-      if (escape(&s, &ch)) a->set = s;
-      else a->set[ch] = true;
-      a->set = fold(a->set);
-      return a;
+      if (!escape(&s, &ch)) s[ch] = true;
+      return lit(fold(s));
     }
     // literal (UTF-8 multi-byte sequences are literal byte strings)
     unsigned char u = (unsigned char)c;
@@ -281,10 +305,9 @@ struct Parser {
       return a;
     }
     ++i;
-    auto a = mk(Ast::LIT);
-    a->set[u] = true;
-    a->set = fold(a->set);
-    return a;
+    CSet one;
+    one[u] = true;
+    return lit(fold(one));
   }
   AstP cls() {
     ++i;  // '['
@@ -330,11 +353,10 @@ struct Parser {
       }
     }
     s = fold(s);
+    if (!neg) return lit(s);
     auto a = mk(Ast::LIT);
-    if (neg) {
-      a->set = ascii_neg(s);
-      utf8_sensitive = true;  // also matches any non-ASCII character
-    } else a->set = s;
+    a->set = ascii_neg(s);
+    utf8_sensitive = true;  // also matches any non-ASCII character
     return a;
   }
 };

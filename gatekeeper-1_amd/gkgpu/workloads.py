@@ -628,9 +628,17 @@ _C3_RULES = {
     "version": "^v[0-9]+\\.[0-9]+\\.[0-9]+$",
     "region": "^[a-z]{2}-[a-z]+-[0-9]$",
     "component": "^[a-z]+(-[a-z]+)*$",
+    # Go RE2 specifics (round 6): `\s` is [\t\n\f\r ] (no \v), and (?i) folds
+    # k with U+212A (KELVIN SIGN) and s with U+017F (LONG S); neither pattern is
+    # utf8-sensitive (no `.`, no negated class), so the device decides every
+    # value, non-ASCII ones included
+    "note": "^[a-z]+(\\s[a-z0-9]+)*$",
+    "kube": "(?i)^(kube|sys)-[a-z]+$",
 }
-# values near each pattern's boundaries (~half match); ASCII only, so no review
-# needs the UTF-8 fallback (non-ASCII subjects are covered by the parity tests)
+# config 4 keeps the first eight (its workload is unchanged since round 4)
+_C3_BASE_KEYS = ("env", "owner", "app", "tier", "team", "version", "region", "component")
+# values near each pattern's boundaries (~half match); no value needs the
+# UTF-8 fallback: the non-ASCII ones are only checked by non-sensitive patterns
 _C3_VALUES = {
     "env": ["dev-1", "prod-9999", "stage-42", "prod-10000", "stage-", "dev-12\n", "qa-1", "", "DEV-1", "prod-0001"],
     "owner": ["alice.agilebank.demo", "Bob.agilebank.demo", "bob_agilebank.demo", "x.agilebank.demo\n",
@@ -641,6 +649,9 @@ _C3_VALUES = {
     "version": ["v1.2.3", "v10.0.1", "1.2.3", "v1.2", "v1.2.3-rc1", "v01.2.3", "v1..3"],
     "region": ["us-east-1", "eu-west-2", "us-east-12", "US-east-1", "ap-south", "eu-central-3"],
     "component": ["api", "api-server", "-api", "api-", "API", "a-b-c-d", "api--server"],
+    "note": ["ok go", "ok\tgo", "ok\vgo", "ok\ngo", "ok  go", "ok go\v", "ok", "ok\r\n1", "x\x0cy", "ok\u00a0go"],
+    "kube": ["kube-ops", "KUBE-ops", "\u212aube-ops", "\u017fys-x", "kube-\u212a\u017f", "kube-", "ube-x",
+             "\u0130kube-x", "sys-\u00e9", "SYS-OK"],
 }
 
 
@@ -789,7 +800,7 @@ def config4(seed=1234, n_namespaces=1000):
             params = {"probes": rng.sample(["readinessProbe", "livenessProbe"], rng.randint(1, 2)),
                       "probeTypes": ["tcpSocket", "httpGet", "exec"]}
         else:
-            keys = rng.sample(list(_C3_RULES), 2)
+            keys = rng.sample(list(_C3_BASE_KEYS), 2)
             params = {"rules": [{"key": k, "allowedRegex": _C3_RULES[k]} for k in keys]}
         ea = "dryrun" if rng.random() < 0.2 else None
         cs.append(constraint(kind, "c4-%02d-%s" % (i, kind.lower()), match=match or None, parameters=params,
@@ -803,7 +814,7 @@ def gen_config4_json(n, seed=1234, start=0, n_namespaces=1000):
     rng = random.Random(seed)
     pools = [[dumps(_container(rng, "c%d" % slot)) for _ in range(1024)] for slot in range(4)]
     init_pool = [dumps(_container(rng, "init")) for _ in range(1024)]
-    keys = list(_C3_VALUES)
+    keys = list(_C3_BASE_KEYS)
 
     def labels():
         d = {"app": "app-%d" % rng.randint(0, 99)}

@@ -77,6 +77,22 @@ def sweep_digest(driver, batch, threads: int = 1, joins: bool = True):
     return out[0], out[1], out[3], out[4]
 
 
+def device_rows_digest(tuples, raw, threads: int = 8):
+    """row_digest of a device evaluation's raw output (DeviceOutput.tuples()
+    and .bytes(), host numpy arrays or CPU tensors): (digest, rows hashed),
+    computed natively (oracle/cpuvm.cc gkcpu_rows_digest)"""
+    import numpy as np
+    lib = load()
+    lib.gkcpu_rows_digest.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,
+                                      C.POINTER(C.c_uint64)]
+    lib.gkcpu_rows_digest.restype = C.c_uint64
+    t = np.ascontiguousarray(np.asarray(tuples, dtype=np.int32))
+    b = np.ascontiguousarray(np.asarray(raw, dtype=np.uint8))
+    n = C.c_uint64()
+    d = lib.gkcpu_rows_digest(t.ctypes.data, t.size // 8, b.ctypes.data, b.size, threads, C.byref(n))
+    return int(d), int(n.value)
+
+
 def row_hash(review: int, constraint: int, msg: bytes, details: bytes) -> int:
     """FNV-1a 64 over (u32 review LE, u32 constraint LE, msg, 0xff, details)"""
     h = 1469598103934665603

@@ -266,19 +266,33 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
     }
     const char* dp = "{}";
     uint32_t dl = 2;
-    if (v.pad & VF_DET_VAL) {
-      // details copied out at emission: the size pass prints them (JSON)
+    if (v.pad & (VF_DET_VAL | VF_DET_KV)) {
+      // details as frec words: VF_DET_VAL the JSON of one value, VF_DET_KV a
+      // one-member object {k: v} (k at word di, v at di + 1) -- what the size
+      // and format passes print (kernels.hip put_det_words)
       const uint32_t di = (v.pad & VF_DEFER) ? (v.msg_len >> 24) : 0u;
-      const uint64_t dv = gk_args.frec[(uint64_t)di * gk_args.out_cap + i];
+      const bool kv = (v.pad & VF_DET_KV) != 0;
+      const uint64_t dk = kv ? gk_args.frec[(uint64_t)di * gk_args.out_cap + i] : 0ull;
+      const uint64_t dv = gk_args.frec[(uint64_t)(di + (kv ? 1u : 0u)) * gk_args.out_cap + i];
+      auto print = [&](auto& o) {
+        if (kv) {
+          put(o, '{');
+          if (!put_json_str(o, sview(L, dk))) return false;
+          put(o, ':');
+        }
+        if (!put_json(L, o, dv)) return false;
+        if (kv) put(o, '}');
+        return true;
+      };
       Cnt cn{0, false};
-      if (!put_json(L, cn, dv)) {
+      if (!print(cn)) {
         ++k.flagged;
         return;
       }
       if (g_digest) {
         dbuf.resize(cn.n + 1);
         Out o{dbuf.data(), 0, (uint32_t)dbuf.size(), false};
-        put_json(L, o, dv);
+        print(o);
         dp = dbuf.data();
         dl = o.n;
       }
@@ -436,6 +450,49 @@ double gkcpu_sweep_digest(const void* args, uint32_t lo, uint32_t hi, int thread
   memcpy(out5, o4, sizeof o4);
   out5[4] = gk::cpu::g_last_digest;
   return s;
+}
+
+// The same row digest over a device evaluation's raw output (the formatted
+// gk_viol records and their message + details bytes, as
+// gk_results_copy_device_output returns them), so a GPU test can compare every
+// row of a 1M-review sweep with gkcpu_sweep_digest.  Records of flagged
+// reviews (VF_NOPRINT) are skipped as every consumer drops them; returns the
+// digest, *nrows the rows hashed.
+uint64_t gkcpu_rows_digest(const void* viols, uint64_t n, const uint8_t* bytes, uint64_t nbytes, int threads,
+                           uint64_t* nrows) {
+  const gk::Viol* V = (const gk::Viol*)viols;
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> dig(threads, 0), cnt(threads, 0);
+  std::atomic<uint64_t> next{0};
+  auto work = [&](int t) {
+    for (;;) {
+      const uint64_t a = next.fetch_add(65536);
+      if (a >= n) break;
+      const uint64_t b = a + 65536 < n ? a + 65536 : n;
+      for (uint64_t i = a; i < b; ++i) {
+        const gk::Viol& v = V[i];
+        if (v.pad & gk::VF_NOPRINT) continue;
+        if (v.msg_off + v.msg_len + v.det_len > nbytes) { dig[t] ^= 0x5bd1e995ull * (i + 1); continue; }
+        uint64_t h = 1469598103934665603ull;
+        const uint32_t rc4[2] = {v.review, v.constraint};
+        h = gk::cpu::fnv_bytes(h, rc4, 8);
+        h = gk::cpu::fnv_bytes(h, bytes + v.msg_off, v.msg_len);
+        const unsigned char sep = 0xff;
+        h = gk::cpu::fnv_bytes(h, &sep, 1);
+        h = gk::cpu::fnv_bytes(h, bytes + v.msg_off + v.msg_len, v.det_len);
+        dig[t] += h;
+        ++cnt[t];
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  uint64_t d = 0, c = 0;
+  for (int t = 0; t < threads; ++t) { d += dig[t]; c += cnt[t]; }
+  if (nrows) *nrows = c;
+  return d;
 }
 
 }  // extern "C"

@@ -13,6 +13,15 @@ sweep) -- staged and evaluated on the GPU exactly as bench.py does, then:
   * Every flagged review (error / CPU fallback) is counted and must be rare;
     flagged reviews in the sample must be flagged because the oracle errors
     (error) or are excluded (fallback), as compare() checks.
+  * FULL POPULATION against the CPU checker: an order-free digest of EVERY
+    row of the device output -- (review, constraint, message bytes, details
+    bytes), oracle/cpuvm.cc gkcpu_rows_digest -- equals the digest of the rows
+    the host build of the same programs produces over the same staged batch
+    (gkcpu_sweep_digest).  The host compiler is independent of the device
+    compiler, so a device miscompile or a lost / duplicated / corrupted row
+    anywhere in the 1M reviews shows here, not only in the sample.  (The
+    checker's rows themselves are pinned to the oracle's by
+    tests/test_checker_digest.py.)
   * SELF-CONSISTENCY (not parity): the audit sweep's exact totals
     (Batch.eval_audit, device sampling) equal the per-constraint counts of the
     decoded device output.
@@ -87,6 +96,15 @@ def _run(cfg, n, gen, max_fallback_frac, inventory=(), oracle_factory=None):
     assert not rep.mismatches, rep.mismatches[:3]
     assert rep.canonical_only == 0, rep  # byte-exact rows (no object-printing template here)
     assert rep.compared >= N_SAMPLE - 64 - 2 * flagged
+    # full population: every row against the CPU checker's
+    from oracle import cpu_baseline
+    gd, gn = cpu_baseline.device_rows_digest(tup.cpu().numpy(), raw.cpu().numpy(), threads=16)
+    ev, cn, cfl, cd = cpu_baseline.sweep_digest(drv, batch, threads=16)
+    print("config %d full population: device rows %d, checker rows %d, checker flagged pairs %d" % (cfg, gn, cn, cfl),
+          flush=True)
+    assert flagged == 0 and cfl == 0, (flagged, cfl)
+    assert gn == cn and gn == len(tup), (gn, cn, len(tup))
+    assert gd == cd, "config %d: the device rows differ from the CPU checker's" % cfg
     # self-consistency: the audit sweep's totals vs the decoded output's counts
     sweep = batch.eval_audit(limit=20)
     if not len(status) or not (status & 3).any():
