@@ -948,6 +948,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         if (pc < S && jump_op(in.op)) ok = false;
         if (pc > N && pc < S && in.op == OP_LIST_ADD && in.a == Lr) adds.push_back(pc);
         if (pc > N && pc < S && in.op == OP_LIST_NEW && in.a == Lr) ok = false;
+        // nothing between the LIST_NEW and the sprintf may read the list but
+        // its own LIST_ADDs (a copy of it, or the list added into another
+        // container, would hold what the unbuilt list's register held)
+        if (pc > N && pc < S && ok) {
+          ins_regs(in, rd, wr);
+          const bool own_add = in.op == OP_LIST_ADD && in.a == Lr && in.b != Lr;
+          for (uint32_t r : rd) if (r == Lr && !own_add) ok = false;
+        }
       }
       if (ok && adds.size() != ff.n) ok = false;
       // escape ranges packed 10 bits each (devrt.h esc_unpack), six arguments at most

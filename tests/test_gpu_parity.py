@@ -713,6 +713,48 @@ def test_string_builtins_trim_split_case_concat_indexof():
     assert rep.violations > 500
 
 
+def test_emission_argument_list_read_elsewhere():
+    """ADVICE r05 (jit.cc dce_sites): a sprintf argument list that is also
+    added into another array the body reads must be built (the emission-only
+    list DCE must not fire); rows equal the oracle's on both back ends"""
+    from test_jit_source import ALIASED_LIST, PLAIN_LIST
+    ts = [W._tmpl("K8sAliasedList", ALIASED_LIST), W._tmpl("K8sPlainList", PLAIN_LIST)]
+    cs = [W.constraint("K8sAliasedList", "aliased"), W.constraint("K8sPlainList", "plain")]
+    objs = [{"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cm-%d" % i, "namespace": "ns"}}
+            for i in range(200)]
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, [W.namespace_obj("ns")] * len(objs))
+    _assert_backend(drv, ["K8sAliasedList", "K8sPlainList"])
+    _assert_clean(rep)
+    assert rep.violations == 400, rep
+
+
+def test_go_regex_whitespace_and_case_folding_on_device():
+    """re_match as Go decides it (topdown/regex.go:21-34): `\\s` excludes \\v,
+    and (?i) folds k / s with U+212A / U+017F -- decided by the device's DFA
+    tables (no fallback: neither pattern is utf8-sensitive)"""
+    ts = [W.ALLOWED_LABEL_REGEX]
+    rules = [{"key": "note", "allowedRegex": "^[a-z]+(\\s[a-z0-9]+)*$"},
+             {"key": "kube", "allowedRegex": "(?i)^(kube|sys)-[a-z]+$"}]
+    cs = [W.constraint("K8sAllowedLabelRegex", "go-rules", match={"kinds": [{"apiGroups": [""], "kinds": ["Service"]}]},
+                       parameters={"rules": rules})]
+    notes = ["ok go", "ok\tgo", "ok\vgo", "ok\ngo", "ok go\v", "x\x0cy", "ok\u00a0go"]
+    kubes = ["kube-ops", "KUBE-ops", "\u212aube-ops", "\u017fys-x", "kube-\u212a\u017f", "ube-x", "\u0130kube-x",
+             "sys-\u00e9"]
+    objs = []
+    for i in range(len(notes) * len(kubes)):
+        lab = {"note": notes[i % len(notes)], "kube": kubes[i // len(notes)]}
+        objs.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "s%d" % i, "namespace": "ns",
+                                                                        "labels": lab}})
+    drv = Driver()
+    rep, res = run_objects(drv, ts, cs, objs, [W.namespace_obj("ns")] * len(objs))
+    _assert_clean(rep)
+    assert rep.fallback == 0, rep
+    bad = {r.msg.split(">")[0] for r in res.results}
+    assert "label <note: ok\vgo" in bad and "label <note: ok go" not in bad
+    assert "label <kube: \u212aube-ops" not in bad and "label <kube: \u0130kube-x" in bad
+
+
 def test_template_kernel_matches_vm_at_scale():
     """Size-independent property at 100k Pods (config 2 policies): the template
     kernels + format pass over size-ordered reviews produce exactly the

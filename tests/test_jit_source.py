@@ -162,3 +162,54 @@ def test_details_object_of_a_fused_emission_is_not_built():
     off = _dump_c3("K8sAllowedLabelRegex", [("GKGPU_JIT_KVDCE", "0")])
     assert "op_emit_args_kvd<true>(L," in on and "op_obj_put(L," not in on.split("_pred(")[1]
     assert "op_emit_args_kvd" not in off.split("_pred(")[1] and "op_obj_put(L," in off
+
+
+ALIASED_LIST = r'''package k8saliasedlist
+
+violation[{"msg": msg}] {
+	name := input.review.object.metadata.name
+	args := [name, "x"]
+	outer := [args]
+	msg := sprintf("%v is %v", args)
+	outer[0][0] == name
+}
+'''
+PLAIN_LIST = r'''package k8splainlist
+
+violation[{"msg": msg}] {
+	name := input.review.object.metadata.name
+	msg := sprintf("%v is %v", [name, "x"])
+}
+'''
+
+
+def _dump_rego(kind, rego):
+    d = tempfile.mkdtemp(prefix="gkjit_test")
+    code = r'''
+import sys
+sys.path[:0] = [%r, %r]
+import gkgpu
+from gkgpu import workloads as W
+from gkgpu.client import Client
+d = gkgpu.Driver()
+cl = Client(d)
+cl.add_template(W._tmpl(%r, %r))
+print(d.template_backend(%r))
+''' % (ROOT, os.path.join(ROOT, "gatekeeper-1_amd"), kind, rego, kind)
+    env = dict(os.environ, GKGPU_JIT_CACHE="0", GKGPU_JIT_DUMP=d, GKGPU_JIT_DUMP_ONLY="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    files = glob.glob(os.path.join(d, "*.hip"))
+    assert len(files) == 1, files
+    return open(files[0]).read()
+
+
+def test_argument_list_read_elsewhere_is_still_built():
+    """ADVICE r05 (jit.cc dce_sites): an emission-only sprintf argument list is
+    not built (its fused emission has the arguments) -- but only when nothing
+    between its LIST_NEW and the sprintf reads it except its own LIST_ADDs.
+    Here the list is also added into `outer`, which the body reads, so it must
+    be built; the plain form still drops it."""
+    marker = "the argument list of a fused emission"
+    assert marker in _dump_rego("K8sPlainList", PLAIN_LIST)
+    assert marker not in _dump_rego("K8sAliasedList", ALIASED_LIST)
