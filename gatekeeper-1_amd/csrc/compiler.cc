@@ -2025,12 +2025,11 @@ class Comp {
           // loop's element, a path below it) meets new arguments every
           // iteration; an impure function's lane memo would only cost
           // registers there.  Pure functions keep theirs: the cross-lane memo
-          // serves other lanes.  GKGPU_MEMO_LOOPVAR=1 memoizes them anyway (A/B).
+          // serves other lanes.
           bool varying = false;
           if (!loop_var_lo_.empty())
             for (int r : regs) varying |= r >= loop_var_lo_.back() && r < kVReg;
-          static const bool memo_loopvar = getenv("GKGPU_MEMO_LOOPVAR") && atoi(getenv("GKGPU_MEMO_LOOPVAR")) != 0;
-          bool skip = varying && !memo_loopvar && !pure_func(rules);
+          bool skip = varying && !pure_func(rules);
           // the set rewrites' helpers (rego.cc optimize_sets) take a document
           // collection as an argument: a memo key nobody else meets
           skip = skip || name.rfind("__gk_", 0) == 0;

@@ -70,15 +70,6 @@ namespace gk {
 #else
 #define GK_HOT
 #endif
-#ifndef GK_VGET_UNROLL
-#define GK_VGET_UNROLL 0
-#endif
-#ifndef GK_VGET_BATCH
-#define GK_VGET_BATCH 0
-#endif
-#ifndef GK_VGET_REC
-#define GK_VGET_REC 1
-#endif
 #ifndef GK_HCAP
 #define GK_HCAP 128
 #endif
@@ -802,52 +793,11 @@ __device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
       uint32_t kt = vtag(key);
       if (n.type == NT_OBJ && kt == V_STR) {
         uint32_t id = (uint32_t)vpay(key);
-#if GK_VGET_BATCH
-        // the keys of the first 8 members in one round trip (dword loads at a
-        // 16-B stride, predicated on the run length only, so they issue
-        // together), then the matching record: two round trips wherever the
-        // member sits instead of one per member scanned
-        {
-          const Node* ch = gk_args.nodes + n.first;
-          const uint32_t m = n.n < 8u ? (uint32_t)n.n : 8u;
-          uint32_t k[8];
-#pragma unroll
-          for (uint32_t j = 0; j < 8; ++j) k[j] = j < m ? ch[j].key : NO_ID;
-          uint32_t hit = 8;
-#pragma unroll
-          for (uint32_t j = 8; j-- > 0;) hit = (j < m && k[j] == id) ? j : hit;
-          if (hit < 8) return nodeval(n.first + hit);
-          for (uint32_t i = 8; i < n.n; ++i) {
-            const Node mm = ch[i];
-            if (mm.key == id) return nodeval_of(mm, n.first + i);
-          }
-        }
-#elif GK_VGET_UNROLL
-        // four member keys per round trip: the loads are independent, so the
-        // lane waits once per four members instead of once per member
-        const Node* ch = gk_args.nodes + n.first;
-        uint32_t i = 0;
-        for (; i + 4 <= n.n; i += 4) {
-          const Node m0 = ch[i], m1 = ch[i + 1], m2 = ch[i + 2], m3 = ch[i + 3];
-          if (m0.key == id) return nodeval_of(m0, n.first + i);
-          if (m1.key == id) return nodeval_of(m1, n.first + i + 1);
-          if (m2.key == id) return nodeval_of(m2, n.first + i + 2);
-          if (m3.key == id) return nodeval_of(m3, n.first + i + 3);
-        }
-        for (; i < n.n; ++i) {
-          const Node m = ch[i];
-          if (m.key == id) return nodeval_of(m, n.first + i);
-        }
-#elif GK_VGET_REC
         // whole member records: the match's value needs no second load
         for (uint32_t i = 0; i < n.n; ++i) {
           const Node m = gk_args.nodes[n.first + i];
           if (m.key == id) return nodeval_of(m, n.first + i);
         }
-#else  // A/B (GKGPU_JIT_PRE=GK_VGET_REC=0): member keys, then the match's record
-        for (uint32_t i = 0; i < n.n; ++i)
-          if (gk_args.nodes[n.first + i].key == id) return nodeval(n.first + i);
-#endif
         return mkv(V_UNDEF, 0);
       }
       if (n.type == NT_ARR && kt == V_INT) {
@@ -2306,15 +2256,6 @@ __device__ __forceinline__ uint64_t gm_mix(uint64_t x) {
 // check is a bijection of h ^ v, so any torn or foreign (key, value) pair
 // that differs from the reader's reads as a miss.  A real key is never 0
 // (every tagged value but undefined is non-zero), so empty entries never match.
-#ifndef GK_GM_HASH_OLD
-#define GK_GM_HASH_OLD 0
-#endif
-#if GK_GM_HASH_OLD  // diagnostics (GKGPU_JIT_PRE="GK_GM_HASH_OLD=1"): the round-2 mixers
-__device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
-  return gm_mix(k0 ^ gm_mix(k1 + (uint64_t)(site + 1) * 0x9e3779b97f4a7c15ull + gk_args.gm_salt));
-}
-__device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) { return gm_mix(h ^ gm_mix(v + 0x5851f42d4c957f2dull)) | 1; }
-#else
 __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t k1) {
   uint64_t h = (k0 ^ ((uint64_t)(site + 1) << 44) ^ gk_args.gm_salt) * 0x9e3779b97f4a7c15ull;
   h ^= h >> 29;
@@ -2324,7 +2265,6 @@ __device__ __forceinline__ uint64_t gm_hash(uint32_t site, uint64_t k0, uint64_t
 __device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) {
   return (h ^ v) * 0x94d049bb133111ebull + 0x632be59bd9b4e019ull;
 }
-#endif
 // keys are scalars and permanent nodes (constraint parameters, data.inventory
 // objects: every lane of the launch meets the same ones, e.g. the Services a
 // unique-selector join scans); a review document's node is met by one lane

@@ -864,12 +864,9 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   // predicate.  Slots of pure functions also have the cross-lane memo (gm_get),
   // which answers them from L2 without the registers: measured on config 2 (1M
   // Pods, tools/gpu_r02h.sh) K8sContainerLimits 6.34 -> 5.02 ms without the
-  // register entries, 5.45 ms with one entry per slot.  GKGPU_JIT_LMEMO=1 keeps
-  // them (A/B); GKGPU_JIT_MEMO2=0 keeps one register entry per other slot.
-  if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) if (atoi(m2) == 0) memo2.clear();
+  // register entries, 5.45 ms with one entry per slot.
   std::set<uint32_t> lslots = memo;  // slots with register entries
-  const char* lm = getenv("GKGPU_JIT_LMEMO");
-  if (!lm || atoi(lm) == 0) for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
+  for (uint32_t m : gslots) { lslots.erase(m); memo2.erase(m); }
   FmtFlow F = fmt_flow(p, bank);
   FmtFlow DF = doc_flow(p, bank);
   LookFlow LK = look_flow(p, bank, F, DF);
@@ -1017,17 +1014,14 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
   // no initializers: the compiler writes every register before reading it (the
   // VM kernel relies on the same), and zero-initialising would make all of them
   // live from entry — register pressure, hence occupancy
-  const char* ji = getenv("GKGPU_JIT_INIT");  // diagnostics: 1 = registers start as undefined (0)
-  bool init = ji && atoi(ji) != 0;
   o << "  uint64_t ";
-  for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r) << (init ? " = 0" : "");
+  for (uint32_t r = 0; r < p.nregs; ++r) o << (r ? ", " : "") << R(r);
   if (!p.nregs) o << "unused_";
   o << ";\n";
   // The shadow and memo locals below start at 0: they are read only behind
   // their valid flags, but a read of an uninitialised local is undefined
   // behaviour, which the optimiser may exploit across the whole predicate
-  const char* z0 = getenv("GKGPU_JIT_ZERO");  // A/B: 0 = shadows uninitialised
-  const std::string Z = (z0 && atoi(z0) == 0) ? "" : " = 0";
+  const std::string Z = " = 0";
   for (uint32_t pc : shadowed) o << "  uint64_t dk" << pc << Z << ";\n";
   for (const auto& es : esites)
     for (size_t i = 0; i < es.second.size(); ++i) o << "  uint64_t es" << es.first << "_" << i << Z << ";\n";
@@ -1374,7 +1368,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
       for (uint32_t q = pc + 1; q < put && ok; ++q) {
         ins_regs(bank.code[q], rd, wr);
         wrs.insert(wr.begin(), wr.end());
-        // register memo entries (GKGPU_JIT_LMEMO) are the predicate's locals
+        // register memo entries are the predicate's locals
         const Ins& qi = bank.code[q];
         if ((qi.op == OP_MEMO_GET || qi.op == OP_MEMO_PUT) && lslots.count(qi.y)) ok = false;
       }
@@ -1610,8 +1604,6 @@ static StagePlan stage_plan(const Program& p, const Gen& g, int depth) {
 static std::string inline_hot_tag(const Program& p) {
   const char* v = getenv("GKGPU_INLINE_HOT");
   std::string t = (!v || atoi(v) != 0) ? "h1" : "h0";
-  if (const char* m2 = getenv("GKGPU_JIT_MEMO2")) t += std::string("m") + m2;
-  if (const char* lm = getenv("GKGPU_JIT_LMEMO")) t += std::string("l") + lm;
   t += "d" + std::to_string(lds_heap_words(p));
   if (!lds_scalars()) t += "s0";
   if (!lds_stage_on()) t += "p0";
