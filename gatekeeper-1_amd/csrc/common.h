@@ -75,6 +75,10 @@ enum Tag : uint32_t {
   V_GSTR = 12,                                     // GSTR: string in the evaluation's memo-string arena (off:40 << 20 | len:20)
   V_GLIST = 13,                                    // GLIST: a list copied out at emission (devrt.h gval_copy): kind in bits
                                                    // 56..59, the word offset of [len, 0, words...] in ebytes
+  // columnar staged batches (colstore.cc): a document object / array read from
+  // the batch's path columns instead of the node store
+  V_ROW = 14,                                      // ROW: object view:12 << 40 | row:40
+  V_ROWS = 15,                                     // ROWS: array -- element table:12 << 48 | first row:32 << 16 | length:16
 };
 enum ListKind : uint32_t { LK_SET = 1, LK_ARR = 2, LK_OBJ = 3 };
 
@@ -319,7 +323,46 @@ struct DevArgs {
   const uint32_t* fmtr;
   const char* fmtb;           // the literals' bytes, padded to a dword
   uint32_t nfmt, nfmtb;       // words of fmtr, bytes of fmtb
+  // columnar staged batch (colstore.cc; cv_on = 0: the review documents are
+  // node trees).  The review at evaluation position r is V_ROW(view 0, row r).
+  const uint32_t* cv_words;   // every path column's value words (CW_*), one per row of its table
+  const struct CvSlot* cv_slots;
+  const struct CvHash* cv_hash;  // (object view, member key) -> slot, open addressing
+  const uint32_t* cv_views;   // per object view: CV_COMPLETE
+  const uint32_t* cv_tabs;    // per element table: the slot of its elements
+  uint32_t cv_hmask;          // hash entries - 1
+  uint32_t cv_on;
 };
+
+// ----------------------------------------------------------------- path columns
+// A column's value word per row: tag in bits 29..31, payload below.
+enum ColWord : uint32_t {
+  CW_ABSENT = 0,  // undefined at this row
+  CW_STR = 1,     // interned string id
+  CW_NUM = 2,     // number-table id
+  CW_LIT = 3,     // 0 null, 1 false, 2 true
+  CW_OBJ = 4,     // an object: V_ROW(the slot's view, this row)
+  CW_ARR = 5,     // an array: its elements are rows [payload, + length column) of the slot's table
+  CW_NODE = 6,    // kept as document nodes (a path used whole): node index
+};
+constexpr uint32_t CW_SHIFT = 29, CW_PAY = (1u << 29) - 1;
+struct CvSlot {
+  uint32_t col;     // word offset of the value column (row r at col + r)
+  uint32_t lencol;  // word offset of the array-length column (CW_ARR rows), NO_ID if none
+  uint16_t view;    // CW_OBJ rows: the object view of this path
+  uint16_t tab;     // CW_ARR rows: the element table of this path
+  uint32_t pad;
+};
+static_assert(sizeof(CvSlot) == 16, "CvSlot layout");
+struct CvHash {
+  uint32_t view, key, slot, pad;  // view == NO_ID: empty entry
+};
+static_assert(sizeof(CvHash) == 16, "CvHash layout");
+constexpr uint32_t CV_COMPLETE = 1;  // every member key the batch has at this path has a slot
+constexpr uint32_t cv_hash_of(uint32_t view, uint32_t key) {  // (constexpr: host and device)
+  uint32_t h = view * 0x9E3779B1u ^ key * 0x85EBCA77u;
+  return h ^ (h >> 15);
+}
 // join sites per template program (compiler.cc join_site)
 constexpr uint32_t JMAX_SITES = 4;
 // keys one leaf may have (a key over a generator, `other.spec.rules[_].host`);

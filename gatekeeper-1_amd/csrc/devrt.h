@@ -539,8 +539,52 @@ __device__ __forceinline__ int tclass(uint64_t v) {
     case V_STR: case V_HSTR: case V_SLICE: case V_GSTR: return 4;
     case V_NODE: GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].type == NT_ARR ? 7 : 8;
     case V_LIST: case V_GLIST: { uint32_t k = list_kind(v); return k == LK_ARR ? 7 : k == LK_OBJ ? 8 : 9; }
+    case V_ROW: return 8;
+    case V_ROWS: return 7;
   }
   return 0;
+}
+
+// ------------------------------------------------------------------ path columns
+// A columnar staged batch (colstore.cc) holds the paths its programs read as
+// value columns: an object is V_ROW(view, row) -- its members are the view's
+// slots, found by (view, key) in a small hash -- and an array V_ROWS(table,
+// first row, length) of element-table rows.  Objects read whole (iterated,
+// counted, compared, printed) stay document nodes (CW_NODE).
+__device__ __forceinline__ uint32_t cv_find(uint32_t view, uint32_t key) {
+  const uint32_t mask = gk_args.cv_hmask;
+  uint32_t i = cv_hash_of(view, key) & mask;
+  for (uint32_t p = 0; p <= mask; ++p, i = (i + 1) & mask) {
+    const CvHash e = gk_args.cv_hash[i];
+    if (e.view == view && e.key == key) return e.slot;
+    if (e.view == NO_ID) return NO_ID;
+  }
+  return NO_ID;
+}
+__device__ __forceinline__ uint32_t row_view(uint64_t v) { return (uint32_t)(vpay(v) >> 40) & 0xfffu; }
+__device__ __forceinline__ uint64_t row_row(uint64_t v) { return vpay(v) & ((1ull << 40) - 1); }
+__device__ __forceinline__ uint32_t rows_tab(uint64_t v) { return (uint32_t)(vpay(v) >> 48) & 0xfffu; }
+__device__ __forceinline__ uint32_t rows_first(uint64_t v) { return (uint32_t)(vpay(v) >> 16); }
+__device__ __forceinline__ uint32_t rows_len(uint64_t v) { return (uint32_t)(vpay(v) & 0xffffu); }
+// the value of slot `slot` at `row`
+__device__ __forceinline__ uint64_t cv_value(uint32_t slot, uint64_t row) {
+  const CvSlot sl = gk_args.cv_slots[slot];
+  const uint32_t w = gk_args.cv_words[(uint64_t)sl.col + row];
+  const uint32_t p = w & CW_PAY;
+  switch (w >> CW_SHIFT) {
+    case CW_STR: return mkv(V_STR, p);
+    case CW_NUM: return mkv(V_NUM, p);
+    case CW_LIT: return p == 0 ? mkv(V_NULL, 0) : mkv(V_BOOL, p == 2 ? 1 : 0);
+    case CW_OBJ: return mkv(V_ROW, ((uint64_t)sl.view << 40) | row);
+    case CW_ARR:
+      return mkv(V_ROWS, ((uint64_t)sl.tab << 48) | ((uint64_t)p << 16) | gk_args.cv_words[(uint64_t)sl.lencol + row]);
+    case CW_NODE: return nodeval(p);
+  }
+  return mkv(V_UNDEF, 0);
+}
+// element i of a V_ROWS array
+__device__ __forceinline__ uint64_t rows_at(uint64_t v, uint32_t i) {
+  return cv_value(gk_args.cv_tabs[rows_tab(v)], (uint64_t)rows_first(v) + i);
 }
 
 // a list copied out at emission (gval_copy), read by the size / format passes
@@ -551,12 +595,20 @@ __device__ __forceinline__ const uint64_t* glist_words(uint64_t v) {
 // collection view helpers (NODE arrays/objects and heap lists)
 __device__ uint32_t coll_len(const PLane& L, uint64_t v) {
   if (vtag(v) == V_NODE) { GK_TOUCH_NODE((uint32_t)vpay(v)); return gk_args.nodes[(uint32_t)vpay(v)].n; }
+  if (vtag(v) == V_ROWS) return rows_len(v);
+  if (vtag(v) == V_ROW) {  // the staging keeps objects read as collections as nodes: not reached
+    PLane& M = const_cast<PLane&>(L);
+    if (!M.fail) { M.fail = RF_FALLBACK; M.reason = FB_UNSUPPORTED; }
+    return 0;
+  }
   if (vtag(v) == V_LIST) { uint32_t n = list_len(L, v); return list_kind(v) == LK_OBJ ? n / 2 : n; }
   if (vtag(v) == V_GLIST) { uint32_t n = (uint32_t)glist_words(v)[0]; return list_kind(v) == LK_OBJ ? n / 2 : n; }
   return 0;
 }
 // i-th (key, value) of a collection
 __device__ void coll_at(const PLane& L, uint64_t v, uint32_t i, uint64_t& k, uint64_t& val) {
+  if (vtag(v) == V_ROWS) { val = rows_at(v, i); k = mkint(i); return; }
+  if (vtag(v) == V_ROW) { k = val = mkv(V_UNDEF, 0); return; }  // (coll_len flagged the lane)
   if (vtag(v) == V_NODE) {
     const Node& n = gk_args.nodes[(uint32_t)vpay(v)];
     uint32_t c = n.first + i;
@@ -603,6 +655,8 @@ __device__ int ecmp(PLane& L, uint64_t a, uint64_t b) {
   if (ca != cb) return ca < cb ? -1 : 1;
   if (ca <= 4) return scmp(L, a, b, ca);
   if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
+  if (vtag(a) >= V_ROW && a == b) return 0;
+  if (vtag(a) == V_ROW || vtag(b) == V_ROW) { lane_fallback(L, FB_DEEP_EQ); return 2; }
   if (coll_len(L, a) == 0 && coll_len(L, b) == 0) return 0;
   lane_fallback(L, FB_DEEP_EQ);
   return 2;
@@ -614,6 +668,8 @@ __device__ int vcmp(PLane& L, uint64_t a, uint64_t b) {
   if (ca != cb) return ca < cb ? -1 : 1;
   if (ca <= 4) return scmp(L, a, b, ca);
   if (vtag(a) == V_NODE && vtag(b) == V_NODE && vpay(a) == vpay(b)) return 0;
+  if (vtag(a) >= V_ROW && a == b) return 0;
+  if (vtag(a) == V_ROW || vtag(b) == V_ROW) { lane_fallback(L, FB_DEEP_EQ); return 2; }
   uint32_t na = coll_len(L, a), nb = coll_len(L, b);
   if (ca == 7) {
     uint32_t n = na < nb ? na : nb;
@@ -733,8 +789,35 @@ __device__ __forceinline__ uint64_t list_add(PLane& L, uint64_t l, uint64_t v) {
 }
 
 // ------------------------------------------------------------------ get
+// a member / element of a column value: an object's member by interned key
+// (a computed key string has no id to look up: CPU fallback), an array's
+// element by index
+__device__ __noinline__ uint64_t row_get_slow(PLane& L, uint64_t c, uint64_t key) {
+  if (vtag(c) == V_ROW) {
+    if (is_strv(key)) lane_fallback(L, FB_UNSUPPORTED);
+    return mkv(V_UNDEF, 0);
+  }
+  if (!is_numv(key)) return mkv(V_UNDEF, 0);
+  int64_t i;
+  if (!num_int(L, key, i) || i < 0 || i >= (int64_t)rows_len(c)) return mkv(V_UNDEF, 0);
+  return rows_at(c, (uint32_t)i);
+}
+__device__ __forceinline__ uint64_t row_get(PLane& L, uint64_t c, uint64_t key) {
+  if (vtag(c) == V_ROW && vtag(key) == V_STR) {
+    const uint32_t view = row_view(c);
+    const uint32_t slot = cv_find(view, (uint32_t)vpay(key));
+    if (slot != NO_ID) return cv_value(slot, row_row(c));
+    // a key the batch never has at this path: undefined where the view holds
+    // every key (the analysis gave the program's constant keys slots)
+    if (!(gk_args.cv_views[view] & CV_COMPLETE)) lane_fallback(L, FB_UNSUPPORTED);
+    return mkv(V_UNDEF, 0);
+  }
+  return row_get_slow(L, c, key);
+}
+
 __device__ __noinline__ uint64_t vget_slow(PLane& L, uint64_t c, uint64_t key) {
   uint32_t t = vtag(c);
+  if (t >= V_ROW) return row_get(L, c, key);
   if (t == V_NODE) {
     GK_TOUCH_NODE((uint32_t)vpay(c));
     const Node& n = gk_args.nodes[(uint32_t)vpay(c)];
@@ -785,6 +868,7 @@ __device__ __noinline__ uint64_t vget_slow(PLane& L, uint64_t c, uint64_t key) {
 // including fallback-flagged nodes, goes through vget_slow: an out-of-line
 // call costs the caller a save/restore of its live registers in scratch.
 __device__ __forceinline__ uint64_t vget(PLane& L, uint64_t c, uint64_t key) {
+  if (vtag(c) >= V_ROW) return row_get(L, c, key);
   if (vtag(c) != V_NODE && vtag(c) != V_LIST) return mkv(V_UNDEF, 0);
   if (vtag(c) == V_NODE) {
     GK_TOUCH_NODE((uint32_t)vpay(c));
@@ -987,6 +1071,7 @@ template <class O> __device__ int put_scalar(PLane& L, O& o, uint64_t v, bool js
     case V_STR: case V_HSTR: case V_SLICE: case V_GSTR:
       return (json ? put_json_str(o, sview(L, v)) : put_quoted(o, sview(L, v))) ? 1 : -1;
     case V_FMT: return -1;  // forced before any printing (jit.cc)
+    case V_ROW: return -1;  // a column object (colstore.cc keeps printed paths as nodes)
     default: return 0;
   }
 }
@@ -1514,7 +1599,7 @@ __device__ __noinline__ void emit_eager(PLane& L, bool want, uint32_t rule, cons
 // register operands (jit.cc); the VM dispatches through call_builtin.
 __device__ __forceinline__ uint64_t bi_count(PLane& L, uint64_t a) {
   uint32_t t = vtag(a);
-  if (t == V_NODE || t == V_LIST) return mkint(coll_len(L, a));
+  if (t == V_NODE || t == V_LIST || t == V_ROWS || t == V_ROW) return mkint(coll_len(L, a));
   if (is_strv(a)) return mkint(sview(L, a).n);
   lane_error(L);
   return mkv(V_UNDEF, 0);
@@ -1977,7 +2062,7 @@ __device__ __forceinline__ uint32_t fmt_fidx(uint64_t f) { return (uint32_t)(vpa
 __device__ __forceinline__ uint64_t lazy_sprintf(PLane& L, uint32_t fidx, uint64_t args) {
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t t = vtag(args);
-  if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
+  if ((t == V_LIST && list_kind(args) != LK_ARR) || t == V_ROWS) return do_sprintf(L, fidx, args);
   uint32_t idx = t == V_NODE ? ((uint32_t)vpay(args) | 0x80000000u) : list_off(args);
   if (t == V_NODE && (uint32_t)vpay(args) >= 0x80000000u) return do_sprintf(L, fidx, args);
   if (coll_len(L, args) != gk_args.fmt[fidx + 1]) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
@@ -1988,7 +2073,7 @@ __device__ __forceinline__ uint64_t lazy_sprintf(PLane& L, uint32_t fidx, uint64
 __device__ __forceinline__ uint64_t lazy_sprintf_n(PLane& L, uint32_t fidx, uint64_t args, uint32_t want) {
   if (tclass(args) != 7) { lane_error(L); return mkv(V_UNDEF, 0); }
   uint32_t t = vtag(args);
-  if (t == V_LIST && list_kind(args) != LK_ARR) return do_sprintf(L, fidx, args);
+  if ((t == V_LIST && list_kind(args) != LK_ARR) || t == V_ROWS) return do_sprintf(L, fidx, args);
   uint32_t idx = t == V_NODE ? ((uint32_t)vpay(args) | 0x80000000u) : list_off(args);
   if (t == V_NODE && (uint32_t)vpay(args) >= 0x80000000u) return do_sprintf(L, fidx, args);
   if (coll_len(L, args) != want) { lane_fallback(L, FB_PRINT); return mkv(V_UNDEF, 0); }
@@ -2024,7 +2109,7 @@ __device__ __forceinline__ bool op_iter_next(PLane& L, uint64_t coll, uint64_t& 
   L.hp = mh > L.keepH[d] ? mh : L.keepH[d];
   L.bp = mb > L.keepB[d] ? mb : L.keepB[d];
   uint32_t t = vtag(coll);
-  if ((t != V_NODE && t != V_LIST) || pos >= coll_len(L, coll)) return false;
+  if ((t != V_NODE && t != V_LIST && t < V_ROW) || pos >= coll_len(L, coll)) return false;
   coll_at(L, coll, pos, k, v);
   st = (st & 0xffffffff00000000ull) | (pos + 1);
   return true;
@@ -2270,7 +2355,7 @@ __device__ __forceinline__ uint64_t gm_check(uint64_t h, uint64_t v) {
 // unique-selector join scans); a review document's node is met by one lane
 // only and would just evict shared entries
 __device__ __forceinline__ bool gm_key(uint64_t v) {
-  return vtag(v) == V_NODE ? (uint32_t)vpay(v) < gk_args.nperm : memo_stable(v);
+  return vtag(v) == V_NODE ? (uint32_t)vpay(v) < gk_args.nperm : vtag(v) < V_ROW && memo_stable(v);
 }
 // a memo value: heap-free as it is, or a lane-buffer string copied into the
 // evaluation's memo-string arena (V_GSTR); 0 = not memoizable.  Each string
@@ -2490,7 +2575,7 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
 #endif
 __device__ __forceinline__ bool plain_scalar(uint64_t v) {
 #if GK_EMIT_WIDE
-  return memo_stable(v) && vtag(v) != V_UNDEF;
+  return memo_stable(v) && vtag(v) != V_UNDEF && vtag(v) < V_ROW;
 #else
   return vtag(v) == V_STR || vtag(v) == V_INT;
 #endif
@@ -2762,7 +2847,7 @@ __device__ __forceinline__ void audit_body(Run run) {
         L.memo_ok = 0;
         for (int d = 0; d < GK_MAXDEPTH; ++d) { L.keepH[d] = 0; L.keepB[d] = 0; }
         uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
-        run(L, mkv(V_NODE, rc.root), params, m.prog, plo, pn);
+        run(L, gk_args.cv_on ? mkv(V_ROW, (uint64_t)rp) : mkv(V_NODE, rc.root), params, m.prog, plo, pn);
       }
     }
   }

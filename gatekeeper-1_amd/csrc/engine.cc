@@ -24,6 +24,8 @@
 #include "compiler.h"
 #include "flatten.h"
 #include "jit.h"
+#include "colplan.h"
+#include "colstore.h"
 #include "json.h"
 #include "rego.h"
 #include "regex.h"
@@ -398,6 +400,12 @@ struct gk_batch {
   gk::DBuf d_nodes;  // the batch's own device node array: permanent region + its documents
   uint64_t dev_bytes = 0;
   bool device_layout = false;  // d_nodes / d_revs hold the device-built path layout (node ids differ from arena's)
+  // column form (colstore.h): d_nodes holds the permanent region + cv.nodes,
+  // d_revs cv.cols, and the programs read the documents from the columns
+  bool columnar = false;
+  std::string col_why;         // why the node form was kept
+  gk::ColStore cv;
+  gk::DBuf d_cv_words, d_cv_slots, d_cv_hash, d_cv_views, d_cv_tabs;
 };
 
 // Webhook micro-batch coalescer: concurrent single-review
@@ -474,6 +482,11 @@ struct gk_engine {
   bool jit_enabled = true;  // opts {"jit": false} / GKGPU_JIT=0 force the bytecode VM kernel
   bool host_only = false;    // opts {"host_only": true}: stage on the host only (CPU baseline / tests); no evaluation
   std::map<std::string, gk::TemplateEnt> templates;  // by constraint kind
+  // the referenced-path plan of every program a constraint runs (colplan.h),
+  // for the column form of staged batches; per engine generation
+  std::mutex plan_mu;
+  uint64_t plan_gen = ~0ull;
+  gk::PathPlan plan;
   bool modules_dirty = true;
   // data
   std::map<std::pair<std::string, std::string>, gk::ConstraintEnt> constraints;
@@ -1711,7 +1724,7 @@ static bool ctx_nodes(gk_engine* e, EvalCtx* x, const NodeArena& arena) {
 // tables as of this call.  Shared lock held.
 static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, const std::vector<ReviewCol>& cols,
                               DBuf* revbuf, bool decode, gk_results* res, const void* nodes, uint64_t n_excluded = 0,
-                              uint32_t nperm = NO_ID, bool audit = false) {
+                              uint32_t nperm = NO_ID, bool audit = false, const gk_batch* colb = nullptr) {
   if (nperm == NO_ID) nperm = e->perm_nodes;  // a query's documents follow the engine's permanent region
   uint32_t nrev = (uint32_t)cols.size();
   uint32_t ncons = (uint32_t)e->corder.size();
@@ -1847,6 +1860,15 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.ebytes_cap = x->ebytes_cap;
     a.lens = (uint32_t*)x->d_lens.p;
     a.part = (unsigned long long*)x->d_part.p;
+    if (colb && colb->columnar) {  // the batch's documents in column form (colstore.h)
+      a.cv_words = (const uint32_t*)colb->d_cv_words.p;
+      a.cv_slots = (const CvSlot*)colb->d_cv_slots.p;
+      a.cv_hash = (const CvHash*)colb->d_cv_hash.p;
+      a.cv_views = (const uint32_t*)colb->d_cv_views.p;
+      a.cv_tabs = (const uint32_t*)colb->d_cv_tabs.p;
+      a.cv_hmask = (uint32_t)colb->cv.hash.size() - 1;
+      a.cv_on = 1;
+    }
     set_join_args(e, a);
     while (x->events.size() < plan.size() + 5) {
       hipEvent_t ev1;
@@ -2628,7 +2650,8 @@ static int audit_from_cache(gk_engine* e, gk_results** out) {
   TablePtrs tp;
   if (!ctx_device(e, lease.x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto res = std::make_unique<gk_results>();
-  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, true, res.get(), b->d_nodes.p, 0, b->node_begin);
+  rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, true, res.get(), b->d_nodes.p, 0, b->node_begin, false,
+                          b.get());
   if (rc != GK_OK) return rc;
   *out = res.release();
   return GK_OK;
@@ -2973,6 +2996,43 @@ static bool batch_upload_layout(gk_engine* e, gk_batch* b, const DevLayout& dl) 
   return true;
 }
 
+// The merged referenced-path plan of the programs the constraints run
+// (colplan.h), cached per engine generation.  Shared lock held.
+static gk::PathPlan batch_plan(gk_engine* e) {
+  std::lock_guard<std::mutex> g(e->plan_mu);
+  if (e->plan_gen != e->gen) {
+    gk::PathPlan P;
+    P.nodes.emplace_back();
+    std::set<uint32_t> progs;
+    for (auto* c : e->corder)
+      if (c->spec.prog != NO_ID && c->spec.prog < e->progs.size()) progs.insert(c->spec.prog);
+    for (uint32_t p : progs) P.merge(gk::plan_paths(e->progs[p], e->bank));
+    e->plan = std::move(P);
+    e->plan_gen = e->gen;
+  }
+  return e->plan;
+}
+
+// GKGPU_COLUMNS (A/B switch): staged batches in column form (colstore.h)
+static bool columns_on() { return env_mode("GKGPU_COLUMNS", 0, 1) != 0; }
+
+// The column form's device arrays: the permanent region and the kept
+// subtrees as the batch's node array, the review columns, the path columns.
+static bool batch_upload_columns(gk_engine* e, gk_batch* b) {
+  const ColStore& cv = b->cv;
+  const size_t perm = b->node_begin, kept = cv.nodes.size();
+  if (!b->d_nodes.reserve((perm + kept + 1) * sizeof(Node))) return false;
+  if (perm && (hipMemcpy(b->d_nodes.p, e->d_nodes.p, perm * sizeof(Node), hipMemcpyDeviceToDevice) != hipSuccess ||
+               hipStreamSynchronize(nullptr) != hipSuccess))  // (see DBuf::reserve)
+    return false;
+  if (kept && hipMemcpy((char*)b->d_nodes.p + perm * sizeof(Node), cv.nodes.data(), kept * sizeof(Node),
+                        hipMemcpyHostToDevice) != hipSuccess)
+    return false;
+  b->d_nodes.used = (perm + kept) * sizeof(Node);
+  return up(b->d_revs, cv.cols, false) && up(b->d_cv_words, cv.words, false) && up(b->d_cv_slots, cv.slots, false) &&
+         up(b->d_cv_hash, cv.hash, false) && up(b->d_cv_views, cv.views, false) && up(b->d_cv_tabs, cv.tabs, false);
+}
+
 static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
   ReadLock rl;
   int rc = read_lock(e, rl, !e->host_only);
@@ -3001,6 +3061,15 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   b->gen = e->gen;
   b->node_count = b->node_end - b->node_begin;
   auto t1 = Clock::now();
+  if (columns_on()) {
+    const gk::PathPlan plan = batch_plan(e);
+    b->columnar = gk::build_columns(plan, e->st.nodes().data(), b->node_begin, b->arena.data(), b->arena.size(), b->cols,
+                                    e->st, e->smu, b->cv, b->col_why);
+    if (getenv("GKGPU_FLATTEN_TRACE"))
+      fprintf(stderr, "columns: %s %.1f ms, %llu bytes%s%s\n", b->columnar ? "built" : "not used", ms_since(t1),
+              (unsigned long long)b->cv.bytes(), b->columnar ? "" : ": ", b->col_why.c_str());
+  }
+  b->ms_flatten = ms_since(t0);
   if (e->host_only) {  // documents stay in the host arena only (gk_debug_host_args)
     *out = b.release();
     return GK_OK;
@@ -3009,10 +3078,15 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
   bool up_ok = sync_strings(e, nullptr);
   const double ms_tables = ms_since(t1);
-  up_ok = up_ok && up(b->d_revs, b->cols, false);
-  const double ms_cols = ms_since(t1);
-  if (dev_layout && dl.nroots != NO_ID) up_ok = up_ok && batch_upload_layout(e, b.get(), dl);
-  else up_ok = up_ok && batch_upload(e, b.get());
+  double ms_cols = ms_tables;
+  if (b->columnar) {
+    up_ok = up_ok && batch_upload_columns(e, b.get());
+  } else {
+    up_ok = up_ok && up(b->d_revs, b->cols, false);
+    ms_cols = ms_since(t1);
+    if (dev_layout && dl.nroots != NO_ID) up_ok = up_ok && batch_upload_layout(e, b.get(), dl);
+    else up_ok = up_ok && batch_upload(e, b.get());
+  }
   if (trace)
     fprintf(stderr, "stage upload: strings %.1f ms, columns %.1f ms, nodes %.1f ms\n", ms_tables, ms_cols - ms_tables,
             ms_since(t1) - ms_cols);
@@ -3022,7 +3096,8 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
     return fail(e, GK_EDEVICE, "upload failed");
   }
   b->ms_upload = ms_since(t1);
-  b->dev_bytes = (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
+  b->dev_bytes = b->columnar ? b->cv.bytes()
+                             : (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
   release_parts_async();
   *out = b.release();
   return GK_OK;
@@ -3084,7 +3159,7 @@ int gk_batch_eval(gk_engine* e, gk_batch* b, int decode, gk_results** out) {
   if (!ctx_device(e, lease.x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto res = std::make_unique<gk_results>();
   rc = launch_and_collect(e, lease.x, tp, b->cols, &b->d_revs, decode != 0, res.get(), b->d_nodes.p, b->excluded,
-                          b->node_begin);
+                          b->node_begin, false, b);
   if (rc != GK_OK) return rc;
   *out = res.release();
   return GK_OK;
@@ -3126,7 +3201,7 @@ static int batch_eval_audit_locked(gk_engine* e, gk_batch* b, uint32_t limit, gk
   if (!ctx_device(e, x) || !sync_strings(e, &tp)) return fail(e, GK_EDEVICE, "device upload failed");
   auto resp = std::make_unique<gk_results>();
   gk_results* res = resp.get();
-  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded, b->node_begin, true);
+  rc = launch_and_collect(e, x, tp, b->cols, &b->d_revs, false, res, b->d_nodes.p, b->excluded, b->node_begin, true, b);
   if (rc != GK_OK) return rc;
   res->audited = true;
   const uint32_t ncons = (uint32_t)e->corder.size(), nrev = b->nrev;
@@ -3262,6 +3337,7 @@ void gk_batch_free(gk_batch* b) {
   if (!b) return;
   b->d_revs.free_();
   b->d_nodes.free_();
+  for (DBuf* d : {&b->d_cv_words, &b->d_cv_slots, &b->d_cv_hash, &b->d_cv_views, &b->d_cv_tabs}) d->free_();
   delete b;
 }
 
@@ -3603,6 +3679,23 @@ int gk_template_joins(gk_engine* e, const char* kind, const char** sites) {
   return n;
 }
 
+// diagnostics: the referenced-path plan of a template's program (colplan.h);
+// *out is malloc'd (gk_free_string)
+extern "C" int gk_debug_template_paths(gk_engine* e, const char* kind, char** out) {
+  if (!e || !kind || !out) return GK_EINVAL;
+  WriteLock g(e);
+  try {
+    rebuild_modules(e);
+  } catch (const std::exception& ex) {
+    return fail(e, GK_EPARSE, ex.what());
+  }
+  auto it = e->templates.find(kind);
+  if (it == e->templates.end() || it->second.prog < 0) return GK_ENOTFOUND;
+  const std::string d = gk::plan_paths(e->progs[it->second.prog], e->bank).describe(e->st);
+  *out = strdup(d.c_str());
+  return GK_OK;
+}
+
 int gk_join_stats(gk_engine* e, uint64_t* indexes, uint64_t* entries, uint64_t* unindexed, uint64_t* leaves,
                   double* build_ms) {
   if (!e) return GK_EINVAL;
@@ -3795,6 +3888,42 @@ extern "C" int gk_debug_host_args(gk_engine* e, const gk_batch* b, void* out, si
   a.ntiles = (a.nrev + 63) / 64;
   memcpy(out, &a, sizeof a);
   return GK_OK;
+}
+
+// gk_debug_host_args over the batch's column form (colstore.h): the
+// permanent region followed by the kept subtrees, the review columns with
+// their ids, and the host path columns -- the CPU checker then evaluates
+// exactly what the device reads.  GK_EINVAL when the batch is in node form.
+extern "C" int gk_debug_host_args_columns(gk_engine* e, const gk_batch* b, void* out, size_t out_size) {
+  if (!e || !b || !b->columnar) return GK_EINVAL;
+  int rc = gk_debug_host_args(e, b, out, out_size);
+  if (rc != GK_OK) return rc;
+  std::lock_guard<std::mutex> dg(e->dbg_mu);
+  e->dbg_nodes.resize(e->perm_nodes);
+  e->dbg_nodes.insert(e->dbg_nodes.end(), b->cv.nodes.begin(), b->cv.nodes.end());
+  DevArgs a;
+  memcpy(&a, out, sizeof a);
+  a.nodes = e->dbg_nodes.data();
+  a.revs = b->cv.cols.data();
+  a.cv_words = b->cv.words.data();
+  a.cv_slots = b->cv.slots.data();
+  a.cv_hash = b->cv.hash.data();
+  a.cv_views = b->cv.views.data();
+  a.cv_tabs = b->cv.tabs.data();
+  a.cv_hmask = (uint32_t)b->cv.hash.size() - 1;
+  a.cv_on = 1;
+  memcpy(out, &a, sizeof a);
+  return GK_OK;
+}
+
+// the batch's storage form: 1 columns (*schema: the path schema, *why: ""),
+// 0 nodes (*why: the reason the columns were not used)
+extern "C" int gk_batch_columns(const gk_batch* b, const char** schema, const char** why, uint64_t* bytes) {
+  if (!b) return GK_EINVAL;
+  if (schema) *schema = b->cv.schema.c_str();
+  if (why) *why = b->col_why.c_str();
+  if (bytes) *bytes = b->cv.bytes();
+  return b->columnar ? 1 : 0;
 }
 
 // Content hash over a staged batch's review columns (in order), the documents

@@ -1739,4 +1739,9 @@ bool jit_compile(const std::string& src, std::string& code, std::string& log) {
   return true;
 }
 
+// the bytecode's register reads / writes and successors, for analyses in
+// other translation units (colplan.cc)
+void bc_regs(const Ins& in, std::vector<uint32_t>& rd, std::vector<uint32_t>& wr) { ins_regs(in, rd, wr); }
+void bc_succ(const Ins& in, uint32_t pc, std::vector<uint32_t>& out) { ins_succ(in, pc, out); }
+
 }  // namespace gk

@@ -32,16 +32,18 @@ def load():
     return _LIB
 
 
-def _host_args(driver, batch, joins: bool, threads: int):
+def _host_args(driver, batch, joins: bool, threads: int, columns: bool = False):
     """the batch's host launch arguments; joins: with the checker's own join
     indexes built from the engine's join plan (cpuvm.cc gkcpu_build_joins),
-    else every join site scans"""
+    else every join site scans; columns: the batch's column form
+    (colstore.h), read as the device reads it"""
     lib = load()
     glib = driver._lib
     n = lib.gkcpu_devargs_size()
     buf = (C.c_uint8 * n)()
-    glib.gk_debug_host_args.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
-    driver._check(glib.gk_debug_host_args(driver._e, batch._h, buf, n))
+    fn = glib.gk_debug_host_args_columns if columns else glib.gk_debug_host_args
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    driver._check(fn(driver._e, batch._h, buf, n))
     if joins:
         glib.gk_debug_join_plan.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
         sites, ns = C.c_void_p(), C.c_uint64()
@@ -63,7 +65,7 @@ def sweep(driver, batch, lo: int = 0, hi=None, threads: int = 1, joins: bool = T
     return s, out[0], out[1], out[2], out[3]
 
 
-def sweep_digest(driver, batch, threads: int = 1, joins: bool = True):
+def sweep_digest(driver, batch, threads: int = 1, joins: bool = True, columns: bool = False):
     """sweep() over the whole batch plus an order-free digest of every result
     row (oracle/cpuvm.cc gkcpu_sweep_digest): (evals, violations, flagged,
     digest).  row_digest computes the same over rows from elsewhere (the
@@ -71,7 +73,7 @@ def sweep_digest(driver, batch, threads: int = 1, joins: bool = True):
     lib = load()
     lib.gkcpu_sweep_digest.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]
     lib.gkcpu_sweep_digest.restype = C.c_double
-    buf = _host_args(driver, batch, joins, threads)
+    buf = _host_args(driver, batch, joins, threads, columns)
     out = (C.c_uint64 * 5)()
     lib.gkcpu_sweep_digest(buf, 0, batch.n, threads, out)
     return out[0], out[1], out[3], out[4]

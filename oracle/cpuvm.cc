@@ -240,7 +240,7 @@ static void eval_pair(uint32_t rp, uint32_t c, Counts& k, char* fbuf, uint32_t f
     else if (mr == 1 && (m.flags & MF_FALLBACK)) lane_fallback(L, FB_TEMPLATE);
     else if (mr == 1 && m.prog != NO_ID) {
       uint64_t params = m.params == NO_ID ? mkv(V_NODE, 0) : nodeval(m.params);
-      run_program(L, gk_args.prog_off[m.prog], mkv(V_NODE, rc.root), params);
+      run_program(L, gk_args.prog_off[m.prog], gk_args.cv_on ? mkv(V_ROW, (uint64_t)rp) : mkv(V_NODE, rc.root), params);
     }
   }
   if (L.fail) { ++k.flagged; return; }
