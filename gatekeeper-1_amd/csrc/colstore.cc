@@ -14,9 +14,13 @@
 #include "colstore.h"
 
 #include <algorithm>
+#include <cstring>
 #include <atomic>
 #include <mutex>
 #include <sstream>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "flatten.h"
@@ -24,7 +28,8 @@
 namespace gk {
 namespace {
 
-constexpr uint8_t S_SCALAR = 1, S_OBJ = 2, S_ARR = 4, S_BIG = 8;  // S_BIG: an object with the fallback flag
+// S_BIG: an object with the fallback flag; S_PAY: a string or number (a payload)
+constexpr uint8_t S_SCALAR = 1, S_OBJ = 2, S_ARR = 4, S_BIG = 8, S_PAY = 16;
 constexpr uint32_t kChunk = 2048;
 constexpr uint32_t kMaxDynKeys = 32;  // a computed-key object with more distinct keys stays nodes
 
@@ -103,15 +108,40 @@ struct Schema {
   }
 };
 
+// per-chunk element counts of a thread's local schema (pass A): the arrays'
+// lengths summed per local snode
+struct ChunkCount {
+  std::vector<uint64_t> n;          // per local snode
+  std::vector<uint32_t> touched;
+  void add(uint32_t s, uint64_t k) {
+    if (s >= n.size()) n.resize(s + 64, 0);
+    if (!n[s]) touched.push_back(s);
+    n[s] += k;
+  }
+};
+
 struct Docs {
   const Node* perm;
   uint32_t nb;
+  size_t na;
   const Node* arena;
   const Node& operator()(uint32_t id) const { return id >= nb ? arena[id - nb] : perm[id]; }
+  // the passes visit reviews in evaluation order, so consecutive documents
+  // lie far apart in the arena: each walk is a chain of dependent misses.  A
+  // document's nodes are one block around its root; fetching the block of a
+  // review a few positions ahead overlaps those misses.
+  void prefetch(uint32_t root) const {
+    if (root == NO_ID || root < nb) return;
+    const size_t a = root - nb;
+    const size_t lo = a >= kPfBefore ? a - kPfBefore : 0, hi = std::min(na, a + kPfAfter);
+    for (size_t i = lo; i < hi; i += 4) __builtin_prefetch(arena + i, 0, 0);
+  }
+  static constexpr size_t kPfBefore = 80, kPfAfter = 2;  // (a root follows its members: the parser places a run at its close)
 };
+constexpr uint32_t kAhead = 6;
 
 // pass A: one document path instance
-void discover(Schema& S, const Docs& D, uint32_t s, uint32_t id) {
+void discover(Schema& S, const Docs& D, uint32_t s, uint32_t id, ChunkCount& cc) {
   const Node& x = D(id);
   if (x.type == NT_OBJ) {
     S.n[s].seen |= S_OBJ;
@@ -132,25 +162,27 @@ void discover(Schema& S, const Docs& D, uint32_t s, uint32_t id) {
         if (!S.n[s].dyn) continue;  // a member no program reads
         k = S.member(s, key);
       }
-      discover(S, D, k, c);
+      discover(S, D, k, c, cc);
     }
   } else if (x.type == NT_ARR) {
     S.n[s].seen |= S_ARR;
     S.n[s].maxlen = std::max<uint32_t>(S.n[s].maxlen, x.n);
     if (S.n[s].uses & PU_WHOLE) return;
+    cc.add(s, x.n);
     const uint32_t e = S.element(s);
-    for (uint32_t i = 0; i < x.n; ++i) discover(S, D, e, x.first + i);
+    for (uint32_t i = 0; i < x.n; ++i) discover(S, D, e, x.first + i, cc);
   } else {
-    S.n[s].seen |= S_SCALAR;
+    S.n[s].seen |= (x.type == NT_STR || x.type == NT_NUM) ? (S_SCALAR | S_PAY) : S_SCALAR;
   }
 }
 
-// merges thread schema b's subtree at bs into a's at as
-void merge_schema(Schema& A, uint32_t as, const Schema& B, uint32_t bs) {
+// merges thread schema b's subtree at bs into a's at as; map[b snode] = a snode
+void merge_schema(Schema& A, uint32_t as, const Schema& B, uint32_t bs, std::vector<uint32_t>& map) {
+  map[bs] = as;
   A.n[as].seen |= B.n[bs].seen;
   A.n[as].maxlen = std::max(A.n[as].maxlen, B.n[bs].maxlen);
-  for (const auto& kv : B.n[bs].kids) merge_schema(A, A.member(as, kv.first), B, kv.second);
-  if (B.n[bs].elem != NO_ID) merge_schema(A, A.element(as), B, B.n[bs].elem);
+  for (const auto& kv : B.n[bs].kids) merge_schema(A, A.member(as, kv.first), B, kv.second, map);
+  if (B.n[bs].elem != NO_ID) merge_schema(A, A.element(as), B, B.n[bs].elem, map);
 }
 
 bool scalar_word(const Node& x, uint32_t& w) {
@@ -169,9 +201,12 @@ bool scalar_word(const Node& x, uint32_t& w) {
 bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, const Node* arena, size_t n_arena,
                    const std::vector<ReviewCol>& cols, const Store& st, std::mutex& smu, ColStore& out,
                    std::string& why) {
-  (void)n_arena;
   if (!plan.ok) { why = plan.why; return false; }
-  const Docs D{perm, node_begin, arena};
+  using Clock = std::chrono::steady_clock;
+  const auto t0 = Clock::now();
+  auto ms = [&]() { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); };
+  const bool trace = getenv("GKGPU_FLATTEN_TRACE") != nullptr;
+  const Docs D{perm, node_begin, n_arena, arena};
   const uint32_t nrev = (uint32_t)cols.size();
   const uint32_t nchunk = (nrev + kChunk - 1) / kChunk;
   const int T = std::max(1, std::min<int>(default_threads(), (int)nchunk));
@@ -179,20 +214,34 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
   std::vector<Schema> local(T);
   for (auto& s : local) { s.P = &plan; s.make({0}); }
   std::atomic<uint32_t> next{0};
+  // per chunk: (thread, [(local snode, elements)])
+  std::vector<std::pair<int, std::vector<std::pair<uint32_t, uint64_t>>>> ccount(nchunk);
   parallel_run(T, [&](int t) {
     Schema& S = local[t];
+    ChunkCount cc;
     for (;;) {
       const uint32_t c = next.fetch_add(1);
       if (c >= nchunk) break;
-      for (uint32_t r = c * kChunk; r < std::min(nrev, (c + 1) * kChunk); ++r)
-        if (cols[r].root != NO_ID) discover(S, D, 0, cols[r].root);
+      const uint32_t r1 = std::min(nrev, (c + 1) * kChunk);
+      for (uint32_t r = c * kChunk; r < r1; ++r) {
+        if (r + kAhead < r1) D.prefetch(cols[r + kAhead].root);
+        if (cols[r].root != NO_ID) discover(S, D, 0, cols[r].root, cc);
+      }
+      ccount[c].first = t;
+      for (uint32_t s : cc.touched) { ccount[c].second.push_back({s, cc.n[s]}); cc.n[s] = 0; }
+      cc.touched.clear();
     }
   });
   Schema S;
   S.P = &plan;
   S.make({0});
-  for (auto& l : local) merge_schema(S, 0, l, 0);
+  std::vector<std::vector<uint32_t>> lmap(T);
+  for (int t = 0; t < T; ++t) {
+    lmap[t].assign(local[t].n.size(), NO_ID);
+    merge_schema(S, 0, local[t], 0, lmap[t]);
+  }
   local.clear();
+  if (trace) fprintf(stderr, "columns: A discover %.1f ms\n", ms());
   // ---- B: storage, views, tables (a breadth-first walk below the root)
   std::vector<uint32_t> views_of, tabs_of;  // snode of each view / table
   {
@@ -228,34 +277,16 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
     }
     if (views_of.size() > 4096 || tabs_of.size() > 4096) { why = "too many object views / element tables"; return false; }
   }
-  // ---- C1: element rows per chunk and table
+  if (trace) fprintf(stderr, "columns: B decide %.1f ms\n", ms());
+  // ---- C1: element rows per chunk and table (counted in pass A)
   const uint32_t ntab = (uint32_t)tabs_of.size();
   std::vector<uint64_t> counts((size_t)nchunk * ntab, 0);
-  std::function<void(uint32_t, uint32_t, uint64_t*)> count = [&](uint32_t s, uint32_t id, uint64_t* cnt) {
-    const SNode& x = S.n[s];
-    if (x.node) return;
-    const Node& d = D(id);
-    if (d.type == NT_OBJ && x.view != NO_ID) {
-      for (const auto& kv : x.kids) {
-        for (uint32_t i = 0; i < d.n; ++i)
-          if (D(d.first + i).key == kv.first) { count(kv.second, d.first + i, cnt); break; }
-      }
-    } else if (d.type == NT_ARR && x.tab != NO_ID) {
-      cnt[x.tab] += d.n;
-      if (x.elem != NO_ID)
-        for (uint32_t i = 0; i < d.n; ++i) count(x.elem, d.first + i, cnt);
+  for (uint32_t c = 0; c < nchunk; ++c)
+    for (const auto& sc : ccount[c].second) {
+      const uint32_t g = lmap[ccount[c].first][sc.first];
+      if (g == NO_ID || S.n[g].node || S.n[g].tab == NO_ID) continue;
+      counts[(size_t)c * ntab + S.n[g].tab] += sc.second;
     }
-  };
-  next = 0;
-  parallel_run(T, [&](int) {
-    for (;;) {
-      const uint32_t c = next.fetch_add(1);
-      if (c >= nchunk) break;
-      uint64_t* cnt = &counts[(size_t)c * ntab];
-      for (uint32_t r = c * kChunk; r < std::min(nrev, (c + 1) * kChunk); ++r)
-        if (cols[r].root != NO_ID) count(0, cols[r].root, cnt);
-    }
-  });
   std::vector<uint64_t> rows(ntab, 0);  // table sizes; counts become each chunk's first row
   rows[0] = nrev;
   for (uint32_t t = 1; t < ntab; ++t) {
@@ -268,10 +299,15 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
     rows[t] = acc;
     if (acc > CW_PAY) { why = "element table too large"; return false; }
   }
+  if (trace) fprintf(stderr, "columns: C1 count %.1f ms\n", ms());
   // slots and their columns
-  out = ColStore{};
+  out.slots.clear();
+  out.hash.clear();
+  out.views.clear();
+  out.tabs.clear();
+  out.nodes.resize(0);
   out.node_begin = node_begin;
-  uint64_t words = 0;
+  uint64_t words = 0, bytes = 0;
   {
     std::vector<uint32_t> q{0};
     for (size_t qi = 0; qi < q.size(); ++qi) {
@@ -283,8 +319,14 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
       if (q[qi] == 0) continue;
       SNode& y = S.n[q[qi]];
       CvSlot sl{};
-      sl.col = (uint32_t)words;
-      words += rows[y.table];
+      if (!(y.seen & (S_ARR | S_PAY)) && !(y.node && (y.seen & S_OBJ))) {
+        sl.flags = CVS_BYTES;  // tags only: objects, literals, undefined
+        sl.col = (uint32_t)bytes;
+        bytes += rows[y.table];
+      } else {
+        sl.col = (uint32_t)words;
+        words += rows[y.table];
+      }
       sl.lencol = NO_ID;
       if (y.tab != NO_ID && !y.node) {
         sl.lencol = (uint32_t)words;
@@ -294,99 +336,219 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
       sl.tab = (uint16_t)(y.tab == NO_ID ? 0 : y.tab);
       y.slot = (uint32_t)out.slots.size();
       out.slots.push_back(sl);
-      if (words > 0xffffffffull) { why = "columns exceed 4G words"; return false; }
+      if (words > 0xffffffffull || bytes > 0xffffffffull) { why = "columns exceed 4G words"; return false; }
     }
   }
-  out.words.assign(words, 0);
+  out.words.resize(words);  // (each chunk zeroes its own rows of every column below)
+  out.bytes.resize(bytes);
   out.rows = 0;
   for (uint64_t r : rows) out.rows += r;
-  // ---- C2: fill
-  struct NodeRef { uint64_t at; uint32_t src; };
-  std::vector<std::vector<NodeRef>> refs(T);
+  if (trace) fprintf(stderr, "columns: alloc %.1f ms (%llu words)\n", ms(), (unsigned long long)words);
+  // the label objects of the Namespace documents (shared by the reviews of a
+  // namespace): copied once, first
+  std::unordered_map<uint32_t, uint32_t> shared;
+  auto copy_into = [&](std::vector<Node>& dst, uint32_t src, uint32_t id0) -> uint32_t {
+    // breadth-first: each composite's children as one contiguous run; ids
+    // are id0 + position in dst
+    const uint32_t root = id0 + (uint32_t)dst.size();
+    const Node top = D(src);
+    dst.push_back(top);
+    if (top.type != NT_OBJ && top.type != NT_ARR) return root;
+    {  // the common case (a label object): scalar members only, no queue
+      bool flat = true;
+      for (uint32_t i = 0; i < top.n && flat; ++i) flat = D(top.first + i).type != NT_OBJ && D(top.first + i).type != NT_ARR;
+      if (flat) {
+        dst.back().first = id0 + (uint32_t)dst.size();
+        for (uint32_t i = 0; i < top.n; ++i) dst.push_back(D(top.first + i));
+        return root;
+      }
+    }
+    thread_local std::vector<std::pair<uint32_t, uint32_t>> q;
+    q.clear();
+    q.push_back({src, root});
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const Node sn = D(q[qi].first);
+      if (sn.type != NT_OBJ && sn.type != NT_ARR) continue;
+      const uint32_t run = id0 + (uint32_t)dst.size();
+      dst[q[qi].second - id0].first = run;
+      for (uint32_t i = 0; i < sn.n; ++i) {
+        dst.push_back(D(sn.first + i));
+        q.push_back({sn.first + i, run + i});
+      }
+    }
+    return root;
+  };
+  std::vector<Node> shared_nodes;
+  for (const ReviewCol& rc : cols)
+    if (rc.ns_labels != NO_ID && rc.ns_labels >= node_begin && !shared.count(rc.ns_labels))
+      shared[rc.ns_labels] = copy_into(shared_nodes, rc.ns_labels, node_begin);
+  const uint32_t nshared = (uint32_t)shared_nodes.size();
+  // a bit per document node: is it one of `shared` (most references are not:
+  // the test spares a hash lookup per reference)
+  std::vector<uint64_t> shared_bit((n_arena + 64) / 64, 0);
+  for (const auto& kv : shared) {
+    const size_t a = kv.first - node_begin;
+    shared_bit[a >> 6] |= 1ull << (a & 63);
+  }
+  auto is_shared = [&](uint32_t src) {
+    const size_t a = src - node_begin;
+    return (shared_bit[a >> 6] >> (a & 63)) & 1;
+  };
+  // ---- C2: fill the words; per chunk, the subtrees kept as nodes go to the
+  // chunk's own node list (ids relocated once the chunks' sizes are known)
+  struct Chunk {
+    std::vector<Node> nodes;                           // .first: local index
+    std::vector<std::pair<uint64_t, uint32_t>> words;  // (word position, local node)
+    std::vector<std::pair<uint64_t, uint32_t>> cols;   // (review * 3 + label field, local node)
+  };
+  std::vector<Chunk> chunks(nchunk);
+  out.cols.resize(nrev);
+  // per slot: its table, for the chunks' zeroing
+  std::vector<std::pair<uint32_t, uint32_t>> slot_tab;  // (slot, table)
+  for (uint32_t s2 = 1; s2 < S.n.size(); ++s2)
+    if (S.n[s2].slot != NO_ID) slot_tab.push_back({S.n[s2].slot, S.n[s2].table});
   std::atomic<bool> bad{false};
-  std::function<void(uint32_t, uint32_t, uint64_t, uint64_t*, std::vector<NodeRef>&)> fill =
-      [&](uint32_t s, uint32_t id, uint64_t row, uint64_t* cur, std::vector<NodeRef>& nr) {
-        const SNode& x = S.n[s];
-        const Node& d = D(id);
+  struct Filler {
+    const Schema& S;
+    const Docs& D;
+    ColStore& out;
+    std::atomic<bool>& bad;
+    uint64_t* cur;
+    std::vector<std::pair<uint32_t, uint64_t>> refs;  // (source node, word position) of the review
+    // the view's member columns of object d: one pass over its members, the
+    // first member of a key wins (as every reader's scan does)
+    void members(const SNode& x, const Node& d, uint64_t row) {
+      const size_t nk = x.kids.size();
+      if (nk > 64) {
+        for (const auto& kv : x.kids)
+          for (uint32_t i = 0; i < d.n; ++i)
+            if (D(d.first + i).key == kv.first) { fill(kv.second, d.first + i, row); break; }
+        return;
+      }
+      uint64_t done = 0;
+      for (uint32_t i = 0; i < d.n; ++i) {
+        const uint32_t key = D(d.first + i).key;
+        for (size_t j = 0; j < nk; ++j)
+          if (x.kids[j].first == key) {
+            if (!(done >> j & 1)) { done |= 1ull << j; fill(x.kids[j].second, d.first + i, row); }
+            break;
+          }
+      }
+    }
+    void put(const SNode& x, uint64_t at, uint32_t w) {
+      if (out.slots[x.slot].flags & CVS_BYTES) out.bytes[at] = cv_word_byte(w);
+      else out.words[at] = w;
+    }
+    void fill(uint32_t s, uint32_t id, uint64_t row) {
+      const SNode& x = S.n[s];
+      const Node& d = D(id);
+      const uint64_t at = (uint64_t)out.slots[x.slot].col + row;
+      if (d.type != NT_OBJ && d.type != NT_ARR) {
         uint32_t w = 0;
-        const uint64_t at = (uint64_t)out.slots[x.slot].col + row;
-        if (d.type != NT_OBJ && d.type != NT_ARR) {
-          if (!scalar_word(d, w)) { bad = true; return; }
-          out.words[at] = w;
-          return;
-        }
-        if (x.node) {
-          nr.push_back({at, id});
-          return;
-        }
-        if (d.type == NT_OBJ) {
-          out.words[at] = CW_OBJ << CW_SHIFT;
-          for (const auto& kv : x.kids)
-            for (uint32_t i = 0; i < d.n; ++i)
-              if (D(d.first + i).key == kv.first) { fill(kv.second, d.first + i, row, cur, nr); break; }
-          return;
-        }
-        const uint64_t first = cur[x.tab];
-        cur[x.tab] += d.n;
-        out.words[at] = (CW_ARR << CW_SHIFT) | (uint32_t)first;
-        out.words[(uint64_t)out.slots[x.slot].lencol + row] = d.n;
-        if (x.elem != NO_ID)
-          for (uint32_t i = 0; i < d.n; ++i) fill(x.elem, d.first + i, first + i, cur, nr);
-      };
+        if (!scalar_word(d, w)) { bad = true; return; }
+        put(x, at, w);
+        return;
+      }
+      if (x.node) { refs.push_back({id, at}); return; }
+      if (d.type == NT_OBJ) {
+        put(x, at, CW_OBJ << CW_SHIFT);
+        members(x, d, row);
+        return;
+      }
+      const uint64_t first = cur[x.tab];
+      cur[x.tab] += d.n;
+      out.words[at] = (CW_ARR << CW_SHIFT) | (uint32_t)first;
+      out.words[(uint64_t)out.slots[x.slot].lencol + row] = d.n;
+      if (x.elem != NO_ID)
+        for (uint32_t i = 0; i < d.n; ++i) fill(x.elem, d.first + i, first + i);
+    }
+  };
   next = 0;
-  parallel_run(T, [&](int t) {
+  parallel_run(T, [&](int) {
     std::vector<uint64_t> cur(ntab);
+    Filler F{S, D, out, bad, cur.data(), {}};
+    std::vector<std::pair<uint32_t, uint32_t>> mine;  // (source, local) copied for this review
     for (;;) {
       const uint32_t c = next.fetch_add(1);
       if (c >= nchunk) break;
+      Chunk& ch = chunks[c];
       for (uint32_t k = 1; k < ntab; ++k) cur[k] = counts[(size_t)c * ntab + k];
-      for (uint32_t r = c * kChunk; r < std::min(nrev, (c + 1) * kChunk); ++r) {
-        if (cols[r].root == NO_ID) continue;
-        const Node& d = D(cols[r].root);
-        if (d.type != NT_OBJ) { bad = true; continue; }
-        for (const auto& kv : S.n[0].kids)
-          for (uint32_t i = 0; i < d.n; ++i)
-            if (D(d.first + i).key == kv.first) { fill(kv.second, d.first + i, r, cur.data(), refs[t]); break; }
+      // this chunk's rows of every column start undefined (CW_ABSENT)
+      for (const auto& st2 : slot_tab) {
+        const uint32_t t = st2.second;
+        const uint64_t lo = t == 0 ? (uint64_t)c * kChunk : counts[(size_t)c * ntab + t];
+        const uint64_t hi = t == 0 ? std::min<uint64_t>(nrev, (uint64_t)(c + 1) * kChunk)
+                                   : (c + 1 < nchunk ? counts[(size_t)(c + 1) * ntab + t] : rows[t]);
+        if (hi <= lo) continue;
+        const CvSlot& sl = out.slots[st2.first];
+        if (sl.flags & CVS_BYTES) memset(out.bytes.data() + sl.col + lo, 0, hi - lo);
+        else memset(out.words.data() + sl.col + lo, 0, (hi - lo) * 4);
+        if (sl.lencol != NO_ID) memset(out.words.data() + sl.lencol + lo, 0, (hi - lo) * 4);
+      }
+      const uint32_t r1 = std::min(nrev, (c + 1) * kChunk);
+      for (uint32_t r = c * kChunk; r < r1; ++r) {
+        if (r + kAhead < r1) D.prefetch(cols[r + kAhead].root);
+        ReviewCol rc = cols[r];
+        F.refs.clear();
+        mine.clear();
+        if (rc.root != NO_ID) {
+          const Node& d = D(rc.root);
+          if (d.type != NT_OBJ) { bad = true; continue; }
+          F.members(S.n[0], d, r);
+        }
+        auto local = [&](uint32_t src) {  // the review's copy of src (once per review)
+          for (const auto& m : mine) if (m.first == src) return m.second;
+          const uint32_t l = copy_into(ch.nodes, src, 0);
+          mine.push_back({src, l});
+          return l;
+        };
+        for (const auto& rf : F.refs) {
+          if (rf.first < node_begin) { out.words[rf.second] = (CW_NODE << CW_SHIFT) | rf.first; continue; }
+          if (is_shared(rf.first)) out.words[rf.second] = (CW_NODE << CW_SHIFT) | shared.at(rf.first);
+          else ch.words.push_back({rf.second, local(rf.first)});
+        }
+        uint32_t* lf[3] = {&rc.labels, &rc.old_labels, &rc.ns_labels};
+        for (int f = 0; f < 3; ++f) {
+          const uint32_t src = *lf[f];
+          if (src == NO_ID || src < node_begin) continue;
+          if (is_shared(src)) { *lf[f] = shared.at(src); continue; }
+          ch.cols.push_back({(uint64_t)r * 3 + f, local(src)});
+        }
+        rc.root = NO_ID;
+        out.cols[r] = rc;
       }
     }
   });
   if (bad) { why = "a value id does not fit a column word"; return false; }
-  // ---- D: subtrees kept as nodes (shared ones once)
-  std::unordered_map<uint32_t, uint32_t> copied;
-  auto copy = [&](uint32_t src) -> uint32_t {
-    if (src < node_begin) return src;  // the permanent region is uploaded as it is
-    auto it = copied.find(src);
-    if (it != copied.end()) return it->second;
-    const uint32_t dst = node_begin + (uint32_t)out.nodes.size();
-    out.nodes.push_back(D(src));
-    // breadth-first: each composite's children as one contiguous run
-    std::vector<std::pair<uint32_t, uint32_t>> q{{src, dst}};
-    for (size_t qi = 0; qi < q.size(); ++qi) {
-      const Node sn = D(q[qi].first);
-      if (sn.type != NT_OBJ && sn.type != NT_ARR) continue;
-      const uint32_t run = node_begin + (uint32_t)out.nodes.size();
-      out.nodes[q[qi].second - node_begin].first = run;
-      for (uint32_t i = 0; i < sn.n; ++i) {
-        out.nodes.push_back(D(sn.first + i));
-        q.push_back({sn.first + i, run + i});
+  if (trace) fprintf(stderr, "columns: C2 fill %.1f ms\n", ms());
+  // ---- D: the kept subtrees in one array: the shared ones, then chunk by chunk
+  std::vector<uint64_t> base(nchunk + 1, nshared);
+  for (uint32_t c = 0; c < nchunk; ++c) base[c + 1] = base[c] + chunks[c].nodes.size();
+  if ((uint64_t)node_begin + base[nchunk] > CW_PAY) { why = "kept nodes exceed the column word"; return false; }
+  out.nodes.resize(base[nchunk]);
+  std::copy(shared_nodes.begin(), shared_nodes.end(), out.nodes.begin());
+  next = 0;
+  parallel_run(T, [&](int) {
+    for (;;) {
+      const uint32_t c = next.fetch_add(1);
+      if (c >= nchunk) break;
+      Chunk& ch = chunks[c];
+      const uint32_t g = node_begin + (uint32_t)base[c];  // global id of local 0
+      Node* dst = out.nodes.data() + base[c];
+      for (size_t i = 0; i < ch.nodes.size(); ++i) {
+        Node nd = ch.nodes[i];
+        if (nd.type == NT_OBJ || nd.type == NT_ARR) nd.first += g;
+        dst[i] = nd;
       }
+      for (const auto& w : ch.words) out.words[w.first] = (CW_NODE << CW_SHIFT) | (g + w.second);
+      for (const auto& f : ch.cols) {
+        ReviewCol& rc = out.cols[f.first / 3];
+        (f.first % 3 == 0 ? rc.labels : f.first % 3 == 1 ? rc.old_labels : rc.ns_labels) = g + f.second;
+      }
+      std::vector<Node>().swap(ch.nodes);
     }
-    copied[src] = dst;
-    return dst;
-  };
-  for (auto& v : refs)
-    for (const NodeRef& r : v) {
-      const uint32_t d = copy(r.src);
-      out.words[r.at] = (CW_NODE << CW_SHIFT) | d;
-    }
-  out.cols = cols;
-  for (ReviewCol& rc : out.cols) {
-    rc.root = NO_ID;
-    if (rc.labels != NO_ID) rc.labels = copy(rc.labels);
-    if (rc.old_labels != NO_ID) rc.old_labels = copy(rc.old_labels);
-    if (rc.ns_labels != NO_ID) rc.ns_labels = copy(rc.ns_labels);
-  }
-  if ((uint64_t)node_begin + out.nodes.size() > CW_PAY) { why = "kept nodes exceed the column word"; return false; }
+  });
+  if (trace) fprintf(stderr, "columns: D nodes %.1f ms (%zu kept)\n", ms(), out.nodes.size());
   // object views, element tables, the (view, key) hash
   out.views.assign(views_of.size(), 0);
   for (size_t v = 0; v < views_of.size(); ++v) out.views[v] = S.n[views_of[v]].dyn ? CV_COMPLETE : 0;
@@ -416,6 +578,7 @@ bool build_columns(const PathPlan& plan, const Node* perm, uint32_t node_begin, 
       const SNode& x = S.n[s];
       o << name << ":" << (x.node ? " nodes" : "") << (x.view != NO_ID ? " view" + std::to_string(x.view) : "")
         << (x.tab != NO_ID ? " table" + std::to_string(x.tab) : "") << ((x.seen & S_SCALAR) ? " scalars" : "")
+        << (x.slot != NO_ID && (out.slots[x.slot].flags & CVS_BYTES) ? " bytes" : "")
         << (x.dyn ? " complete" : "") << "\n";
       if (x.node) continue;
       if (x.elem != NO_ID && x.tab != NO_ID) todo.push_back({x.elem, name + "[*]"});

@@ -10,7 +10,12 @@
 // document nodes only for the paths a program reads whole (label objects the
 // match stage scans, objects a template iterates or prints).
 #pragma once
+#include <sys/mman.h>
+
 #include <cstdint>
+#include <cstdlib>
+#include <new>
+#include <utility>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -21,19 +26,61 @@
 
 namespace gk {
 
+// An uninitialised array (every element is written before it is read): the
+// build's threads write their own chunks' rows, so the first touch of the
+// pages -- and their zeroing -- is spread over them instead of one serial
+// fill of ~250 MB.  Large buffers are 2 MB aligned and marked for huge pages.
+template <class T>
+struct RawBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  RawBuf() = default;
+  RawBuf(const RawBuf&) = delete;
+  RawBuf& operator=(const RawBuf&) = delete;
+  ~RawBuf() { free(p); }
+  void resize(size_t k) {
+    free(p);
+    p = nullptr;
+    n = k;
+    if (!k) return;
+    const size_t bytes = k * sizeof(T);
+    void* m = nullptr;
+    if (bytes >= (32u << 20)) {
+      if (posix_memalign(&m, 2u << 20, bytes) != 0) m = nullptr;
+      if (m) madvise(m, bytes, MADV_HUGEPAGE);
+    } else {
+      m = malloc(bytes);
+    }
+    if (!m) throw std::bad_alloc();
+    p = (T*)m;
+  }
+  size_t size() const { return n; }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
+using WordBuf = RawBuf<uint32_t>;
+using ByteBuf = RawBuf<uint8_t>;
+
 struct ColStore {
-  std::vector<uint32_t> words;  // every column's value words
+  WordBuf words;                // every word column's values
+  ByteBuf bytes;                // the byte columns (CVS_BYTES)
   std::vector<CvSlot> slots;
   std::vector<CvHash> hash;     // power-of-two size
   std::vector<uint32_t> views;  // per object view: CV_COMPLETE
   std::vector<uint32_t> tabs;   // per element table: the slot of its elements
-  std::vector<Node> nodes;      // the subtrees kept as nodes: ids node_begin + k
-  std::vector<ReviewCol> cols;  // the review columns with node ids into `nodes`
+  NodeArena nodes;              // the subtrees kept as nodes: ids node_begin + k
+  RawBuf<ReviewCol> cols;       // the review columns with node ids into `nodes`
   uint32_t node_begin = 0;
   uint64_t rows = 0;            // rows of every table (reviews + elements)
   std::string schema;           // description (diagnostics)
-  uint64_t bytes() const {
-    return words.size() * 4 + slots.size() * sizeof(CvSlot) + hash.size() * sizeof(CvHash) + views.size() * 4 +
+  uint64_t total_bytes() const {
+    return words.size() * 4 + bytes.size() + slots.size() * sizeof(CvSlot) + hash.size() * sizeof(CvHash) + views.size() * 4 +
            tabs.size() * 4 + nodes.size() * sizeof(Node) + cols.size() * sizeof(ReviewCol);
   }
 };

@@ -326,6 +326,7 @@ struct DevArgs {
   // columnar staged batch (colstore.cc; cv_on = 0: the review documents are
   // node trees).  The review at evaluation position r is V_ROW(view 0, row r).
   const uint32_t* cv_words;   // every path column's value words (CW_*), one per row of its table
+  const uint8_t* cv_bytes;    // the byte columns (CVS_BYTES)
   const struct CvSlot* cv_slots;
   const struct CvHash* cv_hash;  // (object view, member key) -> slot, open addressing
   const uint32_t* cv_views;   // per object view: CV_COMPLETE
@@ -351,7 +352,7 @@ struct CvSlot {
   uint32_t lencol;  // word offset of the array-length column (CW_ARR rows), NO_ID if none
   uint16_t view;    // CW_OBJ rows: the object view of this path
   uint16_t tab;     // CW_ARR rows: the element table of this path
-  uint32_t pad;
+  uint32_t flags;   // CVS_BYTES: the column is bytes in cv_bytes (cv_byte_word)
 };
 static_assert(sizeof(CvSlot) == 16, "CvSlot layout");
 struct CvHash {
@@ -359,6 +360,11 @@ struct CvHash {
 };
 static_assert(sizeof(CvHash) == 16, "CvHash layout");
 constexpr uint32_t CV_COMPLETE = 1;  // every member key the batch has at this path has a slot
+// A path whose values carry no payload (objects only tested or navigated,
+// null / booleans, undefined) is a byte column: tag << 2 | the literal
+constexpr uint32_t CVS_BYTES = 1;
+constexpr uint32_t cv_byte_word(uint32_t b) { return ((b >> 2) << CW_SHIFT) | (b & 3u); }
+constexpr uint8_t cv_word_byte(uint32_t w) { return (uint8_t)(((w >> CW_SHIFT) << 2) | (w & 3u)); }
 constexpr uint32_t cv_hash_of(uint32_t view, uint32_t key) {  // (constexpr: host and device)
   uint32_t h = view * 0x9E3779B1u ^ key * 0x85EBCA77u;
   return h ^ (h >> 15);

@@ -569,7 +569,8 @@ __device__ __forceinline__ uint32_t rows_len(uint64_t v) { return (uint32_t)(vpa
 // the value of slot `slot` at `row`
 __device__ __forceinline__ uint64_t cv_value(uint32_t slot, uint64_t row) {
   const CvSlot sl = gk_args.cv_slots[slot];
-  const uint32_t w = gk_args.cv_words[(uint64_t)sl.col + row];
+  const uint32_t w = (sl.flags & CVS_BYTES) ? cv_byte_word(gk_args.cv_bytes[(uint64_t)sl.col + row])
+                                            : gk_args.cv_words[(uint64_t)sl.col + row];
   const uint32_t p = w & CW_PAY;
   switch (w >> CW_SHIFT) {
     case CW_STR: return mkv(V_STR, p);

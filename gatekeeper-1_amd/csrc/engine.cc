@@ -405,7 +405,7 @@ struct gk_batch {
   bool columnar = false;
   std::string col_why;         // why the node form was kept
   gk::ColStore cv;
-  gk::DBuf d_cv_words, d_cv_slots, d_cv_hash, d_cv_views, d_cv_tabs;
+  gk::DBuf d_cv_words, d_cv_bytes, d_cv_slots, d_cv_hash, d_cv_views, d_cv_tabs;
 };
 
 // Webhook micro-batch coalescer: concurrent single-review
@@ -1862,6 +1862,7 @@ static int launch_and_collect(gk_engine* e, EvalCtx* x, const TablePtrs& tp, con
     a.part = (unsigned long long*)x->d_part.p;
     if (colb && colb->columnar) {  // the batch's documents in column form (colstore.h)
       a.cv_words = (const uint32_t*)colb->d_cv_words.p;
+      a.cv_bytes = (const uint8_t*)colb->d_cv_bytes.p;
       a.cv_slots = (const CvSlot*)colb->d_cv_slots.p;
       a.cv_hash = (const CvHash*)colb->d_cv_hash.p;
       a.cv_views = (const uint32_t*)colb->d_cv_views.p;
@@ -3013,12 +3014,13 @@ static gk::PathPlan batch_plan(gk_engine* e) {
   return e->plan;
 }
 
-// GKGPU_COLUMNS (A/B switch): staged batches in column form (colstore.h)
-static bool columns_on() { return env_mode("GKGPU_COLUMNS", 0, 1) != 0; }
+// GKGPU_COLUMNS (A/B switch, default on): staged batches in column form (colstore.h)
+static bool columns_on() { return env_mode("GKGPU_COLUMNS", 1, 1) != 0; }
 
 // The column form's device arrays: the permanent region and the kept
 // subtrees as the batch's node array, the review columns, the path columns.
 static bool batch_upload_columns(gk_engine* e, gk_batch* b) {
+  const auto t0 = Clock::now();
   const ColStore& cv = b->cv;
   const size_t perm = b->node_begin, kept = cv.nodes.size();
   if (!b->d_nodes.reserve((perm + kept + 1) * sizeof(Node))) return false;
@@ -3029,8 +3031,18 @@ static bool batch_upload_columns(gk_engine* e, gk_batch* b) {
                         hipMemcpyHostToDevice) != hipSuccess)
     return false;
   b->d_nodes.used = (perm + kept) * sizeof(Node);
-  return up(b->d_revs, cv.cols, false) && up(b->d_cv_words, cv.words, false) && up(b->d_cv_slots, cv.slots, false) &&
-         up(b->d_cv_hash, cv.hash, false) && up(b->d_cv_views, cv.views, false) && up(b->d_cv_tabs, cv.tabs, false);
+  const double ms_nodes = ms_since(t0);
+  bool ok = b->d_revs.upload(cv.cols.data(), cv.cols.size() * sizeof(ReviewCol), false);
+  const double ms_cols = ms_since(t0);
+  ok = ok && b->d_cv_words.upload(cv.words.data(), cv.words.size() * 4, false) &&
+       b->d_cv_bytes.upload(cv.bytes.data(), cv.bytes.size(), false);
+  const double ms_words = ms_since(t0);
+  ok = ok && up(b->d_cv_slots, cv.slots, false) && up(b->d_cv_hash, cv.hash, false) && up(b->d_cv_views, cv.views, false) &&
+       up(b->d_cv_tabs, cv.tabs, false);
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "upload columns: nodes %.1f ms, review columns %.1f ms, path columns %.1f ms, tables %.1f ms\n", ms_nodes,
+            ms_cols - ms_nodes, ms_words - ms_cols, ms_since(t0) - ms_words);
+  return ok;
 }
 
 static int stage_page(gk_engine* e, const Page& page, gk_batch** out) {
@@ -3051,7 +3063,9 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
   // GKGPU_DEVICE_LAYOUT (A/B switch, default on): the path-grouped layout is
   // built on the device (layout.hip) from the per-document arena
   DevLayout dl;
-  const bool dev_layout = !e->host_only && e->dev_ok && env_mode("GKGPU_DEVICE_LAYOUT", 1, 1) != 0;
+  // (the column form starts from the per-document arena too: no placement)
+  const bool dev_layout =
+      (columns_on() || (!e->host_only && e->dev_ok)) && env_mode("GKGPU_DEVICE_LAYOUT", 1, 1) != 0;
   rc = flatten_page_into(e, page, size_order, b->arena, b->cols, &b->resources, &b->excluded, &b->ms_parse, nullptr,
                          dev_layout ? &dl : nullptr);
   if (rc != GK_OK) return rc;
@@ -3067,7 +3081,7 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
                                     e->st, e->smu, b->cv, b->col_why);
     if (getenv("GKGPU_FLATTEN_TRACE"))
       fprintf(stderr, "columns: %s %.1f ms, %llu bytes%s%s\n", b->columnar ? "built" : "not used", ms_since(t1),
-              (unsigned long long)b->cv.bytes(), b->columnar ? "" : ": ", b->col_why.c_str());
+              (unsigned long long)b->cv.total_bytes(), b->columnar ? "" : ": ", b->col_why.c_str());
   }
   b->ms_flatten = ms_since(t0);
   if (e->host_only) {  // documents stay in the host arena only (gk_debug_host_args)
@@ -3096,7 +3110,7 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
     return fail(e, GK_EDEVICE, "upload failed");
   }
   b->ms_upload = ms_since(t1);
-  b->dev_bytes = b->columnar ? b->cv.bytes()
+  b->dev_bytes = b->columnar ? b->cv.total_bytes()
                              : (uint64_t)(b->node_end - b->node_begin) * sizeof(Node) + b->cols.size() * sizeof(ReviewCol);
   release_parts_async();
   *out = b.release();
@@ -3337,7 +3351,7 @@ void gk_batch_free(gk_batch* b) {
   if (!b) return;
   b->d_revs.free_();
   b->d_nodes.free_();
-  for (DBuf* d : {&b->d_cv_words, &b->d_cv_slots, &b->d_cv_hash, &b->d_cv_views, &b->d_cv_tabs}) d->free_();
+  for (DBuf* d : {&b->d_cv_words, &b->d_cv_bytes, &b->d_cv_slots, &b->d_cv_hash, &b->d_cv_views, &b->d_cv_tabs}) d->free_();
   delete b;
 }
 
@@ -3906,6 +3920,7 @@ extern "C" int gk_debug_host_args_columns(gk_engine* e, const gk_batch* b, void*
   a.nodes = e->dbg_nodes.data();
   a.revs = b->cv.cols.data();
   a.cv_words = b->cv.words.data();
+  a.cv_bytes = b->cv.bytes.data();
   a.cv_slots = b->cv.slots.data();
   a.cv_hash = b->cv.hash.data();
   a.cv_views = b->cv.views.data();
@@ -3922,7 +3937,7 @@ extern "C" int gk_batch_columns(const gk_batch* b, const char** schema, const ch
   if (!b) return GK_EINVAL;
   if (schema) *schema = b->cv.schema.c_str();
   if (why) *why = b->col_why.c_str();
-  if (bytes) *bytes = b->cv.bytes();
+  if (bytes) *bytes = b->cv.total_bytes();
   return b->columnar ? 1 : 0;
 }
 

@@ -439,6 +439,27 @@ class Batch:
     def device_bytes(self) -> int:
         return self._drv._lib.gk_batch_device_bytes(self._h)
 
+    def _columns(self):
+        lib = self._drv._lib
+        lib.gk_batch_columns.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                         C.POINTER(C.c_uint64)]
+        sch, why, nb = C.c_char_p(), C.c_char_p(), C.c_uint64()
+        form = lib.gk_batch_columns(self._h, C.byref(sch), C.byref(why), C.byref(nb))
+        dec = lambda b: (b or b"").decode("utf-8", "replace")  # noqa: E731
+        return form == 1, dec(sch.value), dec(why.value), nb.value
+
+    def columnar(self) -> bool:
+        """staged in column form (csrc/colstore.h), not as document nodes"""
+        return self._columns()[0]
+
+    def columns_why(self) -> str:
+        """why the node form was kept (empty in column form)"""
+        return self._columns()[2]
+
+    def columns_schema(self) -> str:
+        """the column form's path schema (diagnostics)"""
+        return self._columns()[1]
+
     def timing_ms(self):
         """host staging milliseconds: (parse + build documents, flatten total, upload)"""
         t = (C.c_double * 3)()

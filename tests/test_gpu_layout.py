@@ -9,6 +9,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _node_form(monkeypatch):
+    """these tests are about the node form's layouts (the column form,
+    GKGPU_COLUMNS, is checked against it below)"""
+    monkeypatch.setenv("GKGPU_COLUMNS", "0")
+
+
 def _driver(cfg):
     import gkgpu
     from gkgpu import workloads as W
@@ -48,3 +55,10 @@ def test_device_layout_holds_the_host_documents(cfg, n, monkeypatch):
         b.free()
     assert out["1"] == out["0"]
     assert len(out["1"][0]) > 0
+    # the column form of the same page (colstore.h): the same rows
+    monkeypatch.setenv("GKGPU_COLUMNS", "1")
+    b = d.stage_page(pg)
+    assert b.columnar(), b.columns_why()
+    res = b.eval(decode=True, with_status=True)
+    assert (_rows(res), list(res.status), list(res.totals)) == out["1"]
+    b.free()
