@@ -1464,11 +1464,24 @@ __device__ __forceinline__ void mark_holes(uint64_t from, uint64_t k) {
 // reloading what another subset wrote: stale chunk state hands out slots twice
 // and marks live tuples as holes.  Every access is a wave-scope atomic, which
 // the compiler neither forwards nor caches, and is read back uniformly.
+// GK_CHUNK_PLAIN=1 (diagnostic only, GKGPU_JIT_PRE): round 5's plain accesses,
+// to reproduce the row loss (tools/diag_r06.sh).
+#ifndef GK_CHUNK_PLAIN
+#define GK_CHUNK_PLAIN 0
+#endif
 __device__ __forceinline__ uint64_t chunk_ld(unsigned long long* p) {
+#if GK_CHUNK_PLAIN
+  return *p;
+#else
   return rfl64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+#endif
 }
 __device__ __forceinline__ void chunk_st(unsigned long long* p, uint64_t v) {
+#if GK_CHUNK_PLAIN
+  *p = v;
+#else
   __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
 }
 #endif
 // a slot for each lane with `want` (every active lane calls it)

@@ -1371,6 +1371,17 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
         // register memo entries are the predicate's locals
         const Ins& qi = bank.code[q];
         if ((qi.op == OP_MEMO_GET || qi.op == OP_MEMO_PUT) && lslots.count(qi.y)) ok = false;
+        // so are the computed-key CSE shadows (dkN) and a fused emission's
+        // argument shadows (esS_i): a region that sets or reads one stays inline
+        if (shadowed.count(q) || esites.count(q)) ok = false;
+        if (qi.op == OP_GET && LK.konst(q - b0, qi.c) < 0) {
+          const int dyn = LK.find_dyn(q - b0, qi.b, qi.c);
+          if (dyn >= 0 && (uint32_t)dyn != q) ok = false;
+        }
+        if (qi.op == OP_EMIT && qi.b != qi.a) {
+          const EmitFlow::FFact* ff = EFL.find(q - b0, qi.a);
+          if (ff && ff->n > 0) ok = false;
+        }
       }
       for (uint32_t r : wrs)
         if (r != in.a && (is_live(x, r) || r == in.b || r == in.c)) ok = false;
