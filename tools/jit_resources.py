@@ -51,17 +51,27 @@ for t in ts:
 
 
 def notes(path):
+    """per kernel entry of amdhsa.kernels (an entry starts at its `  - .` line:
+    .agpr_count and .group_segment_fixed_size come before .name)"""
     r = subprocess.run([READELF, "--notes", path], capture_output=True, text=True)
-    kernels, cur = {}, None
+    kernels, cur, name = {}, {}, None
+
+    def close():
+        if name and name.startswith("gk_t_"):
+            kernels[name] = dict(cur)
+
     for ln in r.stdout.splitlines():
-        m = re.search(r"\.name:\s+(\S+)", ln)
-        if m and m.group(1).startswith("gk_t_"):
-            cur = kernels.setdefault(m.group(1), {})
-            continue
+        if re.match(r"^  - \.", ln):  # a new kernel entry (argument entries are indented deeper)
+            close()
+            cur, name = {}, None
+        m = re.search(r"^\s+\.name:\s+(\S+)", ln)
+        if m:
+            name = m.group(1)
         for f in FIELDS:
             m = re.search(re.escape(f) + r":\s+(\S+)", ln)
-            if m and cur is not None:
+            if m:
                 cur[f[1:]] = m.group(1)
+    close()
     return kernels
 
 
@@ -82,12 +92,17 @@ def main():
         if not k:
             rep.append("  no code object (bytecode VM)")
             continue
-        regs = int(k.get("vgpr_count", 0)) + int(k.get("agpr_count", 0))
+        # .vgpr_count is the unified total on gfx950 (arch VGPRs aligned to 4,
+        # then the AGPRs: .agpr_count of them); 512 per SIMD lane, granule 8
+        regs = int(k.get("vgpr_count", 0))
         waves = min(8, 512 // max(8, (regs + 7) // 8 * 8)) if regs else 8
+        # LDS: a 256-thread block puts one wave on each SIMD of a CU (160 KB)
+        lds = int(k.get("group_segment_fixed_size", 0))
+        lds_waves = min(8, 163840 // lds) if lds else 8
         for f in FIELDS:
             if f[1:] in k:
                 rep.append("  %s: %s" % (f[1:], k[f[1:]]))
-        rep.append("  waves per SIMD (VGPR-bound): %d" % waves)
+        rep.append("  waves per SIMD: %d (VGPR-bound %d, LDS-bound %d)" % (min(waves, lds_waves), waves, lds_waves))
     text = "\n".join(rep) + "\n"
     print(text)
     if a.out:
