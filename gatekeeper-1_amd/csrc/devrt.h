@@ -2581,9 +2581,9 @@ __device__ __noinline__ bool op_emit_slow(PLane& L, uint64_t m, uint64_t d, uint
 // GK_EMIT_WIDE (GKGPU_JIT_PRE=GK_EMIT_WIDE=0 turns it off): every heap-free
 // argument (numbers, booleans, document and parameter nodes such as
 // k8sallowedrepos' input.parameters.repos) on the fast path, not only
-// interned strings and ints.  It first lost rows on the GPU -- a compiler
-// miscompile, cleared by -amdgpu-prealloc-sgpr-spill-vgprs (jit.cc kOpts);
-// profiles/r05/r05ah_prealloc_wide_ab.txt: config 4 1,995 -> 2,038 M evals/s.
+// interned strings and ints (profiles/r05/r05ah_prealloc_wide_ab.txt: config 4
+// 1,995 -> 2,038 M evals/s).  Round 5 saw it lose rows: a miscompile cleared by
+// -amdgpu-prealloc-sgpr-spill-vgprs (jit.cc kOpts).
 #ifndef GK_EMIT_WIDE
 #define GK_EMIT_WIDE 1
 #endif

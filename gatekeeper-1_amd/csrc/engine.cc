@@ -1246,13 +1246,21 @@ static bool sync_strings(gk_engine* e, TablePtrs* out) {
   std::lock_guard<std::mutex> g(e->smu);
   if (hipSetDevice(e->device) != hipSuccess) return false;
   Store& st = e->st;
+  const auto t0 = Clock::now();
+  const size_t s0 = e->d_strs.used, p0 = e->d_pool.used;
   bool ok = up(e->d_strs, st.strings(), true);
+  const double ms_strs = ms_since(t0);
   // +16: the device reads string bytes a dword at a time (devrt.h puts_) and may
   // touch up to 3 bytes past the last string
   ok = ok && e->d_pool.reserve(st.pool().size() + 16);
+  const double ms_pres = ms_since(t0);
   ok = ok && e->d_pool.upload(st.pool().data(), st.pool().size(), true);
+  const double ms_pool = ms_since(t0);
   ok = ok && up(e->d_sflags, st.str_flags(), true);
   ok = ok && up(e->d_nums, st.numbers(), true);
+  if (getenv("GKGPU_FLATTEN_TRACE"))
+    fprintf(stderr, "sync strings: entries %.1f ms (%zu -> %zu B), pool reserve %.1f ms, pool %.1f ms (%zu -> %zu B), flags+numbers %.1f ms\n",
+            ms_strs, s0, e->d_strs.used, ms_pres - ms_strs, ms_pool - ms_pres, p0, e->d_pool.used, ms_since(t0) - ms_pool);
   if (out) {
     out->strs = (const StrEnt*)e->d_strs.p;
     out->pool = (const uint8_t*)e->d_pool.p;

@@ -30,16 +30,21 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
-// -amdgpu-prealloc-sgpr-spill-vgprs: the lanes of the VGPRs that hold spilled
-// SGPRs are allocated up front.  Without it this toolchain (ROCm 7.2) miscompiled
-// large template kernels: a loop-carried register of K8sContainerLimits'
-// predicate was overwritten with values of uniform (scalar) bookkeeping, and
-// an inventory-join kernel faulted or flagged reviews; which code shape
-// triggered it came and went with unrelated edits.  -O1 and this option
-// each cleared both cases; the option keeps -O3 (profiles/r05/r05ag_sgpr_spill.txt).
+// -amdgpu-prealloc-sgpr-spill-vgprs: the VGPRs whose lanes hold spilled SGPRs
+// are allocated up front and reserved for the whole function.  Without it this
+// toolchain (ROCm 7.2) miscompiles large template kernels: round 5 saw lost
+// rows and a faulting join kernel, round 6 a GPU memory fault in the unfused
+// K8sContainerLimits kernel (tests/test_gpu_parity.py
+// test_emission_order_is_topdown_order[jit-0], profiles/r06/r06h_fault.txt)
+// after the option was turned off because round 5's reproducers ran clean.  In
+// that kernel's ISA without the option the predicate's spill-lane VGPRs
+// (v124-v126) are shuffled through AGPRs that also serve as ordinary spill
+// slots (1,872 other writes of v125); with it they are written only by
+// v_writelane and the epilogue reload (tools/isa_spill_lanes.py,
+// profiles/r06/r06h_isa_spill_lanes.txt).  The option measured neutral
+// (r06e_lanecap_prealloc_ab.txt).  GKGPU_JIT_PREALLOC=0 (diagnostic) drops it.
 const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs"};
 constexpr int kNOpts = 6;
-// GKGPU_JIT_PREALLOC=0 (diagnostic): without the spill preallocation
 std::vector<const char*> base_opts() {
   const char* e = getenv("GKGPU_JIT_PREALLOC");
   const bool pre = !(e && e[0] == '0');
@@ -1524,12 +1529,20 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // emission changes (profiles/r05/r05ay_wpe_recheck_ab.txt): every template at 3
 // or at 2 is slower on config 2 (1,000 -> 938 / 898 M evals/s), and the regex
 // templates at 2 or 4 on config 3 (1,030 -> 762 / 749 M).
+// Round 6, column form (profiles/r06/r06g_wpe_heap_grid.txt: every template at
+// 2 / 3 / 4 waves and 4-16 heap words, configs 2 and 4 in one call): small
+// programs at 3.  A 4-wave request leaves 40 KB of LDS, less than the 16 heap
+// words, the lane scalars and the parameter stage need, so the compiler got
+// no usable bound and K8sRequiredProbes read its parameters (probes x
+// probeTypes, iterated per container) from the node store: 1.62 -> 1.23 ms
+// (config 2) and 8.44 -> 3.43 ms (config 4) at 3; K8sAllowedRepos gives back
+// 0.02 / 0.28 ms.  Fewer heap words at 4 waves stage the parameters too but
+// lose elsewhere (K8sContainerLimits 1.29 -> 2.7 ms).
 static bool small_program(const Program& p) { return p.nregs <= 48; }
 static int wpe_of(const Program& p) {
   const char* w = getenv("GKGPU_JIT_WPE");
   if (w) return atoi(w);
-  if (!small_program(p)) return 2;
-  return p.uses_regex ? 3 : 4;
+  return small_program(p) ? 3 : 2;
 }
 static std::string wpe_suffix(const Program& p) {
   const int n = wpe_of(p);

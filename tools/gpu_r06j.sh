@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-6 HEAD: configs 3/4/6/5/5-coalesced/from-cache with their CPU
+# baselines (tools/gpu_final.sh part b), then a config-2 probe: the template
+# kernels with their emission sites cut out (GKGPU_JIT_PATCH; rows differ, the
+# time is what the emission path costs) and the passes' grid at capacity
+# (GKGPU_PASS_HINT=0).
+#   bash tools/gpu_r06j.sh <tag>
+cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r06j}
+bash tools/gpu_final.sh "$TAG" b || exit 1
+bash tools/gpu_bench_ab.sh ${TAG}_probe "--steps 20 --warmup 3 --shard-leg off --cpu-e2e off" "" \
+  "GKGPU_JIT_PATCH=@tools/probes/noemit_args.txt" "GKGPU_PASS_HINT=0" || exit 1
