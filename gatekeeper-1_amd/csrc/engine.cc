@@ -3091,7 +3091,8 @@ static int stage_page_locked(gk_engine* e, const Page& page, gk_batch** out) {
       fprintf(stderr, "columns: %s %.1f ms, %llu bytes%s%s\n", b->columnar ? "built" : "not used", ms_since(t1),
               (unsigned long long)b->cv.total_bytes(), b->columnar ? "" : ": ", b->col_why.c_str());
   }
-  b->ms_flatten = ms_since(t0);
+  b->ms_flatten = ms_since(t0);  // (the column build included)
+  t1 = Clock::now();              // the upload phase starts here
   if (e->host_only) {  // documents stay in the host arena only (gk_debug_host_args)
     *out = b.release();
     return GK_OK;

@@ -10,3 +10,6 @@ TAG=${1:-r06j}
 bash tools/gpu_final.sh "$TAG" b || exit 1
 bash tools/gpu_bench_ab.sh ${TAG}_probe "--steps 20 --warmup 3 --shard-leg off --cpu-e2e off" "" \
   "GKGPU_JIT_PATCH=@tools/probes/noemit_args.txt" "GKGPU_PASS_HINT=0" || exit 1
+mkdir -p gpurun_out/$TAG
+GKGPU_FLATTEN_TRACE=1 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --cpu-sample 0 --shard-leg off --cpu-e2e off > gpurun_out/$TAG/trace.json 2> gpurun_out/$TAG/trace.err || { echo TRACE_FAIL; exit 1; }
+grep -E "^(sync strings|stage upload|flatten: (parse|intern))" gpurun_out/$TAG/trace.err
