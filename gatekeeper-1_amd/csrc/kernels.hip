@@ -126,6 +126,25 @@ struct LOut {
   uint8_t* p;
   uint32_t pos;
   __device__ __forceinline__ void put(char c) { p[pos++] = (uint8_t)c; }
+  // n bytes of the dword array b starting at byte off (a format literal in
+  // LDS): whole dwords where the destination is dword-aligned -- the bytes of
+  // a lane's own range, so no neighbour's byte is touched -- single bytes at
+  // the two ends.  A byte at a time cost ~5 VALU + one LDS store per byte.
+  __device__ __forceinline__ void put_lit(const uint32_t* b, uint32_t off, uint32_t n) {
+    uint8_t* d = p + pos;
+    pos += n;
+    while (n && ((uint32_t)(uintptr_t)d & 3u)) {
+      *d++ = (uint8_t)(b[off >> 2] >> (8 * (off & 3)));
+      ++off;
+      --n;
+    }
+    const uint32_t sh = off & 3;
+    for (; n >= 4; n -= 4, off += 4, d += 4) {
+      const uint32_t lo = b[off >> 2];
+      *(uint32_t*)d = sh ? __builtin_amdgcn_alignbyte(b[(off >> 2) + 1], lo, sh) : lo;
+    }
+    for (; n; --n, ++off) *d++ = (uint8_t)(b[off >> 2] >> (8 * (off & 3)));
+  }
 };
 // LOut whose string sources are read in 16-B blocks (puts_wide below)
 struct LOutW : LOut {};
@@ -138,6 +157,9 @@ struct WOut {
   __device__ __forceinline__ void put(char c) {
     if ((uint64_t)rel < n) p[rel] = (uint8_t)c;
     ++rel;
+  }
+  __device__ __forceinline__ void put_lit(const uint32_t* b, uint32_t off, uint32_t k) {
+    for (; k; --k, ++off) put((char)(b[off >> 2] >> (8 * (off & 3))));
   }
 };
 
@@ -274,13 +296,8 @@ __device__ __forceinline__ void print_plain_r(O& o, const uint32_t* f, const uin
   for (uint32_t s = 0; s < nseg; ++s) {
     const uint32_t w0 = f[2 + 2 * s], w1 = f[3 + 2 * s];
     if ((w0 & 0xff) == 0) {
-      // the literal's bytes from LDS, a dword at a time
-      const uint32_t off = w1, n = w0 >> 8;
-      uint32_t q = off >> 2, sh = off & 3, cur = gk_fmt_lds.b[q];
-      for (uint32_t k = 0; k < n; ++k) {
-        o.put((char)(cur >> (8 * sh)));
-        if (++sh == 4 && k + 1 < n) { sh = 0; cur = gk_fmt_lds.b[++q]; }
-      }
+      // the literal's bytes from LDS (dword stores where aligned, LOut::put_lit)
+      o.put_lit(gk_fmt_lds.b, w1, w0 >> 8);
       continue;
     }
     const uint32_t j = w1 & 0xffff;
