@@ -670,6 +670,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
 extern "C" int gk_launch_format(const gk::DevArgs* a, hipStream_t stream, hipEvent_t* ev, uint64_t hint) {
   const uint64_t tiles = ((hint && hint < a->out_cap ? hint : a->out_cap) + gk::FTILE - 1) / gk::FTILE;
   const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096));
+  if (getenv("GKGPU_LAUNCH_TRACE"))
+    fprintf(stderr, "passes: hint %llu, out_cap %llu, tiles %llu, blocks %u\n", (unsigned long long)hint,
+            (unsigned long long)a->out_cap, (unsigned long long)tiles, blocks);
   hipLaunchKernelGGL(gk::gk_size_kernel, dim3(blocks), dim3(256), 0, stream, *a);
   if (ev) hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(gk::gk_scan_spine, dim3(1), dim3(1024), 0, stream, *a);
