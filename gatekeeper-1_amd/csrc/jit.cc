@@ -1544,6 +1544,9 @@ static int wpe_of(const Program& p) {
   if (w) return atoi(w);
   return small_program(p) ? 3 : 2;
 }
+// (Launch bounds at 3 or 4 waves with the LDS plan of the default left
+// unchanged measured slower for K8sContainerLimits -- 1.28 -> 1.56 / 2.71 ms
+// -- and neutral elsewhere: profiles/r06/r06n_launch_bound_ab.txt.)
 static std::string wpe_suffix(const Program& p) {
   const int n = wpe_of(p);
   return n > 0 ? ", " + std::to_string(n) : std::string();
