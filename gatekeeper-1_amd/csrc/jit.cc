@@ -839,6 +839,7 @@ struct Gen {
   std::string body;  // body of the predicate function
   bool param_reads = false;  // lookups / iterations over parameter nodes (vget_p, op_iter_next_p)
   bool param_regex = false;  // re_match with a computed (parameter) pattern (re_run -> re_run_lds)
+  uint32_t param_iter_depth = 0;  // deepest loop level of an iteration over a parameter collection
 };
 
 // Body of the predicate function: one statement per bytecode instruction.
@@ -1112,6 +1113,7 @@ Gen generate(const Program& p, const CodeBank& bank, const Store& st) {
           o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next_p(L, " << a << ", " << R(in.a + 1)
             << ", " << y << ", k_, v_, plo, pn)) goto " << x << ";";
           g.param_reads = true;
+          g.param_iter_depth = std::max<uint32_t>(g.param_iter_depth, in.y);
         } else {
           o << "{ uint64_t k_ = " << UND << ", v_ = " << UND << "; if (!op_iter_next(L, " << a << ", " << R(in.a + 1)
             << ", " << y << ", k_, v_)) goto " << x << ";";
@@ -1538,17 +1540,25 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 // (config 2) and 8.44 -> 3.43 ms (config 4) at 3; K8sAllowedRepos gives back
 // 0.02 / 0.28 ms.  Fewer heap words at 4 waves stage the parameters too but
 // lose elsewhere (K8sContainerLimits 1.29 -> 2.7 ms).
+// Refined at the end of round 6: the small programs that need the parameter
+// stage are those iterating a parameter collection inside a loop over another
+// one (loop level >= 3: RequiredProbes' probeTypes inside probes inside
+// containers) and those with regular expressions (their DFAs are staged too);
+// they get 3 waves.  Other small programs keep round 5's 4: K8sAllowedRepos
+// (one parameter loop per container) 0.157 -> 0.143 ms config 2, 3.17 -> 2.89
+// ms config 4 (profiles/r06/r06g_wpe_heap_grid.txt, ab1 vs ab2).
 static bool small_program(const Program& p) { return p.nregs <= 48; }
-static int wpe_of(const Program& p) {
+static int wpe_of(const Program& p, const Gen& g) {
   const char* w = getenv("GKGPU_JIT_WPE");
   if (w) return atoi(w);
-  return small_program(p) ? 3 : 2;
+  if (!small_program(p)) return 2;
+  return (p.uses_regex || g.param_iter_depth >= 3) ? 3 : 4;
 }
 // (Launch bounds at 3 or 4 waves with the LDS plan of the default left
 // unchanged measured slower for K8sContainerLimits -- 1.28 -> 1.56 / 2.71 ms
 // -- and neutral elsewhere: profiles/r06/r06n_launch_bound_ab.txt.)
-static std::string wpe_suffix(const Program& p) {
-  const int n = wpe_of(p);
+static std::string wpe_suffix(const Program& p, const Gen& g) {
+  const int n = wpe_of(p, g);
   return n > 0 ? ", " + std::to_string(n) : std::string();
 }
 static int lds_heap_words(const Program& p) {
@@ -1601,7 +1611,7 @@ struct StagePlan { bool params = false, dfa = false; int memo = 0; };
 static StagePlan stage_plan(const Program& p, const Gen& g, int depth) {
   StagePlan sp;
   if (!lds_stage_on()) return sp;
-  const int wpe = wpe_of(p);
+  const int wpe = wpe_of(p, g);
   const uint32_t limit = (wpe > 0 ? 163840u / (uint32_t)wpe : 163840u) - 512u;  // allocation granularity slack
   // lane heap words, lane scalars and (with the scalars) the loop watermarks;
   // then, as they fit: the memo cache, the DFAs, the parameters
@@ -1639,7 +1649,7 @@ static std::string inline_hot_tag(const Program& p) {
 
 std::string jit_name(const Program& p, const CodeBank& bank, const Store& st) {
   Gen g = generate(p, bank, st);
-  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix(p) + inline_hot_tag(p) + "lm" + std::to_string(lds_memo_entries(g))));
+  return "gk_t_" + hex16(fnv1a(g.pre + g.body + wpe_suffix(p, g) + inline_hot_tag(p) + "lm" + std::to_string(lds_memo_entries(g))));
 }
 
 std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, const std::string& name) {
@@ -1674,7 +1684,7 @@ std::string jit_source(const Program& p, const CodeBank& bank, const Store& st, 
     << "__device__ void " << name << "_pred(PLane& L, uint64_t review, uint64_t params, uint32_t plo, uint32_t pn) {\n"
     << g.body << "}\n"
     << "}  // namespace gk\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p) << ") " << name << "(gk::DevArgs) {\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256" << wpe_suffix(p, g) << ") " << name << "(gk::DevArgs) {\n"
     << "  gk::audit_body([&](gk::PLane& L, uint64_t review, uint64_t params, uint32_t, uint32_t plo, uint32_t pn) {\n"
     << "    gk::" << name << "_pred(L, review, params, plo, pn);\n"
     << "  });\n"
